@@ -1,0 +1,172 @@
+/*
+ * otfuse.h — C ABI of the MI355X-native (gfx950) Sinkhorn OT fusion path.
+ *
+ * Drop-in boundary for the reference's transport-plan API.  Every entry point
+ * takes caller-owned DEVICE buffers (plain pointers + sizes/leading dimensions),
+ * a caller-provided workspace where needed, and the hipStream_t to enqueue on.
+ * Nothing here allocates device memory or synchronises the device unless the
+ * function says so.  No torch types: the Python host layer (otfuse/) binds this
+ * with ctypes; a C/C++ caller links libotfuse.so directly.
+ *
+ * Reference interfaces replaced (file:line into the reference tree):
+ *   otf_cost_pairwise      ot.dist(x, y, metric) [+ "/= max"]        MRI_PET_OT_nojax.py:70-75
+ *                          PointCloud(x, y, scale_cost="max_cost")   MRI_PET_OT_OT_per_epoch_attn.py:155-156,
+ *                                                                    perturbot/perturbot/match/ott_egwl.py:350
+ *   otf_feature_cost       cost block of get_feature_coupling_pot    MRI_PET_OT_nojax.py:100-136
+ *                          init_matrix_np / M = constC - hC1 Ts hC2^T  perturbot/perturbot/match/fot.py:118-124
+ *   otf_sinkhorn           ot.sinkhorn(a, b, M, reg, numItermax, stopThr)  MRI_PET_OT_nojax.py:143
+ *                          (POT sinkhorn_knopp; vendored twin perturbot/perturbot/match/utils.py:6-115)
+ *                          and OTT linear.solve(Geometry(M, eps, "max_cost"))  perturbot/perturbot/match/fot.py:128-134
+ *   otf_plan_postprocess   NaN->1e-8 + row normalisation            MRI_PET_OT_nojax.py:702-715
+ *   otf_gemm_f32           ot_mri_from_pet = pet_fused @ T^T         MRI_PET_OT_nojax.py:718,
+ *                                                                    MRI_PET_OT_OT_per_epoch_attn.py:728
+ *
+ * Error convention: every function returns OTF_OK (0), a positive argument
+ * error (OTF_EINVAL / OTF_EUNSUPPORTED) or a negative HIP error (OTF_EHIP).
+ * Solver outcomes (converged / max_iter / numerical break) are reported through
+ * the device-side otf_sinkhorn_info, mirroring POT's "revert to the previous
+ * iterate and stop" behaviour.
+ */
+#ifndef OTFUSE_H_
+#define OTFUSE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* otf_stream_t; /* == hipStream_t */
+
+enum {
+    OTF_OK = 0,
+    OTF_EINVAL = 1,
+    OTF_EUNSUPPORTED = 2,
+    OTF_EHIP = -1
+};
+
+typedef enum { OTF_F32 = 0, OTF_F64 = 1 } otf_dtype;
+typedef enum { OTF_SQEUCLIDEAN = 0, OTF_EUCLIDEAN = 1 } otf_metric;
+
+/* Sinkhorn flavours.
+ * OTF_FLAVOR_POT: POT sinkhorn_knopp — kernel-domain scaling vectors u, v,
+ *   u0 = 1/n, v0 = 1/m, v-update then u-update, numerical break (zero in K^T u,
+ *   nan/inf in u or v) reverts to the previous iterate and stops, the L2
+ *   marginal error is checked every `check_every` iterations against stop_thr.
+ * OTF_FLAVOR_OTT: OTT-jax lse_mode — log-domain potentials f, g (returned in
+ *   u_out / v_out), L1 marginal error every `check_every` iterations against
+ *   stop_thr (OTT's threshold).                                                */
+typedef enum { OTF_FLAVOR_POT = 0, OTF_FLAVOR_OTT = 1 } otf_flavor;
+
+/* Status codes written to otf_sinkhorn_info.status. */
+enum {
+    OTF_SK_RUNNING = 0,
+    OTF_SK_CONVERGED = 1,
+    OTF_SK_MAX_ITER = 2,
+    OTF_SK_NUMERICAL_BREAK = 3
+};
+
+typedef struct {
+    double reg;         /* entropic regularisation (absolute, on the scaled cost)      */
+    double stop_thr;    /* POT stopThr / OTT threshold; <= 0 runs exactly max_iter     */
+    int32_t max_iter;   /* POT numItermax / OTT max_iterations                         */
+    int32_t check_every;/* 10 in POT and OTT (inner_iterations)                        */
+    int32_t flavor;     /* otf_flavor                                                  */
+    int32_t err_squared;/* 1: compare the SQUARED L2 error (vendored utils.py:88-89)   */
+    int32_t sync_every; /* host polls the device stop flag every N iterations; 0 = never
+                           (all max_iter passes are enqueued; finished passes no-op)   */
+    int32_t reserved;
+} otf_sinkhorn_opts;
+
+/* Written on the device by otf_sinkhorn (read it after the stream completes). */
+typedef struct {
+    int32_t stop;       /* 1 once converged or broken                                  */
+    int32_t last_good;  /* iteration whose (u, v) are returned; -1 = initial u0, v0    */
+    int32_t niter;      /* POT log['niter'] (last iteration index ii)                  */
+    int32_t status;     /* OTF_SK_*                                                    */
+    int32_t n_err;      /* number of entries written to the err log                    */
+    int32_t break_iter; /* iteration of the numerical break, or -1                     */
+    int32_t pad[2];
+} otf_sinkhorn_info;
+
+/* Library identification; returns a static string ("otfuse <ver> gfx950"). */
+const char* otf_version(void);
+
+/* Pairwise cost C (n x m, row stride ldc) between rows of X (n x d, ldx) and Y
+ * (m x d, ldy), float32 in/out, MFMA contraction (v_mfma_f32_32x32x2_f32):
+ *   C_ij = max(|x_i|^2 + |y_j|^2 - 2 x_i.y_j, 0)      [sqrt if OTF_EUCLIDEAN]
+ *   C_ii = 0 if zero_diag (POT's "X is Y" case).
+ * If cmax != NULL the kernel also writes max_ij C_ij to *cmax (device float,
+ * zeroed by the function first): scale_cost="max_cost" / "/= C.max()" without
+ * a second pass over C.  Requirements: ldx, ldy multiples of 4, 16-B aligned. */
+int otf_cost_pairwise(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
+                      int64_t m, int64_t d, int32_t metric, int32_t zero_diag, float* C,
+                      int64_t ldc, float* cmax, otf_stream_t stream);
+
+/* Divides C (n x m, ldc) by the device scalar *s (in place).  float32/64. */
+int otf_scale_inplace(void* C, int64_t n, int64_t m, int64_t ldc, int32_t dtype, const void* s,
+                      otf_stream_t stream);
+
+/* Feature cost (float64 compute, like the reference):
+ *   weights_mode 0 (get_feature_coupling_pot, MRI_PET_OT_nojax.py:121-136):
+ *       w1 = Ts.sum(1), w2 = Ts.sum(0)
+ *   weights_mode 1 (fot_numpy + init_matrix_np, perturbot/.../fot.py:108-124,
+ *       utils.py:125-184; needs n == n2):  w1 = Ts.sum(0), w2 = Ts.sum(1)
+ *   t1 = (X^2)^T w1, t2 = (Y^2)^T w2,
+ *   M (d x d2, ldm) = t1[:,None] + t2[None,:] - 2 X^T Ts Y
+ * X: n x d float32 (ldx), Y: n2 x d2 float32 (ldy).  Ts: n x n2 float64 (ldts),
+ * or NULL with ts_diag (length n == n2, float64) for a diagonal Ts such as
+ * np.eye(B)/B.  Workspace: otf_feature_cost_workspace_size() bytes.           */
+size_t otf_feature_cost_workspace_size(int64_t n, int64_t n2, int64_t d, int64_t d2);
+int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
+                     int64_t n2, int64_t d, int64_t d2, const double* Ts, int64_t ldts,
+                     const double* ts_diag, int32_t weights_mode, double* M, int64_t ldm,
+                     void* workspace, size_t ws_bytes, otf_stream_t stream);
+
+/* Entropic OT between histograms a (n) and b (m) with cost C (n x m, ldc), all
+ * of `dtype` (float32 or float64), on the device:
+ *   K = exp(-C * cscale / reg)      (cscale = 1/(*cost_scale) if cost_scale != NULL)
+ * POT flavour: u_out (n), v_out (m) receive the scaling vectors, P_out (n x m,
+ * ldp, optional) the plan u_i K_ij v_j.  OTT flavour: u_out, v_out receive the
+ * potentials f, g and P_out = exp((f_i + g_j - C_ij*cscale)/reg).
+ * info (device) receives the outcome; errlog (device float64, optional, length
+ * max_iter / check_every + 1) the marginal errors.
+ * Layout requirements: ldc and ldp multiples of 16/sizeof(dtype) and 16-B
+ * aligned rows.  Workspace: otf_sinkhorn_workspace_size() bytes.
+ * Host synchronisation happens only if opts->sync_every > 0.                   */
+size_t otf_sinkhorn_workspace_size(int64_t n, int64_t m, int32_t dtype, int32_t max_iter);
+int otf_sinkhorn(const void* a, const void* b, const void* C, int64_t n, int64_t m, int64_t ldc,
+                 int32_t dtype, const void* cost_scale, const otf_sinkhorn_opts* opts,
+                 void* u_out, void* v_out, void* P_out, int64_t ldp, int32_t P_dtype,
+                 otf_sinkhorn_info* info, double* errlog, void* workspace, size_t ws_bytes,
+                 otf_stream_t stream);
+
+/* Profiling helper for bench.py: runs the same solve as otf_sinkhorn with
+ * stop_thr ignored (exactly max_iter iterations) and records a hipEvent pair
+ * around every iteration pass; *avg_pass_ms receives the mean pass duration.
+ * Synchronises the stream.                                                     */
+int otf_sinkhorn_profile(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                         int64_t ldc, int32_t dtype, const void* cost_scale,
+                         const otf_sinkhorn_opts* opts, void* u_out, void* v_out,
+                         otf_sinkhorn_info* info, void* workspace, size_t ws_bytes,
+                         float* avg_pass_ms, otf_stream_t stream);
+
+/* Plan post-processing (MRI_PET_OT_nojax.py:702-715): T (d x d2, ldt, dtype
+ * float32/64) -> Tn float32 (ldtn): NaN -> nan_fill, row sums (0 -> 1e-8),
+ * Tn = T / rowsum.  rownorm = 0 only converts + fills.                          */
+int otf_plan_postprocess(const void* T, int64_t d, int64_t d2, int64_t ldt, int32_t dtype,
+                         float nan_fill, int32_t rownorm, float* Tn, int64_t ldtn,
+                         otf_stream_t stream);
+
+/* out (M x N, ldo) = alpha * op(A) op(B) (+ beta * out), float32, where
+ * op(A)_{ik} = A[i*sa0 + k*sa1] and op(B)_{kj} = B[k*sb0 + j*sb1]: the plan
+ * application Z @ T^T and its backward G @ T.                                  */
+int otf_gemm_f32(const float* A, int64_t sa0, int64_t sa1, const float* B, int64_t sb0,
+                 int64_t sb1, float* out, int64_t ldo, int64_t M, int64_t N, int64_t K,
+                 float alpha, float beta, otf_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OTFUSE_H_ */

@@ -1,0 +1,231 @@
+"""CPU oracle for the Sinkhorn OT fusion path — TEST INFRASTRUCTURE ONLY.
+
+This module is the parity checker (tests/), the smoke check
+(``__graft_entry__.smoke``) and the timed CPU baseline (``bench.py``'s
+``cpu_baseline`` leg).  Nothing in the product package imports it; the product
+path is the HIP library and fails loudly when that library is missing.
+
+Two restatements of the reference algorithm live here:
+
+* ``libotoracle.so`` (``otoracle.c``, float64, OpenMP) — the fast one, used for
+  the CPU baseline and the large parity cases;
+* pure-NumPy functions (``*_np``) — small cases, and a cross-check of the C code.
+
+Both follow the reference (file:line into /root/reference):
+
+* feature cost     MRI_PET_OT_nojax.py:121-136
+* pairwise cost    MRI_PET_OT_nojax.py:70-75 -> POT 0.9.6 ``ot.dist`` (not vendored)
+* Sinkhorn-Knopp   MRI_PET_OT_nojax.py:143 -> POT ``sinkhorn_knopp``; vendored twin
+                   perturbot/perturbot/match/utils.py:6-115
+* log-domain       perturbot/perturbot/match/fot.py:128-134 -> OTT-jax 0.6.0
+                   (absent here: parity unpinned)
+* plan apply       MRI_PET_OT_nojax.py:701-721
+
+Pinning: the Sinkhorn, feature-cost and plan-apply restatements are checked
+against golden vectors produced by the reference's own code in the survey
+container (tests/golden/make_golden.py -> tests/golden/*.npz).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libotoracle.so")
+_lib = None
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_fp = ctypes.POINTER(ctypes.c_float)
+_ip = ctypes.POINTER(ctypes.c_int64)
+
+
+def build() -> str:
+    """Compile ``libotoracle.so`` with the committed Makefile."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oro_set_threads.argtypes = [ctypes.c_int]
+        L.oro_set_threads.restype = ctypes.c_int
+        L.oro_pairwise_cost.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp]
+        L.oro_pairwise_cost.restype = ctypes.c_double
+        L.oro_feature_cost.argtypes = [_dp, _dp, _dp, ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                       _dp]
+        L.oro_feature_cost.restype = None
+        L.oro_sinkhorn_knopp.argtypes = [_dp, _dp, _dp, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                         ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                         _dp, _dp, _dp, _ip, _dp]
+        L.oro_sinkhorn_knopp.restype = ctypes.c_int
+        L.oro_sinkhorn_log.argtypes = [_dp, _dp, _dp, ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                       ctypes.c_double, ctypes.c_int, _dp, _dp, _dp, _ip]
+        L.oro_sinkhorn_log.restype = None
+        L.oro_plan_apply.argtypes = [_dp, ctypes.c_int64, ctypes.c_int64, _fp, ctypes.c_int64,
+                                     _fp, _fp]
+        L.oro_plan_apply.restype = None
+        _lib = L
+    return _lib
+
+
+def set_threads(n: int) -> int:
+    return lib().oro_set_threads(int(n))
+
+
+def _d(x):
+    return np.ascontiguousarray(x, dtype=np.float64)
+
+
+def _ptr(a, t=_dp):
+    return a.ctypes.data_as(t)
+
+
+# --------------------------------------------------------------------------- C-backed
+def pairwise_cost(X, Y, metric="sqeuclidean", zero_diag=False, scale_max=False):
+    """Returns ``(C float64 (n, m), max of unscaled C)``."""
+    X, Y = _d(X), _d(Y)
+    n, d = X.shape
+    m = Y.shape[0]
+    C = np.empty((n, m), np.float64)
+    mx = lib().oro_pairwise_cost(_ptr(X), _ptr(Y), n, m, d, int(metric == "euclidean"),
+                                 int(zero_diag), int(scale_max), _ptr(C))
+    return C, mx
+
+
+def feature_cost(X, Y, Ts, weights="pot"):
+    """Feature cost; float32 inputs are squared in float32 like the reference's X**2."""
+    sq_f32 = int(np.asarray(X).dtype == np.float32 and np.asarray(Y).dtype == np.float32)
+    X, Y, Ts = _d(X), _d(Y), _d(Ts)
+    n, d = X.shape
+    n2, d2 = Y.shape
+    M = np.empty((d, d2), np.float64)
+    lib().oro_feature_cost(_ptr(X), _ptr(Y), _ptr(Ts), n, n2, d, d2, sq_f32,
+                           int(weights == "fot"), _ptr(M))
+    return M
+
+
+def sinkhorn_knopp(a, b, C, reg, numItermax=1000, stopThr=1e-9, cscale=1.0, check_every=10,
+                   err_squared=False, want_plan=True):
+    """POT ``sinkhorn_knopp`` semantics.  Returns ``(P|None, u, v, info dict)``."""
+    a, b, C = _d(a), _d(b), _d(C)
+    n, m = C.shape
+    u = np.empty(n)
+    v = np.empty(m)
+    P = np.empty((n, m)) if want_plan else None
+    info = np.zeros(4, np.int64)
+    errlog = np.zeros(numItermax // max(check_every, 1) + 2)
+    lib().oro_sinkhorn_knopp(_ptr(a), _ptr(b), _ptr(C), n, m, float(reg), float(cscale),
+                             int(numItermax), float(stopThr), int(check_every), int(err_squared),
+                             _ptr(u), _ptr(v), _ptr(P) if P is not None else None,
+                             _ptr(info, _ip), _ptr(errlog))
+    return P, u, v, {"niter": int(info[0]), "n_updates": int(info[1]),
+                     "break_iter": int(info[2]), "err": errlog[: int(info[3])].tolist()}
+
+
+def sinkhorn_log(a, b, C, reg, max_iter=2000, threshold=1e-3, inner=10, cscale=1.0):
+    """OTT-flavour log-domain Sinkhorn (parity unpinned).  Returns ``(P, f, g, info)``."""
+    a, b, C = _d(a), _d(b), _d(C)
+    n, m = C.shape
+    f = np.empty(n)
+    g = np.empty(m)
+    P = np.empty((n, m))
+    info = np.zeros(2, np.int64)
+    lib().oro_sinkhorn_log(_ptr(a), _ptr(b), _ptr(C), n, m, float(reg), float(cscale),
+                           int(max_iter), float(threshold), int(inner), _ptr(f), _ptr(g),
+                           _ptr(P), _ptr(info, _ip))
+    return P, f, g, {"n_iters": int(info[0]), "converged": bool(info[1])}
+
+
+def plan_apply(T, Z=None):
+    """MRI_PET_OT_nojax.py:701-721 in float32.  Returns ``(T_normalised, Z @ T_n^T | None)``."""
+    T = _d(T)
+    d, d2 = T.shape
+    Tn = np.empty((d, d2), np.float32)
+    out = None
+    if Z is not None:
+        Z = np.ascontiguousarray(Z, dtype=np.float32)
+        out = np.empty((Z.shape[0], d), np.float32)
+    lib().oro_plan_apply(_ptr(T), d, d2, _ptr(Z, _fp) if Z is not None else None,
+                         Z.shape[0] if Z is not None else 0, _ptr(Tn, _fp),
+                         _ptr(out, _fp) if out is not None else None)
+    return Tn, out
+
+
+# --------------------------------------------------------------------------- NumPy
+def pairwise_cost_np(X, Y, metric="sqeuclidean", zero_diag=False):
+    """POT ``euclidean_distances`` (via ``ot.dist``) in float64."""
+    X, Y = _d(X), _d(Y)
+    c = -2.0 * (X @ Y.T)
+    c += np.einsum("ij,ij->i", X, X)[:, None]
+    c += np.einsum("ij,ij->i", Y, Y)[None, :]
+    c = np.maximum(c, 0.0)
+    if metric == "euclidean":
+        c = np.sqrt(c)
+    if zero_diag:
+        c = c * (1.0 - np.eye(c.shape[0], c.shape[1]))
+    return c
+
+
+def feature_cost_np(X, Y, Ts):
+    """MRI_PET_OT_nojax.py:121-136 (keeps the inputs' dtype for X**2, as the reference)."""
+    X, Y, Ts = np.asarray(X), np.asarray(Y), _d(Ts)
+    w1 = Ts.sum(axis=1)
+    t1 = (X ** 2).T @ w1
+    w2 = Ts.sum(axis=0)
+    t2 = (Y ** 2).T @ w2
+    t3 = -2 * X.T @ Ts @ Y
+    return t1[:, None] + t2[None, :] + t3
+
+
+def block_diag_ts(ts_dict, x_dict, y_dict):
+    """Block-diagonal Ts from a per-label dict, sorted label order (MRI_PET_OT_nojax.py:105-119)."""
+    keys = sorted(x_dict.keys())
+    nx = sum(len(x_dict[k]) for k in keys)
+    ny = sum(len(y_dict[k]) for k in keys)
+    T = np.zeros((nx, ny))
+    ix = iy = 0
+    for k in keys:
+        a, b = len(x_dict[k]), len(y_dict[k])
+        if k in ts_dict:
+            T[ix:ix + a, iy:iy + b] = ts_dict[k]
+        ix += a
+        iy += b
+    return T
+
+
+def sinkhorn_knopp_np(a, b, M, reg, numItermax=1000, stopThr=1e-9, check_every=10):
+    """POT 0.9.6 ``sinkhorn_knopp`` restated in NumPy (small problems only)."""
+    a, b, M = _d(a), _d(b), _d(M)
+    u = np.ones(len(a)) / len(a)
+    v = np.ones(len(b)) / len(b)
+    K = np.exp(M / (-reg))
+    Kp = (1 / a).reshape(-1, 1) * K
+    niter = 0
+    errs = []
+    for ii in range(numItermax):
+        niter = ii
+        uprev, vprev = u, v
+        ktu = K.T @ u
+        v = b / ktu
+        u = 1.0 / (Kp @ v)
+        if (np.any(ktu == 0) or np.any(np.isnan(u)) or np.any(np.isnan(v))
+                or np.any(np.isinf(u)) or np.any(np.isinf(v))):
+            u, v = uprev, vprev
+            break
+        if ii % check_every == 0:
+            err = np.linalg.norm(np.einsum("i,ij,j->j", u, K, v) - b)
+            errs.append(err)
+            if err < stopThr:
+                break
+    return u.reshape(-1, 1) * K * v.reshape(1, -1), u, v, {"niter": niter, "err": errs}

@@ -1,0 +1,210 @@
+// otf_cost.hip — pairwise embedding cost on MFMA (gfx950).
+//
+// Replaces ot.dist(x, y, metric) (+ "C /= C.max()") at MRI_PET_OT_nojax.py:70-75 and
+// PointCloud(x, y, scale_cost="max_cost") at MRI_PET_OT_OT_per_epoch_attn.py:155-156 /
+// perturbot/perturbot/match/ott_egwl.py:350.  POT's euclidean_distances expansion
+//     C = max(|x|^2 + |y|^2 - 2 X Y^T, 0)   [sqrt for 'euclidean'; diag = 0 when X is Y]
+// with the X Y^T contraction on v_mfma_f32_32x32x2_f32 (exact f32 FMA chain: the cost
+// feeds exp(-C/reg), where a bf16 contraction's ~1e-3 error would break the 1e-4
+// plan tolerance).  The squared norms are folded into the same pass from the staged
+// tiles, and the global max for scale_cost="max_cost" is reduced in the epilogue
+// (one uint atomicMax per workgroup), so C is written exactly once.
+//
+// Tile: 128 x 128 per 256-thread workgroup (2 x 2 waves, 64 x 64 per wave as 2 x 2
+// MFMA 32x32 tiles), BK = 32, LDS double buffer in k-major [BK][128 + 1] images
+// (row-contiguous fragment reads, conflict-free transposed writes), XCD-grouped
+// block order.
+#include "otf_device.h"
+
+namespace otf {
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, LDSW = BM + 1;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ f32x4 load4(const float* base, int64_t ld, int row, int nrows, int k,
+                                       int kmax, bool vec_ok) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row >= nrows) return v;
+    const float* p = base + (int64_t)row * ld + k;
+    if (vec_ok && k + 3 < kmax) {
+        v = *reinterpret_cast<const f32x4*>(p);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (k + e < kmax) v[e] = p[e];
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void cost_pairwise_kernel(
+    const float* __restrict__ X, int64_t ldx, const float* __restrict__ Y, int64_t ldy, int n,
+    int m, int d, int metric, int zero_diag, float* __restrict__ C, int64_t ldc,
+    unsigned int* cmax, int tiles_n, bool vec_ok) {
+    __shared__ float As[2][BK][LDSW];
+    __shared__ float Bs[2][BK][LDSW];
+    __shared__ float sxx[BM], syy[BN];
+
+    // XCD-grouped bijective block order: blocks b and b+8 share an XCD, give each
+    // XCD a contiguous run of tiles (same X row panel, streaming Y panels).
+    const int nwg = gridDim.x;
+    const int bid = blockIdx.x;
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int tm = wg / tiles_n, tn = wg % tiles_n;
+    const int i0 = tm * BM, j0 = tn * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int lrow = tid >> 3, lk = (tid & 7) * 4;
+
+    f32x4 ra[4], rb[4];
+    float nx[4] = {0.f, 0.f, 0.f, 0.f}, ny[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            ra[qq] = load4(X, ldx, i0 + lrow + 32 * qq, n, k0 + lk, d, vec_ok);
+            rb[qq] = load4(Y, ldy, j0 + lrow + 32 * qq, m, k0 + lk, d, vec_ok);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                As[buf][lk + e][lrow + 32 * qq] = ra[qq][e];
+                Bs[buf][lk + e][lrow + 32 * qq] = rb[qq][e];
+                nx[qq] = fmaf(ra[qq][e], ra[qq][e], nx[qq]);
+                ny[qq] = fmaf(rb[qq][e], rb[qq][e], ny[qq]);
+            }
+        }
+    };
+
+    const int nk = (d + BK - 1) / BK;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) gload((kt + 1) * BK);
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; ++kk) {
+            const int k = 2 * kk + (lane >> 5);
+            float a[2], b[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                a[t] = As[buf][k][wm * 64 + t * 32 + (lane & 31)];
+                b[t] = Bs[buf][k][wn * 64 + t * 32 + (lane & 31)];
+            }
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int nj = 0; nj < 2; ++nj)
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mi], b[nj], acc[mi][nj], 0, 0, 0);
+        }
+        if (kt + 1 < nk) lstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    // squared norms: the 8 lanes sharing a staged row hold its partial sums
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+        float sx = nx[qq], sy = ny[qq];
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            sx += __shfl_xor(sx, o, 64);
+            sy += __shfl_xor(sy, o, 64);
+        }
+        if ((tid & 7) == 0) {
+            sxx[lrow + 32 * qq] = sx;
+            syy[lrow + 32 * qq] = sy;
+        }
+    }
+    __syncthreads();
+
+    float lmax = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int rl = wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                const int cl = wn * 64 + nj * 32 + (lane & 31);
+                const int gi = i0 + rl, gj = j0 + cl;
+                float c = sxx[rl] + syy[cl] - 2.f * acc[mi][nj][e];
+                c = c > 0.f ? c : 0.f;
+                if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
+                if (zero_diag && gi == gj) c = 0.f;
+                if (gi < n && gj < m) {
+                    C[(int64_t)gi * ldc + gj] = c;
+                    lmax = fmaxf(lmax, c);
+                }
+            }
+    if (cmax) {
+        lmax = wave_max(lmax);
+        if (lane == 0) atomicMax(cmax, __float_as_uint(lmax));
+    }
+}
+
+template <typename T>
+__global__ void scale_inplace_kernel(T* C, int64_t n, int64_t m, int64_t ldc, const T* s) {
+    const T inv = s[0];
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n * m;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / m, j = t % m;
+        C[i * ldc + j] = C[i * ldc + j] / inv;
+    }
+}
+
+}  // namespace
+}  // namespace otf
+
+extern "C" {
+
+int otf_cost_pairwise(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
+                      int64_t m, int64_t d, int32_t metric, int32_t zero_diag, float* C,
+                      int64_t ldc, float* cmax, otf_stream_t stream) {
+    if (!X || !Y || !C || n <= 0 || m <= 0 || d <= 0) return OTF_EINVAL;
+    if (ldx < d || ldy < d || ldc < m) return OTF_EINVAL;
+    if (metric != OTF_SQEUCLIDEAN && metric != OTF_EUCLIDEAN) return OTF_EINVAL;
+    if (n > INT32_MAX || m > INT32_MAX || d > INT32_MAX) return OTF_EUNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    const bool vec_ok = (ldx % 4 == 0) && (ldy % 4 == 0) && ((uintptr_t)X % 16 == 0) &&
+                        ((uintptr_t)Y % 16 == 0);
+    if (cmax) OTF_HIP(hipMemsetAsync(cmax, 0, sizeof(float), s));
+    const int tiles_m = (int)((n + otf::BM - 1) / otf::BM);
+    const int tiles_n = (int)((m + otf::BN - 1) / otf::BN);
+    const int64_t nwg = (int64_t)tiles_m * tiles_n;
+    if (nwg > INT32_MAX) return OTF_EUNSUPPORTED;
+    otf::cost_pairwise_kernel<<<(int)nwg, 256, 0, s>>>(X, ldx, Y, ldy, (int)n, (int)m, (int)d,
+                                                       metric, zero_diag, C, ldc,
+                                                       (unsigned int*)cmax, tiles_n, vec_ok);
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+int otf_scale_inplace(void* C, int64_t n, int64_t m, int64_t ldc, int32_t dtype, const void* s,
+                      otf_stream_t stream) {
+    if (!C || !s || n <= 0 || m <= 0 || ldc < m) return OTF_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == OTF_F32)
+        otf::scale_inplace_kernel<float><<<1024, 256, 0, st>>>((float*)C, n, m, ldc, (const float*)s);
+    else if (dtype == OTF_F64)
+        otf::scale_inplace_kernel<double><<<1024, 256, 0, st>>>((double*)C, n, m, ldc, (const double*)s);
+    else
+        return OTF_EINVAL;
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,241 @@
+// otf_linalg.hip — feature cost (float64), plan post-processing and the small
+// GEMMs that apply a plan.
+//
+// Feature cost, MRI_PET_OT_nojax.py:121-136 (get_feature_coupling_pot):
+//     w1 = Ts.sum(1); t1 = (X**2).T @ w1;  w2 = Ts.sum(0); t2 = (Y**2).T @ w2
+//     M  = t1[:, None] + t2[None, :] - 2 X^T Ts Y
+// computed in float64 like the reference (X, Y are float32 numpy arrays that numpy
+// promotes through the float64 Ts; X**2 is squared in float32 first, as there).
+// Plan post-processing, MRI_PET_OT_nojax.py:702-715, and application
+// ot_mri_from_pet = pet_fused @ T^T (:718; MRI_PET_OT_OT_per_epoch_attn.py:728).
+#include "otf_device.h"
+
+namespace otf {
+namespace {
+
+// Generic tiled GEMM  out[i][j] = alpha * sum_k A(i,k) B(k,j) + beta * out[i][j]
+//                                 + rowadd[i] + coladd[j]
+// with A(i,k) = A[i*sa0 + k*sa1], B(k,j) = B[k*sb0 + j*sb1].  64 x 64 tile, BK 16,
+// 256 threads, 4 x 4 outputs per thread, accumulation in TACC.
+constexpr int GT = 64, GK = 16;
+
+template <typename TA, typename TB, typename TACC, typename TOUT>
+__global__ __launch_bounds__(256) void gemm_kernel(const TA* __restrict__ A, int64_t sa0,
+                                                   int64_t sa1, const TB* __restrict__ B,
+                                                   int64_t sb0, int64_t sb1, TOUT* out,
+                                                   int64_t ldo, int M, int N, int K, TACC alpha,
+                                                   TACC beta, const TACC* rowadd,
+                                                   const TACC* coladd) {
+    __shared__ TACC As[GK][GT + 1];
+    __shared__ TACC Bs[GK][GT + 1];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int i0 = blockIdx.y * GT, j0 = blockIdx.x * GT;
+    TACC acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = 0;
+    for (int k0 = 0; k0 < K; k0 += GK) {
+        for (int t = threadIdx.x; t < GK * GT; t += 256) {
+            // A tile: element (i, k) with i fastest when sa0 == 1, else k fastest
+            int ii, kk;
+            if (sa0 == 1) { ii = t % GT; kk = t / GT; } else { kk = t % GK; ii = t / GK; }
+            const int gi = i0 + ii, gk = k0 + kk;
+            As[kk][ii] = (gi < M && gk < K) ? (TACC)A[(int64_t)gi * sa0 + (int64_t)gk * sa1] : (TACC)0;
+            int jj, kb;
+            if (sb1 == 1) { jj = t % GT; kb = t / GT; } else { kb = t % GK; jj = t / GK; }
+            const int gj = j0 + jj, gkb = k0 + kb;
+            Bs[kb][jj] = (gj < N && gkb < K) ? (TACC)B[(int64_t)gkb * sb0 + (int64_t)gj * sb1] : (TACC)0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < GK; ++kk) {
+            TACC av[4], bv[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) av[a] = As[kk][ty + 16 * a];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bv[b] = Bs[kk][tx + 16 * b];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[a][b] = fma(av[a], bv[b], acc[a][b]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const int gi = i0 + ty + 16 * a;
+        if (gi >= M) continue;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int gj = j0 + tx + 16 * b;
+            if (gj >= N) continue;
+            TACC v = alpha * acc[a][b];
+            if (beta != (TACC)0) v += beta * (TACC)out[(int64_t)gi * ldo + gj];
+            if (rowadd) v += rowadd[gi];
+            if (coladd) v += coladd[gj];
+            out[(int64_t)gi * ldo + gj] = (TOUT)v;
+        }
+    }
+}
+
+// w1[i] = sum_j Ts[i][j] (rows), w2[j] = sum_i Ts[i][j] (cols); diag form copies.
+// mode 1 swaps them (fot_numpy's w1 = Ts.sum(axis=0), w2 = Ts.sum(axis=1)).
+__global__ void ts_sums_kernel(const double* Ts, int64_t ldts, const double* diag, int n, int n2,
+                               int mode, double* w1, double* w2) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (diag) {
+        if (t < n) w1[t] = w2[t] = diag[t];
+        return;
+    }
+    double* rows = mode ? w2 : w1;
+    double* cols = mode ? w1 : w2;
+    if (t < n) {
+        double s = 0.0;
+        for (int j = 0; j < n2; ++j) s += Ts[(int64_t)t * ldts + j];
+        rows[t] = s;
+    }
+    if (t < n2) {
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += Ts[(int64_t)i * ldts + t];
+        cols[t] = s;
+    }
+}
+
+// t[k] = sum_i float(x_ik * x_ik) * w[i]   ((X**2).T @ w with X**2 in float32)
+__global__ void weighted_sq_colsum_kernel(const float* X, int64_t ldx, int n, int d,
+                                          const double* w, double* t) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= d) return;
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const float x = X[(int64_t)i * ldx + k];
+        s += (double)(x * x) * w[i];
+    }
+    t[k] = s;
+}
+
+// Z[i][l] = diag[i] * Y[i][l]   (Ts diagonal, e.g. np.eye(B)/B)
+__global__ void diag_scale_kernel(const float* Y, int64_t ldy, int n, int d2, const double* diag,
+                                  double* Z) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < (int64_t)n * d2;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(t / d2), l = (int)(t % d2);
+        Z[t] = diag[i] * (double)Y[(int64_t)i * ldy + l];
+    }
+}
+
+// One workgroup per row: Tn = fill_nan(float(T)) / rowsum (0 -> 1e-8).
+template <typename T>
+__global__ __launch_bounds__(256) void postprocess_kernel(const T* Tm, int d, int d2, int64_t ldt,
+                                                          float nan_fill, int rownorm, float* Tn,
+                                                          int64_t ldtn) {
+    __shared__ float red[17];
+    for (int row = blockIdx.x; row < d; row += gridDim.x) {
+        const T* src = Tm + (int64_t)row * ldt;
+        float* dst = Tn + (int64_t)row * ldtn;
+        float s = 0.f;
+        for (int j = threadIdx.x; j < d2; j += blockDim.x) {
+            float v = (float)src[j];
+            if (isnan(v)) v = nan_fill;
+            dst[j] = v;
+            s += v;
+        }
+        if (!rownorm) continue;
+        s = block_sum<float>(s, red);
+        if (s == 0.f) s = 1e-8f;
+        for (int j = threadIdx.x; j < d2; j += blockDim.x) dst[j] = dst[j] / s;
+        __syncthreads();
+    }
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+}  // namespace otf
+
+extern "C" {
+
+size_t otf_feature_cost_workspace_size(int64_t n, int64_t n2, int64_t d, int64_t d2) {
+    using otf::align_up;
+    return align_up(8 * (size_t)n, 256) + align_up(8 * (size_t)n2, 256) +
+           align_up(8 * (size_t)d, 256) + align_up(8 * (size_t)d2, 256) +
+           align_up(8 * (size_t)(n * d2), 256);
+}
+
+int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
+                     int64_t n2, int64_t d, int64_t d2, const double* Ts, int64_t ldts,
+                     const double* ts_diag, int32_t weights_mode, double* M, int64_t ldm,
+                     void* workspace, size_t ws_bytes, otf_stream_t stream) {
+    using otf::align_up;
+    if (!X || !Y || !M || !workspace || n <= 0 || n2 <= 0 || d <= 0 || d2 <= 0) return OTF_EINVAL;
+    if (!Ts && !ts_diag) return OTF_EINVAL;
+    if ((ts_diag || weights_mode == 1) && n != n2) return OTF_EINVAL;
+    if (weights_mode != 0 && weights_mode != 1) return OTF_EINVAL;
+    if (ldx < d || ldy < d2 || ldm < d2 || (Ts && ldts < n2)) return OTF_EINVAL;
+    if (ws_bytes < otf_feature_cost_workspace_size(n, n2, d, d2)) return OTF_EINVAL;
+    if (n > 65535 * 64 || d > 65535 * 64 || d2 > 65535 * 64) return OTF_EUNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    char* p = (char*)workspace;
+    double* w1 = (double*)p; p += align_up(8 * (size_t)n, 256);
+    double* w2 = (double*)p; p += align_up(8 * (size_t)n2, 256);
+    double* t1 = (double*)p; p += align_up(8 * (size_t)d, 256);
+    double* t2 = (double*)p; p += align_up(8 * (size_t)d2, 256);
+    double* Z = (double*)p;
+
+    const int nmax = (int)(n > n2 ? n : n2);
+    otf::ts_sums_kernel<<<(nmax + 255) / 256, 256, 0, s>>>(Ts, ldts, ts_diag, (int)n, (int)n2,
+                                                          weights_mode, w1, w2);
+    OTF_HIP(hipGetLastError());
+    otf::weighted_sq_colsum_kernel<<<(int)((d + 255) / 256), 256, 0, s>>>(X, ldx, (int)n, (int)d, w1, t1);
+    otf::weighted_sq_colsum_kernel<<<(int)((d2 + 255) / 256), 256, 0, s>>>(Y, ldy, (int)n2, (int)d2, w2, t2);
+    OTF_HIP(hipGetLastError());
+    // Z = Ts @ Y  (n x d2)
+    if (ts_diag) {
+        otf::diag_scale_kernel<<<256, 256, 0, s>>>(Y, ldy, (int)n, (int)d2, ts_diag, Z);
+    } else {
+        dim3 grid((unsigned)((d2 + otf::GT - 1) / otf::GT), (unsigned)((n + otf::GT - 1) / otf::GT));
+        otf::gemm_kernel<double, float, double, double><<<grid, 256, 0, s>>>(
+            Ts, ldts, 1, Y, ldy, 1, Z, d2, (int)n, (int)d2, (int)n2, 1.0, 0.0, nullptr, nullptr);
+    }
+    OTF_HIP(hipGetLastError());
+    // M = -2 X^T Z + t1[:, None] + t2[None, :]   (d x d2, sum over the n samples)
+    dim3 grid((unsigned)((d2 + otf::GT - 1) / otf::GT), (unsigned)((d + otf::GT - 1) / otf::GT));
+    otf::gemm_kernel<float, double, double, double><<<grid, 256, 0, s>>>(
+        X, 1, ldx, Z, d2, 1, M, ldm, (int)d, (int)d2, (int)n, -2.0, 0.0, t1, t2);
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+int otf_plan_postprocess(const void* T, int64_t d, int64_t d2, int64_t ldt, int32_t dtype,
+                         float nan_fill, int32_t rownorm, float* Tn, int64_t ldtn,
+                         otf_stream_t stream) {
+    if (!T || !Tn || d <= 0 || d2 <= 0 || ldt < d2 || ldtn < d2) return OTF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const int grid = d < 4096 ? (int)d : 4096;
+    if (dtype == OTF_F64)
+        otf::postprocess_kernel<double><<<grid, 256, 0, s>>>((const double*)T, (int)d, (int)d2, ldt,
+                                                             nan_fill, rownorm, Tn, ldtn);
+    else if (dtype == OTF_F32)
+        otf::postprocess_kernel<float><<<grid, 256, 0, s>>>((const float*)T, (int)d, (int)d2, ldt,
+                                                            nan_fill, rownorm, Tn, ldtn);
+    else
+        return OTF_EINVAL;
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+int otf_gemm_f32(const float* A, int64_t sa0, int64_t sa1, const float* B, int64_t sb0,
+                 int64_t sb1, float* out, int64_t ldo, int64_t M, int64_t N, int64_t K,
+                 float alpha, float beta, otf_stream_t stream) {
+    if (!A || !B || !out || M <= 0 || N <= 0 || K <= 0 || ldo < N) return OTF_EINVAL;
+    if (M > 65535LL * otf::GT || N > 2147483647LL) return OTF_EUNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    dim3 grid((unsigned)((N + otf::GT - 1) / otf::GT), (unsigned)((M + otf::GT - 1) / otf::GT));
+    otf::gemm_kernel<float, float, float, float><<<grid, 256, 0, s>>>(
+        A, sa0, sa1, B, sb0, sb1, out, ldo, (int)M, (int)N, (int)K, alpha, beta, nullptr, nullptr);
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+}  // extern "C"

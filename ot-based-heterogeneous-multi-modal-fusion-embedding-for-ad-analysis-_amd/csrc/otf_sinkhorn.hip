@@ -1,0 +1,713 @@
+// otf_sinkhorn.hip — entropic Sinkhorn on gfx950 as fused single-read HBM sweeps.
+//
+// Replaces ot.sinkhorn (POT 0.9.6 sinkhorn_knopp) at MRI_PET_OT_nojax.py:143 and the
+// vendored loop perturbot/perturbot/match/utils.py:6-115 (POT flavour), and OTT's
+// lse-mode Sinkhorn behind perturbot/perturbot/match/fot.py:128-134 (OTT flavour).
+//
+// One launch = one Sinkhorn iteration = ONE read of the materialised cost C.
+// Workgroup w owns blocks of R rows and ALL m columns; a row block's K values stay
+// in registers between
+//   (1) the row reduction with the current column scaling -> the new row scaling
+//       (exact POT order: v-update first, then u-update), and
+//   (2) the column update with the NEW row scaling, flushed with one float atomic
+//       per column per workgroup: that is K^T u for the NEXT iteration's v-update,
+//       and v_j (K^T u)_j is POT's marginal-error term, so the err check is free.
+// K = exp(-C/reg) is recomputed from C in registers (one v_exp per element), so
+// only C is streamed.  Both flavours run the same pass:
+//   e_ij = exp(C_ij * ks + fo_i + go_j)
+//   POT: fo = go = 0, row sums weighted by v_j = b_j / colsum_j, w_i = u_i = a_i / rowsum_i
+//   OTT: e_ij = exp((f_prev_i + g_j - C_ij)/reg) with g_j = reg (log b_j - log colsum_j)
+//        + g_prev_j; rows unweighted, w_i = a_i / rowsum_i, f_i = reg log w_i + f_prev_i.
+//        Every e_ij <= 1 by construction (the previous update normalised that
+//        marginal), so the shifted sums never overflow — a log-sum-exp without a
+//        max pass.  The first g-update is shifted by the column minima of C.
+// Control (marginal error every check_every iterations, POT's revert-and-break on
+// zero / nan / inf) lives on the device: every workgroup re-derives the same
+// decision from the same buffers at the top of the next launch, so no host sync
+// is needed between iterations.  Column-sum buffers are triple-buffered
+// (read p-1, accumulate p, zero p+1) so a pass never races the zeroing.
+#include "otf_device.h"
+
+namespace otf {
+namespace {
+
+template <typename T> struct SkArgs {
+    const T* C;
+    int64_t ldc;
+    int n, m;
+    const T* a;            // padded copy (workspace)
+    const T* b;            // padded copy, zero beyond m (workspace)
+    const T* cost_scale;   // device scalar; cost is C / cost_scale (nullable)
+    double reg;
+    int it;                // iteration index ii; -1 = prologue pass
+    const T* cs_src;       // column sums accumulated by the previous pass
+    T* cs_dst;             // column sums accumulated by this pass
+    T* cs_zero;            // zeroed by this pass (accumulated by the next)
+    T* u_cur;              // u (POT) / f (OTT) of iteration it
+    T* v_cur;              // v / g of iteration it
+    const T* u_prev;       // f of iteration it-1 (OTT)
+    const T* v_prev;       // v / g of iteration it-1
+    const int* cmin_key;   // OTT prologue: ordered-int column minima of C
+    otf_sinkhorn_info* info;
+    int* bad;              // bad[it] = 1 if the row scaling of iteration it is not finite
+    double* errlog;
+    double stop_thr;
+    int check_every;
+    int check_off;         // POT checks at ii % 10 == 0, OTT after every 10th update
+    int err_squared;
+    int m_pad;
+};
+
+__device__ __forceinline__ void sk_stop(otf_sinkhorn_info* info, int last_good, int niter,
+                                        int status, int break_iter) {
+    info->last_good = last_good;
+    info->niter = niter;
+    info->status = status;
+    if (break_iter >= 0) info->break_iter = break_iter;
+    __hip_atomic_store(&info->stop, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ordered int key of a float (monotone), for atomicMin on signed ints
+__device__ __forceinline__ int ord_key(float x) {
+    const int b = __float_as_int(x);
+    return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float key_val(int k) {
+    return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff);
+}
+
+template <typename T> __device__ __forceinline__ T unit_log(T x);
+template <> __device__ __forceinline__ float unit_log(float x) { return __builtin_amdgcn_logf(x); }   // log2
+template <> __device__ __forceinline__ double unit_log(double x) { return log(x); }
+
+template <typename T> __device__ __forceinline__ bool check_now(const SkArgs<T>& p, int it) {
+    return ((it + p.check_off) % p.check_every) == 0;
+}
+
+template <typename T>
+__device__ __forceinline__ bool is_conv(const SkArgs<T>& p, double err) {
+    return p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr);
+}
+
+// Marginal error of iteration `it` from its column scaling and the column sums
+// accumulated with its row scaling.  Block-wide, identical in every workgroup.
+template <typename T, bool LOG, int G, int VEC>
+__device__ __forceinline__ double marginal_err(const SkArgs<T>& p, const T* vit, const T* cs,
+                                               const int (&colc)[G], const bool (&cok)[G][VEC],
+                                               T* red) {
+    using V = typename Vec<T>::type;
+    T e = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const V s = *reinterpret_cast<const V*>(cs + colc[g]);
+        const V bb = *reinterpret_cast<const V*>(p.b + colc[g]);
+        V vv = *reinterpret_cast<const V*>(vit + colc[g]);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            T r;
+            if (LOG) {
+                r = fabs(s[k] - bb[k]);
+            } else {
+                r = vv[k] * s[k] - bb[k];
+                r = r * r;
+            }
+            e += cok[g][k] ? r : (T)0;
+        }
+    }
+    e = block_sum<T>(e, red);
+    if (LOG) return (double)e;
+    return p.err_squared ? (double)e : sqrt((double)e);
+}
+
+// One fused Sinkhorn pass.  NT threads own G chunks of VEC contiguous columns each
+// (chunk q = tid + NT*g), R rows per row block; K values for a row block stay in
+// registers (R*G*VEC of them) between the row reduction and the column update.
+template <typename T, bool LOG, int G, int R>
+__global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
+    constexpr int VEC = Vec<T>::N;
+    using V = typename Vec<T>::type;
+    __shared__ T red[17 * R + 17];
+    __shared__ int s_flag;
+    const int tid = threadIdx.x;
+    const int NT = blockDim.x;
+
+    if (tid == 0) s_flag = __hip_atomic_load(&p.info->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_flag) return;
+
+    const bool lead = (blockIdx.x == 0 && tid == 0);
+    // exponent units: float works in log2 (v_exp_f32), double in natural log
+    const double unit = exp_unit<T>();
+    double cinv = 1.0;
+    if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
+    const T ks = (T)(-unit / p.reg * cinv);  // multiplies C
+    const T gl = (T)(unit / p.reg);          // potential -> exponent units (OTT)
+    const T regn = (T)(p.reg / unit);        // unit log -> potential
+
+    // ---- per-thread column ownership; clamped addresses + masks (branch-free loads)
+    int colc[G];
+    bool cok[G][VEC];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int c0 = (tid + NT * g) * VEC;
+        colc[g] = c0 < p.m ? c0 : 0;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) cok[g][k] = c0 + k < p.m;
+    }
+
+    // ---- decisions about iteration it-1 (identical in every workgroup)
+    if (p.it >= 1) {
+        const int prev = p.it - 1;
+        if (p.bad[prev]) {  // row scaling of prev not finite: revert to prev-1, stop
+            if (lead) sk_stop(p.info, prev - 1, prev, OTF_SK_NUMERICAL_BREAK, prev);
+            return;
+        }
+        if (check_now(p, prev)) {
+            const double err = marginal_err<T, LOG, G, VEC>(p, p.v_prev, p.cs_src, colc, cok, red);
+            if (lead) {
+                const int slot = (prev + p.check_off) / p.check_every - p.check_off;
+                p.errlog[slot] = err;
+                p.info->n_err = slot + 1;
+            }
+            if (is_conv(p, err)) {
+                if (lead) sk_stop(p.info, prev, prev, OTF_SK_CONVERGED, -1);
+                return;
+            }
+        }
+    }
+
+    // ---- column scaling of iteration it (POT: v; OTT: g) and the column exponent offset
+    T vw[G][VEC];  // POT: v_j (row-sum weights); OTT: 1
+    T go[G][VEC];  // OTT: g_j in exponent units; POT: 0
+    if (p.it >= 0) {
+        int badv = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const V s = *reinterpret_cast<const V*>(p.cs_src + colc[g]);
+            const V bb = *reinterpret_cast<const V*>(p.b + colc[g]);
+            const V gp = *reinterpret_cast<const V*>(p.v_prev + colc[g]);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                T val;
+                if (LOG) val = regn * (unit_log(bb[k]) - unit_log(s[k])) + gp[k];
+                else val = bb[k] / s[k];
+                const bool bad = (s[k] == (T)0) || !finite_val(val);
+                badv |= (cok[g][k] && bad) ? 1 : 0;
+                val = cok[g][k] ? val : (T)0;
+                if (LOG) {
+                    go[g][k] = val * gl;
+                    vw[g][k] = 1;
+                } else {
+                    vw[g][k] = val;
+                    go[g][k] = 0;
+                }
+                if (blockIdx.x == 0 && cok[g][k]) p.v_cur[colc[g] + k] = val;
+            }
+        }
+        badv = __syncthreads_or(badv);
+        if (badv) {  // zero column sum or nan/inf column scaling: revert to it-1, stop
+            if (lead) sk_stop(p.info, p.it - 1, p.it, OTF_SK_NUMERICAL_BREAK, p.it);
+            return;
+        }
+    } else {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                vw[g][k] = 1;
+                go[g][k] = 0;
+                if (LOG) {  // g_{-1} = column minima of the scaled cost: every term <= 1
+                    const T h = (T)((double)key_val(p.cmin_key[colc[g] + k]) * cinv);
+                    go[g][k] = cok[g][k] ? h * gl : (T)0;
+                    if (blockIdx.x == 0 && cok[g][k]) p.v_cur[colc[g] + k] = h;
+                }
+            }
+    }
+
+    // ---- row blocks: row scaling, then column partials with the new row scaling
+    T colacc[G][VEC];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) colacc[g][k] = 0;
+
+    const int nrb = (p.n + R - 1) / R;
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+        const int r0 = rb * R;
+        T kv[R][G][VEC];
+        const T* crow = p.C + (int64_t)r0 * p.ldc;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const T* src = (r0 + r < p.n) ? crow : p.C;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const V c = *reinterpret_cast<const V*>(src + colc[g]);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
+            }
+            crow += p.ldc;
+        }
+        T fo[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int row = r0 + r < p.n ? r0 + r : p.n - 1;
+            fo[r] = (LOG && p.it >= 0) ? p.u_prev[row] * gl : (T)0;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool rok = r0 + r < p.n;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    T z = kv[r][g][k] * ks;
+                    if (LOG) z += fo[r] + go[g][k];
+                    kv[r][g][k] = (rok && cok[g][k]) ? fast_exp(z) : (T)0;
+                }
+        }
+        T ur[R];
+        if (p.it >= 0) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                T s = 0;
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) s += LOG ? kv[r][g][k] : kv[r][g][k] * vw[g][k];
+                ur[r] = s;
+            }
+            block_sum_multi<T, R>(ur, red);
+            T outv[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int row = r0 + r < p.n ? r0 + r : p.n - 1;
+                const T ar = p.a[row];
+                if (LOG) {
+                    ur[r] = ar / ur[r];                                // w_i = a_i / rowsum_i
+                    outv[r] = regn * unit_log(ur[r]) + p.u_prev[row];  // f_i
+                } else {
+                    ur[r] = (T)1 / (ur[r] * ((T)1 / ar));              // POT: 1 / (Kp v)
+                    outv[r] = ur[r];
+                }
+            }
+            if (tid < R) {
+                T mine = outv[0];
+                T wmine = ur[0];
+#pragma unroll
+                for (int r = 1; r < R; ++r)
+                    if (tid == r) {
+                        mine = outv[r];
+                        wmine = ur[r];
+                    }
+                const int row = r0 + tid;
+                if (row < p.n) {
+                    p.u_cur[row] = mine;
+                    if (!finite_val(mine) || !finite_val(wmine)) p.bad[p.it] = 1;
+                }
+            }
+        } else {
+            const T u0 = LOG ? (T)1 : (T)1 / (T)p.n;
+#pragma unroll
+            for (int r = 0; r < R; ++r) ur[r] = u0;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) colacc[g][k] += kv[r][g][k] * ur[r];
+    }
+
+    // ---- flush column partials (one float atomic per column per workgroup)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+            if (cok[g][k]) atomicAdd(p.cs_dst + colc[g] + k, colacc[g][k]);
+
+    // ---- zero the column-sum buffer of the next pass (nobody touches it now)
+    for (int j = blockIdx.x * NT + tid; j < p.m_pad; j += gridDim.x * NT) p.cs_zero[j] = 0;
+}
+
+template <typename T>
+__global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, T* a_pad, T* b_pad,
+                               T* cs, T* u2, T* v2, int* bad, int nbad, int* cmin_key,
+                               otf_sinkhorn_info* info) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int stride = gridDim.x * blockDim.x;
+    for (int j = t; j < m_pad; j += stride) {
+        b_pad[j] = j < m ? b[j] : (T)0;
+        cs[j] = cs[m_pad + j] = cs[2 * m_pad + j] = 0;
+        v2[j] = v2[m_pad + j] = 0;
+        cmin_key[j] = 0x7fffffff;
+    }
+    for (int i = t; i < n; i += stride) {
+        a_pad[i] = a[i];
+        u2[i] = u2[n + i] = 0;
+    }
+    for (int j = t; j < nbad; j += stride) bad[j] = 0;
+    if (t == 0) {
+        info->stop = 0;
+        info->last_good = -1;
+        info->niter = 0;
+        info->status = OTF_SK_RUNNING;
+        info->n_err = 0;
+        info->break_iter = -1;
+        info->pad[0] = info->pad[1] = 0;
+    }
+}
+
+// Column minima of C (OTT prologue shift), ordered-int atomicMin per column.
+template <typename T>
+__global__ __launch_bounds__(256) void sk_colmin_kernel(const T* C, int64_t ldc, int n, int m,
+                                                        int* cmin_key) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const int rows_per = (n + gridDim.y - 1) / gridDim.y;
+    const int i0 = blockIdx.y * rows_per;
+    const int i1 = i0 + rows_per < n ? i0 + rows_per : n;
+    float mn = INFINITY;
+    for (int i = i0; i < i1; ++i) mn = fminf(mn, (float)C[(int64_t)i * ldc + j]);
+    if (i0 < i1) atomicMin(cmin_key + j, ord_key(mn));
+}
+
+// Decides the outcome of the last pass when the loop ran to max_iter.
+template <typename T, bool LOG>
+__global__ __launch_bounds__(512) void sk_finalize_kernel(SkArgs<T> p, int max_iter) {
+    __shared__ T red[17 * 2];
+    __shared__ int s_flag;
+    if (threadIdx.x == 0) s_flag = __hip_atomic_load(&p.info->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_flag) return;
+    const bool lead = threadIdx.x == 0;
+    if (max_iter <= 0) {
+        if (lead) sk_stop(p.info, -1, 0, OTF_SK_MAX_ITER, -1);
+        return;
+    }
+    const int it = max_iter - 1;
+    if (p.bad[it]) {
+        if (lead) sk_stop(p.info, it - 1, it, OTF_SK_NUMERICAL_BREAK, it);
+        return;
+    }
+    int status = OTF_SK_MAX_ITER;
+    if (check_now(p, it)) {
+        T e = 0;
+        for (int j = threadIdx.x; j < p.m; j += blockDim.x) {
+            T r;
+            if (LOG) {
+                r = fabs(p.cs_src[j] - p.b[j]);
+            } else {
+                r = p.v_cur[j] * p.cs_src[j] - p.b[j];
+                r = r * r;
+            }
+            e += r;
+        }
+        e = block_sum<T>(e, red);
+        const double err = LOG ? (double)e : (p.err_squared ? (double)e : sqrt((double)e));
+        if (lead) {
+            const int slot = (it + p.check_off) / p.check_every - p.check_off;
+            p.errlog[slot] = err;
+            p.info->n_err = slot + 1;
+        }
+        if (is_conv(p, err)) status = OTF_SK_CONVERGED;
+    }
+    if (lead) sk_stop(p.info, it, it, status, -1);
+}
+
+// Copies the scalings of info->last_good (or the initial ones) to the outputs.
+template <typename T, bool LOG>
+__global__ void sk_output_kernel(const T* u2, const T* v2, int n, int m, int m_pad,
+                                 const otf_sinkhorn_info* info, T* u_out, T* v_out) {
+    const int lg = info->last_good;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int stride = gridDim.x * blockDim.x;
+    const T u0 = LOG ? (T)0 : (T)1 / (T)n;
+    const T v0 = LOG ? (T)0 : (T)1 / (T)m;
+    for (int i = t; i < n; i += stride) u_out[i] = lg >= 0 ? u2[(lg & 1) * n + i] : u0;
+    for (int j = t; j < m; j += stride) v_out[j] = lg >= 0 ? v2[(lg & 1) * m_pad + j] : v0;
+}
+
+// POT: P_ij = u_i exp(-C_ij/reg') v_j;  OTT: P_ij = exp((f_i + g_j - C_ij/scale)/reg).
+template <typename T, typename TP, bool LOG>
+__global__ __launch_bounds__(256) void sk_plan_kernel(const T* C, int64_t ldc, int n, int m,
+                                                      const T* u, const T* v, const T* cost_scale,
+                                                      double reg, TP* P, int64_t ldp) {
+    const double unit = exp_unit<T>();
+    double cinv = 1.0;
+    if (cost_scale) cinv = 1.0 / (double)cost_scale[0];
+    const T ks = (T)(-unit / reg * cinv);
+    const T gl = (T)(unit / reg);
+    constexpr int VEC = Vec<T>::N;
+    using V = typename Vec<T>::type;
+    for (int row = blockIdx.x; row < n; row += gridDim.x) {
+        const T ui = u[row];
+        const T* crow = C + (int64_t)row * ldc;
+        TP* prow = P + (int64_t)row * ldp;
+        for (int j0 = threadIdx.x * VEC; j0 < m; j0 += blockDim.x * VEC) {
+            const V c = *reinterpret_cast<const V*>(crow + j0);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k)
+                if (j0 + k < m) {
+                    T val;
+                    if (LOG) val = fast_exp(c[k] * ks + (ui + v[j0 + k]) * gl);
+                    else val = ui * fast_exp(c[k] * ks) * v[j0 + k];
+                    prow[j0 + k] = (TP)val;
+                }
+        }
+    }
+}
+
+struct PassCfg {
+    int G, R, NT;
+};
+
+// Register budget: 512-thread workgroups, one per CU (2 waves per SIMD -> up to 256
+// VGPRs); each thread keeps R * G * VEC cost values of its row block live between
+// the row reduction and the column update (<= 128 floats / 32 doubles).
+constexpr int kPassThreads = 512;
+constexpr int kMaxG = 8;
+
+template <typename T> constexpr int pass_rows(int G) {
+    return sizeof(T) == 4 ? (G == 1 ? 16 : 128 / (G * 4)) : (G == 1 ? 16 : 32 / (G * 2));
+}
+
+template <typename T> PassCfg pick_cfg(int m) {
+    constexpr int VEC = Vec<T>::N;
+    const int chunks = (m + VEC - 1) / VEC;
+    int G = 1;
+    while (G < kMaxG && (chunks + G - 1) / G > kPassThreads) G *= 2;
+    int nt = (chunks + G - 1) / G;
+    nt = ((nt + 63) / 64) * 64;
+    if (nt < 64) nt = 64;
+    return {G, pass_rows<T>(G), nt};
+}
+
+template <typename T, bool LOG>
+hipError_t launch_pass(const PassCfg& c, int grid, const SkArgs<T>& p, hipStream_t s) {
+    switch (c.G) {
+        case 1: sk_pass_kernel<T, LOG, 1, pass_rows<T>(1)><<<grid, c.NT, 0, s>>>(p); break;
+        case 2: sk_pass_kernel<T, LOG, 2, pass_rows<T>(2)><<<grid, c.NT, 0, s>>>(p); break;
+        case 4: sk_pass_kernel<T, LOG, 4, pass_rows<T>(4)><<<grid, c.NT, 0, s>>>(p); break;
+        case 8: sk_pass_kernel<T, LOG, 8, pass_rows<T>(8)><<<grid, c.NT, 0, s>>>(p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct Workspace {
+    void* a_pad;
+    void* b_pad;
+    void* cs;
+    void* u2;
+    void* v2;
+    int* bad;
+    int* cmin_key;
+    double* errlog;
+    size_t bytes;
+    int64_t m_pad;
+};
+
+Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter) {
+    Workspace w{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        void* p = base ? (char*)base + off : nullptr;
+        off = align_up(off + bytes, 256);
+        return p;
+    };
+    w.m_pad = (int64_t)align_up((size_t)m, 64);
+    w.a_pad = take(n * esz);
+    w.b_pad = take(w.m_pad * esz);
+    w.cs = take(3 * w.m_pad * esz);
+    w.u2 = take(2 * n * esz);
+    w.v2 = take(2 * w.m_pad * esz);
+    w.cmin_key = (int*)take(sizeof(int) * (size_t)w.m_pad);
+    w.bad = (int*)take(sizeof(int) * (size_t)(max_iter + 2));
+    w.errlog = (double*)take(sizeof(double) * (size_t)(max_iter + 2));
+    w.bytes = off;
+    return w;
+}
+
+template <typename T, bool LOG>
+int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64_t ldc,
+                 const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out, void* P_out,
+                 int64_t ldp, int P_dtype, otf_sinkhorn_info* info, double* errlog_user,
+                 void* ws, size_t ws_bytes, hipStream_t s, float* avg_pass_ms) {
+    constexpr int VEC = Vec<T>::N;
+    if (n <= 0 || m <= 0 || !a || !b || !C || !u_out || !v_out || !info || !ws) return OTF_EINVAL;
+    if (ldc < m || ldc % VEC != 0 || ((uintptr_t)C % 16) != 0) return OTF_EINVAL;
+    if (!(o.reg > 0.0) || o.max_iter < 0 || o.check_every <= 0) return OTF_EINVAL;
+    if (P_out && (ldp < m || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
+    if (n > INT32_MAX || m > (int64_t)kPassThreads * kMaxG * VEC) return OTF_EUNSUPPORTED;
+    Workspace w = carve(ws, n, m, sizeof(T), o.max_iter);
+    if (ws_bytes < w.bytes) return OTF_EINVAL;
+    double* errlog = errlog_user ? errlog_user : w.errlog;
+    const int m_pad = (int)w.m_pad;
+
+    const PassCfg cfg = pick_cfg<T>((int)m);
+    const int nrb = (int)((n + cfg.R - 1) / cfg.R);
+    const int grid = nrb < device_cu_count() ? nrb : device_cu_count();
+    T* cs = (T*)w.cs;
+    T* u2 = (T*)w.u2;
+    T* v2 = (T*)w.v2;
+
+    sk_init_kernel<T><<<64, 256, 0, s>>>(a, b, (int)n, (int)m, m_pad, (T*)w.a_pad, (T*)w.b_pad, cs,
+                                         u2, v2, w.bad, o.max_iter + 2, w.cmin_key, info);
+    OTF_HIP(hipGetLastError());
+    if (LOG) {
+        dim3 g((unsigned)((m + 255) / 256), (unsigned)(n < 64 ? n : 64));
+        sk_colmin_kernel<T><<<g, 256, 0, s>>>(C, ldc, (int)n, (int)m, w.cmin_key);
+        OTF_HIP(hipGetLastError());
+    }
+
+    SkArgs<T> p{};
+    p.C = C;
+    p.ldc = ldc;
+    p.n = (int)n;
+    p.m = (int)m;
+    p.a = (const T*)w.a_pad;
+    p.b = (const T*)w.b_pad;
+    p.cost_scale = cost_scale;
+    p.reg = o.reg;
+    p.cmin_key = w.cmin_key;
+    p.info = info;
+    p.bad = w.bad;
+    p.errlog = errlog;
+    p.stop_thr = avg_pass_ms ? -1.0 : o.stop_thr;
+    p.check_every = o.check_every;
+    p.check_off = LOG ? 1 : 0;
+    p.err_squared = LOG ? 0 : o.err_squared;
+    p.m_pad = m_pad;
+
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double total_ms = 0.0;
+    int timed = 0;
+    if (avg_pass_ms) {
+        OTF_HIP(hipEventCreate(&ev0));
+        OTF_HIP(hipEventCreate(&ev1));
+    }
+    int* host_stop = nullptr;
+    if (o.sync_every > 0) OTF_HIP(hipHostMalloc((void**)&host_stop, sizeof(int), hipHostMallocDefault));
+
+    for (int pass = 0; pass <= o.max_iter; ++pass) {
+        const int it = pass - 1;
+        p.it = it;
+        p.cs_src = pass >= 1 ? cs + (size_t)((pass - 1) % 3) * m_pad : nullptr;
+        p.cs_dst = cs + (size_t)(pass % 3) * m_pad;
+        p.cs_zero = cs + (size_t)((pass + 1) % 3) * m_pad;
+        // iteration it writes slot (it & 1); the prologue (it = -1) writes slot 1 (OTT g_{-1})
+        p.u_cur = u2 + (size_t)(it & 1) * n;
+        p.v_cur = v2 + (size_t)(it & 1) * m_pad;
+        p.u_prev = u2 + (size_t)((it - 1) & 1) * n;
+        p.v_prev = v2 + (size_t)((it - 1) & 1) * m_pad;
+        if (avg_pass_ms && pass >= 1) OTF_HIP(hipEventRecord(ev0, s));
+        OTF_HIP((launch_pass<T, LOG>(cfg, grid, p, s)));
+        if (avg_pass_ms && pass >= 1) {
+            OTF_HIP(hipEventRecord(ev1, s));
+            OTF_HIP(hipEventSynchronize(ev1));
+            float ms = 0.f;
+            OTF_HIP(hipEventElapsedTime(&ms, ev0, ev1));
+            total_ms += ms;
+            ++timed;
+        }
+        if (host_stop && pass >= 1 && pass % o.sync_every == 0 && pass < o.max_iter) {
+            OTF_HIP(hipMemcpyAsync(host_stop, &info->stop, sizeof(int), hipMemcpyDeviceToHost, s));
+            OTF_HIP(hipStreamSynchronize(s));
+            if (*host_stop) break;
+        }
+    }
+    if (host_stop) OTF_HIP(hipHostFree(host_stop));
+
+    // finalize: pass max_iter (iteration max_iter-1) accumulated into cs[max_iter % 3]
+    {
+        const int it = o.max_iter - 1;
+        p.it = it;
+        p.cs_src = cs + (size_t)(o.max_iter % 3) * m_pad;
+        p.v_cur = v2 + (size_t)(it & 1) * m_pad;
+        sk_finalize_kernel<T, LOG><<<1, 512, 0, s>>>(p, o.max_iter);
+        OTF_HIP(hipGetLastError());
+    }
+    sk_output_kernel<T, LOG><<<64, 256, 0, s>>>(u2, v2, (int)n, (int)m, m_pad, info, u_out, v_out);
+    OTF_HIP(hipGetLastError());
+    if (P_out) {
+        const int pgrid = n < 4096 ? (int)n : 4096;
+        if (P_dtype == OTF_F32)
+            sk_plan_kernel<T, float, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
+                                                               cost_scale, o.reg, (float*)P_out, ldp);
+        else
+            sk_plan_kernel<T, double, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
+                                                                cost_scale, o.reg, (double*)P_out, ldp);
+        OTF_HIP(hipGetLastError());
+    }
+    if (avg_pass_ms) {
+        OTF_HIP(hipStreamSynchronize(s));
+        *avg_pass_ms = timed ? (float)(total_ms / timed) : 0.f;
+        (void)hipEventDestroy(ev0);
+        (void)hipEventDestroy(ev1);
+    }
+    return OTF_OK;
+}
+
+template <typename T>
+int dispatch(const void* a, const void* b, const void* C, int64_t n, int64_t m, int64_t ldc,
+             const void* cost_scale, const otf_sinkhorn_opts& o, void* u_out, void* v_out,
+             void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info, double* errlog,
+             void* ws, size_t ws_bytes, hipStream_t s, float* avg_ms) {
+    if (o.flavor == OTF_FLAVOR_POT)
+        return run_sinkhorn<T, false>((const T*)a, (const T*)b, (const T*)C, n, m, ldc,
+                                      (const T*)cost_scale, o, (T*)u_out, (T*)v_out, P_out, ldp,
+                                      P_dtype, info, errlog, ws, ws_bytes, s, avg_ms);
+    if (o.flavor == OTF_FLAVOR_OTT)
+        return run_sinkhorn<T, true>((const T*)a, (const T*)b, (const T*)C, n, m, ldc,
+                                     (const T*)cost_scale, o, (T*)u_out, (T*)v_out, P_out, ldp,
+                                     P_dtype, info, errlog, ws, ws_bytes, s, avg_ms);
+    return OTF_EINVAL;
+}
+
+}  // namespace
+}  // namespace otf
+
+extern "C" {
+
+size_t otf_sinkhorn_workspace_size(int64_t n, int64_t m, int32_t dtype, int32_t max_iter) {
+    const size_t esz = dtype == OTF_F64 ? 8 : 4;
+    return otf::carve(nullptr, n, m, esz, max_iter < 0 ? 0 : max_iter).bytes;
+}
+
+int otf_sinkhorn(const void* a, const void* b, const void* C, int64_t n, int64_t m, int64_t ldc,
+                 int32_t dtype, const void* cost_scale, const otf_sinkhorn_opts* opts, void* u_out,
+                 void* v_out, void* P_out, int64_t ldp, int32_t P_dtype, otf_sinkhorn_info* info,
+                 double* errlog, void* workspace, size_t ws_bytes, otf_stream_t stream) {
+    if (!opts) return OTF_EINVAL;
+    if (P_out && P_dtype != OTF_F32 && P_dtype != OTF_F64) return OTF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == OTF_F32)
+        return otf::dispatch<float>(a, b, C, n, m, ldc, cost_scale, *opts, u_out, v_out, P_out, ldp,
+                                    P_dtype, info, errlog, workspace, ws_bytes, s, nullptr);
+    if (dtype == OTF_F64)
+        return otf::dispatch<double>(a, b, C, n, m, ldc, cost_scale, *opts, u_out, v_out, P_out,
+                                     ldp, P_dtype, info, errlog, workspace, ws_bytes, s, nullptr);
+    return OTF_EINVAL;
+}
+
+int otf_sinkhorn_profile(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                         int64_t ldc, int32_t dtype, const void* cost_scale,
+                         const otf_sinkhorn_opts* opts, void* u_out, void* v_out,
+                         otf_sinkhorn_info* info, void* workspace, size_t ws_bytes,
+                         float* avg_pass_ms, otf_stream_t stream) {
+    if (!opts || !avg_pass_ms) return OTF_EINVAL;
+    otf_sinkhorn_opts o = *opts;
+    o.sync_every = 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == OTF_F32)
+        return otf::dispatch<float>(a, b, C, n, m, ldc, cost_scale, o, u_out, v_out, nullptr, 0,
+                                    OTF_F32, info, nullptr, workspace, ws_bytes, s, avg_pass_ms);
+    if (dtype == OTF_F64)
+        return otf::dispatch<double>(a, b, C, n, m, ldc, cost_scale, o, u_out, v_out, nullptr, 0,
+                                     OTF_F64, info, nullptr, workspace, ws_bytes, s, avg_pass_ms);
+    return OTF_EINVAL;
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+"""ctypes binding of ``libotfuse.so`` — the C ABI declared in ``include/otfuse.h``.
+
+The library is the product: every op in this package calls into it and there is
+no CPU fallback.  ``lib()`` raises if the shared object is missing, so a GPU box
+without the built extension fails loudly instead of silently computing elsewhere.
+
+``torch`` is imported first on purpose: PyTorch-ROCm ships its own
+``libamdhip64.so`` (soname ``libamdhip64.so.7``); loading it before
+``libotfuse.so`` makes the dynamic linker bind our NEEDED entry to the same HIP
+runtime, so torch's device pointers and streams are valid on our side.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libotfuse.so")
+HEADER_PATH = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "otfuse.h"))
+
+OTF_OK, OTF_EINVAL, OTF_EUNSUPPORTED, OTF_EHIP = 0, 1, 2, -1
+OTF_F32, OTF_F64 = 0, 1
+OTF_SQEUCLIDEAN, OTF_EUCLIDEAN = 0, 1
+OTF_FLAVOR_POT, OTF_FLAVOR_OTT = 0, 1
+SK_RUNNING, SK_CONVERGED, SK_MAX_ITER, SK_NUMERICAL_BREAK = 0, 1, 2, 3
+STATUS_NAMES = {0: "running", 1: "converged", 2: "max_iter", 3: "numerical_break"}
+
+
+class SinkhornOpts(ctypes.Structure):
+    _fields_ = [("reg", ctypes.c_double), ("stop_thr", ctypes.c_double),
+                ("max_iter", ctypes.c_int32), ("check_every", ctypes.c_int32),
+                ("flavor", ctypes.c_int32), ("err_squared", ctypes.c_int32),
+                ("sync_every", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "pad0", "pad1")
+INFO_INT32S = len(INFO_FIELDS)  # otf_sinkhorn_info is 8 x int32
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_SIGS = {
+    "otf_version": (ctypes.c_char_p, []),
+    "otf_cost_pairwise": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _vp,
+                                         _i64, _vp, _vp]),
+    "otf_scale_inplace": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i32, _vp, _vp]),
+    "otf_feature_cost_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i64]),
+    "otf_feature_cost": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64,
+                                        _vp, _i32, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
+    "otf_sinkhorn_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i32, _i32]),
+    "otf_sinkhorn": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
+                                    ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _i64, _i32, _vp,
+                                    _vp, _vp, ctypes.c_size_t, _vp]),
+    "otf_sinkhorn_profile": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
+                                            ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _vp,
+                                            ctypes.c_size_t, ctypes.POINTER(ctypes.c_float), _vp]),
+    "otf_plan_postprocess": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i32, ctypes.c_float, _i32,
+                                            _vp, _i64, _vp]),
+    "otf_gemm_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
+                                    ctypes.c_float, ctypes.c_float, _vp]),
+}
+
+_lib = None
+
+
+class OtfError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load ``libotfuse.so`` (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OtfError(
+                f"otfuse HIP library not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def declared_symbols():
+    """Entry points declared in include/otfuse.h (used by the ABI tests)."""
+    src = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"\b(otf_[a-z0-9_]+)\s*\(", src)))
+
+
+def check(rc: int, what: str):
+    if rc != OTF_OK:
+        kind = {OTF_EINVAL: "invalid argument", OTF_EUNSUPPORTED: "unsupported shape/config",
+                OTF_EHIP: "HIP runtime error"}.get(rc, f"error {rc}")
+        raise OtfError(f"{what}: {kind} (rc={rc})")
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,270 @@
+"""Device-tensor ops over the C ABI (include/otfuse.h).
+
+Every function takes / returns torch tensors that live on a ROCm device, enqueues
+HIP kernels on the current torch stream and never copies through the host (the
+Sinkhorn solver syncs only when ``sync_every > 0``).  Shapes and dtypes are
+checked here so the C side only sees layouts it supports; anything else raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib as L
+
+_VEC = {torch.float32: 4, torch.float64: 2}
+_DT = {torch.float32: L.OTF_F32, torch.float64: L.OTF_F64}
+
+
+def _dev(t: torch.Tensor, name: str):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a ROCm device tensor")
+    return t
+
+
+def _rowmajor(t: torch.Tensor, vec: int = 1) -> torch.Tensor:
+    """A row-major view whose leading dimension is a multiple of ``vec`` and whose
+    rows start 16-byte aligned; copies into a padded buffer only when needed."""
+    if (t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]
+            and t.stride(0) % vec == 0 and t.data_ptr() % 16 == 0):
+        return t
+    n, m = t.shape
+    ld = -(-m // vec) * vec
+    buf = torch.zeros((n, ld), dtype=t.dtype, device=t.device)
+    buf[:, :m].copy_(t)
+    return buf[:, :m]
+
+
+def _alloc_rowmajor(n: int, m: int, dtype, device, vec: int) -> torch.Tensor:
+    ld = -(-m // vec) * vec
+    return torch.empty((n, ld), dtype=dtype, device=device)[:, :m]
+
+
+# --------------------------------------------------------------------------- cost
+def pairwise_cost(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = "sqeuclidean",
+                  zero_diag: bool | None = None, want_max: bool = True):
+    """``ot.dist``-style pairwise cost on MFMA.  Returns ``(C float32 (n, m), cmax (1,))``.
+
+    ``zero_diag`` defaults to POT's ``X is Y`` rule (MRI_PET_OT_nojax.py:70-71 passes the
+    same array twice).  ``cmax`` is a device scalar with max(C) (None if not wanted).
+    """
+    _dev(X, "X")
+    same = Y is None or Y is X
+    Y = X if Y is None else _dev(Y, "Y")
+    if zero_diag is None:
+        zero_diag = same
+    if metric not in ("sqeuclidean", "euclidean"):
+        raise ValueError(f"metric {metric!r} not supported (sqeuclidean | euclidean)")
+    if X.dim() != 2 or Y.dim() != 2 or X.shape[1] != Y.shape[1]:
+        raise ValueError(f"X {tuple(X.shape)} and Y {tuple(Y.shape)} must be (n, d) and (m, d)")
+    X = _rowmajor(X.float(), 4)
+    Y = X if same else _rowmajor(Y.float(), 4)
+    n, d = X.shape
+    m = Y.shape[0]
+    C = _alloc_rowmajor(n, m, torch.float32, X.device, 4)
+    cmax = torch.empty(1, dtype=torch.float32, device=X.device) if want_max else None
+    L.check(L.lib().otf_cost_pairwise(
+        X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, m, d,
+        L.OTF_EUCLIDEAN if metric == "euclidean" else L.OTF_SQEUCLIDEAN, int(zero_diag),
+        C.data_ptr(), C.stride(0), L.ptr(cmax), L.stream_handle(X.device)), "otf_cost_pairwise")
+    return C, cmax
+
+
+def scale_inplace(C: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """``C /= s`` with a device scalar ``s`` (MRI_PET_OT_nojax.py:74-75)."""
+    if s.dtype != C.dtype:
+        s = s.to(C.dtype)
+    L.check(L.lib().otf_scale_inplace(C.data_ptr(), C.shape[0], C.shape[1], C.stride(0),
+                                      _DT[C.dtype], s.data_ptr(), L.stream_handle(C.device)),
+            "otf_scale_inplace")
+    return C
+
+
+def feature_cost(X: torch.Tensor, Y: torch.Tensor, Ts: torch.Tensor | None = None,
+                 ts_diag: torch.Tensor | None = None, weights: str = "pot") -> torch.Tensor:
+    """Feature cost ``M = t1 + t2 - 2 X^T Ts Y`` in float64 (MRI_PET_OT_nojax.py:121-136).
+
+    ``weights="pot"``: w1 = Ts.sum(1), w2 = Ts.sum(0) (get_feature_coupling_pot);
+    ``weights="fot"``: w1 = Ts.sum(0), w2 = Ts.sum(1) (perturbot fot.py:109-118).
+    Give ``Ts`` (n, n2) or its diagonal ``ts_diag`` (n,).
+    """
+    _dev(X, "X")
+    _dev(Y, "Y")
+    if (Ts is None) == (ts_diag is None):
+        raise ValueError("pass exactly one of Ts / ts_diag")
+    X = _rowmajor(X.float())
+    Y = _rowmajor(Y.float())
+    n, d = X.shape
+    n2, d2 = Y.shape
+    if Ts is not None:
+        Ts = _rowmajor(Ts.to(torch.float64))
+        if tuple(Ts.shape) != (n, n2):
+            raise ValueError(f"Ts {tuple(Ts.shape)} must be ({n}, {n2})")
+    else:
+        ts_diag = ts_diag.to(torch.float64).contiguous()
+        if n != n2 or ts_diag.numel() != n:
+            raise ValueError("diagonal Ts needs n == n2 == len(ts_diag)")
+    mode = {"pot": 0, "fot": 1}[weights]
+    M = torch.empty((d, d2), dtype=torch.float64, device=X.device)
+    lib = L.lib()
+    wsb = lib.otf_feature_cost_workspace_size(n, n2, d, d2)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=X.device)
+    L.check(lib.otf_feature_cost(
+        X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, n2, d, d2, L.ptr(Ts),
+        Ts.stride(0) if Ts is not None else 0, L.ptr(ts_diag), mode, M.data_ptr(), M.stride(0),
+        ws.data_ptr(), wsb, L.stream_handle(X.device)), "otf_feature_cost")
+    return M
+
+
+# --------------------------------------------------------------------------- Sinkhorn
+@dataclass
+class SinkhornResult:
+    u: torch.Tensor                 # POT: scaling u; OTT: potential f
+    v: torch.Tensor                 # POT: scaling v; OTT: potential g
+    plan: torch.Tensor | None
+    info_dev: torch.Tensor          # int32[8] otf_sinkhorn_info on the device
+    errlog_dev: torch.Tensor        # float64 marginal errors on the device
+    flavor: str = "pot"
+    _info: dict | None = field(default=None, repr=False)
+
+    def info(self) -> dict:
+        """Reads the device-side outcome (synchronises on first call)."""
+        if self._info is None:
+            vals = self.info_dev.cpu().tolist()
+            d = dict(zip(L.INFO_FIELDS, vals))
+            d["status_name"] = L.STATUS_NAMES.get(d["status"], "?")
+            d["err"] = self.errlog_dev[: max(d["n_err"], 0)].cpu().tolist()
+            self._info = d
+        return self._info
+
+
+def sinkhorn_workspace(n: int, m: int, dtype, max_iter: int, device) -> torch.Tensor:
+    wsb = L.lib().otf_sinkhorn_workspace_size(n, m, _DT[dtype], max_iter)
+    return torch.empty(wsb, dtype=torch.uint8, device=device)
+
+
+def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_iter: int = 1000,
+             stop_thr: float = 1e-9, flavor: str = "pot", cost_scale: torch.Tensor | None = None,
+             check_every: int = 10, err_squared: bool = False, sync_every: int = 0,
+             want_plan: bool = True, plan_dtype=None, workspace: torch.Tensor | None = None,
+             plan_out: torch.Tensor | None = None) -> SinkhornResult:
+    """Entropic OT on the device.  ``flavor="pot"`` is POT's sinkhorn_knopp (u, v scalings,
+    revert-and-break), ``flavor="ott"`` OTT's lse-mode solver (potentials f, g).
+
+    ``cost_scale`` (device scalar) divides the cost first (scale_cost="max_cost").
+    Compute dtype = ``C.dtype`` (float32 or float64).
+    """
+    _dev(C, "C")
+    if C.dtype not in _VEC:
+        raise TypeError("C must be float32 or float64")
+    dt = C.dtype
+    n, m = C.shape
+    C = _rowmajor(C, _VEC[dt])
+    a = _dev(a, "a").to(dt).contiguous()
+    b = _dev(b, "b").to(dt).contiguous()
+    if a.numel() != n or b.numel() != m:
+        raise ValueError(f"a ({a.numel()}) / b ({b.numel()}) do not match C {tuple(C.shape)}")
+    if cost_scale is not None:
+        cost_scale = cost_scale.to(dt).contiguous()
+    dev = C.device
+    u = torch.empty(n, dtype=dt, device=dev)
+    v = torch.empty(m, dtype=dt, device=dev)
+    info = torch.empty(L.INFO_INT32S, dtype=torch.int32, device=dev)
+    errlog = torch.zeros(max_iter // max(check_every, 1) + 2, dtype=torch.float64, device=dev)
+    if workspace is None:
+        workspace = sinkhorn_workspace(n, m, dt, max_iter, dev)
+    P = None
+    if want_plan:
+        pdt = dt if plan_dtype is None else plan_dtype
+        P = plan_out if plan_out is not None else _alloc_rowmajor(n, m, pdt, dev, 4)
+        if P.dtype not in _DT or tuple(P.shape) != (n, m):
+            raise ValueError("plan_out must be (n, m) float32/float64")
+    opts = L.SinkhornOpts(reg=float(reg), stop_thr=float(stop_thr), max_iter=int(max_iter),
+                          check_every=int(check_every),
+                          flavor=L.OTF_FLAVOR_OTT if flavor == "ott" else L.OTF_FLAVOR_POT,
+                          err_squared=int(err_squared), sync_every=int(sync_every), reserved=0)
+    L.check(L.lib().otf_sinkhorn(
+        a.data_ptr(), b.data_ptr(), C.data_ptr(), n, m, C.stride(0), _DT[dt], L.ptr(cost_scale),
+        ctypes.byref(opts), u.data_ptr(), v.data_ptr(), L.ptr(P), P.stride(0) if P is not None else 0,
+        _DT[P.dtype] if P is not None else 0, info.data_ptr(), errlog.data_ptr(),
+        workspace.data_ptr(), workspace.numel(), L.stream_handle(dev)), "otf_sinkhorn")
+    return SinkhornResult(u=u, v=v, plan=P, info_dev=info, errlog_dev=errlog, flavor=flavor)
+
+
+def sinkhorn_profile(a, b, C, reg, iters, cost_scale=None, flavor="pot", workspace=None) -> float:
+    """Runs exactly ``iters`` iterations with a HIP event pair around every pass;
+    returns the mean pass duration in ms (bench.py's roofline probe)."""
+    dt = C.dtype
+    n, m = C.shape
+    C = _rowmajor(C, _VEC[dt])
+    a = a.to(dt).contiguous()
+    b = b.to(dt).contiguous()
+    if cost_scale is not None:
+        cost_scale = cost_scale.to(dt).contiguous()
+    u = torch.empty(n, dtype=dt, device=C.device)
+    v = torch.empty(m, dtype=dt, device=C.device)
+    info = torch.empty(L.INFO_INT32S, dtype=torch.int32, device=C.device)
+    if workspace is None:
+        workspace = sinkhorn_workspace(n, m, dt, iters, C.device)
+    opts = L.SinkhornOpts(reg=float(reg), stop_thr=-1.0, max_iter=int(iters), check_every=10,
+                          flavor=L.OTF_FLAVOR_OTT if flavor == "ott" else L.OTF_FLAVOR_POT,
+                          err_squared=0, sync_every=0, reserved=0)
+    avg = ctypes.c_float(0.0)
+    L.check(L.lib().otf_sinkhorn_profile(
+        a.data_ptr(), b.data_ptr(), C.data_ptr(), n, m, C.stride(0), _DT[dt], L.ptr(cost_scale),
+        ctypes.byref(opts), u.data_ptr(), v.data_ptr(), info.data_ptr(), workspace.data_ptr(),
+        workspace.numel(), ctypes.byref(avg), L.stream_handle(C.device)), "otf_sinkhorn_profile")
+    return float(avg.value)
+
+
+# --------------------------------------------------------------------------- plan use
+def plan_postprocess(T: torch.Tensor, nan_fill: float = 1e-8, rownorm: bool = True) -> torch.Tensor:
+    """MRI_PET_OT_nojax.py:702-715: float32 cast, NaN -> 1e-8, row normalisation."""
+    _dev(T, "T")
+    T = _rowmajor(T if T.dtype in _DT else T.double())
+    d, d2 = T.shape
+    Tn = torch.empty((d, d2), dtype=torch.float32, device=T.device)
+    L.check(L.lib().otf_plan_postprocess(T.data_ptr(), d, d2, T.stride(0), _DT[T.dtype],
+                                         float(nan_fill), int(rownorm), Tn.data_ptr(), Tn.stride(0),
+                                         L.stream_handle(T.device)), "otf_plan_postprocess")
+    return Tn
+
+
+def gemm_f32(A: torch.Tensor, B: torch.Tensor, transpose_b: bool = False) -> torch.Tensor:
+    """``A @ B`` (or ``A @ B^T``) in float32 on the HIP GEMM kernel."""
+    A = _dev(A, "A").float()
+    B = _dev(B, "B").float()
+    M, K = A.shape
+    if transpose_b:
+        N, K2 = B.shape
+        sb0, sb1 = B.stride(1), B.stride(0)
+    else:
+        K2, N = B.shape
+        sb0, sb1 = B.stride(0), B.stride(1)
+    if K != K2:
+        raise ValueError(f"inner dimensions differ: {K} vs {K2}")
+    out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    L.check(L.lib().otf_gemm_f32(A.data_ptr(), A.stride(0), A.stride(1), B.data_ptr(), sb0, sb1,
+                                 out.data_ptr(), out.stride(0), M, N, K, 1.0, 0.0,
+                                 L.stream_handle(A.device)), "otf_gemm_f32")
+    return out
+
+
+class PlanApply(torch.autograd.Function):
+    """``Z @ T^T`` with a constant plan T (MRI_PET_OT_nojax.py:718); backward ``G @ T``."""
+
+    @staticmethod
+    def forward(ctx, Z, T):
+        ctx.save_for_backward(T)
+        return gemm_f32(Z, T, transpose_b=True)
+
+    @staticmethod
+    def backward(ctx, grad):
+        (T,) = ctx.saved_tensors
+        return gemm_f32(grad.contiguous(), T), None
+
+
+def apply_plan(Z: torch.Tensor, T: torch.Tensor) -> torch.Tensor:
+    return PlanApply.apply(Z, T.detach())

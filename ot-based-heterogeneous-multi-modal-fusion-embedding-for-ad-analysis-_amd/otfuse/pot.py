@@ -1,0 +1,187 @@
+"""Drop-ins for the POT calls and the POT-based coupling functions of the reference.
+
+Same names, argument meaning and return conventions as the reference call sites:
+
+* ``sinkhorn``  -> ``ot.sinkhorn(a, b, M, reg, numItermax, stopThr)`` used at
+  MRI_PET_OT_nojax.py:143 (POT 0.9.6 ``sinkhorn_knopp``);
+* ``dist`` / ``unif`` -> ``ot.dist`` / ``ot.unif`` (MRI_PET_OT_nojax.py:70-79);
+* ``get_feature_coupling_pot`` -> MRI_PET_OT_nojax.py:91-145 (copy in MRI_T1_T2_OT.py:92-146).
+
+NumPy inputs give NumPy outputs (float64 plans, like POT on the reference's
+float64 ``M``) so the functions drop into the unchanged training scripts; torch
+device tensors stay on the device end to end.  All arithmetic runs in the HIP
+library — there is no CPU path.
+"""
+from __future__ import annotations
+
+import warnings
+from typing import Dict, Tuple, Union
+from numbers import Number
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("otfuse needs a ROCm GPU (torch.cuda.is_available() is False)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _as_dev(x, dtype, device):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype)
+    return torch.as_tensor(np.asarray(x), dtype=dtype, device=device)
+
+
+def unif(n: int, type_as=None):
+    """``ot.unif``: uniform histogram of length n."""
+    if isinstance(type_as, torch.Tensor):
+        return torch.full((n,), 1.0 / n, dtype=type_as.dtype, device=type_as.device)
+    return np.ones((n,)) / n
+
+
+def dist(x1, x2=None, metric: str = "sqeuclidean"):
+    """``ot.dist`` for the metrics the reference uses ('sqeuclidean', 'euclidean').
+
+    POT zeroes the diagonal when ``x2`` is ``x1`` (or omitted).  The contraction runs
+    on float32 MFMA; float64 inputs are rounded to float32 first.
+    """
+    same = x2 is None or x2 is x1
+    is_torch = isinstance(x1, torch.Tensor) and x1.is_cuda
+    dev = x1.device if is_torch else _device()
+    X = _as_dev(x1, torch.float32, dev)
+    Y = X if same else _as_dev(x2, torch.float32, dev)
+    C, _ = ops.pairwise_cost(X, None if same else Y, metric=metric, zero_diag=same, want_max=False)
+    if is_torch:
+        return C.to(x1.dtype)
+    dt = np.result_type(np.asarray(x1).dtype, np.float32) if x2 is None else \
+        np.result_type(np.asarray(x1).dtype, np.asarray(x2).dtype)
+    return C.cpu().numpy().astype(dt, copy=False)
+
+
+def sinkhorn(a, b, M, reg: float, method: str = "sinkhorn", numItermax: int = 1000,
+             stopThr: float = 1e-9, verbose: bool = False, log: bool = False, warn: bool = True,
+             warmstart=None, **kwargs):
+    """``ot.sinkhorn`` (method 'sinkhorn' = ``sinkhorn_knopp``) on the device.
+
+    Semantics follow POT 0.9.6: u0 = 1/n, v0 = 1/m, v-update then u-update, revert to
+    the previous iterate and stop on a zero in K^T u or nan/inf in u, v ("numerical
+    errors" warning), L2 marginal error every 10 iterations against ``stopThr``.
+    Computes in the dtype of ``M`` (float64 for the reference's feature costs).
+    Extra keyword ``sync_every`` (default 50) sets how often the host polls the
+    device-side convergence flag.
+    """
+    if method.lower() not in ("sinkhorn", "sinkhorn_knopp"):
+        raise NotImplementedError(f"method {method!r}: only POT's sinkhorn_knopp is provided")
+    if warmstart is not None:
+        raise NotImplementedError("warmstart is not supported")
+    is_torch = isinstance(M, torch.Tensor) and M.is_cuda
+    dev = M.device if is_torch else _device()
+    mdt = (M.dtype if is_torch else np.asarray(M).dtype)
+    dt = torch.float32 if mdt in (torch.float32, np.float32) else torch.float64
+    Md = _as_dev(M, dt, dev)
+    n, m = Md.shape
+    a = unif(n) if a is None or len(a) == 0 else a
+    b = unif(m) if b is None or len(b) == 0 else b
+    if np.ndim(b.cpu() if isinstance(b, torch.Tensor) else b) > 1:
+        raise NotImplementedError("multiple target histograms (2-D b) are not supported")
+    ad = _as_dev(a, dt, dev)
+    bd = _as_dev(b, dt, dev)
+    res = ops.sinkhorn(ad, bd, Md, float(reg), max_iter=int(numItermax), stop_thr=float(stopThr),
+                       flavor="pot", sync_every=int(kwargs.get("sync_every", 50)), want_plan=True)
+    info = res.info()
+    if warn and info["status"] == 3:
+        warnings.warn("Warning: numerical errors at iteration %d" % info["break_iter"])
+    if warn and info["status"] == 2:
+        warnings.warn("Sinkhorn did not converge. You might want to increase the number of "
+                      "iterations `numItermax` or the regularization parameter `reg`.")
+    if verbose:
+        for k, e in enumerate(info["err"]):
+            print("{:5d}|{:8e}|".format(10 * k, e))
+    P = res.plan if is_torch else res.plan.cpu().numpy()
+    if not log:
+        return P
+    u = res.u if is_torch else res.u.cpu().numpy()
+    v = res.v if is_torch else res.v.cpu().numpy()
+    return P, {"err": info["err"], "niter": info["niter"], "u": u, "v": v,
+               "status": info["status_name"]}
+
+
+def _concat_sorted(X_dict, Y_dict):
+    keys = sorted(X_dict.keys())
+    X = np.concatenate([X_dict[k] for k in keys])
+    Y = np.concatenate([Y_dict[k] for k in keys])
+    return keys, X, Y
+
+
+def block_diag_ts(Ts: Dict[Number, np.ndarray], X_dict, Y_dict) -> np.ndarray:
+    """Per-label sample plans -> block-diagonal Ts in sorted label order
+    (MRI_PET_OT_nojax.py:105-119; labels missing from ``Ts`` leave zero blocks)."""
+    keys = sorted(X_dict.keys())
+    n_x = sum(len(X_dict[k]) for k in keys)
+    n_y = sum(len(Y_dict[k]) for k in keys)
+    T = np.zeros((n_x, n_y))
+    ix = iy = 0
+    for k in keys:
+        nx, ny = len(X_dict[k]), len(Y_dict[k])
+        if k in Ts:
+            T[ix:ix + nx, iy:iy + ny] = Ts[k]
+        ix += nx
+        iy += ny
+    return T
+
+
+def feature_coupling_pot_device(X: torch.Tensor, Y: torch.Tensor, Ts=None, ts_diag=None,
+                                eps: float = 5e-3, numItermax: int = 2000, stopThr: float = 1e-9,
+                                sync_every: int = 50):
+    """Device form of get_feature_coupling_pot on already-concatenated X (n, d), Y (n2, d2):
+    float64 feature cost + POT-flavour float64 Sinkhorn.  Returns ``ops.SinkhornResult``."""
+    M = ops.feature_cost(X, Y, Ts=Ts, ts_diag=ts_diag, weights="pot")
+    d, d2 = M.shape
+    a = torch.full((d,), 1.0 / d, dtype=torch.float64, device=M.device)
+    b = torch.full((d2,), 1.0 / d2, dtype=torch.float64, device=M.device)
+    return ops.sinkhorn(a, b, M, float(eps), max_iter=numItermax, stop_thr=stopThr, flavor="pot",
+                        sync_every=sync_every, want_plan=True)
+
+
+def _diag_or_none(T: np.ndarray):
+    if T.ndim == 2 and T.shape[0] == T.shape[1]:
+        d = np.diag(T)
+        if np.count_nonzero(T - np.diag(d)) == 0:
+            return d
+    return None
+
+
+def get_feature_coupling_pot(
+    data: Tuple[Dict[Number, np.ndarray], Dict[Number, np.ndarray]],
+    Ts: Union[Dict[Number, np.ndarray], np.ndarray],
+    eps=5e-3,
+):
+    """Feature coupling using POT-semantics Sinkhorn (MRI_PET_OT_nojax.py:91-145).
+
+    Concatenates the per-label arrays in sorted label order, assembles a block
+    diagonal Ts from a dict, builds M = t1 + t2 - 2 X^T Ts Y in float64 and solves
+    ``sinkhorn(1/d, 1/d', M, reg=eps, numItermax=2000)``.  Returns ``(Tv, {})`` with
+    Tv a float64 (d, d') ndarray, like the reference.
+    """
+    X_dict, Y_dict = data
+    _, X, Y = _concat_sorted(X_dict, Y_dict)
+    if isinstance(Ts, dict):
+        Ts = block_diag_ts(Ts, X_dict, Y_dict)
+    Ts = np.asarray(Ts, dtype=np.float64)
+    dev = _device()
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=dev)
+    Yd = torch.as_tensor(Y, dtype=torch.float32, device=dev)
+    diag = _diag_or_none(Ts)
+    if diag is not None:
+        res = feature_coupling_pot_device(Xd, Yd, ts_diag=torch.as_tensor(diag, device=dev),
+                                          eps=eps)
+    else:
+        res = feature_coupling_pot_device(Xd, Yd, Ts=torch.as_tensor(Ts, device=dev), eps=eps)
+    info = res.info()
+    if info["status"] == 3:
+        warnings.warn("Warning: numerical errors at iteration %d" % info["break_iter"])
+    return res.plan.cpu().numpy(), {}

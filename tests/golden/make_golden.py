@@ -1,0 +1,175 @@
+"""Generate the golden parity fixtures from the reference's OWN code.
+
+Runs only in the survey/build container, where /root/reference exists.  It never
+copies reference source into the repo: the reference functions are parsed out of
+the read-only tree at run time (``ast``) and executed; only their numeric inputs
+and outputs are written, as small ``.npz`` files next to this script.
+
+What is the reference here:
+
+* ``get_feature_coupling_pot`` — AST-extracted from
+  /root/reference/MRI_PET_OT_nojax.py:91-145 and executed verbatim.
+* ``ot.sinkhorn`` — POT is not installed.  Its call at MRI_PET_OT_nojax.py:143 is
+  bound to the vendored reference Sinkhorn
+  ``perturbot/perturbot/match/utils.py:6-115`` (``sinkhorn_scaling``), which runs
+  the identical update sequence as POT 0.9.6 ``sinkhorn_knopp``.  The vendored
+  loop tests the SQUARED marginal error against ``stopThr``; POT tests the norm,
+  so the stub passes ``stopThr ** 2`` to reproduce POT's stopping iteration.
+* ``cosine_loss`` — AST-extracted from MRI_PET_OT_nojax.py:552-560.
+* ``ot.dist`` (POT) has no in-container implementation: the pairwise cost of F1
+  is the oracle's restatement, so F1 pins the Sinkhorn, not the cost.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import ast
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(REF, "perturbot"))
+sys.path.insert(0, os.path.join(REPO, "ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd"))
+sys.path.insert(0, REPO)
+
+from perturbot.match.utils import sinkhorn_scaling  # noqa: E402  (reference code)
+from otfuse.synthetic import paired_embeddings  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+_CALLS = []
+
+
+def _stub_ot():
+    """A stand-in ``ot`` module whose ``sinkhorn`` is the vendored reference loop."""
+    def sinkhorn(a, b, M, reg, numItermax=1000, stopThr=1e-9, **kw):
+        K = np.exp(M / (-reg))  # POT: K = nx.exp(M / (-reg))
+        P, log = sinkhorn_scaling(a, b, K, numItermax=numItermax, stopThr=stopThr ** 2, log=True)
+        _CALLS.append({"u": log["u"], "v": log["v"], "err2": np.asarray(log["err"])})
+        return P
+
+    mod = types.ModuleType("ot")
+    mod.sinkhorn = sinkhorn
+    return mod
+
+
+def _extract(path, name):
+    src = open(path).read()
+    tree = ast.parse(src)
+    for node in tree.body:
+        if isinstance(node, ast.FunctionDef) and node.name == name:
+            return ast.get_source_segment(src, node)
+    raise KeyError(name)
+
+
+def _ref_functions():
+    import torch
+    import torch.nn.functional as F
+    from numbers import Number
+    from typing import Dict, Tuple, Union
+    ns = {"np": np, "ot": _stub_ot(), "Dict": Dict, "Tuple": Tuple, "Union": Union,
+          "Number": Number, "torch": torch, "F": F}
+    path = os.path.join(REF, "MRI_PET_OT_nojax.py")
+    for fn in ("get_feature_coupling_pot", "cosine_loss"):
+        exec(compile(_extract(path, fn), path, "exec"), ns)
+    return ns["get_feature_coupling_pot"], ns["cosine_loss"]
+
+
+def _postprocess_torch(T_np):
+    """MRI_PET_OT_nojax.py:702-715, the torch lines restated (they sit inside forward)."""
+    import torch
+    T = torch.from_numpy(T_np).float()
+    T = torch.where(torch.isnan(T), torch.full_like(T, 1e-8), T)
+    rs = T.sum(dim=1, keepdim=True)
+    rs = torch.where(rs == 0, torch.full_like(rs, 1e-8), rs)
+    return T / rs
+
+
+def _sample_idx(rng, shape, k=512):
+    return np.stack([rng.integers(0, shape[0], k), rng.integers(0, shape[1], k)], 1)
+
+
+def main():
+    import torch
+    gfc, cosine_loss = _ref_functions()
+    rng = np.random.default_rng(7)
+
+    # F1: config-1 Sinkhorn, 256 x 256, eps = 0.1 on the max-normalised sq-Euclid cost,
+    #     50 iterations, stopThr = 0 (fixed count).
+    X, Y, _ = paired_embeddings(256, 64, seed=1234)
+    C = orc.pairwise_cost_np(X, Y)
+    C = C / C.max()
+    a = np.ones(256) / 256
+    _CALLS.clear()
+    P = _stub_ot().sinkhorn(a, a, C, 0.1, numItermax=50, stopThr=0.0)
+    call = _CALLS[-1]
+    idx1 = _sample_idx(rng, P.shape)
+    np.savez_compressed(os.path.join(HERE, "f1_sinkhorn_256.npz"), X=X, Y=Y, reg=0.1, iters=50,
+                        u=call["u"], v=call["v"], idx=idx1, plan_samples=P[idx1[:, 0], idx1[:, 1]],
+                        plan_rowsum=P.sum(1), plan_colsum=P.sum(0))
+
+    # F2: per-batch feature coupling exactly as forward() calls it
+    #     (MRI_PET_OT_nojax.py:683-699): B = 8, d = 512, Ts = {0: eye(8)/8}, eps = 1e-2,
+    #     numItermax = 2000, default stopThr = 1e-9 (converged mode).
+    Xb, Yb, _ = paired_embeddings(8, 512, seed=2024)
+    Ts = np.eye(8) / 8
+    _CALLS.clear()
+    Tv, _ = gfc(({0: Xb}, {0: Yb}), Ts={0: Ts}, eps=1e-2)
+    call = _CALLS[-1]
+    M = orc.feature_cost_np(Xb, Yb, Ts)
+    idx = _sample_idx(rng, Tv.shape)
+    Tn = _postprocess_torch(Tv)
+    Zpet = torch.from_numpy(Yb)
+    ot_mri = torch.matmul(Zpet, Tn.t())
+    loss = cosine_loss(torch.from_numpy(Xb), ot_mri)
+    np.savez_compressed(os.path.join(HERE, "f2_feature_pot_b8_d512.npz"), X=Xb, Y=Yb, eps=1e-2,
+                        numItermax=2000, stopThr=1e-9, u=call["u"], v=call["v"],
+                        err=np.sqrt(call["err2"]), n_err=len(call["err2"]),
+                        idx=idx, plan_samples=Tv[idx[:, 0], idx[:, 1]],
+                        plan_rowsum=Tv.sum(1), plan_colsum=Tv.sum(0),
+                        M_samples=M[idx[:, 0], idx[:, 1]], M_rowsum=M.sum(1),
+                        Tn_samples=Tn.numpy()[idx[:, 0], idx[:, 1]],
+                        ot_mri_from_pet=ot_mri.numpy(), ot_loss=float(loss))
+
+    # F3: numerical break at iteration 0: a column of K underflows to zero in float64
+    #     (M / eps > 745), so POT reverts to u = 1/n, v = 1/m: plan = K / (n m).
+    Xc, Yc, _ = paired_embeddings(8, 64, seed=99)
+    Xc = Xc * 40.0
+    Yc[:, :4] += 60.0
+    _CALLS.clear()
+    Tv3, _ = gfc(({0: Xc}, {0: Yc}), Ts={0: np.eye(8) / 8}, eps=1e-3)
+    call = _CALLS[-1]
+    np.savez_compressed(os.path.join(HERE, "f3_numerical_break.npz"), X=Xc, Y=Yc, eps=1e-3,
+                        u=call["u"], v=call["v"], plan=Tv3, n_err=len(call["err2"]))
+
+    # F4: per-epoch form: block-diagonal Ts from a per-label dict (2 labels x 16 samples,
+    #     non-symmetric, non-uniform blocks), d = 64 vs d2 = 48, default eps = 5e-3.
+    xd, yd, tsd = {}, {}, {}
+    for lab, (nx, ny) in {1: (16, 12), 0: (14, 16)}.items():
+        xl, yl, _ = paired_embeddings(max(nx, ny), 64, seed=300 + lab, d2=48)
+        xd[lab], yd[lab] = xl[:nx], yl[:ny]
+        blk = rng.random((nx, ny)) ** 3
+        tsd[lab] = blk / blk.sum()
+    _CALLS.clear()
+    Tv4, _ = gfc((xd, yd), Ts=tsd, eps=5e-3)
+    call = _CALLS[-1]
+    keys = sorted(xd)
+    Xs = np.concatenate([xd[k] for k in keys])
+    Ys = np.concatenate([yd[k] for k in keys])
+    Tsm = orc.block_diag_ts(tsd, xd, yd)
+    np.savez_compressed(os.path.join(HERE, "f4_feature_blockdiag.npz"),
+                        X0=xd[0], X1=xd[1], Y0=yd[0], Y1=yd[1], Ts0=tsd[0], Ts1=tsd[1],
+                        Xcat=Xs, Ycat=Ys, Ts=Tsm, M=orc.feature_cost_np(Xs, Ys, Tsm), eps=5e-3,
+                        u=call["u"], v=call["v"], plan=Tv4, err=np.sqrt(call["err2"]),
+                        n_err=len(call["err2"]))
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,106 @@
+"""C-ABI surface and host-side logic.  CPU only (no compute calls into the GPU)."""
+import ctypes
+import re
+
+import numpy as np
+import pytest
+
+
+def test_library_exports_every_declared_symbol():
+    from otfuse import _lib as L
+    lib = L.lib()
+    declared = L.declared_symbols()
+    assert len(declared) >= 10
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(L._SIGS) == set(declared), "ctypes table and header differ"
+
+
+def test_version_and_workspace_queries_are_host_only():
+    from otfuse import _lib as L
+    lib = L.lib()
+    assert lib.otf_version().decode().startswith("otfuse")
+    ws = lib.otf_sinkhorn_workspace_size(4096, 4096, L.OTF_F32, 100)
+    assert 4 * 4096 * 9 < ws < 4 * 4096 * 32
+    assert lib.otf_sinkhorn_workspace_size(8, 512, L.OTF_F64, 2000) > 8 * 512 * 7
+    assert lib.otf_feature_cost_workspace_size(8, 8, 512, 512) >= 8 * (8 * 512)
+
+
+def test_abi_structs_and_enums_match_header():
+    from otfuse import _lib as L
+    src = open(L.HEADER_PATH).read()
+    assert ctypes.sizeof(L.SinkhornOpts) == 40
+    assert L.INFO_INT32S * 4 == 32
+    for name, val in [("OTF_F32", 0), ("OTF_F64", 1), ("OTF_FLAVOR_POT", 0), ("OTF_FLAVOR_OTT", 1),
+                      ("OTF_SK_CONVERGED", 1), ("OTF_SK_MAX_ITER", 2),
+                      ("OTF_SK_NUMERICAL_BREAK", 3)]:
+        m = re.search(rf"\b{name}\s*=\s*(-?\d+)", src)
+        assert m and int(m.group(1)) == val, name
+
+
+def test_invalid_arguments_are_rejected_without_a_gpu():
+    """Argument validation runs before any HIP call."""
+    from otfuse import _lib as L
+    lib = L.lib()
+    opts = L.SinkhornOpts(reg=0.1, stop_thr=0.0, max_iter=10, check_every=10, flavor=0,
+                          err_squared=0, sync_every=0, reserved=0)
+    rc = lib.otf_sinkhorn(None, None, None, 0, 0, 0, L.OTF_F32, None, ctypes.byref(opts), None,
+                          None, None, 0, 0, None, None, None, 0, None)
+    assert rc == L.OTF_EINVAL
+    assert lib.otf_cost_pairwise(None, 0, None, 0, 4, 4, 4, 0, 0, None, 4, None, None) == L.OTF_EINVAL
+    assert lib.otf_gemm_f32(None, 1, 1, None, 1, 1, None, 1, 1, 1, 1, 1.0, 0.0, None) == L.OTF_EINVAL
+
+
+def test_group_features_by_label_mirrors_reference():
+    from otfuse.fusion import group_features_by_label
+    y = np.array([1, 0, 1, 1, 0, 2])
+    p = np.arange(12, dtype=np.float32).reshape(6, 2)
+    g = group_features_by_label(y, p, max_samples_per_label=2)
+    assert list(g.keys()) == [0, 1, 2]
+    np.testing.assert_array_equal(g[1], p[[0, 2]])
+    np.testing.assert_array_equal(g[0], p[[1, 4]])
+    np.testing.assert_array_equal(g[2], p[[5]])
+    g2 = group_features_by_label(y, p)
+    assert g2[1].shape == (3, 2)
+
+
+def test_mdict_to_matrix_and_block_diag(orc):
+    from otfuse.perturbot import mdict_to_matrix
+    from otfuse.pot import block_diag_ts
+    rng = np.random.default_rng(0)
+    xd = {1: rng.random((3, 2)), 0: rng.random((2, 2))}
+    yd = {1: rng.random((4, 2)), 0: rng.random((2, 2))}
+    ts = {0: rng.random((2, 2)), 1: rng.random((3, 4))}
+    # nojax: sorted label order
+    np.testing.assert_array_equal(block_diag_ts(ts, xd, yd), orc.block_diag_ts(ts, xd, yd))
+    B = block_diag_ts(ts, xd, yd)
+    np.testing.assert_array_equal(B[:2, :2], ts[0])
+    np.testing.assert_array_equal(B[2:, 2:], ts[1])
+    # perturbot: insertion order of data[0] through label masks
+    src = np.concatenate([np.ones(xd[k].shape[0]) * k for k in xd])
+    tgt = np.concatenate([np.ones(yd[k].shape[0]) * k for k in xd])
+    Mt = mdict_to_matrix(ts, src, tgt)
+    np.testing.assert_array_equal(Mt[:3, :4], ts[1])
+    np.testing.assert_array_equal(Mt[3:, 4:], ts[0])
+    assert Mt[:3, 4:].sum() == 0
+
+
+def test_synthetic_inputs_are_seeded_and_structured():
+    from otfuse.synthetic import paired_embeddings
+    X1, Y1, l1 = paired_embeddings(64, 32, seed=9)
+    X2, Y2, l2 = paired_embeddings(64, 32, seed=9)
+    np.testing.assert_array_equal(X1, X2)
+    np.testing.assert_array_equal(l1, l2)
+    assert X1.dtype == np.float32 and (X1 >= 0).all()
+    # paired: a subject's MRI embedding is closer to its own PET embedding's latent
+    # neighbourhood than to a random subject's (structure, not iid noise)
+    c = np.corrcoef(X1.reshape(-1), Y1.reshape(-1))[0, 1]
+    assert np.isfinite(c)
+
+
+def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
+    from otfuse import _lib as L
+    monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(L.OtfError):
+        L.lib()

@@ -1,0 +1,278 @@
+"""HIP path vs the oracle and the golden vectors (needs an MI355X).
+
+Tolerances: the north star asks for plans within 1e-4 relative of the reference
+CPU path.  "Relative" is normwise: max|P - P_ref| / max|P_ref| (entries of
+exp(-M/reg) far below the plan's scale carry no information and exp() amplifies
+last-bit cost differences in them).  float64 paths are held to 1e-9..1e-10.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def nrel(x, ref):
+    x = np.asarray(x, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    return np.abs(x - ref).max() / np.abs(ref).max()
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from otfuse import ops as o
+    return o
+
+
+def _t(x, dev, dt=None):
+    return torch.as_tensor(np.asarray(x), device=dev, dtype=dt)
+
+
+# ----------------------------------------------------------------------------- cost
+@pytest.mark.parametrize("n,m,d", [(256, 256, 64), (130, 77, 40), (4096, 4096, 512), (1, 5, 3)])
+def test_pairwise_cost_vs_oracle(ops, orc, dev, n, m, d):
+    from otfuse.synthetic import paired_embeddings
+    X, _, _ = paired_embeddings(n, d, seed=n)
+    _, Y, _ = paired_embeddings(m, d, seed=m + 1)
+    C, cmax = ops.pairwise_cost(_t(X, dev), _t(Y, dev))
+    Cr, mr = orc.pairwise_cost(X, Y)
+    assert nrel(C.cpu().numpy(), Cr) < 2e-6
+    assert float(cmax) == pytest.approx(mr, rel=1e-5)
+
+
+def test_pairwise_cost_euclidean_same_input_zero_diag(ops, orc, dev):
+    rng = np.random.default_rng(1)
+    X = rng.random((70, 33)).astype(np.float32)
+    Xd = _t(X, dev)
+    C, _ = ops.pairwise_cost(Xd, metric="euclidean")
+    Cr, _ = orc.pairwise_cost(X, X, metric="euclidean", zero_diag=True)
+    Cg = C.cpu().numpy()
+    assert np.all(np.diag(Cg) == 0)
+    assert nrel(Cg, Cr) < 1e-5
+
+
+def test_pairwise_cost_asymmetric_identity_check(ops, dev):
+    """A = I against an asymmetric B catches a transposed C/D write."""
+    d = 64
+    X = torch.eye(d, device=dev)
+    Y = torch.arange(d * d, dtype=torch.float32, device=dev).reshape(d, d) / (d * d)
+    C, _ = ops.pairwise_cost(X, Y)
+    ref = (X[:, None, :] - Y[None, :, :]).pow(2).sum(-1)
+    assert torch.allclose(C, ref, rtol=1e-5, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- Sinkhorn POT
+def test_f1_sinkhorn_config1_golden(ops, golden, dev):
+    f = golden("f1_sinkhorn_256.npz")
+    X, Y = _t(f["X"], dev), _t(f["Y"], dev)
+    C, cmax = ops.pairwise_cost(X, Y)
+    a = torch.full((256,), 1 / 256, device=dev)
+    res = ops.sinkhorn(a, a, C, float(f["reg"]), max_iter=int(f["iters"]), stop_thr=0.0,
+                       cost_scale=cmax)
+    info = res.info()
+    assert info["status_name"] == "max_iter" and info["niter"] == 49
+    P = res.plan.cpu().numpy()
+    idx = f["idx"]
+    assert nrel(P[idx[:, 0], idx[:, 1]], f["plan_samples"]) < 1e-4
+    assert nrel(P.sum(0), f["plan_colsum"]) < 1e-4
+    assert nrel(P.sum(1), f["plan_rowsum"]) < 1e-4
+
+
+def test_f1_float64_path_is_tight(ops, golden, orc, dev):
+    f = golden("f1_sinkhorn_256.npz")
+    C, _ = orc.pairwise_cost(f["X"], f["Y"], scale_max=True)
+    a = torch.full((256,), 1 / 256, device=dev, dtype=torch.float64)
+    res = ops.sinkhorn(a, a, _t(C, dev), 0.1, max_iter=50, stop_thr=0.0)
+    u, v = res.u.cpu().numpy(), res.v.cpu().numpy()
+    s = np.linalg.norm(u) / np.linalg.norm(f["u"])
+    np.testing.assert_allclose(u / s, f["u"], rtol=1e-11)
+    np.testing.assert_allclose(v * s, f["v"], rtol=1e-11)
+
+
+def test_f2_per_batch_feature_coupling_golden(ops, golden, dev):
+    from otfuse.pot import feature_coupling_pot_device
+    f = golden("f2_feature_pot_b8_d512.npz")
+    ts = torch.full((8,), 1 / 8, dtype=torch.float64, device=dev)
+    res = feature_coupling_pot_device(_t(f["X"], dev), _t(f["Y"], dev), ts_diag=ts, eps=1e-2)
+    info = res.info()
+    assert info["n_err"] == int(f["n_err"]) and info["status_name"] == "max_iter"
+    np.testing.assert_allclose(info["err"], f["err"], rtol=1e-5)
+    P = res.plan.cpu().numpy()
+    idx = f["idx"]
+    assert nrel(P[idx[:, 0], idx[:, 1]], f["plan_samples"]) < 1e-9
+    assert nrel(P.sum(1), f["plan_rowsum"]) < 1e-9
+
+
+def test_f2_drop_in_numpy_api(golden, dev):
+    from otfuse.pot import get_feature_coupling_pot
+    f = golden("f2_feature_pot_b8_d512.npz")
+    Tv, log = get_feature_coupling_pot(({0: f["X"]}, {0: f["Y"]}), Ts={0: np.eye(8) / 8}, eps=1e-2)
+    assert isinstance(Tv, np.ndarray) and Tv.dtype == np.float64 and log == {}
+    idx = f["idx"]
+    assert nrel(Tv[idx[:, 0], idx[:, 1]], f["plan_samples"]) < 1e-9
+
+
+def test_f3_numerical_break_golden(ops, golden, dev):
+    from otfuse.pot import feature_coupling_pot_device
+    f = golden("f3_numerical_break.npz")
+    ts = torch.full((8,), 1 / 8, dtype=torch.float64, device=dev)
+    res = feature_coupling_pot_device(_t(f["X"], dev), _t(f["Y"], dev), ts_diag=ts, eps=1e-3)
+    info = res.info()
+    assert info["status_name"] == "numerical_break" and info["break_iter"] == 0
+    assert info["last_good"] == -1
+    P = res.plan.cpu().numpy()
+    assert nrel(P, f["plan"]) < 1e-9
+    assert np.array_equal(P == 0, f["plan"] == 0)
+
+
+def test_f4_blockdiag_nonsquare_golden(golden, dev):
+    from otfuse.pot import get_feature_coupling_pot
+    f = golden("f4_feature_blockdiag.npz")
+    data = ({1: f["X1"], 0: f["X0"]}, {1: f["Y1"], 0: f["Y0"]})   # insertion order != sorted
+    Tv, _ = get_feature_coupling_pot(data, Ts={0: f["Ts0"], 1: f["Ts1"]}, eps=float(f["eps"]))
+    assert Tv.shape == (64, 48)
+    assert nrel(Tv, f["plan"]) < 1e-9
+
+
+def test_feature_cost_dense_ts_vs_oracle(ops, orc, dev):
+    rng = np.random.default_rng(4)
+    X = rng.random((20, 70)).astype(np.float32)
+    Y = rng.random((13, 50)).astype(np.float32)
+    Ts = rng.random((20, 13))
+    M = ops.feature_cost(_t(X, dev), _t(Y, dev), Ts=_t(Ts, dev)).cpu().numpy()
+    assert nrel(M, orc.feature_cost(X, Y, Ts)) < 1e-13
+    Tsq = rng.random((20, 20))
+    Y2 = rng.random((20, 50)).astype(np.float32)
+    M2 = ops.feature_cost(_t(X, dev), _t(Y2, dev), Ts=_t(Tsq, dev), weights="fot").cpu().numpy()
+    assert nrel(M2, orc.feature_cost(X, Y2, Tsq, weights="fot")) < 1e-13
+
+
+@pytest.mark.parametrize("n,m,dt", [(300, 200, torch.float32), (64, 4099, torch.float32),
+                                    (1000, 8191, torch.float32), (513, 2049, torch.float64),
+                                    (3, 7, torch.float64), (1, 1, torch.float32)])
+def test_sinkhorn_ragged_shapes_vs_oracle(ops, orc, dev, n, m, dt):
+    rng = np.random.default_rng(n + m)
+    C = rng.random((n, m))
+    a = rng.random(n) + 0.5
+    a /= a.sum()
+    b = rng.random(m) + 0.5
+    b /= b.sum()
+    P_r, u_r, v_r, info_r = orc.sinkhorn_knopp(a, b, C, 0.1, 60, 0.0)
+    res = ops.sinkhorn(_t(a, dev, dt), _t(b, dev, dt), _t(C, dev, dt), 0.1, max_iter=60,
+                       stop_thr=0.0)
+    tol = 1e-4 if dt == torch.float32 else 1e-10
+    assert nrel(res.plan.cpu().numpy(), P_r) < tol
+    assert res.info()["niter"] == info_r["niter"]
+
+
+def test_converged_mode_stops_at_same_iteration(ops, orc, dev):
+    rng = np.random.default_rng(8)
+    C = rng.random((200, 150))
+    a = np.ones(200) / 200
+    b = np.ones(150) / 150
+    P_r, *_, info_r = orc.sinkhorn_knopp(a, b, C, 0.05, 2000, 1e-9)
+    res = ops.sinkhorn(_t(a, dev), _t(b, dev), _t(C, dev), 0.05, max_iter=2000, stop_thr=1e-9,
+                       sync_every=20)
+    info = res.info()
+    assert info["status_name"] == "converged"
+    assert info["niter"] == info_r["niter"]
+    np.testing.assert_allclose(info["err"], info_r["err"], rtol=1e-6, atol=1e-15)
+    assert nrel(res.plan.cpu().numpy(), P_r) < 1e-10
+
+
+def test_vendored_squared_error_mode(ops, orc, dev):
+    rng = np.random.default_rng(9)
+    C = rng.random((64, 64))
+    a = np.ones(64) / 64
+    _, _, _, info_r = orc.sinkhorn_knopp(a, a, C, 0.05, 2000, 1e-12, err_squared=True)
+    res = ops.sinkhorn(_t(a, dev), _t(a, dev), _t(C, dev), 0.05, max_iter=2000, stop_thr=1e-12,
+                       err_squared=True)
+    assert res.info()["niter"] == info_r["niter"]
+
+
+# ----------------------------------------------------------------------------- full size
+def test_metric_config_full_size_properties(ops, orc, dev):
+    """BASELINE metric config at full size: N = 4096, d = 512, eps = 0.1, 100 iterations,
+    against the float64 oracle (a few seconds on the host) and marginal properties."""
+    from otfuse.synthetic import paired_embeddings
+    N, d = 4096, 512
+    X, Y, _ = paired_embeddings(N, d, seed=1234)
+    C, cmax = ops.pairwise_cost(_t(X, dev), _t(Y, dev))
+    a = torch.full((N,), 1.0 / N, device=dev)
+    res = ops.sinkhorn(a, a, C, 0.1, max_iter=100, stop_thr=0.0, cost_scale=cmax)
+    P = res.plan.cpu().numpy().astype(np.float64)
+    # row marginals are exact after a u-update; column marginals carry the residual
+    np.testing.assert_allclose(P.sum(1), 1.0 / N, rtol=1e-4)
+    Cr, _ = orc.pairwise_cost(X, Y, scale_max=True)
+    Pr, *_ = orc.sinkhorn_knopp(np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cr, 0.1, 100, 0.0)
+    assert nrel(P, Pr) < 1e-4
+    assert np.linalg.norm(P - Pr) / np.linalg.norm(Pr) < 1e-4
+
+
+# ----------------------------------------------------------------------------- OTT flavour
+def test_ott_flavour_vs_log_restatement(ops, orc, dev):
+    """OTT lse-mode semantics (parity unpinned: OTT absent); vs the oracle restatement."""
+    rng = np.random.default_rng(12)
+    C = rng.random((150, 120))
+    a = np.ones(150) / 150
+    b = np.ones(120) / 120
+    P_r, f_r, g_r, info_r = orc.sinkhorn_log(a, b, C, 5e-3, max_iter=2000, threshold=1e-3,
+                                             cscale=1.0 / C.max())
+    M = _t(C, dev, torch.float64)
+    from otfuse.perturbot import solve_ott
+    res, _ = solve_ott(M, 5e-3)
+    info = res.info()
+    assert info["niter"] + 1 == info_r["n_iters"]
+    assert nrel(res.plan.cpu().numpy(), P_r) < 1e-9
+    assert abs(res.plan.sum().item() - 1.0) < 1e-6
+
+
+def test_get_coupling_fot_blockdiag(golden, dev):
+    from otfuse.perturbot import get_coupling_fot
+    f = golden("f4_feature_blockdiag.npz")
+    xd = {0: f["X0"][:12], 1: f["X1"][:12]}
+    yd = {0: f["Y0"][:12], 1: f["Y1"][:12]}
+    rng = np.random.default_rng(2)
+    ts = {k: rng.random((12, 12)) for k in (0, 1)}
+    Tv, log = get_coupling_fot((xd, yd), ts, eps=5e-3)
+    assert Tv.shape == (64, 48) and len(log["cost"]) == 2
+    np.testing.assert_allclose(Tv.sum(1), 1 / 64, rtol=1e-6)
+    np.testing.assert_allclose(Tv.sum(0), 1 / 48, rtol=1e-3)
+
+
+# ----------------------------------------------------------------------------- plan use
+def test_plan_postprocess_and_apply_golden(ops, golden, dev):
+    from otfuse.fusion import ot_alignment_loss
+    f = golden("f2_feature_pot_b8_d512.npz")
+    X = _t(f["X"], dev).requires_grad_(True)
+    Y = _t(f["Y"], dev).requires_grad_(True)
+    loss, ot_mri, T = ot_alignment_loss(X, Y, eps=1e-2)
+    idx = f["idx"]
+    Tc = T.cpu().numpy()
+    np.testing.assert_allclose(Tc[idx[:, 0], idx[:, 1]], f["Tn_samples"], rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(ot_mri.detach().cpu().numpy(), f["ot_mri_from_pet"], rtol=1e-5,
+                               atol=1e-6)
+    assert abs(float(loss) - float(f["ot_loss"])) < 1e-5
+    loss.backward()
+    # gradient through the HIP plan-apply matches torch's matmul
+    Y2 = _t(f["Y"], dev).requires_grad_(True)
+    from otfuse.fusion import cosine_loss
+    cosine_loss(X.detach(), Y2 @ T.t()).backward()
+    assert torch.allclose(Y.grad, Y2.grad, rtol=1e-4, atol=1e-7)
+
+
+def test_plan_postprocess_nan_and_zero_rows(ops, dev):
+    T = torch.rand(5, 7, dtype=torch.float64, device=dev)
+    T[1, 3] = float("nan")
+    T[2] = 0
+    Tn = ops.plan_postprocess(T).cpu()
+    Tr = T.cpu().float()
+    Tr = torch.where(torch.isnan(Tr), torch.full_like(Tr, 1e-8), Tr)
+    rs = Tr.sum(1, keepdim=True)
+    rs = torch.where(rs == 0, torch.full_like(rs, 1e-8), rs)
+    assert torch.allclose(Tn, Tr / rs, rtol=1e-6, atol=0)
+
+
+def test_smoke_entry_point_runs(dev):
+    import __graft_entry__ as g
+    g.smoke()
