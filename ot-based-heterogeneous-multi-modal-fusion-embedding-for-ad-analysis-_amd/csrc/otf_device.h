@@ -95,6 +95,41 @@ __device__ __forceinline__ void block_sum_multi(T (&x)[R], T* red) {
     for (int r = 0; r < R; ++r) x[r] = red[16 * R + r];
 }
 
+// Block-wide sums of R values per thread through an LDS transpose (R divides 64,
+// blockDim.x a multiple of 64):
+//   1. every thread stores its R partials contiguously: tbuf[t*R + r];
+//   2. thread t takes row r = t % R, slot q = t / R of Q = NT / R slots and sums
+//      tbuf[(q + Q k) * R + r] over k < R — one wave's 64 lanes read 64 consecutive
+//      words per step, conflict-free;
+//   3. lanes with equal t % R finish with log2(64 / R) xor shuffles, one lane per
+//      (wave, row) writes wbuf[w * R + r], and the R row totals are summed over waves.
+// Deterministic; 3 barriers; results broadcast in x.  tbuf: NT * R, wbuf: 17 * R.
+template <typename T, int R>
+__device__ __forceinline__ void block_sum_rows(T (&x)[R], T* tbuf, T* wbuf) {
+    static_assert(R >= 1 && R <= 64 && (64 % R) == 0, "R must divide 64");
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int NT = blockDim.x, nw = NT >> 6, Q = NT / R;
+#pragma unroll
+    for (int r = 0; r < R; ++r) tbuf[t * R + r] = x[r];
+    __syncthreads();
+    const int r = t % R, q = t / R;
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) s += tbuf[(q + Q * k) * R + r];
+#pragma unroll
+    for (int o = R; o < kWave; o <<= 1) s += __shfl_xor(s, o, kWave);
+    if (lane < R) wbuf[wid * R + lane] = s;
+    __syncthreads();
+    if (t < R) {
+        T tot = 0;
+        for (int w = 0; w < nw; ++w) tot += wbuf[w * R + t];
+        wbuf[16 * R + t] = tot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) x[rr] = wbuf[16 * R + rr];
+}
+
 template <typename T> __device__ __forceinline__ T block_sum(T x, T* red) {
     T v[1] = {x};
     block_sum_multi<T, 1>(v, red);

@@ -26,6 +26,8 @@
 // decision from the same buffers at the top of the next launch, so no host sync
 // is needed between iterations.  Column-sum buffers are triple-buffered
 // (read p-1, accumulate p, zero p+1) so a pass never races the zeroing.
+#include <stdlib.h>
+
 #include "otf_device.h"
 
 namespace otf {
@@ -56,6 +58,7 @@ template <typename T> struct SkArgs {
     int check_off;         // POT checks at ii % 10 == 0, OTT after every 10th update
     int err_squared;
     int m_pad;
+    int ablate;            // diagnostic builds only (env OTF_ABLATE); 0 in production
 };
 
 __device__ __forceinline__ void sk_stop(otf_sinkhorn_info* info, int last_good, int niter,
@@ -126,14 +129,17 @@ template <typename T, bool LOG, int G, int R>
 __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
     constexpr int VEC = Vec<T>::N;
     using V = typename Vec<T>::type;
+    __shared__ __attribute__((aligned(16))) T colbuf[512 * G * VEC];  // column partials
+    __shared__ __attribute__((aligned(16))) T tbuf[512 * R];          // row-sum transpose
     __shared__ T red[17 * R + 17];
     __shared__ int s_flag;
     const int tid = threadIdx.x;
     const int NT = blockDim.x;
 
-    if (tid == 0) s_flag = __hip_atomic_load(&p.info->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (s_flag) return;
+    // stop flag: written by an earlier launch (a flag raised by WG0 of THIS launch is
+    // a decision every workgroup re-derives identically), so a uniform plain load.
+    if (__builtin_amdgcn_readfirstlane(*(volatile const int*)&p.info->stop)) return;
+    (void)s_flag;
 
     const bool lead = (blockIdx.x == 0 && tid == 0);
     // exponent units: float works in log2 (v_exp_f32), double in natural log
@@ -176,76 +182,84 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
         }
     }
 
-    // ---- column scaling of iteration it (POT: v; OTT: g) and the column exponent offset
+    // ---- row blocks.  The first block's cost rows are put in flight BEFORE the
+    // column-scaling prologue (its loads, arithmetic and barrier), so the prologue's
+    // latency hides under the stream instead of preceding it.
+    const bool have_prev = p.it >= 0 && !(p.ablate & 1);
+    const int nrb = (p.n + R - 1) / R;
     T vw[G][VEC];  // POT: v_j (row-sum weights); OTT: 1
     T go[G][VEC];  // OTT: g_j in exponent units; POT: 0
-    if (p.it >= 0) {
-        int badv = 0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const V s = *reinterpret_cast<const V*>(p.cs_src + colc[g]);
-            const V bb = *reinterpret_cast<const V*>(p.b + colc[g]);
-            const V gp = *reinterpret_cast<const V*>(p.v_prev + colc[g]);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                T val;
-                if (LOG) val = regn * (unit_log(bb[k]) - unit_log(s[k])) + gp[k];
-                else val = bb[k] / s[k];
-                const bool bad = (s[k] == (T)0) || !finite_val(val);
-                badv |= (cok[g][k] && bad) ? 1 : 0;
-                val = cok[g][k] ? val : (T)0;
-                if (LOG) {
-                    go[g][k] = val * gl;
-                    vw[g][k] = 1;
-                } else {
-                    vw[g][k] = val;
-                    go[g][k] = 0;
-                }
-                if (blockIdx.x == 0 && cok[g][k]) p.v_cur[colc[g] + k] = val;
-            }
-        }
-        badv = __syncthreads_or(badv);
-        if (badv) {  // zero column sum or nan/inf column scaling: revert to it-1, stop
-            if (lead) sk_stop(p.info, p.it - 1, p.it, OTF_SK_NUMERICAL_BREAK, p.it);
-            return;
-        }
-    } else {
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                vw[g][k] = 1;
-                go[g][k] = 0;
-                if (LOG) {  // g_{-1} = column minima of the scaled cost: every term <= 1
-                    const T h = (T)((double)key_val(p.cmin_key[colc[g] + k]) * cinv);
-                    go[g][k] = cok[g][k] ? h * gl : (T)0;
-                    if (blockIdx.x == 0 && cok[g][k]) p.v_cur[colc[g] + k] = h;
-                }
-            }
-    }
-
-    // ---- row blocks: row scaling, then column partials with the new row scaling
     T colacc[G][VEC];
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int k = 0; k < VEC; ++k) colacc[g][k] = 0;
 
-    const int nrb = (p.n + R - 1) / R;
-    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+    for (int rb = blockIdx.x; rb < nrb || rb == (int)blockIdx.x; rb += gridDim.x) {
         const int r0 = rb * R;
         T kv[R][G][VEC];
-        const T* crow = p.C + (int64_t)r0 * p.ldc;
+        if (rb < nrb) {
+            const T* crow = p.C + (int64_t)r0 * p.ldc;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const T* src = (r0 + r < p.n) ? crow : p.C;
+            for (int r = 0; r < R; ++r) {
+                const T* src = (r0 + r < p.n) ? crow : p.C;
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const V c = *reinterpret_cast<const V*>(src + colc[g]);
+                for (int g = 0; g < G; ++g) {
+                    const V c = *reinterpret_cast<const V*>(src + colc[g]);
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
+                    for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
+                }
+                crow += p.ldc;
             }
-            crow += p.ldc;
+        }
+        if (rb == (int)blockIdx.x) {
+            // column scaling of iteration it (POT: v; OTT: g), every workgroup, all columns
+            if (have_prev) {
+                int badv = 0;
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const V sv = *reinterpret_cast<const V*>(p.cs_src + colc[g]);
+                    const V bv = *reinterpret_cast<const V*>(p.b + colc[g]);
+                    V gp;
+                    if (LOG) gp = *reinterpret_cast<const V*>(p.v_prev + colc[g]);
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) {
+                        T val;
+                        if (LOG) val = regn * (unit_log(bv[k]) - unit_log(sv[k])) + gp[k];
+                        else val = bv[k] / sv[k];
+                        const bool bad = (sv[k] == (T)0) || !finite_val(val);
+                        badv |= (cok[g][k] && bad) ? 1 : 0;
+                        val = cok[g][k] ? val : (T)0;
+                        if (LOG) {
+                            go[g][k] = val * gl;
+                            vw[g][k] = 1;
+                        } else {
+                            vw[g][k] = val;
+                            go[g][k] = 0;
+                        }
+                        if (blockIdx.x == 0 && cok[g][k]) p.v_cur[colc[g] + k] = val;
+                    }
+                }
+                badv = __syncthreads_or(badv);
+                if (badv) {  // zero column sum or nan/inf column scaling: revert to it-1, stop
+                    if (lead) sk_stop(p.info, p.it - 1, p.it, OTF_SK_NUMERICAL_BREAK, p.it);
+                    return;
+                }
+            } else {
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) {
+                        vw[g][k] = 1;
+                        go[g][k] = 0;
+                        if (LOG) {  // g_{-1} = column minima of the scaled cost: terms <= 1
+                            const T h = (T)((double)key_val(p.cmin_key[colc[g] + k]) * cinv);
+                            go[g][k] = cok[g][k] ? h * gl : (T)0;
+                            if (blockIdx.x == 0 && cok[g][k]) p.v_cur[colc[g] + k] = h;
+                        }
+                    }
+            }
+            if (rb >= nrb) break;  // more workgroups than row blocks: prologue duty only
         }
         T fo[R];
 #pragma unroll
@@ -262,7 +276,7 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
                 for (int k = 0; k < VEC; ++k) {
                     T z = kv[r][g][k] * ks;
                     if (LOG) z += fo[r] + go[g][k];
-                    kv[r][g][k] = (rok && cok[g][k]) ? fast_exp(z) : (T)0;
+                    kv[r][g][k] = (rok && cok[g][k]) ? ((p.ablate & 8) ? z : fast_exp(z)) : (T)0;
                 }
         }
         T ur[R];
@@ -276,11 +290,12 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
                     for (int k = 0; k < VEC; ++k) s += LOG ? kv[r][g][k] : kv[r][g][k] * vw[g][k];
                 ur[r] = s;
             }
-            block_sum_multi<T, R>(ur, red);
+            if (!(p.ablate & 2)) block_sum_rows<T, R>(ur, tbuf, red);
             T outv[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int row = r0 + r < p.n ? r0 + r : p.n - 1;
+                const bool rok = r0 + r < p.n;
+                const int row = rok ? r0 + r : p.n - 1;
                 const T ar = p.a[row];
                 if (LOG) {
                     ur[r] = ar / ur[r];                                // w_i = a_i / rowsum_i
@@ -289,6 +304,7 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
                     ur[r] = (T)1 / (ur[r] * ((T)1 / ar));              // POT: 1 / (Kp v)
                     outv[r] = ur[r];
                 }
+                if (!rok) ur[r] = 0;  // padding rows: 1/0 = inf would poison 0 * inf
             }
             if (tid < R) {
                 T mine = outv[0];
@@ -318,12 +334,25 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
                 for (int k = 0; k < VEC; ++k) colacc[g][k] += kv[r][g][k] * ur[r];
     }
 
-    // ---- flush column partials (one float atomic per column per workgroup)
+    // ---- flush column partials: one float atomic per column per workgroup, staged
+    // through LDS so every atomic wave-instruction covers 256 contiguous bytes (a
+    // 16-B lane stride runs the memory-side atomics an order of magnitude slower).
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+    for (int g = 0; g < G; ++g) {
+        const int c0 = (tid + NT * g) * VEC;
+        if (c0 < p.m_pad) {
+            V w;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k)
-            if (cok[g][k]) atomicAdd(p.cs_dst + colc[g] + k, colacc[g][k]);
+            for (int k = 0; k < VEC; ++k) w[k] = colacc[g][k];
+            *reinterpret_cast<V*>(colbuf + c0) = w;
+        }
+    }
+    __syncthreads();
+    if (!(p.ablate & 4)) {
+        for (int j = tid; j < p.m; j += NT) atomicAdd(p.cs_dst + j, colbuf[j]);
+    } else if (colbuf[tid] == (T)12345) {
+        p.cs_dst[tid] = 0;
+    }
 
     // ---- zero the column-sum buffer of the next pass (nobody touches it now)
     for (int j = blockIdx.x * NT + tid; j < p.m_pad; j += gridDim.x * NT) p.cs_zero[j] = 0;
@@ -439,20 +468,29 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const T* C, int64_t ldc, i
     const T gl = (T)(unit / reg);
     constexpr int VEC = Vec<T>::N;
     using V = typename Vec<T>::type;
+    using VP = __attribute__((ext_vector_type(VEC))) TP;
     for (int row = blockIdx.x; row < n; row += gridDim.x) {
         const T ui = u[row];
         const T* crow = C + (int64_t)row * ldc;
         TP* prow = P + (int64_t)row * ldp;
         for (int j0 = threadIdx.x * VEC; j0 < m; j0 += blockDim.x * VEC) {
             const V c = *reinterpret_cast<const V*>(crow + j0);
+            VP out;
 #pragma unroll
-            for (int k = 0; k < VEC; ++k)
-                if (j0 + k < m) {
-                    T val;
-                    if (LOG) val = fast_exp(c[k] * ks + (ui + v[j0 + k]) * gl);
-                    else val = ui * fast_exp(c[k] * ks) * v[j0 + k];
-                    prow[j0 + k] = (TP)val;
-                }
+            for (int k = 0; k < VEC; ++k) {
+                const T vj = j0 + k < m ? v[j0 + k] : (T)0;
+                T val;
+                if (LOG) val = fast_exp(c[k] * ks + (ui + vj) * gl);
+                else val = ui * fast_exp(c[k] * ks) * vj;
+                out[k] = (TP)val;
+            }
+            if (j0 + VEC <= m) {
+                *reinterpret_cast<VP*>(prow + j0) = out;  // ldp is a multiple of VEC
+            } else {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k)
+                    if (j0 + k < m) prow[j0 + k] = out[k];
+            }
         }
     }
 }
@@ -468,7 +506,7 @@ constexpr int kPassThreads = 512;
 constexpr int kMaxG = 8;
 
 template <typename T> constexpr int pass_rows(int G) {
-    return sizeof(T) == 4 ? (G == 1 ? 16 : 128 / (G * 4)) : (G == 1 ? 16 : 32 / (G * 2));
+    return sizeof(T) == 4 ? (G == 1 ? 16 : G == 8 ? 2 : 128 / (G * 4)) : (G == 1 ? 16 : 32 / (G * 2));
 }
 
 template <typename T> PassCfg pick_cfg(int m) {
@@ -539,7 +577,7 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
     if (n <= 0 || m <= 0 || !a || !b || !C || !u_out || !v_out || !info || !ws) return OTF_EINVAL;
     if (ldc < m || ldc % VEC != 0 || ((uintptr_t)C % 16) != 0) return OTF_EINVAL;
     if (!(o.reg > 0.0) || o.max_iter < 0 || o.check_every <= 0) return OTF_EINVAL;
-    if (P_out && (ldp < m || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
+    if (P_out && (ldp < m || ldp % VEC != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
     if (n > INT32_MAX || m > (int64_t)kPassThreads * kMaxG * VEC) return OTF_EUNSUPPORTED;
     Workspace w = carve(ws, n, m, sizeof(T), o.max_iter);
     if (ws_bytes < w.bytes) return OTF_EINVAL;
@@ -580,6 +618,7 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
     p.check_off = LOG ? 1 : 0;
     p.err_squared = LOG ? 0 : o.err_squared;
     p.m_pad = m_pad;
+    p.ablate = getenv("OTF_ABLATE") ? atoi(getenv("OTF_ABLATE")) : 0;
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double total_ms = 0.0;

@@ -236,8 +236,9 @@ def test_get_coupling_fot_blockdiag(golden, dev):
     ts = {k: rng.random((12, 12)) for k in (0, 1)}
     Tv, log = get_coupling_fot((xd, yd), ts, eps=5e-3)
     assert Tv.shape == (64, 48) and len(log["cost"]) == 2
+    # OTT: rows exact after the f-update; stop rule = L1 column-marginal error < 1e-3
     np.testing.assert_allclose(Tv.sum(1), 1 / 64, rtol=1e-6)
-    np.testing.assert_allclose(Tv.sum(0), 1 / 48, rtol=1e-3)
+    assert np.abs(Tv.sum(0) - 1 / 48).sum() < 1e-3
 
 
 # ----------------------------------------------------------------------------- plan use

@@ -1,20 +1,29 @@
 #!/bin/bash
-# One GPU-box session: parity tests, bench, rocprofv3 kernel trace.  Each GPU step has
-# its own time limit; a crash / abort / timeout (rc not 0 or 1) ends the session.
+# One GPU-box session: parity tests, bench, rocprofv3 kernel trace (+ optional PMC
+# passes).  Each GPU step has its own time limit; a crash / abort / timeout (rc not
+# 0 or 1) ends the session.  Env: TESTS=0/1 BENCH=0/1 PROFILE=0/1 PMC=0/1
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 stop_if_fatal() { if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "fatal rc=$1 in $2, stopping"; exit "$1"; fi; }
 
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/gpu_tests.log; stop_if_fatal $rc pytest
-
-timeout -k 10 420 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log; stop_if_fatal $rc bench
-
+if [ "${TESTS:-1}" = "1" ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/gpu_tests.log; stop_if_fatal $rc pytest
+fi
+if [ "${BENCH:-1}" = "1" ]; then
+  timeout -k 10 420 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1
+  rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log; stop_if_fatal $rc bench
+fi
 if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --profile-only --steps 10 --warmup 2 > gpurun_out/rocprof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; stop_if_fatal $rc rocprof
+fi
+if [ "${PMC:-0}" = "1" ]; then
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 420 rocprofv3 --pmc $ctr --kernel-trace --stats -d gpurun_out/pmc_$ctr -o run --output-format csv -- python3 bench.py --profile-only --steps 3 --warmup 1 > gpurun_out/pmc_$ctr.log 2>&1
+    rc=$?; echo "pmc $ctr rc=$rc"; stop_if_fatal $rc pmc
+  done
 fi
 exit 0
