@@ -112,25 +112,43 @@ def main():
             dist.destroy_process_group()
         return
 
-    # per-phase split of one extra step (events on the current stream)
-    step(True)
-    torch.cuda.synchronize()
-    cost_ms = ev[0].elapsed_time(ev[1])
-    sk_ms = ev[1].elapsed_time(ev[2])
-
-    # roofline probe: HIP event pair around every fused pass (same stream as the kernel)
+    # per-phase split of extra steps (events on the current stream = the kernels' stream)
+    cost_l, sk_l = [], []
+    for _ in range(5):
+        step(True)
+        torch.cuda.synchronize()
+        cost_l.append(ev[0].elapsed_time(ev[1]))
+        sk_l.append(ev[1].elapsed_time(ev[2]))
+    cost_ms = sorted(cost_l)[2]
+    sk_ms = sorted(sk_l)[2]
     C, cmax = ops.pairwise_cost(X, Y)
-    pass_ms = ops.sinkhorn_profile(a, a, C, eps, iters, cost_scale=cmax, workspace=ws)
-    pass_bytes = N * N * 4
-    achieved = pass_bytes / (pass_ms * 1e-3) / 1e9
+    res = ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, cost_scale=cmax, workspace=ws,
+                       plan_out=P)
+    engine = res.info()["engine_name"]
+
+    # roofline of the dominant kernel.  Algorithmic bytes: one compulsory
+    # read of the N x N fp32 cost per Sinkhorn iteration.  resident engine: ONE launch
+    # does all iterations (+ the plan write) with the cost held in registers, so its
+    # algorithmic rate can exceed the HBM peak — the PMC traffic shows the real bytes.
+    iter_bytes = N * N * 4
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if int(tj.get("n", 0)) == N:
+            if int(tj.get("n", 0)) == N and tj.get("engine", "stream") == engine:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    # streaming engine for reference: HIP event pair around every fused pass
+    pass_ms = ops.sinkhorn_profile(a, a, C, eps, iters, cost_scale=cmax, workspace=ws)
+    if engine == "resident":
+        launch_bytes = iter_bytes * iters
+        achieved = launch_bytes / (sk_ms * 1e-3) / 1e9
+        kernel_name = "sk_resident_kernel"
+    else:
+        launch_bytes = iter_bytes
+        achieved = iter_bytes / (pass_ms * 1e-3) / 1e9
+        kernel_name = "sk_pass_kernel"
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * N * args.steps / elapsed
@@ -153,12 +171,17 @@ def main():
                    "plan": "N x N float32 written per step", "global_batch": N * world,
                    "parallelism": f"replicas x{world} (independent problems)"},
         "sinkhorn_iters_per_sec": iters / (sk_ms * 1e-3),
+        "engine": engine,
         "breakdown_ms": {"cost": cost_ms, "sinkhorn_incl_plan": sk_ms,
-                         "sinkhorn_pass_mean": pass_ms},
-        "roofline": {"bound": "hbm", "kernel": "sk_pass_kernel", "achieved": achieved,
+                         "stream_engine_pass_mean": pass_ms},
+        "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": pass_bytes,
-                     "note": "C (64 MiB) fits the 256 MiB Infinity Cache at N=4096"},
+                     "traffic": traffic, "algorithmic_bytes_per_launch": launch_bytes,
+                     "note": ("resident: all iterations in one launch, cost held in registers; "
+                              "algorithmic bytes = iters x N*N*4" if engine == "resident" else
+                              "one launch per iteration; C (64 MiB) fits the 256 MiB Infinity Cache")},
+        "stream_engine": {"pass_ms": pass_ms, "achieved": iter_bytes / (pass_ms * 1e-3) / 1e9,
+                          "frac": iter_bytes / (pass_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(X_np, Y_np, N, iters, eps, args.cpu_threads)

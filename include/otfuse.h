@@ -64,8 +64,18 @@ enum {
     OTF_SK_RUNNING = 0,
     OTF_SK_CONVERGED = 1,
     OTF_SK_MAX_ITER = 2,
-    OTF_SK_NUMERICAL_BREAK = 3
+    OTF_SK_NUMERICAL_BREAK = 3,
+    OTF_SK_TIMEOUT = 4  /* resident solver: a device-wide barrier did not complete */
 };
+
+/* Solver engines (otf_sinkhorn_opts.engine).
+ * OTF_ENGINE_AUTO: resident when the problem fits the register files of the chip
+ *   (one row block per CU), streaming otherwise.
+ * OTF_ENGINE_STREAM: one launch per iteration, C re-read from HBM every iteration.
+ * OTF_ENGINE_RESIDENT: one persistent launch for the whole solve; every workgroup
+ *   keeps its rows of K = exp(-C/reg) in registers; iterations are separated by a
+ *   device-wide barrier.  POT flavour only.                                      */
+typedef enum { OTF_ENGINE_AUTO = 0, OTF_ENGINE_STREAM = 1, OTF_ENGINE_RESIDENT = 2 } otf_engine;
 
 typedef struct {
     double reg;         /* entropic regularisation (absolute, on the scaled cost)      */
@@ -74,9 +84,9 @@ typedef struct {
     int32_t check_every;/* 10 in POT and OTT (inner_iterations)                        */
     int32_t flavor;     /* otf_flavor                                                  */
     int32_t err_squared;/* 1: compare the SQUARED L2 error (vendored utils.py:88-89)   */
-    int32_t sync_every; /* host polls the device stop flag every N iterations; 0 = never
-                           (all max_iter passes are enqueued; finished passes no-op)   */
-    int32_t reserved;
+    int32_t sync_every; /* streaming engine: host polls the device stop flag every N
+                           iterations; 0 = never (finished passes no-op)             */
+    int32_t engine;     /* otf_engine                                                  */
 } otf_sinkhorn_opts;
 
 /* Written on the device by otf_sinkhorn (read it after the stream completes). */
@@ -87,7 +97,8 @@ typedef struct {
     int32_t status;     /* OTF_SK_*                                                    */
     int32_t n_err;      /* number of entries written to the err log                    */
     int32_t break_iter; /* iteration of the numerical break, or -1                     */
-    int32_t pad[2];
+    int32_t engine;     /* engine that ran (OTF_ENGINE_STREAM / OTF_ENGINE_RESIDENT)     */
+    int32_t pad;
 } otf_sinkhorn_info;
 
 /* Library identification; returns a static string ("otfuse <ver> gfx950"). */

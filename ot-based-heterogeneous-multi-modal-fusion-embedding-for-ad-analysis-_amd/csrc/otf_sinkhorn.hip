@@ -382,7 +382,8 @@ __global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, 
         info->status = OTF_SK_RUNNING;
         info->n_err = 0;
         info->break_iter = -1;
-        info->pad[0] = info->pad[1] = 0;
+        info->engine = OTF_ENGINE_STREAM;
+        info->pad = 0;
     }
 }
 
@@ -495,6 +496,393 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const T* C, int64_t ldc, i
     }
 }
 
+// ============================================================================
+// Resident engine: ONE persistent launch for the whole solve (POT flavour).
+//
+// Workgroup w owns row block w (R rows x all m columns) and keeps K = exp(-C/reg)
+// for it in registers for every iteration, so C crosses HBM once per solve.  Per
+// iteration each workgroup reads the column sums K^T u of the previous iteration,
+// forms v, decides convergence / numerical break exactly like the streaming pass
+// (every workgroup derives the same decision from the same sums), updates u for
+// its rows and adds its column partials K_w^T u_w into a FRESH per-iteration sum
+// buffer with memory-side float atomics; a device-wide counter barrier separates
+// iterations.  Sums are read with device-scope (sc1) loads and each iteration uses
+// a buffer nobody has cached, so no cache level can return a stale sum.  Every
+// spin is bounded by wall-clock time (s_memrealtime, 100 MHz): a barrier that
+// does not complete sets OTF_SK_TIMEOUT instead of hanging.  Co-residency of the
+// grid (<= one workgroup per CU) is checked by the cooperative launch.
+// ============================================================================
+template <typename T> struct SkResArgs {
+    const T* C;
+    int64_t ldc;
+    int n, m, m_pad;
+    const T* a;
+    const T* b;
+    const T* cost_scale;
+    double reg;
+    int max_iter, check_every, err_squared;
+    double stop_thr;
+    T* cs;            // (max_iter + 1) x m_pad column-sum buffers, zeroed before launch
+    int* bad_cnt;     // max_iter + 1 counters, zeroed
+    int* bar;         // barrier counter, zeroed
+    otf_sinkhorn_info* info;
+    double* errlog;
+    T* u_out;
+    T* v_out;
+    void* P;
+    int64_t ldp;
+    int p_f64;
+    unsigned long long timeout_ticks;
+};
+
+// Diagnostic build only (-DOTF_STAMPS, tools/stamps_resident.hip): per-phase wall-clock
+// stamps of the resident loop; compiled out of the library.
+#ifdef OTF_STAMPS
+__device__ unsigned long long g_stamps[256 * 16 * 8];
+#define OTF_STAMP(it, ph)                                                                   \
+    do {                                                                                    \
+        if (threadIdx.x == 0 && (it) < 16 && blockIdx.x < 256)                              \
+            g_stamps[(blockIdx.x * 16 + (it)) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define OTF_STAMP(it, ph) \
+    do {                  \
+    } while (0)
+#endif
+
+template <typename T> __device__ __forceinline__ T load_agent(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Device-wide barrier: every wave drains its own memory operations (the atomics that
+// carry the payload are then performed at memory), one lane per workgroup arrives
+// on the counter and polls it.  Returns false on timeout (flag broadcast via LDS).
+__device__ __forceinline__ bool grid_barrier(int* bar, int target, unsigned long long deadline,
+                                             int* s_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (load_agent(bar) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() > deadline) {
+                ok = 0;
+                break;
+            }
+        }
+        *s_flag = ok;
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+template <typename T, typename TP, int G, int R>
+__global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
+    constexpr int VEC = Vec<T>::N;
+    using V = typename Vec<T>::type;
+    using VP = __attribute__((ext_vector_type(VEC))) TP;
+    __shared__ __attribute__((aligned(16))) T colbuf[512 * G * VEC];
+    __shared__ __attribute__((aligned(16))) T tbuf[512 * R];
+    __shared__ __attribute__((aligned(16))) T vhist[2][512 * G * VEC];  // v of iterations by parity
+    __shared__ T uhist[2][R];                                             // u of this block's rows
+    __shared__ T red[17 * R + 17];
+    __shared__ int s_flag;
+    const int tid = threadIdx.x;
+    const int NT = blockDim.x;
+    const int nwg = gridDim.x;
+    const bool lead = (blockIdx.x == 0 && tid == 0);
+    const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+
+    const double unit = exp_unit<T>();
+    double cinv = 1.0;
+    if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
+    const T ks = (T)(-unit / p.reg * cinv);
+
+    int colc[G];
+    bool cok[G][VEC];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int c0 = (tid + NT * g) * VEC;
+        colc[g] = c0 < p.m ? c0 : 0;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) cok[g][k] = c0 + k < p.m;
+    }
+
+    // ---- this workgroup's rows of K, once
+    const int r0 = blockIdx.x * R;
+    T kv[R][G][VEC];
+    {
+        const T* crow = p.C + (int64_t)r0 * p.ldc;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const T* src = (r0 + r < p.n) ? crow : p.C;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const V c = *reinterpret_cast<const V*>(src + colc[g]);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
+            }
+            crow += p.ldc;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool rok = r0 + r < p.n;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k)
+                    kv[r][g][k] = (rok && cok[g][k]) ? fast_exp(kv[r][g][k] * ks) : (T)0;
+        }
+    }
+    T ia[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = r0 + r < p.n ? r0 + r : p.n - 1;
+        ia[r] = (T)1 / p.a[row];
+    }
+
+    // iteration history in LDS, slot = iteration & 1 (slots start as u0 = 1/n, v0 = 1/m):
+    // iteration it reads v(it-1) from slot (it-1)&1 and writes u(it), v(it) into slot it&1
+    // only after its checks pass, so slot it&1 still holds iteration it-2 when a
+    // numerical break in it-1 has to revert two iterations.
+    const T u0 = (T)1 / (T)p.n, v0 = (T)1 / (T)p.m;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            vhist[0][(tid + NT * g) * VEC + k] = v0;
+            vhist[1][(tid + NT * g) * VEC + k] = v0;
+        }
+    if (tid < R) uhist[0][tid] = uhist[1][tid] = u0;
+    int idxB = -1;
+
+    auto flush = [&](const T (&w)[R], T* dst) {
+        T colacc[G][VEC];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                T s = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) s += kv[r][g][k] * w[r];
+                colacc[g][k] = s;
+            }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int c0 = (tid + NT * g) * VEC;
+            if (c0 < p.m_pad) {
+                V wv;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) wv[k] = colacc[g][k];
+                *reinterpret_cast<V*>(colbuf + c0) = wv;
+            }
+        }
+        __syncthreads();
+        for (int j = tid; j < p.m; j += NT) atomicAdd(dst + j, colbuf[j]);
+    };
+
+    // ---- prologue: K^T u0 into sums[0]
+    {
+        T w[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) w[r] = (r0 + r < p.n) ? u0 : (T)0;
+        flush(w, p.cs);
+    }
+    int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
+    bool done = false;
+    if (!grid_barrier(p.bar, nwg, deadline, &s_flag)) {
+        status = OTF_SK_TIMEOUT;
+        done = true;
+    }
+
+    for (int it = 0; it < p.max_iter && !done; ++it) {
+        OTF_STAMP(it, 0);
+        const T* cs_it = p.cs + (size_t)it * p.m_pad;   // K^T u(it-1)
+        T s[G][VEC], vn[G][VEC];
+        int badv = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                s[g][k] = cok[g][k] ? load_agent(cs_it + colc[g] + k) : (T)1;
+                const T bj = p.b[colc[g] + k];
+                const T val = bj / s[g][k];
+                badv |= (cok[g][k] && ((s[g][k] == (T)0) || !finite_val(val))) ? 1 : 0;
+                vn[g][k] = cok[g][k] ? val : (T)0;
+            }
+        // numerical break in u(it-1) -> revert to it-2
+        if (it >= 1 && load_agent(p.bad_cnt + it - 1) > 0) {
+            last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
+            break;
+        }
+        // marginal error of iteration it-1: v(it-1) * K^T u(it-1) - b
+        if (it >= 1 && ((it - 1) % p.check_every) == 0) {
+            T e = 0;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const T vb = vhist[(it - 1) & 1][(tid + NT * g) * VEC + k];
+                    const T rr = vb * s[g][k] - p.b[colc[g] + k];
+                    e += cok[g][k] ? rr * rr : (T)0;
+                }
+            e = block_sum<T>(e, red);
+            const double err = p.err_squared ? (double)e : sqrt((double)e);
+            if (lead) p.errlog[(it - 1) / p.check_every] = err;
+            n_err = (it - 1) / p.check_every + 1;
+            if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) {
+                last_good = it - 1; niter = it - 1; status = OTF_SK_CONVERGED;
+                break;
+            }
+        }
+        badv = __syncthreads_or(badv);
+        OTF_STAMP(it, 1);
+        if (badv) {  // zero in K^T u or nan/inf in v: revert to it-1
+            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
+            break;
+        }
+        // u(it) for this workgroup's rows
+        T un[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            T acc = 0;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) acc += kv[r][g][k] * vn[g][k];
+            un[r] = acc;
+        }
+        block_sum_rows<T, R>(un, tbuf, red);
+        OTF_STAMP(it, 2);
+        int badu = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool rok = r0 + r < p.n;
+            un[r] = (T)1 / (un[r] * ia[r]);
+            badu |= (rok && !finite_val(un[r])) ? 1 : 0;
+            if (!rok) un[r] = 0;
+        }
+        if (badu && tid == 0) atomicAdd(p.bad_cnt + it, 1);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) vhist[it & 1][(tid + NT * g) * VEC + k] = vn[g][k];
+        if (tid < R) {
+            T mine = un[0];
+#pragma unroll
+            for (int r = 1; r < R; ++r)
+                if (tid == r) mine = un[r];
+            uhist[it & 1][tid] = mine;
+        }
+        flush(un, p.cs + (size_t)(it + 1) * p.m_pad);
+        idxB = it;
+        OTF_STAMP(it, 3);
+#ifdef OTF_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        OTF_STAMP(it, 4);
+#endif
+        if (!grid_barrier(p.bar, (it + 2) * nwg, deadline, &s_flag)) {
+            status = OTF_SK_TIMEOUT;
+            done = true;
+        }
+        OTF_STAMP(it, 5);
+    }
+    if (status == OTF_SK_MAX_ITER && p.max_iter > 0 && idxB == p.max_iter - 1) {
+        const int it = p.max_iter - 1;
+        if (load_agent(p.bad_cnt + it) > 0) {
+            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
+        } else {
+            last_good = it; niter = it;
+            if ((it % p.check_every) == 0) {
+                const T* cs_last = p.cs + (size_t)p.max_iter * p.m_pad;
+                T e = 0;
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) {
+                        const T sk = cok[g][k] ? load_agent(cs_last + colc[g] + k) : (T)0;
+                        const T vb = vhist[it & 1][(tid + NT * g) * VEC + k];
+                        const T rr = vb * sk - p.b[colc[g] + k];
+                        e += cok[g][k] ? rr * rr : (T)0;
+                    }
+                e = block_sum<T>(e, red);
+                const double err = p.err_squared ? (double)e : sqrt((double)e);
+                if (lead) p.errlog[it / p.check_every] = err;
+                n_err = it / p.check_every + 1;
+                if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) status = OTF_SK_CONVERGED;
+            }
+        }
+    }
+
+    // ---- outputs from registers: (u, v) of last_good, and the plan rows
+    (void)idxB;
+    __syncthreads();
+    const int slot = last_good & 1;
+    T uo[R], vo[G][VEC];
+#pragma unroll
+    for (int r = 0; r < R; ++r) uo[r] = uhist[slot][r];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) vo[g][k] = vhist[slot][(tid + NT * g) * VEC + k];
+    if (last_good < 0) {  // initial scalings
+#pragma unroll
+        for (int r = 0; r < R; ++r) uo[r] = u0;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) vo[g][k] = v0;
+    }
+    if (tid < R && r0 + tid < p.n) {
+        T mine = uo[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r)
+            if (tid == r) mine = uo[r];
+        p.u_out[r0 + tid] = mine;
+    }
+    if (blockIdx.x == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k)
+                if (cok[g][k]) p.v_out[colc[g] + k] = vo[g][k];
+    }
+    if (p.P) {
+        TP* P = (TP*)p.P;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r0 + r >= p.n) break;
+            TP* prow = P + (int64_t)(r0 + r) * p.ldp;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int c0 = (tid + NT * g) * VEC;
+                if (c0 >= p.m) continue;
+                VP o;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) o[k] = (TP)(uo[r] * kv[r][g][k] * vo[g][k]);
+                if (c0 + VEC <= p.m) {
+                    *reinterpret_cast<VP*>(prow + c0) = o;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k)
+                        if (c0 + k < p.m) prow[c0 + k] = o[k];
+                }
+            }
+        }
+    }
+    if (lead) {
+        p.info->last_good = last_good;
+        p.info->niter = niter;
+        p.info->status = status;
+        p.info->break_iter = brk;
+        p.info->n_err = n_err;
+        p.info->engine = OTF_ENGINE_RESIDENT;
+        p.info->stop = 1;
+    }
+}
+
 struct PassCfg {
     int G, R, NT;
 };
@@ -543,6 +931,8 @@ struct Workspace {
     int* bad;
     int* cmin_key;
     double* errlog;
+    void* res;        // resident engine: sums (max_iter+1) x m_pad | bad_cnt | barrier
+    size_t res_bytes;
     size_t bytes;
     int64_t m_pad;
 };
@@ -564,8 +954,66 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter) {
     w.cmin_key = (int*)take(sizeof(int) * (size_t)w.m_pad);
     w.bad = (int*)take(sizeof(int) * (size_t)(max_iter + 2));
     w.errlog = (double*)take(sizeof(double) * (size_t)(max_iter + 2));
+    w.res_bytes = align_up((size_t)(max_iter + 1) * w.m_pad * esz, 256) +
+                  align_up(sizeof(int) * (size_t)(max_iter + 1), 256) + 256;
+    w.res = take(w.res_bytes);
     w.bytes = off;
     return w;
+}
+
+template <typename T, typename TP, int G, int R>
+hipError_t launch_resident_g(int grid, int nt, SkResArgs<T>& p, hipStream_t s) {
+    void* args[] = {&p};
+    return hipLaunchCooperativeKernel((const void*)sk_resident_kernel<T, TP, G, R>, dim3(grid),
+                                      dim3(nt), args, 0, s);
+}
+
+template <typename T, typename TP>
+hipError_t launch_resident(const PassCfg& c, int grid, SkResArgs<T>& p, hipStream_t s) {
+    switch (c.G) {
+        case 1: return launch_resident_g<T, TP, 1, pass_rows<T>(1)>(grid, c.NT, p, s);
+        case 2: return launch_resident_g<T, TP, 2, pass_rows<T>(2)>(grid, c.NT, p, s);
+        case 4: return launch_resident_g<T, TP, 4, pass_rows<T>(4)>(grid, c.NT, p, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// Resident solve.  Returns hipSuccess, or the launch error (the caller then falls
+// back to the streaming engine — nothing has been enqueued in that case).
+template <typename T>
+hipError_t run_resident(const PassCfg& cfg, int grid, const T* C, int64_t ldc, int n, int m,
+                        const T* cost_scale, const otf_sinkhorn_opts& o, Workspace& w, T* u_out,
+                        T* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
+                        double* errlog, hipStream_t s) {
+    SkResArgs<T> p{};
+    p.C = C;
+    p.ldc = ldc;
+    p.n = n;
+    p.m = m;
+    p.m_pad = (int)w.m_pad;
+    p.a = (const T*)w.a_pad;
+    p.b = (const T*)w.b_pad;
+    p.cost_scale = cost_scale;
+    p.reg = o.reg;
+    p.max_iter = o.max_iter;
+    p.check_every = o.check_every;
+    p.err_squared = o.err_squared;
+    p.stop_thr = o.stop_thr;
+    p.cs = (T*)w.res;
+    p.bad_cnt = (int*)((char*)w.res + align_up((size_t)(o.max_iter + 1) * w.m_pad * sizeof(T), 256));
+    p.bar = (int*)((char*)p.bad_cnt + align_up(sizeof(int) * (size_t)(o.max_iter + 1), 256));
+    p.info = info;
+    p.errlog = errlog;
+    p.u_out = u_out;
+    p.v_out = v_out;
+    p.P = P_out;
+    p.ldp = ldp;
+    p.p_f64 = P_dtype == OTF_F64;
+    p.timeout_ticks = 500000000ull;  // 5 s at the 100 MHz s_memrealtime clock
+    hipError_t e = hipMemsetAsync(w.res, 0, w.res_bytes, s);
+    if (e != hipSuccess) return e;
+    if (P_out && P_dtype == OTF_F64) return launch_resident<T, double>(cfg, grid, p, s);
+    return launch_resident<T, float>(cfg, grid, p, s);
 }
 
 template <typename T, bool LOG>
@@ -594,6 +1042,21 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
     sk_init_kernel<T><<<64, 256, 0, s>>>(a, b, (int)n, (int)m, m_pad, (T*)w.a_pad, (T*)w.b_pad, cs,
                                          u2, v2, w.bad, o.max_iter + 2, w.cmin_key, info);
     OTF_HIP(hipGetLastError());
+
+    // resident engine: the whole solve in one persistent launch when every row block
+    // gets its own CU (POT flavour, no per-pass profiling requested)
+    const bool fits = nrb <= device_cu_count() && cfg.G <= 4;
+    const bool want_res = !LOG && !avg_pass_ms && fits && o.max_iter >= 1 &&
+                          (o.engine == OTF_ENGINE_RESIDENT || o.engine == OTF_ENGINE_AUTO);
+    if (o.engine == OTF_ENGINE_RESIDENT && (LOG || !fits)) return OTF_EUNSUPPORTED;
+    if (want_res) {
+        const hipError_t e = run_resident<T>(cfg, nrb, C, ldc, (int)n, (int)m, cost_scale, o, w,
+                                             u_out, v_out, P_out, ldp, P_dtype, info, errlog, s);
+        if (e == hipSuccess) return OTF_OK;
+        (void)hipGetLastError();
+        if (o.engine == OTF_ENGINE_RESIDENT) return check_hip(e);
+        // co-residency refused (e.g. a smaller device): fall back to streaming
+    }
     if (LOG) {
         dim3 g((unsigned)((m + 255) / 256), (unsigned)(n < 64 ? n : 64));
         sk_colmin_kernel<T><<<g, 256, 0, s>>>(C, ldc, (int)n, (int)m, w.cmin_key);

@@ -25,18 +25,22 @@ OTF_OK, OTF_EINVAL, OTF_EUNSUPPORTED, OTF_EHIP = 0, 1, 2, -1
 OTF_F32, OTF_F64 = 0, 1
 OTF_SQEUCLIDEAN, OTF_EUCLIDEAN = 0, 1
 OTF_FLAVOR_POT, OTF_FLAVOR_OTT = 0, 1
-SK_RUNNING, SK_CONVERGED, SK_MAX_ITER, SK_NUMERICAL_BREAK = 0, 1, 2, 3
-STATUS_NAMES = {0: "running", 1: "converged", 2: "max_iter", 3: "numerical_break"}
+SK_RUNNING, SK_CONVERGED, SK_MAX_ITER, SK_NUMERICAL_BREAK, SK_TIMEOUT = 0, 1, 2, 3, 4
+STATUS_NAMES = {0: "running", 1: "converged", 2: "max_iter", 3: "numerical_break",
+                4: "timeout"}
+ENGINE_AUTO, ENGINE_STREAM, ENGINE_RESIDENT = 0, 1, 2
+ENGINES = {"auto": ENGINE_AUTO, "stream": ENGINE_STREAM, "resident": ENGINE_RESIDENT}
+ENGINE_NAMES = {v: k for k, v in ENGINES.items()}
 
 
 class SinkhornOpts(ctypes.Structure):
     _fields_ = [("reg", ctypes.c_double), ("stop_thr", ctypes.c_double),
                 ("max_iter", ctypes.c_int32), ("check_every", ctypes.c_int32),
                 ("flavor", ctypes.c_int32), ("err_squared", ctypes.c_int32),
-                ("sync_every", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("sync_every", ctypes.c_int32), ("engine", ctypes.c_int32)]
 
 
-INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "pad0", "pad1")
+INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "engine", "pad")
 INFO_INT32S = len(INFO_FIELDS)  # otf_sinkhorn_info is 8 x int32
 
 _vp = ctypes.c_void_p

@@ -135,6 +135,10 @@ class SinkhornResult:
             vals = self.info_dev.cpu().tolist()
             d = dict(zip(L.INFO_FIELDS, vals))
             d["status_name"] = L.STATUS_NAMES.get(d["status"], "?")
+            d["engine_name"] = L.ENGINE_NAMES.get(d["engine"], "?")
+            if d["status"] == L.SK_TIMEOUT:
+                raise L.OtfError("resident Sinkhorn: device-wide barrier timed out "
+                                 "(grid not co-resident?); results are invalid")
             d["err"] = self.errlog_dev[: max(d["n_err"], 0)].cpu().tolist()
             self._info = d
         return self._info
@@ -149,7 +153,7 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
              stop_thr: float = 1e-9, flavor: str = "pot", cost_scale: torch.Tensor | None = None,
              check_every: int = 10, err_squared: bool = False, sync_every: int = 0,
              want_plan: bool = True, plan_dtype=None, workspace: torch.Tensor | None = None,
-             plan_out: torch.Tensor | None = None) -> SinkhornResult:
+             plan_out: torch.Tensor | None = None, engine: str = "auto") -> SinkhornResult:
     """Entropic OT on the device.  ``flavor="pot"`` is POT's sinkhorn_knopp (u, v scalings,
     revert-and-break), ``flavor="ott"`` OTT's lse-mode solver (potentials f, g).
 
@@ -184,7 +188,8 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
     opts = L.SinkhornOpts(reg=float(reg), stop_thr=float(stop_thr), max_iter=int(max_iter),
                           check_every=int(check_every),
                           flavor=L.OTF_FLAVOR_OTT if flavor == "ott" else L.OTF_FLAVOR_POT,
-                          err_squared=int(err_squared), sync_every=int(sync_every), reserved=0)
+                          err_squared=int(err_squared), sync_every=int(sync_every),
+                          engine=L.ENGINES[engine])
     L.check(L.lib().otf_sinkhorn(
         a.data_ptr(), b.data_ptr(), C.data_ptr(), n, m, C.stride(0), _DT[dt], L.ptr(cost_scale),
         ctypes.byref(opts), u.data_ptr(), v.data_ptr(), L.ptr(P), P.stride(0) if P is not None else 0,
@@ -210,7 +215,7 @@ def sinkhorn_profile(a, b, C, reg, iters, cost_scale=None, flavor="pot", workspa
         workspace = sinkhorn_workspace(n, m, dt, iters, C.device)
     opts = L.SinkhornOpts(reg=float(reg), stop_thr=-1.0, max_iter=int(iters), check_every=10,
                           flavor=L.OTF_FLAVOR_OTT if flavor == "ott" else L.OTF_FLAVOR_POT,
-                          err_squared=0, sync_every=0, reserved=0)
+                          err_squared=0, sync_every=0, engine=L.ENGINE_STREAM)
     avg = ctypes.c_float(0.0)
     L.check(L.lib().otf_sinkhorn_profile(
         a.data_ptr(), b.data_ptr(), C.data_ptr(), n, m, C.stride(0), _DT[dt], L.ptr(cost_scale),

@@ -21,7 +21,8 @@ def test_version_and_workspace_queries_are_host_only():
     lib = L.lib()
     assert lib.otf_version().decode().startswith("otfuse")
     ws = lib.otf_sinkhorn_workspace_size(4096, 4096, L.OTF_F32, 100)
-    assert 4 * 4096 * 9 < ws < 4 * 4096 * 32
+    # streaming buffers (~9 vectors) + the resident engine's per-iteration sums (101 x N)
+    assert 4 * 4096 * (9 + 101) < ws < 4 * 4096 * (32 + 101)
     assert lib.otf_sinkhorn_workspace_size(8, 512, L.OTF_F64, 2000) > 8 * 512 * 7
     assert lib.otf_feature_cost_workspace_size(8, 8, 512, 512) >= 8 * (8 * 512)
 
@@ -43,7 +44,7 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     from otfuse import _lib as L
     lib = L.lib()
     opts = L.SinkhornOpts(reg=0.1, stop_thr=0.0, max_iter=10, check_every=10, flavor=0,
-                          err_squared=0, sync_every=0, reserved=0)
+                          err_squared=0, sync_every=0, engine=0)
     rc = lib.otf_sinkhorn(None, None, None, 0, 0, 0, L.OTF_F32, None, ctypes.byref(opts), None,
                           None, None, 0, 0, None, None, None, 0, None)
     assert rc == L.OTF_EINVAL
