@@ -115,6 +115,17 @@ int otf_cost_pairwise(const float* X, int64_t ldx, const float* Y, int64_t ldy, 
                       int64_t m, int64_t d, int32_t metric, int32_t zero_diag, float* C,
                       int64_t ldc, float* cmax, otf_stream_t stream);
 
+/* Same contract as otf_cost_pairwise, fp32-accurate at the fp16 MFMA rate: each row
+ * is scaled by a power of two and split into hi + lo fp16 halves (22 significant
+ * bits); X Y^T = hi.hi + hi.lo + lo.hi on v_mfma_f32_32x32x16_f16 with fp32
+ * accumulation.  Workspace: otf_cost_split16_workspace_size() bytes (the hi/lo
+ * images, scales and squared norms).                                            */
+size_t otf_cost_split16_workspace_size(int64_t n, int64_t m, int64_t d);
+int otf_cost_pairwise_split16(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
+                              int64_t m, int64_t d, int32_t metric, int32_t zero_diag, float* C,
+                              int64_t ldc, float* cmax, void* workspace, size_t ws_bytes,
+                              otf_stream_t stream);
+
 /* Divides C (n x m, ldc) by the device scalar *s (in place).  float32/64. */
 int otf_scale_inplace(void* C, int64_t n, int64_t m, int64_t ldc, int32_t dtype, const void* s,
                       otf_stream_t stream);

@@ -50,6 +50,9 @@ _SIGS = {
     "otf_version": (ctypes.c_char_p, []),
     "otf_cost_pairwise": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _vp,
                                          _i64, _vp, _vp]),
+    "otf_cost_split16_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64]),
+    "otf_cost_pairwise_split16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i32,
+                                                 _i32, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
     "otf_scale_inplace": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i32, _vp, _vp]),
     "otf_feature_cost_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i64]),
     "otf_feature_cost": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64,

@@ -44,11 +44,14 @@ def _alloc_rowmajor(n: int, m: int, dtype, device, vec: int) -> torch.Tensor:
 
 # --------------------------------------------------------------------------- cost
 def pairwise_cost(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = "sqeuclidean",
-                  zero_diag: bool | None = None, want_max: bool = True):
+                  zero_diag: bool | None = None, want_max: bool = True, algo: str = "split16",
+                  workspace: torch.Tensor | None = None):
     """``ot.dist``-style pairwise cost on MFMA.  Returns ``(C float32 (n, m), cmax (1,))``.
 
     ``zero_diag`` defaults to POT's ``X is Y`` rule (MRI_PET_OT_nojax.py:70-71 passes the
     same array twice).  ``cmax`` is a device scalar with max(C) (None if not wanted).
+    ``algo``: "split16" (hi/lo fp16 MFMA, fp32-accurate, default) or "f32"
+    (v_mfma_f32_32x32x2_f32).
     """
     _dev(X, "X")
     same = Y is None or Y is X
@@ -65,10 +68,22 @@ def pairwise_cost(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = 
     m = Y.shape[0]
     C = _alloc_rowmajor(n, m, torch.float32, X.device, 4)
     cmax = torch.empty(1, dtype=torch.float32, device=X.device) if want_max else None
-    L.check(L.lib().otf_cost_pairwise(
-        X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, m, d,
-        L.OTF_EUCLIDEAN if metric == "euclidean" else L.OTF_SQEUCLIDEAN, int(zero_diag),
-        C.data_ptr(), C.stride(0), L.ptr(cmax), L.stream_handle(X.device)), "otf_cost_pairwise")
+    met = L.OTF_EUCLIDEAN if metric == "euclidean" else L.OTF_SQEUCLIDEAN
+    lib = L.lib()
+    if algo == "split16":
+        wsb = lib.otf_cost_split16_workspace_size(n, m, d)
+        if workspace is None or workspace.numel() < wsb:
+            workspace = torch.empty(wsb, dtype=torch.uint8, device=X.device)
+        L.check(lib.otf_cost_pairwise_split16(
+            X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, m, d, met, int(zero_diag),
+            C.data_ptr(), C.stride(0), L.ptr(cmax), workspace.data_ptr(), workspace.numel(),
+            L.stream_handle(X.device)), "otf_cost_pairwise_split16")
+    elif algo == "f32":
+        L.check(lib.otf_cost_pairwise(
+            X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, m, d, met, int(zero_diag),
+            C.data_ptr(), C.stride(0), L.ptr(cmax), L.stream_handle(X.device)), "otf_cost_pairwise")
+    else:
+        raise ValueError(f"algo {algo!r}")
     return C, cmax
 
 

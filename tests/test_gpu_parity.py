@@ -29,15 +29,30 @@ def _t(x, dev, dt=None):
 
 
 # ----------------------------------------------------------------------------- cost
-@pytest.mark.parametrize("n,m,d", [(256, 256, 64), (130, 77, 40), (4096, 4096, 512), (1, 5, 3)])
-def test_pairwise_cost_vs_oracle(ops, orc, dev, n, m, d):
+@pytest.mark.parametrize("algo", ["split16", "f32"])
+@pytest.mark.parametrize("n,m,d", [(256, 256, 64), (130, 77, 40), (4096, 4096, 512), (1, 5, 3),
+                                   (300, 129, 1000)])
+def test_pairwise_cost_vs_oracle(ops, orc, dev, n, m, d, algo):
     from otfuse.synthetic import paired_embeddings
     X, _, _ = paired_embeddings(n, d, seed=n)
     _, Y, _ = paired_embeddings(m, d, seed=m + 1)
-    C, cmax = ops.pairwise_cost(_t(X, dev), _t(Y, dev))
+    C, cmax = ops.pairwise_cost(_t(X, dev), _t(Y, dev), algo=algo)
     Cr, mr = orc.pairwise_cost(X, Y)
     assert nrel(C.cpu().numpy(), Cr) < 2e-6
     assert float(cmax) == pytest.approx(mr, rel=1e-5)
+
+
+def test_split16_wide_dynamic_range(ops, orc, dev):
+    """Rows with very different magnitudes and tiny entries (per-row power-of-two scale)."""
+    rng = np.random.default_rng(17)
+    X = (rng.standard_normal((200, 96)) * np.logspace(-3, 3, 200)[:, None]).astype(np.float32)
+    Y = (rng.standard_normal((150, 96)) * np.logspace(2, -2, 150)[:, None]).astype(np.float32)
+    X[5, :10] = 1e-7
+    C, _ = ops.pairwise_cost(_t(X, dev), _t(Y, dev), algo="split16")
+    Cr, _ = orc.pairwise_cost(X, Y)
+    # per-element error relative to the entry's own scale |x|^2 + |y|^2
+    scale = (X.astype(np.float64) ** 2).sum(1)[:, None] + (Y.astype(np.float64) ** 2).sum(1)[None]
+    assert (np.abs(C.cpu().numpy() - Cr) / scale).max() < 1e-6
 
 
 def test_pairwise_cost_euclidean_same_input_zero_diag(ops, orc, dev):
