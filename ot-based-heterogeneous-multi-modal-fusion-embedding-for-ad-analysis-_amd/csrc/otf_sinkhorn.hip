@@ -512,6 +512,13 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const T* C, int64_t ldc, i
 // does not complete sets OTF_SK_TIMEOUT instead of hanging.  Co-residency of the
 // grid (<= one workgroup per CU) is checked by the cooperative launch.
 // ============================================================================
+struct SkSync {
+    int* reg;   // [8 * 64]  workgroups per XCD (registration, before the first barrier)
+    int* xcnt;  // [8 * 64]  arrivals per XCD
+    int* top;   // [64]      XCD arrivals
+    int* gen;   // [8 * 64]  published epoch per XCD
+};
+
 template <typename T> struct SkResArgs {
     const T* C;
     int64_t ldc;
@@ -522,7 +529,9 @@ template <typename T> struct SkResArgs {
     double reg;
     int max_iter, check_every, err_squared;
     double stop_thr;
-    T* cs;            // (max_iter + 1) x m_pad column-sum buffers, zeroed before launch
+    T* cs;            // (max_iter + 1) x nrep x m_pad column-sum buffers, zeroed before launch
+    SkSync sync;      // hierarchical barrier words, zeroed before launch
+    int nrep;         // replicas per iteration (= the kernel's NREP)
     int* bad_cnt;     // max_iter + 1 counters, zeroed
     int* bar;         // barrier counter, zeroed
     otf_sinkhorn_info* info;
@@ -550,8 +559,33 @@ __device__ unsigned long long g_stamps[256 * 16 * 8];
     } while (0)
 #endif
 
+// XCD this wave runs on (0..7): selects the column-sum replica so that the ~32
+// workgroups of one XCD share a replica (32 adders per address instead of 256, and
+// the replica readers of one XCD hit the same L2 lines).  Only speed depends on it.
+__device__ __forceinline__ int xcc_id() {
+    int v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+    return v;
+}
+
 template <typename T> __device__ __forceinline__ T load_agent(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Column sums are handed off inside the launch: producers add with agent-scope
+// atomics (performed past L2, the line is dropped from the adder's L2), every adding
+// wave drains them (s_waitcnt vmcnt(0)) before its workgroup arrives on the barrier,
+// and EVERY consumer load of the sums is a 16-B sc1 buffer load to registers (bypasses
+// this CU's L1, which is never refreshed by other CUs' stores) -- the no-acquire form
+// of the hand-off (MI355X microarch guide, inter-workgroup visibility, valid forms).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sums_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ typename Vec<T>::type load_sum_vec(__amdgpu_buffer_rsrc_t rs,
+                                                              uint32_t byte_off) {
+    const auto raw = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16 /* sc1 */);
+    return __builtin_bit_cast(typename Vec<T>::type, raw);
 }
 
 // Device-wide barrier: every wave drains its own memory operations (the atomics that
@@ -577,7 +611,46 @@ __device__ __forceinline__ bool grid_barrier(int* bar, int target, unsigned long
     return *s_flag != 0;
 }
 
-template <typename T, typename TP, int G, int R>
+// XCD-hierarchical grid barrier for epoch e >= 1 (all counters zeroed per call):
+// each workgroup arrives on its XCD's counter (~32 adders instead of 256 on one
+// word); the last arriver of an XCD (told by the value its add returned) arrives
+// on the top counter; the last of those publishes e to every XCD's generation
+// word, which only that XCD's workgroups poll.  Placement affects speed only: the
+// per-XCD populations are counted in the launch (sync.reg), not assumed.
+__device__ __forceinline__ bool xcd_barrier(const SkSync& sy, int xcd, int nx, int nact,
+                                            unsigned act_mask, int e,
+                                            unsigned long long deadline, int* s_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        const int old = __hip_atomic_fetch_add(sy.xcnt + xcd * 64, 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        if (old == e * nx - 1) {
+            const int o2 = __hip_atomic_fetch_add(sy.top, 1, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            if (o2 == e * nact - 1) {
+                for (int x = 0; x < 8; ++x)
+                    if (act_mask & (1u << x))
+                        __hip_atomic_store(sy.gen + x * 64, e, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        while (__hip_atomic_load(sy.gen + xcd * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() > deadline) {
+                ok = 0;
+                break;
+            }
+        }
+        *s_flag = ok;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+template <typename T, typename TP, int G, int R, int NREP>
 __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     constexpr int VEC = Vec<T>::N;
     using V = typename Vec<T>::type;
@@ -588,6 +661,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     __shared__ T uhist[2][R];                                             // u of this block's rows
     __shared__ T red[17 * R + 17];
     __shared__ int s_flag;
+    __shared__ int s_pop[3];
     const int tid = threadIdx.x;
     const int NT = blockDim.x;
     const int nwg = gridDim.x;
@@ -656,6 +730,41 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
         }
     if (tid < R) uhist[0][tid] = uhist[1][tid] = u0;
     int idxB = -1;
+    const size_t it_stride = (size_t)NREP * p.m_pad;
+    const int xcd = xcc_id();
+    const int my_rep = xcd % NREP;
+    // K^T u(it-1) for this thread's columns: the sum of one buffer's replicas.  Whole
+    // vectors are loaded unmasked (every buffer is m_pad wide and zero past m) so all
+    // G x NREP loads are in flight together; masks are applied afterwards.
+    const __amdgpu_buffer_rsrc_t rs = sums_rsrc(p.cs);
+    auto load_sums = [&](const T* base, T (&out)[G][VEC], T fill) {
+        const uint32_t boff = (uint32_t)((base - p.cs) * sizeof(T));
+        V acc[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] = load_sum_vec<T>(rs, boff + colc[g] * (uint32_t)sizeof(T));
+#pragma unroll
+        for (int q = 1; q < NREP; ++q) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const V t = load_sum_vec<T>(
+                    rs, boff + (uint32_t)((q * p.m_pad + colc[g]) * sizeof(T)));
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) acc[g][k] += t[k];
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) out[g][k] = cok[g][k] ? acc[g][k] : fill;
+    };
+    // target column marginal, constant over the solve (b_pad is zero past m)
+    T bcol[G][VEC];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const V t = *reinterpret_cast<const V*>(p.b + colc[g]);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) bcol[g][k] = t[k];
+    }
 
     auto flush = [&](const T (&w)[R], T* dst) {
         T colacc[G][VEC];
@@ -679,6 +788,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
             }
         }
         __syncthreads();
+        dst += (size_t)my_rep * p.m_pad;
         for (int j = tid; j < p.m; j += NT) atomicAdd(dst + j, colbuf[j]);
     };
 
@@ -691,22 +801,42 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     }
     int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
     bool done = false;
+    // register on this XCD's population, then the one flat barrier of the launch
+    if (tid == 0)
+        __hip_atomic_fetch_add(p.sync.reg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!grid_barrier(p.bar, nwg, deadline, &s_flag)) {
         status = OTF_SK_TIMEOUT;
         done = true;
     }
+    if (tid == 0) {
+        int nact = 0;
+        unsigned mask = 0;
+        for (int x = 0; x < 8; ++x) {
+            const int c = __hip_atomic_load(p.sync.reg + x * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c > 0) {
+                ++nact;
+                mask |= 1u << x;
+            }
+        }
+        s_pop[0] = __hip_atomic_load(p.sync.reg + xcd * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_pop[1] = nact;
+        s_pop[2] = (int)mask;
+    }
+    __syncthreads();
+    const int nx = s_pop[0], nact = s_pop[1];
+    const unsigned act_mask = (unsigned)s_pop[2];
 
     for (int it = 0; it < p.max_iter && !done; ++it) {
         OTF_STAMP(it, 0);
-        const T* cs_it = p.cs + (size_t)it * p.m_pad;   // K^T u(it-1)
+        const T* cs_it = p.cs + (size_t)it * it_stride;   // K^T u(it-1)
         T s[G][VEC], vn[G][VEC];
         int badv = 0;
+        load_sums(cs_it, s, (T)1);
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
-                s[g][k] = cok[g][k] ? load_agent(cs_it + colc[g] + k) : (T)1;
-                const T bj = p.b[colc[g] + k];
+                const T bj = bcol[g][k];
                 const T val = bj / s[g][k];
                 badv |= (cok[g][k] && ((s[g][k] == (T)0) || !finite_val(val))) ? 1 : 0;
                 vn[g][k] = cok[g][k] ? val : (T)0;
@@ -724,7 +854,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
                     const T vb = vhist[(it - 1) & 1][(tid + NT * g) * VEC + k];
-                    const T rr = vb * s[g][k] - p.b[colc[g] + k];
+                    const T rr = vb * s[g][k] - bcol[g][k];
                     e += cok[g][k] ? rr * rr : (T)0;
                 }
             e = block_sum<T>(e, red);
@@ -775,7 +905,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
                 if (tid == r) mine = un[r];
             uhist[it & 1][tid] = mine;
         }
-        flush(un, p.cs + (size_t)(it + 1) * p.m_pad);
+        flush(un, p.cs + (size_t)(it + 1) * it_stride);
         idxB = it;
         OTF_STAMP(it, 3);
 #ifdef OTF_STAMPS
@@ -783,7 +913,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
         __syncthreads();
         OTF_STAMP(it, 4);
 #endif
-        if (!grid_barrier(p.bar, (it + 2) * nwg, deadline, &s_flag)) {
+        if (!xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 1, deadline, &s_flag)) {
             status = OTF_SK_TIMEOUT;
             done = true;
         }
@@ -796,15 +926,16 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
         } else {
             last_good = it; niter = it;
             if ((it % p.check_every) == 0) {
-                const T* cs_last = p.cs + (size_t)p.max_iter * p.m_pad;
-                T e = 0;
+                const T* cs_last = p.cs + (size_t)p.max_iter * it_stride;
+                T e = 0, sl[G][VEC];
+                load_sums(cs_last, sl, (T)0);
 #pragma unroll
                 for (int g = 0; g < G; ++g)
 #pragma unroll
                     for (int k = 0; k < VEC; ++k) {
-                        const T sk = cok[g][k] ? load_agent(cs_last + colc[g] + k) : (T)0;
+                        const T sk = sl[g][k];
                         const T vb = vhist[it & 1][(tid + NT * g) * VEC + k];
-                        const T rr = vb * sk - p.b[colc[g] + k];
+                        const T rr = vb * sk - bcol[g][k];
                         e += cok[g][k] ? rr * rr : (T)0;
                     }
                 e = block_sum<T>(e, red);
@@ -908,6 +1039,13 @@ template <typename T> PassCfg pick_cfg(int m) {
     return {G, pass_rows<T>(G), nt};
 }
 
+// Row blocks of the pass/resident kernels for an n x m problem (host-side, no device).
+template <typename T> int64_t row_blocks(int64_t n, int64_t m) {
+    constexpr int64_t mmax = (int64_t)kPassThreads * kMaxG * Vec<T>::N;
+    const PassCfg c = pick_cfg<T>((int)(m < 1 ? 1 : m > mmax ? mmax : m));
+    return (n + c.R - 1) / c.R;
+}
+
 template <typename T, bool LOG>
 hipError_t launch_pass(const PassCfg& c, int grid, const SkArgs<T>& p, hipStream_t s) {
     switch (c.G) {
@@ -933,11 +1071,23 @@ struct Workspace {
     double* errlog;
     void* res;        // resident engine: sums (max_iter+1) x m_pad | bad_cnt | barrier
     size_t res_bytes;
+    int nrep;
     size_t bytes;
     int64_t m_pad;
 };
 
-Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter) {
+// hierarchical barrier words: reg[8], xcnt[8], top, gen[8], each on a 256-B line
+constexpr size_t kSyncBytes = 25 * 64 * sizeof(int);
+
+// Column-sum replicas of the resident engine (grids of >= 128 row blocks; workgroups
+// add into replica xcc_id % NREP, readers load all NREP replicas at once).  A
+// function of the shape only, so the workspace size needs no device.
+#ifndef OTF_RES_NREP
+#define OTF_RES_NREP 4
+#endif
+int res_replicas(int64_t nrb) { return nrb >= 128 ? OTF_RES_NREP : 1; }
+
+Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int64_t nrb) {
     Workspace w{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -954,8 +1104,9 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter) {
     w.cmin_key = (int*)take(sizeof(int) * (size_t)w.m_pad);
     w.bad = (int*)take(sizeof(int) * (size_t)(max_iter + 2));
     w.errlog = (double*)take(sizeof(double) * (size_t)(max_iter + 2));
-    w.res_bytes = align_up((size_t)(max_iter + 1) * w.m_pad * esz, 256) +
-                  align_up(sizeof(int) * (size_t)(max_iter + 1), 256) + 256;
+    w.nrep = res_replicas(nrb);
+    w.res_bytes = align_up((size_t)(max_iter + 1) * w.nrep * w.m_pad * esz, 256) +
+                  align_up(sizeof(int) * (size_t)(max_iter + 1), 256) + 256 + kSyncBytes;
     w.res = take(w.res_bytes);
     w.bytes = off;
     return w;
@@ -964,8 +1115,9 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter) {
 template <typename T, typename TP, int G, int R>
 hipError_t launch_resident_g(int grid, int nt, SkResArgs<T>& p, hipStream_t s) {
     void* args[] = {&p};
-    return hipLaunchCooperativeKernel((const void*)sk_resident_kernel<T, TP, G, R>, dim3(grid),
-                                      dim3(nt), args, 0, s);
+    const void* k = p.nrep == 1 ? (const void*)sk_resident_kernel<T, TP, G, R, 1>
+                                : (const void*)sk_resident_kernel<T, TP, G, R, OTF_RES_NREP>;
+    return hipLaunchCooperativeKernel(k, dim3(grid), dim3(nt), args, 0, s);
 }
 
 template <typename T, typename TP>
@@ -1000,8 +1152,15 @@ hipError_t run_resident(const PassCfg& cfg, int grid, const T* C, int64_t ldc, i
     p.err_squared = o.err_squared;
     p.stop_thr = o.stop_thr;
     p.cs = (T*)w.res;
-    p.bad_cnt = (int*)((char*)w.res + align_up((size_t)(o.max_iter + 1) * w.m_pad * sizeof(T), 256));
+    p.nrep = w.nrep;
+    p.bad_cnt = (int*)((char*)w.res +
+                       align_up((size_t)(o.max_iter + 1) * w.nrep * w.m_pad * sizeof(T), 256));
     p.bar = (int*)((char*)p.bad_cnt + align_up(sizeof(int) * (size_t)(o.max_iter + 1), 256));
+    int* sw = (int*)((char*)p.bar + 256);
+    p.sync.reg = sw;
+    p.sync.xcnt = sw + 8 * 64;
+    p.sync.top = sw + 16 * 64;
+    p.sync.gen = sw + 17 * 64;
     p.info = info;
     p.errlog = errlog;
     p.u_out = u_out;
@@ -1027,13 +1186,12 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
     if (!(o.reg > 0.0) || o.max_iter < 0 || o.check_every <= 0) return OTF_EINVAL;
     if (P_out && (ldp < m || ldp % VEC != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
     if (n > INT32_MAX || m > (int64_t)kPassThreads * kMaxG * VEC) return OTF_EUNSUPPORTED;
-    Workspace w = carve(ws, n, m, sizeof(T), o.max_iter);
+    const PassCfg cfg = pick_cfg<T>((int)m);
+    const int nrb = (int)((n + cfg.R - 1) / cfg.R);
+    Workspace w = carve(ws, n, m, sizeof(T), o.max_iter, nrb);
     if (ws_bytes < w.bytes) return OTF_EINVAL;
     double* errlog = errlog_user ? errlog_user : w.errlog;
     const int m_pad = (int)w.m_pad;
-
-    const PassCfg cfg = pick_cfg<T>((int)m);
-    const int nrb = (int)((n + cfg.R - 1) / cfg.R);
     const int grid = nrb < device_cu_count() ? nrb : device_cu_count();
     T* cs = (T*)w.cs;
     T* u2 = (T*)w.u2;
@@ -1175,7 +1333,8 @@ extern "C" {
 
 size_t otf_sinkhorn_workspace_size(int64_t n, int64_t m, int32_t dtype, int32_t max_iter) {
     const size_t esz = dtype == OTF_F64 ? 8 : 4;
-    return otf::carve(nullptr, n, m, esz, max_iter < 0 ? 0 : max_iter).bytes;
+    const int64_t nrb = dtype == OTF_F64 ? otf::row_blocks<double>(n, m) : otf::row_blocks<float>(n, m);
+    return otf::carve(nullptr, n, m, esz, max_iter < 0 ? 0 : max_iter, nrb).bytes;
 }
 
 int otf_sinkhorn(const void* a, const void* b, const void* C, int64_t n, int64_t m, int64_t ldc,

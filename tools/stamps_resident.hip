@@ -10,6 +10,7 @@
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_common.hip"
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sinkhorn.hip"
 
+#include <cmath>
 #include <cstdio>
 #include <vector>
 
@@ -51,6 +52,30 @@ int main(int argc, char** argv) {
         (void)hipMemcpy(&hi, info, sizeof(hi), hipMemcpyDeviceToHost);
         printf("rc=%d status=%d engine=%d solve %.3f ms (%.2f us/iter)\n", rc, hi.status, hi.engine,
                ms, ms * 1000 / iters);
+    }
+    // correctness: the resident result against the streaming engine on the same input
+    {
+        std::vector<float> ur(N), vr(N), us(N), vs(N);
+        (void)hipMemcpy(ur.data(), u, N * 4, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(vr.data(), v, N * 4, hipMemcpyDeviceToHost);
+        otf_sinkhorn_opts os = o;
+        os.engine = OTF_ENGINE_STREAM;
+        int rc = otf_sinkhorn(a, a, C, N, N, N, OTF_F32, nullptr, &os, u, v, nullptr, N, OTF_F32,
+                              info, nullptr, ws, wsb, 0);
+        (void)hipDeviceSynchronize();
+        (void)hipMemcpy(us.data(), u, N * 4, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(vs.data(), v, N * 4, hipMemcpyDeviceToHost);
+        // u, v are defined up to a scale (u*c, v/c): compare the products u_i v_j
+        double umax = 0, vmax = 0, du = 0, dv = 0;
+        const double cu = (double)ur[0] / us[0];
+        for (int i = 0; i < N; ++i) {
+            umax = fmax(umax, fabs((double)us[i]));
+            vmax = fmax(vmax, fabs((double)vs[i]));
+            du = fmax(du, fabs((double)ur[i] / cu - us[i]));
+            dv = fmax(dv, fabs((double)vr[i] * cu - vs[i]));
+        }
+        printf("stream rc=%d  resident vs stream: rel u %.3e  rel v %.3e  %s\n", rc, du / umax,
+               dv / vmax, (du / umax < 1e-4 && dv / vmax < 1e-4) ? "OK" : "MISMATCH");
     }
     std::vector<unsigned long long> st(256 * 16 * 8);
     (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(otf::g_stamps), st.size() * 8);
