@@ -7,10 +7,15 @@ so every iteration runs) -> N x N transport plan written to HBM.
 
   value            = MRI+PET pairs aligned per second, whole job (N x ranks / step time)
   sinkhorn_iters_per_sec = iterations / time of the Sinkhorn call (incl. plan write)
-  roofline         = dominant kernel (the fused Sinkhorn pass): algorithmic bytes
-                     N*N*4 per launch / mean pass time from HIP events on its stream
+  roofline         = dominant kernel (the resident Sinkhorn kernel: one launch runs
+                     all iterations): algorithmic bytes iters * N*N*4 per launch / its
+                     duration from HIP events on its stream; traffic = PMC HBM bytes
+                     per launch from profiles/kernel_traffic.json (same kernel)
+  cost_roofline    = the split-fp16 MFMA cost kernel: 2*N*N*d flops / event time
+  hbm_probe        = streaming engine at N = 16384 (1 GiB cost, past the 256 MiB
+                     Infinity Cache): true-HBM rate of one fused pass
   cpu_baseline     = the float64 C/OpenMP restatement (oracle/, POT semantics) on the
-                     host cores, same workload, rank 0 at N = 1 only
+                     host cores, same workload, rank 0 at N = 1 only (+ 1-core run)
 
 Multi-GPU: one process per GPU (torchrun); every rank solves its own independent
 N = 4096 problem (per-rank minibatch) — "weak" scaling, no collective on the data
@@ -47,9 +52,13 @@ def parse():
     p.add_argument("--eps", type=float, default=0.1)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pass_traffic.json"))
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "kernel_traffic.json"))
+    p.add_argument("--no-hbm-probe", action="store_true")
+    p.add_argument("--hbm-probe-n", type=int, default=16384)
     p.add_argument("--profile-only", action="store_true",
                    help="run warmup + steps only (for rocprofv3 runs); no probes, no JSON")
+    p.add_argument("--engine", default="auto", choices=("auto", "stream", "resident"),
+                   help="Sinkhorn engine (auto = resident when the cost fits the register file)")
     return p.parse_args()
 
 
@@ -76,6 +85,7 @@ def main():
     ws = ops.sinkhorn_workspace(N, N, torch.float32, iters, dev)
     P = torch.empty((N, N), dtype=torch.float32, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    MFMA_F32_PEAK_TFLOPS = 157.3   # dense fp32 MFMA (MI355X_MICROARCH.md chip table)
 
     def step(record):
         if record:
@@ -84,7 +94,7 @@ def main():
         if record:
             ev[1].record()
         ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, cost_scale=cmax, workspace=ws,
-                     plan_out=P)
+                     plan_out=P, engine=args.engine)
         if record:
             ev[2].record()
         return C, cmax
@@ -123,7 +133,7 @@ def main():
     sk_ms = sorted(sk_l)[2]
     C, cmax = ops.pairwise_cost(X, Y)
     res = ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, cost_scale=cmax, workspace=ws,
-                       plan_out=P)
+                       plan_out=P, engine=args.engine)
     engine = res.info()["engine_name"]
 
     # roofline of the dominant kernel.  Algorithmic bytes: one compulsory
@@ -131,24 +141,27 @@ def main():
     # does all iterations (+ the plan write) with the cost held in registers, so its
     # algorithmic rate can exceed the HBM peak — the PMC traffic shows the real bytes.
     iter_bytes = N * N * 4
-    traffic = None
-    if os.path.exists(args.traffic_json):
+    kernel_name = "sk_resident_kernel" if engine == "resident" else "sk_pass_kernel"
+
+    def pmc_traffic(kname):
         try:
             tj = json.load(open(args.traffic_json))
-            if int(tj.get("n", 0)) == N and tj.get("engine", "stream") == engine:
-                traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
-            traffic = None
+            return None
+        if int(tj.get("n", 0)) != N or int(tj.get("iters", 0)) != iters:
+            return None
+        return tj.get("kernels", {}).get(kname, {}).get("hbm_bytes_per_launch")
+    traffic = pmc_traffic(kernel_name)
     # streaming engine for reference: HIP event pair around every fused pass
     pass_ms = ops.sinkhorn_profile(a, a, C, eps, iters, cost_scale=cmax, workspace=ws)
     if engine == "resident":
         launch_bytes = iter_bytes * iters
         achieved = launch_bytes / (sk_ms * 1e-3) / 1e9
-        kernel_name = "sk_resident_kernel"
     else:
         launch_bytes = iter_bytes
         achieved = iter_bytes / (pass_ms * 1e-3) / 1e9
-        kernel_name = "sk_pass_kernel"
+    cost_flops = 2.0 * N * N * d
+    cost_tflops = cost_flops / (cost_ms * 1e-3) / 1e12
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * N * args.steps / elapsed
@@ -166,8 +179,8 @@ def main():
         "dtype": "f32",
         "data": "synthetic: seeded paired structured embeddings (SURVEY.md 8d), resident in HBM",
         "config": {"workload": f"sinkhorn_pairwise_N{N}_d{d}_it{iters}", "N": N, "d": d,
-                   "iters": iters, "eps": eps, "cost": "sqeuclidean / max (MFMA f32)",
-                   "sinkhorn": "POT sinkhorn_knopp semantics, stopThr=0, fused single-read pass",
+                   "iters": iters, "eps": eps, "cost": "sqeuclidean / max (split-fp16 MFMA, fp32-accurate)",
+                   "sinkhorn": "POT sinkhorn_knopp semantics, stopThr=0",
                    "plan": "N x N float32 written per step", "global_batch": N * world,
                    "parallelism": f"replicas x{world} (independent problems)"},
         "sinkhorn_iters_per_sec": iters / (sk_ms * 1e-3),
@@ -180,9 +193,17 @@ def main():
                      "note": ("resident: all iterations in one launch, cost held in registers; "
                               "algorithmic bytes = iters x N*N*4" if engine == "resident" else
                               "one launch per iteration; C (64 MiB) fits the 256 MiB Infinity Cache")},
+        "cost_roofline": {"bound": "mfma", "kernel": "cost_split16_kernel", "achieved": cost_tflops,
+                          "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": cost_tflops / MFMA_F32_PEAK_TFLOPS,
+                          "traffic": pmc_traffic("cost_split16_kernel"),
+                          "note": "2*N*N*d fp32-equivalent flops (3 f16 MFMAs per product) incl. "
+                                  "the split/prep kernel, vs the dense fp32 MFMA peak"},
         "stream_engine": {"pass_ms": pass_ms, "achieved": iter_bytes / (pass_ms * 1e-3) / 1e9,
                           "frac": iter_bytes / (pass_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
     }
+    if not args.no_hbm_probe:
+        out["hbm_probe"] = hbm_probe(ops, paired_embeddings, args.hbm_probe_n, d, eps, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(X_np, Y_np, N, iters, eps, args.cpu_threads)
         out["vs_cpu"] = value / out["cpu_baseline"]["value"]
@@ -190,6 +211,25 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def hbm_probe(ops, paired_embeddings, n, d, eps, dev):
+    """Streaming engine on an n x n fp32 cost (1 GiB at n = 16384, 4x the Infinity
+    Cache): mean HIP-event time of one fused pass -> true-HBM GB/s."""
+    Xn, Yn, _ = paired_embeddings(n, d, seed=99)
+    X = torch.from_numpy(Xn).to(dev)
+    Y = torch.from_numpy(Yn).to(dev)
+    C, cmax = ops.pairwise_cost(X, Y)
+    del X, Y
+    a = torch.full((n,), 1.0 / n, device=dev)
+    ws = ops.sinkhorn_workspace(n, n, torch.float32, 10, dev)
+    ms = ops.sinkhorn_profile(a, a, C, eps, 10, cost_scale=cmax, workspace=ws)
+    gbs = n * n * 4 / (ms * 1e-3) / 1e9
+    del C, ws
+    torch.cuda.empty_cache()
+    return {"kernel": "sk_pass_kernel", "N": n, "pass_ms": ms, "achieved": gbs,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "note": "streaming engine, 10 passes, cost 4x the Infinity Cache"}
 
 
 def cpu_baseline(X, Y, N, iters, eps, threads):
@@ -209,10 +249,22 @@ def cpu_baseline(X, Y, N, iters, eps, threads):
         t2 = time.perf_counter()
         runs.append((t2 - t0, t1 - t0, t2 - t1))
     tot, tc, tl = sorted(runs)[1]  # median run
+    # one core: the same workload with 10 iterations, loop time scaled to `iters`
+    orc.set_threads(1)
+    t0 = time.perf_counter()
+    C, _ = orc.pairwise_cost(X, Y, scale_max=True)
+    t1 = time.perf_counter()
+    orc.sinkhorn_knopp(a, a, C, eps, 10, 0.0, want_plan=True)
+    t2 = time.perf_counter()
+    orc.set_threads(n_threads)
+    one = (t1 - t0) + (t2 - t1) * iters / 10.0
     return {"value": N / tot, "unit": "pairs/s", "cores": used, "kind": "port",
             "sinkhorn_iters_per_sec": iters / tl, "seconds": tot,
             "sample": f"full workload, median of 3: N={N} d={X.shape[1]} {iters} iters float64 "
-                      f"(cost {tc:.2f}s + loop/plan {tl:.2f}s)"}
+                      f"(cost {tc:.2f}s + loop/plan {tl:.2f}s)",
+            "single_core": {"value": N / one, "unit": "pairs/s", "cores": 1,
+                            "sinkhorn_iters_per_sec": 10.0 / (t2 - t1),
+                            "sample": f"cost {t1 - t0:.2f}s + 10 iters {t2 - t1:.2f}s, scaled to {iters}"}}
 
 
 if __name__ == "__main__":

@@ -58,7 +58,6 @@ template <typename T> struct SkArgs {
     int check_off;         // POT checks at ii % 10 == 0, OTT after every 10th update
     int err_squared;
     int m_pad;
-    int ablate;            // diagnostic builds only (env OTF_ABLATE); 0 in production
 };
 
 __device__ __forceinline__ void sk_stop(otf_sinkhorn_info* info, int last_good, int niter,
@@ -185,7 +184,7 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
     // ---- row blocks.  The first block's cost rows are put in flight BEFORE the
     // column-scaling prologue (its loads, arithmetic and barrier), so the prologue's
     // latency hides under the stream instead of preceding it.
-    const bool have_prev = p.it >= 0 && !(p.ablate & 1);
+    const bool have_prev = p.it >= 0;
     const int nrb = (p.n + R - 1) / R;
     T vw[G][VEC];  // POT: v_j (row-sum weights); OTT: 1
     T go[G][VEC];  // OTT: g_j in exponent units; POT: 0
@@ -276,7 +275,7 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
                 for (int k = 0; k < VEC; ++k) {
                     T z = kv[r][g][k] * ks;
                     if (LOG) z += fo[r] + go[g][k];
-                    kv[r][g][k] = (rok && cok[g][k]) ? ((p.ablate & 8) ? z : fast_exp(z)) : (T)0;
+                    kv[r][g][k] = (rok && cok[g][k]) ? fast_exp(z) : (T)0;
                 }
         }
         T ur[R];
@@ -290,7 +289,7 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
                     for (int k = 0; k < VEC; ++k) s += LOG ? kv[r][g][k] : kv[r][g][k] * vw[g][k];
                 ur[r] = s;
             }
-            if (!(p.ablate & 2)) block_sum_rows<T, R>(ur, tbuf, red);
+            block_sum_rows<T, R>(ur, tbuf, red);
             T outv[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -348,11 +347,7 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
         }
     }
     __syncthreads();
-    if (!(p.ablate & 4)) {
-        for (int j = tid; j < p.m; j += NT) atomicAdd(p.cs_dst + j, colbuf[j]);
-    } else if (colbuf[tid] == (T)12345) {
-        p.cs_dst[tid] = 0;
-    }
+    for (int j = tid; j < p.m; j += NT) atomicAdd(p.cs_dst + j, colbuf[j]);
 
     // ---- zero the column-sum buffer of the next pass (nobody touches it now)
     for (int j = blockIdx.x * NT + tid; j < p.m_pad; j += gridDim.x * NT) p.cs_zero[j] = 0;
@@ -505,12 +500,13 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const T* C, int64_t ldc, i
 // forms v, decides convergence / numerical break exactly like the streaming pass
 // (every workgroup derives the same decision from the same sums), updates u for
 // its rows and adds its column partials K_w^T u_w into a FRESH per-iteration sum
-// buffer with memory-side float atomics; a device-wide counter barrier separates
-// iterations.  Sums are read with device-scope (sc1) loads and each iteration uses
-// a buffer nobody has cached, so no cache level can return a stale sum.  Every
-// spin is bounded by wall-clock time (s_memrealtime, 100 MHz): a barrier that
-// does not complete sets OTF_SK_TIMEOUT instead of hanging.  Co-residency of the
-// grid (<= one workgroup per CU) is checked by the cooperative launch.
+// buffer with memory-side float atomics -- into one of NREP replicas picked by the
+// workgroup's XCD, so ~256/NREP adders share an address instead of 256.  An
+// XCD-hierarchical barrier (xcd_barrier) separates iterations; the sums are then
+// read with 16-B sc1 buffer loads (the no-acquire hand-off form).  Every spin is
+// bounded by wall-clock time (s_memrealtime, 100 MHz): a barrier that does not
+// complete sets OTF_SK_TIMEOUT instead of hanging.  Co-residency of the grid
+// (<= one workgroup per CU) is checked before the launch (launch_resident_g).
 // ============================================================================
 struct SkSync {
     int* reg;   // [8 * 64]  workgroups per XCD (registration, before the first barrier)
@@ -1112,12 +1108,21 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     return w;
 }
 
+// Plain launch of the persistent grid after an explicit residency check (every
+// workgroup must be resident at once for the in-kernel barrier; plain and cooperative
+// launches get identical residency, and a plain launch replays in a graph at no
+// extra cost).  Every spin in the kernel is bounded, so a grid that cannot become
+// resident (another persistent kernel on the device) ends in OTF_SK_TIMEOUT.
 template <typename T, typename TP, int G, int R>
 hipError_t launch_resident_g(int grid, int nt, SkResArgs<T>& p, hipStream_t s) {
     void* args[] = {&p};
     const void* k = p.nrep == 1 ? (const void*)sk_resident_kernel<T, TP, G, R, 1>
                                 : (const void*)sk_resident_kernel<T, TP, G, R, OTF_RES_NREP>;
-    return hipLaunchCooperativeKernel(k, dim3(grid), dim3(nt), args, 0, s);
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, nt, 0);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1 || grid > per_cu * device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
+    return hipLaunchKernel(k, dim3(grid), dim3(nt), args, 0, s);
 }
 
 template <typename T, typename TP>
@@ -1239,7 +1244,6 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
     p.check_off = LOG ? 1 : 0;
     p.err_squared = LOG ? 0 : o.err_squared;
     p.m_pad = m_pad;
-    p.ablate = getenv("OTF_ABLATE") ? atoi(getenv("OTF_ABLATE")) : 0;
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double total_ms = 0.0;

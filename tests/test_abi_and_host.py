@@ -22,8 +22,8 @@ def test_version_and_workspace_queries_are_host_only():
     assert lib.otf_version().decode().startswith("otfuse")
     ws = lib.otf_sinkhorn_workspace_size(4096, 4096, L.OTF_F32, 100)
     # streaming buffers (~9 vectors) + the resident engine's per-iteration sums
-    # (101 iterations x 8 XCD replicas x N: 256 row blocks of 16 rows)
-    assert 4 * 4096 * (9 + 808) < ws < 4 * 4096 * (32 + 808)
+    # (101 iterations x 4 replicas x N: 256 row blocks of 16 rows)
+    assert 4 * 4096 * (9 + 404) < ws < 4 * 4096 * (32 + 404)
     # a small problem (8 row blocks) keeps a single replica
     ws_small = lib.otf_sinkhorn_workspace_size(128, 4096, L.OTF_F32, 100)
     assert ws_small < 4 * 4096 * (32 + 101)

@@ -21,9 +21,11 @@ if [ "${PROFILE:-1}" = "1" ]; then
   rc=$?; echo "rocprof rc=$rc"; stop_if_fatal $rc rocprof
 fi
 if [ "${PMC:-0}" = "1" ]; then
-  for ctr in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 420 rocprofv3 --pmc $ctr --kernel-trace --stats -d gpurun_out/pmc_$ctr -o run --output-format csv -- python3 bench.py --profile-only --steps 3 --warmup 1 > gpurun_out/pmc_$ctr.log 2>&1
-    rc=$?; echo "pmc $ctr rc=$rc"; stop_if_fatal $rc pmc
+  for eng in auto stream; do
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      timeout -k 10 420 rocprofv3 --pmc $ctr --kernel-trace --stats -d gpurun_out/pmc_${ctr}_$eng -o run --output-format csv -- python3 bench.py --profile-only --engine $eng --steps 3 --warmup 1 > gpurun_out/pmc_${ctr}_$eng.log 2>&1
+      rc=$?; echo "pmc $ctr $eng rc=$rc"; stop_if_fatal $rc pmc
+    done
   done
 fi
 exit 0
