@@ -46,7 +46,7 @@ enum {
     OTF_EHIP = -1
 };
 
-typedef enum { OTF_F32 = 0, OTF_F64 = 1 } otf_dtype;
+typedef enum { OTF_F32 = 0, OTF_F64 = 1, OTF_F16 = 2 } otf_dtype;
 typedef enum { OTF_SQEUCLIDEAN = 0, OTF_EUCLIDEAN = 1 } otf_metric;
 
 /* Sinkhorn flavours.
@@ -87,6 +87,8 @@ typedef struct {
     int32_t sync_every; /* streaming engine: host polls the device stop flag every N
                            iterations; 0 = never (finished passes no-op)             */
     int32_t engine;     /* otf_engine                                                  */
+    int32_t cost_f16;   /* 1: C is stored as fp16 (dtype must be OTF_F32; compute fp32)  */
+    int32_t reserved;   /* 0                                                           */
 } otf_sinkhorn_opts;
 
 /* Written on the device by otf_sinkhorn (read it after the stream completes). */
@@ -126,6 +128,24 @@ int otf_cost_pairwise_split16(const float* X, int64_t ldx, const float* Y, int64
                               int64_t ldc, float* cmax, void* workspace, size_t ws_bytes,
                               otf_stream_t stream);
 
+/* General pairwise cost (BASELINE config 5: fp16 embeddings / fp16 cost storage).
+ * in_dtype OTF_F32: X, Y float32, contraction as otf_cost_pairwise_split16;
+ * in_dtype OTF_F16: X, Y fp16, one v_mfma_f32_32x32x16_f16 per 16-deep step,
+ *   fp32 accumulation, norms in fp32 from the fp16 values.
+ * c_dtype OTF_F32: C float32 holds the cost itself (*c_unit = 1);
+ * c_dtype OTF_F16: C fp16 holds cost * 2^-k, k chosen from the row norms so that
+ *   every stored value is <= 1 (max C <= (max|x| + max|y|)^2, no overflow, one
+ *   pass); *c_unit = 2^k (device float, nullable) recovers the cost.
+ * cmax (device float, nullable) receives the max of the STORED values, i.e. the
+ * cost_scale that makes otf_sinkhorn see C / max(C) ("max_cost").  Rows of X/Y:
+ * ldx, ldy elements; C rows 16-B aligned when it feeds otf_sinkhorn.
+ * Workspace: otf_cost_ex_workspace_size() bytes.                                 */
+size_t otf_cost_ex_workspace_size(int64_t n, int64_t m, int64_t d, int32_t in_dtype);
+int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
+                         int32_t in_dtype, int64_t n, int64_t m, int64_t d, int32_t metric,
+                         int32_t zero_diag, void* C, int64_t ldc, int32_t c_dtype, float* cmax,
+                         float* c_unit, void* workspace, size_t ws_bytes, otf_stream_t stream);
+
 /* Divides C (n x m, ldc) by the device scalar *s (in place).  float32/64. */
 int otf_scale_inplace(void* C, int64_t n, int64_t m, int64_t ldc, int32_t dtype, const void* s,
                       otf_stream_t stream);
@@ -154,6 +174,8 @@ int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, i
  * potentials f, g and P_out = exp((f_i + g_j - C_ij*cscale)/reg).
  * info (device) receives the outcome; errlog (device float64, optional, length
  * max_iter / check_every + 1) the marginal errors.
+ * opts->cost_f16 = 1: C is fp16 (e.g. from otf_cost_pairwise_ex with c_dtype
+ * OTF_F16, cost_scale = its cmax), dtype OTF_F32; K is formed in fp32.
  * Layout requirements: ldc and ldp multiples of 16/sizeof(dtype) and 16-B
  * aligned rows.  Workspace: otf_sinkhorn_workspace_size() bytes.
  * Host synchronisation happens only if opts->sync_every > 0.                   */

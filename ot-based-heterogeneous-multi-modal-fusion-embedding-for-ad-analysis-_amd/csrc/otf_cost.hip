@@ -179,56 +179,89 @@ constexpr int SBK = 32;        // K per LDS stage
 constexpr int SLD = SBK + 8;   // padded LDS row (80 B): conflict-free ds_read_b128
 
 // One 256-thread workgroup per row: squared norm (fp32, same expansion as the fp32
-// path), power-of-two scale, hi / lo fp16 rows (zero-padded to ldh).
-__global__ __launch_bounds__(256) void split16_prep_kernel(const float* __restrict__ X, int64_t ldx,
+// path) and the fp16 image(s) of the row, zero-padded to ldh.
+//   SPLIT (fp32 input): power-of-two scale s, hi = fp16(x s), lo = fp16(x s - hi);
+//   !SPLIT (fp16 input): hi = x, inv_scale = 1.
+// max_norm (nullable): running max of the squared norms (bit pattern, >= 0).
+template <typename TI, bool SPLIT>
+__global__ __launch_bounds__(256) void split16_prep_kernel(const TI* __restrict__ X, int64_t ldx,
                                                           int n, int d, _Float16* hi, _Float16* lo,
-                                                          int ldh, float* inv_scale, float* norm) {
+                                                          int ldh, float* inv_scale, float* norm,
+                                                          unsigned int* max_norm) {
     __shared__ float red[17];
+    __shared__ float wm[16];
+    float nmax = 0.f;
     for (int row = blockIdx.x; row < n; row += gridDim.x) {
-        const float* x = X + (int64_t)row * ldx;
+        const TI* x = X + (int64_t)row * ldx;
         float mx = 0.f, s2 = 0.f;
         for (int k = threadIdx.x; k < d; k += blockDim.x) {
-            const float v = x[k];
+            const float v = (float)x[k];
             mx = fmaxf(mx, fabsf(v));
             s2 = fmaf(v, v, s2);
         }
         s2 = block_sum<float>(s2, red);
-        mx = wave_max(mx);
-        __shared__ float wm[16];
-        if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            float m2 = 0.f;
-            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m2 = fmaxf(m2, wm[w]);
-            wm[0] = m2;
+        int e = 0;
+        if (SPLIT) {
+            mx = wave_max(mx);
+            if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                float m2 = 0.f;
+                for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m2 = fmaxf(m2, wm[w]);
+                wm[0] = m2;
+            }
+            __syncthreads();
+            mx = wm[0];
+            e = mx > 0.f ? ilogbf(mx) : 0;
         }
-        __syncthreads();
-        mx = wm[0];
-        const int e = mx > 0.f ? ilogbf(mx) : 0;
-        const float sc = ldexpf(1.0f, 14 - e);
+        const float sc = SPLIT ? ldexpf(1.0f, 14 - e) : 1.0f;
         _Float16* h = hi + (int64_t)row * ldh;
-        _Float16* l = lo + (int64_t)row * ldh;
+        _Float16* l = SPLIT ? lo + (int64_t)row * ldh : nullptr;
         for (int k = threadIdx.x; k < ldh; k += blockDim.x) {
-            const float v = k < d ? x[k] * sc : 0.f;
+            const float v = k < d ? (float)x[k] * sc : 0.f;
             const _Float16 vh = (_Float16)v;
             h[k] = vh;
-            l[k] = (_Float16)(v - (float)vh);
+            if (SPLIT) l[k] = (_Float16)(v - (float)vh);
         }
         if (threadIdx.x == 0) {
-            inv_scale[row] = ldexpf(1.0f, e - 14);
+            inv_scale[row] = SPLIT ? ldexpf(1.0f, e - 14) : 1.0f;
             norm[row] = s2;
+            nmax = fmaxf(nmax, s2);
         }
         __syncthreads();
     }
+    if (max_norm && threadIdx.x == 0) atomicMax(max_norm, __float_as_uint(nmax));
 }
 
+// fp16 cost storage scale: 2^-k with 2^k >= the largest possible cost given the row
+// norms ((|x|max + |y|max)^2, or its root for the Euclidean metric); exact in fp16.
+__global__ void cost_store_scale_kernel(const unsigned int* max_norms, int metric, float* scale,
+                                        float* unit) {
+    const float nx = __uint_as_float(max_norms[0]), ny = __uint_as_float(max_norms[1]);
+    float bound = sqrtf(nx) + sqrtf(ny);
+    if (metric != OTF_EUCLIDEAN) bound = bound * bound;
+    int k = 0;
+    if (bound > 0.f && isfinite(bound)) {
+        k = ilogbf(bound) + 1;  // 2^k > bound
+        k = k < -100 ? -100 : k;
+    }
+    scale[0] = ldexpf(1.0f, -k);
+    if (unit) unit[0] = ldexpf(1.0f, k);
+}
+
+// 128x128 output tile per 256-thread workgroup on v_mfma_f32_32x32x16_f16.
+// NS = 3: split-fp16 (hi.hi + hi.lo + lo.hi, fp32-accurate); NS = 1: fp16 inputs.
+// TC: stored cost type (float, or _Float16 scaled by *store_scale).
+template <int NS, typename TC>
 __global__ __launch_bounds__(256) void cost_split16_kernel(
     const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
     const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
     const float* __restrict__ ys, const float* __restrict__ yy, int ldh, int n, int m, int kpad,
-    int metric, int zero_diag, float* __restrict__ C, int64_t ldc, unsigned int* cmax, int tiles_n) {
-    __shared__ __attribute__((aligned(16))) _Float16 As[2][BM][SLD];  // [hi|lo][row][k]
-    __shared__ __attribute__((aligned(16))) _Float16 Bs[2][BN][SLD];
+    int metric, int zero_diag, TC* __restrict__ C, int64_t ldc, unsigned int* cmax, int tiles_n,
+    const float* __restrict__ store_scale) {
+    constexpr int NI = NS == 3 ? 2 : 1;  // fp16 images per operand
+    __shared__ __attribute__((aligned(16))) _Float16 As[NI][BM][SLD];  // [hi|lo][row][k]
+    __shared__ __attribute__((aligned(16))) _Float16 Bs[NI][BN][SLD];
 
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
@@ -247,9 +280,9 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
             for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
     // staging: a 128-row x 32-half tile is 512 16-B chunks; 256 threads x 2 chunks,
-    // for each of {A hi, A lo, B hi, B lo}
+    // for each of {A hi, A lo, B hi, B lo} (lo only when NS == 3)
     using u4 = __attribute__((ext_vector_type(4))) unsigned int;
-    u4 st[2][4];
+    u4 st[2][2 * NI];
     auto gload = [&](int k0) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -258,9 +291,11 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
             const int gi = i0 + row < n ? i0 + row : n - 1;
             const int gj = j0 + row < m ? j0 + row : m - 1;
             st[c][0] = *reinterpret_cast<const u4*>(Xh + (int64_t)gi * ldh + k0 + kc);
-            st[c][1] = *reinterpret_cast<const u4*>(Xl + (int64_t)gi * ldh + k0 + kc);
-            st[c][2] = *reinterpret_cast<const u4*>(Yh + (int64_t)gj * ldh + k0 + kc);
-            st[c][3] = *reinterpret_cast<const u4*>(Yl + (int64_t)gj * ldh + k0 + kc);
+            st[c][NI] = *reinterpret_cast<const u4*>(Yh + (int64_t)gj * ldh + k0 + kc);
+            if (NI == 2) {
+                st[c][1] = *reinterpret_cast<const u4*>(Xl + (int64_t)gi * ldh + k0 + kc);
+                st[c][NI + 1] = *reinterpret_cast<const u4*>(Yl + (int64_t)gj * ldh + k0 + kc);
+            }
         }
     };
     auto lstore = [&]() {
@@ -268,10 +303,11 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
         for (int c = 0; c < 2; ++c) {
             const int chunk = tid + 256 * c;
             const int row = chunk >> 2, kc = (chunk & 3) * 8;
-            *reinterpret_cast<u4*>(&As[0][row][kc]) = st[c][0];
-            *reinterpret_cast<u4*>(&As[1][row][kc]) = st[c][1];
-            *reinterpret_cast<u4*>(&Bs[0][row][kc]) = st[c][2];
-            *reinterpret_cast<u4*>(&Bs[1][row][kc]) = st[c][3];
+#pragma unroll
+            for (int h = 0; h < NI; ++h) {
+                *reinterpret_cast<u4*>(&As[h][row][kc]) = st[c][h];
+                *reinterpret_cast<u4*>(&Bs[h][row][kc]) = st[c][NI + h];
+            }
         }
     };
 
@@ -291,21 +327,26 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
                 const int ar = wm * 64 + t * 32 + (lane & 31);
                 const int br = wn * 64 + t * 32 + (lane & 31);
                 ah[t] = *reinterpret_cast<const f16x8*>(&As[0][ar][kk]);
-                al[t] = *reinterpret_cast<const f16x8*>(&As[1][ar][kk]);
                 bh[t] = *reinterpret_cast<const f16x8*>(&Bs[0][br][kk]);
-                bl[t] = *reinterpret_cast<const f16x8*>(&Bs[1][br][kk]);
+                if (NI == 2) {
+                    al[t] = *reinterpret_cast<const f16x8*>(&As[NI - 1][ar][kk]);
+                    bl[t] = *reinterpret_cast<const f16x8*>(&Bs[NI - 1][br][kk]);
+                }
             }
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
                 for (int nj = 0; nj < 2; ++nj) {
-                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mi], bh[nj], acc[mi][nj], 0, 0, 0);
-                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bl[nj], acc[mi][nj], 0, 0, 0);
+                    if (NS == 3) {
+                        acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mi], bh[nj], acc[mi][nj], 0, 0, 0);
+                        acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bl[nj], acc[mi][nj], 0, 0, 0);
+                    }
                     acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bh[nj], acc[mi][nj], 0, 0, 0);
                 }
         }
     }
 
+    const float os = store_scale ? store_scale[0] : 1.0f;
     float lmax = 0.f;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -322,8 +363,9 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
                     c = c > 0.f ? c : 0.f;
                     if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
                     if (zero_diag && gi == gj) c = 0.f;
-                    C[(int64_t)gi * ldc + gj] = c;
-                    lmax = fmaxf(lmax, c);
+                    const TC cs = (TC)(c * os);
+                    C[(int64_t)gi * ldc + gj] = cs;
+                    lmax = fmaxf(lmax, (float)cs);
                 }
             }
     if (cmax) {
@@ -361,52 +403,97 @@ int otf_cost_pairwise(const float* X, int64_t ldx, const float* Y, int64_t ldy, 
 
 static size_t otf_al(size_t x) { return (x + 255) / 256 * 256; }
 
-size_t otf_cost_split16_workspace_size(int64_t n, int64_t m, int64_t d) {
+size_t otf_cost_ex_workspace_size(int64_t n, int64_t m, int64_t d, int32_t in_dtype) {
     const size_t ldh = (size_t)((d + otf::SBK - 1) / otf::SBK * otf::SBK);
-    return 2 * otf_al((size_t)n * ldh * 2) + 2 * otf_al((size_t)m * ldh * 2) +
-           2 * otf_al((size_t)n * 4) + 2 * otf_al((size_t)m * 4);
+    const size_t ni = in_dtype == OTF_F16 ? 1 : 2;
+    return ni * otf_al((size_t)n * ldh * 2) + ni * otf_al((size_t)m * ldh * 2) +
+           2 * otf_al((size_t)n * 4) + 2 * otf_al((size_t)m * 4) + 256;
 }
 
-int otf_cost_pairwise_split16(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
-                              int64_t m, int64_t d, int32_t metric, int32_t zero_diag, float* C,
-                              int64_t ldc, float* cmax, void* workspace, size_t ws_bytes,
-                              otf_stream_t stream) {
+size_t otf_cost_split16_workspace_size(int64_t n, int64_t m, int64_t d) {
+    return otf_cost_ex_workspace_size(n, m, d, OTF_F32);
+}
+
+int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
+                         int32_t in_dtype, int64_t n, int64_t m, int64_t d, int32_t metric,
+                         int32_t zero_diag, void* C, int64_t ldc, int32_t c_dtype, float* cmax,
+                         float* c_unit, void* workspace, size_t ws_bytes, otf_stream_t stream) {
     if (!X || !Y || !C || !workspace || n <= 0 || m <= 0 || d <= 0) return OTF_EINVAL;
     if (ldx < d || ldy < d || ldc < m) return OTF_EINVAL;
     if (metric != OTF_SQEUCLIDEAN && metric != OTF_EUCLIDEAN) return OTF_EINVAL;
-    if (ws_bytes < otf_cost_split16_workspace_size(n, m, d)) return OTF_EINVAL;
+    if (in_dtype != OTF_F32 && in_dtype != OTF_F16) return OTF_EINVAL;
+    if (c_dtype != OTF_F32 && c_dtype != OTF_F16) return OTF_EINVAL;
+    if (ws_bytes < otf_cost_ex_workspace_size(n, m, d, in_dtype)) return OTF_EINVAL;
     if (n > INT32_MAX || m > INT32_MAX || d > (1 << 20)) return OTF_EUNSUPPORTED;
     hipStream_t s = (hipStream_t)stream;
+    const bool split = in_dtype == OTF_F32;
     const int ldh = (int)((d + otf::SBK - 1) / otf::SBK * otf::SBK);
     char* p = (char*)workspace;
     auto take = [&](size_t bytes) { void* q = p; p += otf_al(bytes); return q; };
     _Float16* Xh = (_Float16*)take((size_t)n * ldh * 2);
-    _Float16* Xl = (_Float16*)take((size_t)n * ldh * 2);
+    _Float16* Xl = split ? (_Float16*)take((size_t)n * ldh * 2) : nullptr;
     _Float16* Yh = (_Float16*)take((size_t)m * ldh * 2);
-    _Float16* Yl = (_Float16*)take((size_t)m * ldh * 2);
+    _Float16* Yl = split ? (_Float16*)take((size_t)m * ldh * 2) : nullptr;
     float* xs = (float*)take((size_t)n * 4);
     float* xx = (float*)take((size_t)n * 4);
     float* ys = (float*)take((size_t)m * 4);
     float* yy = (float*)take((size_t)m * 4);
+    float* small = (float*)take(256);  // [0..1] max squared norms, [2] store scale
+    const bool f16out = c_dtype == OTF_F16;
+    unsigned int* mn = f16out ? (unsigned int*)small : nullptr;
+    if (f16out) OTF_HIP(hipMemsetAsync(small, 0, 2 * sizeof(float), s));
     const bool same = (X == Y && n == m && ldx == ldy);
-    otf::split16_prep_kernel<<<(int)(n < 4096 ? n : 4096), 256, 0, s>>>(X, ldx, (int)n, (int)d, Xh, Xl,
-                                                                      ldh, xs, xx);
+    const int gx = (int)(n < 4096 ? n : 4096), gy = (int)(m < 4096 ? m : 4096);
+    if (split) {
+        otf::split16_prep_kernel<float, true><<<gx, 256, 0, s>>>((const float*)X, ldx, (int)n, (int)d,
+                                                                Xh, Xl, ldh, xs, xx, mn);
+        if (!same)
+            otf::split16_prep_kernel<float, true><<<gy, 256, 0, s>>>((const float*)Y, ldy, (int)m, (int)d,
+                                                                    Yh, Yl, ldh, ys, yy, mn ? mn + 1 : nullptr);
+    } else {
+        otf::split16_prep_kernel<_Float16, false><<<gx, 256, 0, s>>>((const _Float16*)X, ldx, (int)n,
+                                                                    (int)d, Xh, nullptr, ldh, xs, xx, mn);
+        if (!same)
+            otf::split16_prep_kernel<_Float16, false><<<gy, 256, 0, s>>>(
+                (const _Float16*)Y, ldy, (int)m, (int)d, Yh, nullptr, ldh, ys, yy, mn ? mn + 1 : nullptr);
+    }
     OTF_HIP(hipGetLastError());
-    if (!same) {
-        otf::split16_prep_kernel<<<(int)(m < 4096 ? m : 4096), 256, 0, s>>>(Y, ldy, (int)m, (int)d, Yh,
-                                                                          Yl, ldh, ys, yy);
+    if (same) {
+        Yh = Xh; Yl = Xl; ys = xs; yy = xx;
+        if (f16out) OTF_HIP(hipMemcpyAsync(mn + 1, mn, sizeof(float), hipMemcpyDeviceToDevice, s));
+    }
+    const float* store_scale = nullptr;
+    if (f16out) {
+        otf::cost_store_scale_kernel<<<1, 1, 0, s>>>(mn, metric, small + 2, c_unit);
         OTF_HIP(hipGetLastError());
+        store_scale = small + 2;
+    } else if (c_unit) {
+        OTF_HIP(hipMemsetD32Async((hipDeviceptr_t)c_unit, 0x3f800000u /* 1.0f */, 1, s));
     }
     if (cmax) OTF_HIP(hipMemsetAsync(cmax, 0, sizeof(float), s));
     const int tiles_m = (int)((n + otf::BM - 1) / otf::BM);
     const int tiles_n = (int)((m + otf::BN - 1) / otf::BN);
     const int64_t nwg = (int64_t)tiles_m * tiles_n;
     if (nwg > INT32_MAX) return OTF_EUNSUPPORTED;
-    otf::cost_split16_kernel<<<(int)nwg, 256, 0, s>>>(
-        Xh, Xl, xs, xx, same ? Xh : Yh, same ? Xl : Yl, same ? xs : ys, same ? xx : yy, ldh, (int)n,
-        (int)m, ldh, metric, zero_diag, C, ldc, (unsigned int*)cmax, tiles_n);
+#define OTF_COST_LAUNCH(NS, TC)                                                                   \
+    otf::cost_split16_kernel<NS, TC><<<(int)nwg, 256, 0, s>>>(                                  \
+        Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldh, (int)n, (int)m, ldh, metric, zero_diag, (TC*)C, ldc, \
+        (unsigned int*)cmax, tiles_n, store_scale)
+    if (split && !f16out) OTF_COST_LAUNCH(3, float);
+    else if (split) OTF_COST_LAUNCH(3, _Float16);
+    else if (!f16out) OTF_COST_LAUNCH(1, float);
+    else OTF_COST_LAUNCH(1, _Float16);
+#undef OTF_COST_LAUNCH
     OTF_HIP(hipGetLastError());
     return OTF_OK;
+}
+
+int otf_cost_pairwise_split16(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
+                              int64_t m, int64_t d, int32_t metric, int32_t zero_diag, float* C,
+                              int64_t ldc, float* cmax, void* workspace, size_t ws_bytes,
+                              otf_stream_t stream) {
+    return otf_cost_pairwise_ex(X, ldx, Y, ldy, OTF_F32, n, m, d, metric, zero_diag, C, ldc,
+                                OTF_F32, cmax, nullptr, workspace, ws_bytes, stream);
 }
 
 int otf_scale_inplace(void* C, int64_t n, int64_t m, int64_t ldc, int32_t dtype, const void* s,

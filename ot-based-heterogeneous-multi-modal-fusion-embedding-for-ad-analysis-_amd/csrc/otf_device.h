@@ -19,6 +19,20 @@ template <> struct Vec<double> {
     using type = __attribute__((ext_vector_type(2))) double;
 };
 
+// VEC consecutive cost values as the compute type: a vector load when the cost is
+// stored in the compute type, else a narrower vector load (fp16 storage: 8 B for 4
+// values) widened in registers.
+template <typename T, typename CT>
+__device__ __forceinline__ typename Vec<T>::type load_cost(const CT* p) {
+    using V = typename Vec<T>::type;
+    if constexpr (sizeof(T) == sizeof(CT)) {
+        return *reinterpret_cast<const V*>(p);
+    } else {
+        using H = __attribute__((ext_vector_type(Vec<T>::N))) CT;
+        return __builtin_convertvector(*reinterpret_cast<const H*>(p), V);
+    }
+}
+
 __device__ __forceinline__ float fast_exp(float x) {
     // x is pre-multiplied by log2(e) by the caller: one v_exp_f32.
     return __builtin_amdgcn_exp2f(x);

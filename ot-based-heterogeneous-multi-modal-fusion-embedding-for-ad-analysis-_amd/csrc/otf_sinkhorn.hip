@@ -34,7 +34,7 @@ namespace otf {
 namespace {
 
 template <typename T> struct SkArgs {
-    const T* C;
+    const void* C;         // cost, element type CT (T, or fp16 storage with fp32 compute)
     int64_t ldc;
     int n, m;
     const T* a;            // padded copy (workspace)
@@ -124,7 +124,7 @@ __device__ __forceinline__ double marginal_err(const SkArgs<T>& p, const T* vit,
 // One fused Sinkhorn pass.  NT threads own G chunks of VEC contiguous columns each
 // (chunk q = tid + NT*g), R rows per row block; K values for a row block stay in
 // registers (R*G*VEC of them) between the row reduction and the column update.
-template <typename T, bool LOG, int G, int R>
+template <typename T, typename CT, bool LOG, int G, int R>
 __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
     constexpr int VEC = Vec<T>::N;
     using V = typename Vec<T>::type;
@@ -198,13 +198,13 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
         const int r0 = rb * R;
         T kv[R][G][VEC];
         if (rb < nrb) {
-            const T* crow = p.C + (int64_t)r0 * p.ldc;
+            const CT* crow = (const CT*)p.C + (int64_t)r0 * p.ldc;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const T* src = (r0 + r < p.n) ? crow : p.C;
+                const CT* src = (r0 + r < p.n) ? crow : (const CT*)p.C;
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    const V c = *reinterpret_cast<const V*>(src + colc[g]);
+                    const V c = load_cost<T>(src + colc[g]);
 #pragma unroll
                     for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
                 }
@@ -383,8 +383,8 @@ __global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, 
 }
 
 // Column minima of C (OTT prologue shift), ordered-int atomicMin per column.
-template <typename T>
-__global__ __launch_bounds__(256) void sk_colmin_kernel(const T* C, int64_t ldc, int n, int m,
+template <typename CT>
+__global__ __launch_bounds__(256) void sk_colmin_kernel(const CT* C, int64_t ldc, int n, int m,
                                                         int* cmin_key) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
@@ -453,8 +453,8 @@ __global__ void sk_output_kernel(const T* u2, const T* v2, int n, int m, int m_p
 }
 
 // POT: P_ij = u_i exp(-C_ij/reg') v_j;  OTT: P_ij = exp((f_i + g_j - C_ij/scale)/reg).
-template <typename T, typename TP, bool LOG>
-__global__ __launch_bounds__(256) void sk_plan_kernel(const T* C, int64_t ldc, int n, int m,
+template <typename T, typename CT, typename TP, bool LOG>
+__global__ __launch_bounds__(256) void sk_plan_kernel(const CT* C, int64_t ldc, int n, int m,
                                                       const T* u, const T* v, const T* cost_scale,
                                                       double reg, TP* P, int64_t ldp) {
     const double unit = exp_unit<T>();
@@ -467,10 +467,10 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const T* C, int64_t ldc, i
     using VP = __attribute__((ext_vector_type(VEC))) TP;
     for (int row = blockIdx.x; row < n; row += gridDim.x) {
         const T ui = u[row];
-        const T* crow = C + (int64_t)row * ldc;
+        const CT* crow = C + (int64_t)row * ldc;
         TP* prow = P + (int64_t)row * ldp;
         for (int j0 = threadIdx.x * VEC; j0 < m; j0 += blockDim.x * VEC) {
-            const V c = *reinterpret_cast<const V*>(crow + j0);
+            const V c = load_cost<T>(crow + j0);
             VP out;
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
@@ -516,7 +516,7 @@ struct SkSync {
 };
 
 template <typename T> struct SkResArgs {
-    const T* C;
+    const void* C;    // cost, element type CT
     int64_t ldc;
     int n, m, m_pad;
     const T* a;
@@ -646,7 +646,7 @@ __device__ __forceinline__ bool xcd_barrier(const SkSync& sy, int xcd, int nx, i
     return *s_flag != 0;
 }
 
-template <typename T, typename TP, int G, int R, int NREP>
+template <typename T, typename CT, typename TP, int G, int R, int NREP>
 __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     constexpr int VEC = Vec<T>::N;
     using V = typename Vec<T>::type;
@@ -683,13 +683,13 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     const int r0 = blockIdx.x * R;
     T kv[R][G][VEC];
     {
-        const T* crow = p.C + (int64_t)r0 * p.ldc;
+        const CT* crow = (const CT*)p.C + (int64_t)r0 * p.ldc;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const T* src = (r0 + r < p.n) ? crow : p.C;
+            const CT* src = (r0 + r < p.n) ? crow : (const CT*)p.C;
 #pragma unroll
             for (int g = 0; g < G; ++g) {
-                const V c = *reinterpret_cast<const V*>(src + colc[g]);
+                const V c = load_cost<T>(src + colc[g]);
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
             }
@@ -1042,13 +1042,13 @@ template <typename T> int64_t row_blocks(int64_t n, int64_t m) {
     return (n + c.R - 1) / c.R;
 }
 
-template <typename T, bool LOG>
+template <typename T, typename CT, bool LOG>
 hipError_t launch_pass(const PassCfg& c, int grid, const SkArgs<T>& p, hipStream_t s) {
     switch (c.G) {
-        case 1: sk_pass_kernel<T, LOG, 1, pass_rows<T>(1)><<<grid, c.NT, 0, s>>>(p); break;
-        case 2: sk_pass_kernel<T, LOG, 2, pass_rows<T>(2)><<<grid, c.NT, 0, s>>>(p); break;
-        case 4: sk_pass_kernel<T, LOG, 4, pass_rows<T>(4)><<<grid, c.NT, 0, s>>>(p); break;
-        case 8: sk_pass_kernel<T, LOG, 8, pass_rows<T>(8)><<<grid, c.NT, 0, s>>>(p); break;
+        case 1: sk_pass_kernel<T, CT, LOG, 1, pass_rows<T>(1)><<<grid, c.NT, 0, s>>>(p); break;
+        case 2: sk_pass_kernel<T, CT, LOG, 2, pass_rows<T>(2)><<<grid, c.NT, 0, s>>>(p); break;
+        case 4: sk_pass_kernel<T, CT, LOG, 4, pass_rows<T>(4)><<<grid, c.NT, 0, s>>>(p); break;
+        case 8: sk_pass_kernel<T, CT, LOG, 8, pass_rows<T>(8)><<<grid, c.NT, 0, s>>>(p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1113,11 +1113,11 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
 // launches get identical residency, and a plain launch replays in a graph at no
 // extra cost).  Every spin in the kernel is bounded, so a grid that cannot become
 // resident (another persistent kernel on the device) ends in OTF_SK_TIMEOUT.
-template <typename T, typename TP, int G, int R>
+template <typename T, typename CT, typename TP, int G, int R>
 hipError_t launch_resident_g(int grid, int nt, SkResArgs<T>& p, hipStream_t s) {
     void* args[] = {&p};
-    const void* k = p.nrep == 1 ? (const void*)sk_resident_kernel<T, TP, G, R, 1>
-                                : (const void*)sk_resident_kernel<T, TP, G, R, OTF_RES_NREP>;
+    const void* k = p.nrep == 1 ? (const void*)sk_resident_kernel<T, CT, TP, G, R, 1>
+                                : (const void*)sk_resident_kernel<T, CT, TP, G, R, OTF_RES_NREP>;
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, nt, 0);
     if (e != hipSuccess) return e;
@@ -1125,20 +1125,20 @@ hipError_t launch_resident_g(int grid, int nt, SkResArgs<T>& p, hipStream_t s) {
     return hipLaunchKernel(k, dim3(grid), dim3(nt), args, 0, s);
 }
 
-template <typename T, typename TP>
+template <typename T, typename CT, typename TP>
 hipError_t launch_resident(const PassCfg& c, int grid, SkResArgs<T>& p, hipStream_t s) {
     switch (c.G) {
-        case 1: return launch_resident_g<T, TP, 1, pass_rows<T>(1)>(grid, c.NT, p, s);
-        case 2: return launch_resident_g<T, TP, 2, pass_rows<T>(2)>(grid, c.NT, p, s);
-        case 4: return launch_resident_g<T, TP, 4, pass_rows<T>(4)>(grid, c.NT, p, s);
+        case 1: return launch_resident_g<T, CT, TP, 1, pass_rows<T>(1)>(grid, c.NT, p, s);
+        case 2: return launch_resident_g<T, CT, TP, 2, pass_rows<T>(2)>(grid, c.NT, p, s);
+        case 4: return launch_resident_g<T, CT, TP, 4, pass_rows<T>(4)>(grid, c.NT, p, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 // Resident solve.  Returns hipSuccess, or the launch error (the caller then falls
 // back to the streaming engine — nothing has been enqueued in that case).
-template <typename T>
-hipError_t run_resident(const PassCfg& cfg, int grid, const T* C, int64_t ldc, int n, int m,
+template <typename T, typename CT>
+hipError_t run_resident(const PassCfg& cfg, int grid, const CT* C, int64_t ldc, int n, int m,
                         const T* cost_scale, const otf_sinkhorn_opts& o, Workspace& w, T* u_out,
                         T* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                         double* errlog, hipStream_t s) {
@@ -1176,12 +1176,12 @@ hipError_t run_resident(const PassCfg& cfg, int grid, const T* C, int64_t ldc, i
     p.timeout_ticks = 500000000ull;  // 5 s at the 100 MHz s_memrealtime clock
     hipError_t e = hipMemsetAsync(w.res, 0, w.res_bytes, s);
     if (e != hipSuccess) return e;
-    if (P_out && P_dtype == OTF_F64) return launch_resident<T, double>(cfg, grid, p, s);
-    return launch_resident<T, float>(cfg, grid, p, s);
+    if (P_out && P_dtype == OTF_F64) return launch_resident<T, CT, double>(cfg, grid, p, s);
+    return launch_resident<T, CT, float>(cfg, grid, p, s);
 }
 
-template <typename T, bool LOG>
-int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64_t ldc,
+template <typename T, typename CT, bool LOG>
+int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_t ldc,
                  const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out, void* P_out,
                  int64_t ldp, int P_dtype, otf_sinkhorn_info* info, double* errlog_user,
                  void* ws, size_t ws_bytes, hipStream_t s, float* avg_pass_ms) {
@@ -1213,7 +1213,7 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
                           (o.engine == OTF_ENGINE_RESIDENT || o.engine == OTF_ENGINE_AUTO);
     if (o.engine == OTF_ENGINE_RESIDENT && (LOG || !fits)) return OTF_EUNSUPPORTED;
     if (want_res) {
-        const hipError_t e = run_resident<T>(cfg, nrb, C, ldc, (int)n, (int)m, cost_scale, o, w,
+        const hipError_t e = run_resident<T, CT>(cfg, nrb, C, ldc, (int)n, (int)m, cost_scale, o, w,
                                              u_out, v_out, P_out, ldp, P_dtype, info, errlog, s);
         if (e == hipSuccess) return OTF_OK;
         (void)hipGetLastError();
@@ -1222,7 +1222,7 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
     }
     if (LOG) {
         dim3 g((unsigned)((m + 255) / 256), (unsigned)(n < 64 ? n : 64));
-        sk_colmin_kernel<T><<<g, 256, 0, s>>>(C, ldc, (int)n, (int)m, w.cmin_key);
+        sk_colmin_kernel<CT><<<g, 256, 0, s>>>(C, ldc, (int)n, (int)m, w.cmin_key);
         OTF_HIP(hipGetLastError());
     }
 
@@ -1267,7 +1267,7 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
         p.u_prev = u2 + (size_t)((it - 1) & 1) * n;
         p.v_prev = v2 + (size_t)((it - 1) & 1) * m_pad;
         if (avg_pass_ms && pass >= 1) OTF_HIP(hipEventRecord(ev0, s));
-        OTF_HIP((launch_pass<T, LOG>(cfg, grid, p, s)));
+        OTF_HIP((launch_pass<T, CT, LOG>(cfg, grid, p, s)));
         if (avg_pass_ms && pass >= 1) {
             OTF_HIP(hipEventRecord(ev1, s));
             OTF_HIP(hipEventSynchronize(ev1));
@@ -1298,10 +1298,10 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
     if (P_out) {
         const int pgrid = n < 4096 ? (int)n : 4096;
         if (P_dtype == OTF_F32)
-            sk_plan_kernel<T, float, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
+            sk_plan_kernel<T, CT, float, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
                                                                cost_scale, o.reg, (float*)P_out, ldp);
         else
-            sk_plan_kernel<T, double, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
+            sk_plan_kernel<T, CT, double, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
                                                                 cost_scale, o.reg, (double*)P_out, ldp);
         OTF_HIP(hipGetLastError());
     }
@@ -1314,20 +1314,35 @@ int run_sinkhorn(const T* a, const T* b, const T* C, int64_t n, int64_t m, int64
     return OTF_OK;
 }
 
+template <typename T, typename CT>
+int dispatch_ct(const void* a, const void* b, const void* C, int64_t n, int64_t m, int64_t ldc,
+                const void* cost_scale, const otf_sinkhorn_opts& o, void* u_out, void* v_out,
+                void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info, double* errlog,
+                void* ws, size_t ws_bytes, hipStream_t s, float* avg_ms) {
+    if (o.flavor == OTF_FLAVOR_POT)
+        return run_sinkhorn<T, CT, false>((const T*)a, (const T*)b, (const CT*)C, n, m, ldc,
+                                          (const T*)cost_scale, o, (T*)u_out, (T*)v_out, P_out, ldp,
+                                          P_dtype, info, errlog, ws, ws_bytes, s, avg_ms);
+    if (o.flavor == OTF_FLAVOR_OTT)
+        return run_sinkhorn<T, CT, true>((const T*)a, (const T*)b, (const CT*)C, n, m, ldc,
+                                         (const T*)cost_scale, o, (T*)u_out, (T*)v_out, P_out, ldp,
+                                         P_dtype, info, errlog, ws, ws_bytes, s, avg_ms);
+    return OTF_EINVAL;
+}
+
+// cost stored as fp16 (opts.cost_f16) is supported with fp32 compute
 template <typename T>
 int dispatch(const void* a, const void* b, const void* C, int64_t n, int64_t m, int64_t ldc,
              const void* cost_scale, const otf_sinkhorn_opts& o, void* u_out, void* v_out,
              void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info, double* errlog,
              void* ws, size_t ws_bytes, hipStream_t s, float* avg_ms) {
-    if (o.flavor == OTF_FLAVOR_POT)
-        return run_sinkhorn<T, false>((const T*)a, (const T*)b, (const T*)C, n, m, ldc,
-                                      (const T*)cost_scale, o, (T*)u_out, (T*)v_out, P_out, ldp,
-                                      P_dtype, info, errlog, ws, ws_bytes, s, avg_ms);
-    if (o.flavor == OTF_FLAVOR_OTT)
-        return run_sinkhorn<T, true>((const T*)a, (const T*)b, (const T*)C, n, m, ldc,
-                                     (const T*)cost_scale, o, (T*)u_out, (T*)v_out, P_out, ldp,
-                                     P_dtype, info, errlog, ws, ws_bytes, s, avg_ms);
-    return OTF_EINVAL;
+    if (!o.cost_f16)
+        return dispatch_ct<T, T>(a, b, C, n, m, ldc, cost_scale, o, u_out, v_out, P_out, ldp,
+                                 P_dtype, info, errlog, ws, ws_bytes, s, avg_ms);
+    if constexpr (sizeof(T) == 4)
+        return dispatch_ct<T, _Float16>(a, b, C, n, m, ldc, cost_scale, o, u_out, v_out, P_out,
+                                        ldp, P_dtype, info, errlog, ws, ws_bytes, s, avg_ms);
+    return OTF_EUNSUPPORTED;
 }
 
 }  // namespace

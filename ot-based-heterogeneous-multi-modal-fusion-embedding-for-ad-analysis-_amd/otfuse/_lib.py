@@ -22,7 +22,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libotfuse.so")
 HEADER_PATH = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "otfuse.h"))
 
 OTF_OK, OTF_EINVAL, OTF_EUNSUPPORTED, OTF_EHIP = 0, 1, 2, -1
-OTF_F32, OTF_F64 = 0, 1
+OTF_F32, OTF_F64, OTF_F16 = 0, 1, 2
 OTF_SQEUCLIDEAN, OTF_EUCLIDEAN = 0, 1
 OTF_FLAVOR_POT, OTF_FLAVOR_OTT = 0, 1
 SK_RUNNING, SK_CONVERGED, SK_MAX_ITER, SK_NUMERICAL_BREAK, SK_TIMEOUT = 0, 1, 2, 3, 4
@@ -37,7 +37,8 @@ class SinkhornOpts(ctypes.Structure):
     _fields_ = [("reg", ctypes.c_double), ("stop_thr", ctypes.c_double),
                 ("max_iter", ctypes.c_int32), ("check_every", ctypes.c_int32),
                 ("flavor", ctypes.c_int32), ("err_squared", ctypes.c_int32),
-                ("sync_every", ctypes.c_int32), ("engine", ctypes.c_int32)]
+                ("sync_every", ctypes.c_int32), ("engine", ctypes.c_int32),
+                ("cost_f16", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "engine", "pad")
@@ -53,6 +54,9 @@ _SIGS = {
     "otf_cost_split16_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64]),
     "otf_cost_pairwise_split16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i32,
                                                  _i32, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
+"otf_cost_ex_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i32]),
+    "otf_cost_pairwise_ex": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i32, _i64, _i64, _i64, _i32, _i32,
+                                            _vp, _i64, _i32, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "otf_scale_inplace": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i32, _vp, _vp]),
     "otf_feature_cost_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i64]),
     "otf_feature_cost": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64,

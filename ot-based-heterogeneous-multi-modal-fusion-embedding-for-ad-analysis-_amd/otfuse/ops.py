@@ -14,8 +14,8 @@ import torch
 
 from . import _lib as L
 
-_VEC = {torch.float32: 4, torch.float64: 2}
-_DT = {torch.float32: L.OTF_F32, torch.float64: L.OTF_F64}
+_VEC = {torch.float32: 4, torch.float64: 2, torch.float16: 8}   # elements per 16 B
+_DT = {torch.float32: L.OTF_F32, torch.float64: L.OTF_F64, torch.float16: L.OTF_F16}
 
 
 def _dev(t: torch.Tensor, name: str):
@@ -62,6 +62,10 @@ def pairwise_cost(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = 
         raise ValueError(f"metric {metric!r} not supported (sqeuclidean | euclidean)")
     if X.dim() != 2 or Y.dim() != 2 or X.shape[1] != Y.shape[1]:
         raise ValueError(f"X {tuple(X.shape)} and Y {tuple(Y.shape)} must be (n, d) and (m, d)")
+    if algo == "split16":
+        C, cmax, _ = pairwise_cost_ex(X, None if same else Y, metric, zero_diag, torch.float32,
+                                      workspace, in_dtype=torch.float32)
+        return C, (cmax if want_max else None)
     X = _rowmajor(X.float(), 4)
     Y = X if same else _rowmajor(Y.float(), 4)
     n, d = X.shape
@@ -70,15 +74,7 @@ def pairwise_cost(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = 
     cmax = torch.empty(1, dtype=torch.float32, device=X.device) if want_max else None
     met = L.OTF_EUCLIDEAN if metric == "euclidean" else L.OTF_SQEUCLIDEAN
     lib = L.lib()
-    if algo == "split16":
-        wsb = lib.otf_cost_split16_workspace_size(n, m, d)
-        if workspace is None or workspace.numel() < wsb:
-            workspace = torch.empty(wsb, dtype=torch.uint8, device=X.device)
-        L.check(lib.otf_cost_pairwise_split16(
-            X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, m, d, met, int(zero_diag),
-            C.data_ptr(), C.stride(0), L.ptr(cmax), workspace.data_ptr(), workspace.numel(),
-            L.stream_handle(X.device)), "otf_cost_pairwise_split16")
-    elif algo == "f32":
+    if algo == "f32":
         L.check(lib.otf_cost_pairwise(
             X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, m, d, met, int(zero_diag),
             C.data_ptr(), C.stride(0), L.ptr(cmax), L.stream_handle(X.device)), "otf_cost_pairwise")
@@ -87,10 +83,55 @@ def pairwise_cost(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = 
     return C, cmax
 
 
+def pairwise_cost_ex(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = "sqeuclidean",
+                     zero_diag: bool | None = None, out_dtype=torch.float32,
+                     workspace: torch.Tensor | None = None, in_dtype=None):
+    """Pairwise cost with fp16 inputs and / or fp16 storage (BASELINE config 5).
+
+    ``in_dtype`` (default: float16 if X is float16 else float32): float32 runs the
+    split-fp16 contraction, float16 the native fp16 MFMA.  ``out_dtype`` float16
+    stores ``C * 2^-k`` (<= 1, k from the row norms).  Returns ``(C, cmax, unit)``:
+    ``cmax`` = max of the stored values (the ``cost_scale`` for "max_cost"),
+    ``unit`` = 2^k (true cost = stored * unit), both device float scalars.
+    """
+    _dev(X, "X")
+    same = Y is None or Y is X
+    Y = X if Y is None else _dev(Y, "Y")
+    if zero_diag is None:
+        zero_diag = same
+    if metric not in ("sqeuclidean", "euclidean"):
+        raise ValueError(f"metric {metric!r} not supported (sqeuclidean | euclidean)")
+    if X.dim() != 2 or Y.dim() != 2 or X.shape[1] != Y.shape[1]:
+        raise ValueError(f"X {tuple(X.shape)} and Y {tuple(Y.shape)} must be (n, d) and (m, d)")
+    if in_dtype is None:
+        in_dtype = torch.float16 if X.dtype == torch.float16 else torch.float32
+    if in_dtype not in (torch.float32, torch.float16) or out_dtype not in (torch.float32, torch.float16):
+        raise TypeError("pairwise_cost_ex: float32 / float16 inputs and outputs only")
+    X = _rowmajor(X.to(in_dtype), 1)
+    Y = X if same else _rowmajor(Y.to(in_dtype), 1)
+    n, d = X.shape
+    m = Y.shape[0]
+    C = _alloc_rowmajor(n, m, out_dtype, X.device, _VEC[out_dtype])
+    cmax = torch.empty(1, dtype=torch.float32, device=X.device)
+    unit = torch.empty(1, dtype=torch.float32, device=X.device)
+    met = L.OTF_EUCLIDEAN if metric == "euclidean" else L.OTF_SQEUCLIDEAN
+    lib = L.lib()
+    wsb = lib.otf_cost_ex_workspace_size(n, m, d, _DT[in_dtype])
+    if workspace is None or workspace.numel() < wsb:
+        workspace = torch.empty(wsb, dtype=torch.uint8, device=X.device)
+    L.check(lib.otf_cost_pairwise_ex(
+        X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), _DT[in_dtype], n, m, d, met,
+        int(zero_diag), C.data_ptr(), C.stride(0), _DT[out_dtype], cmax.data_ptr(), unit.data_ptr(),
+        workspace.data_ptr(), workspace.numel(), L.stream_handle(X.device)), "otf_cost_pairwise_ex")
+    return C, cmax, unit
+
+
 def scale_inplace(C: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
     """``C /= s`` with a device scalar ``s`` (MRI_PET_OT_nojax.py:74-75)."""
     if s.dtype != C.dtype:
         s = s.to(C.dtype)
+    if C.dtype not in (torch.float32, torch.float64):
+        raise TypeError("scale_inplace: C must be float32 or float64")
     L.check(L.lib().otf_scale_inplace(C.data_ptr(), C.shape[0], C.shape[1], C.stride(0),
                                       _DT[C.dtype], s.data_ptr(), L.stream_handle(C.device)),
             "otf_scale_inplace")
@@ -173,14 +214,16 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
     revert-and-break), ``flavor="ott"`` OTT's lse-mode solver (potentials f, g).
 
     ``cost_scale`` (device scalar) divides the cost first (scale_cost="max_cost").
-    Compute dtype = ``C.dtype`` (float32 or float64).
+    Compute dtype = ``C.dtype`` (float32 or float64); a float16 ``C`` (fp16 cost
+    storage, BASELINE config 5) is computed in float32.
     """
     _dev(C, "C")
     if C.dtype not in _VEC:
-        raise TypeError("C must be float32 or float64")
-    dt = C.dtype
+        raise TypeError("C must be float16, float32 or float64")
+    cost_f16 = C.dtype == torch.float16
+    dt = torch.float32 if cost_f16 else C.dtype
     n, m = C.shape
-    C = _rowmajor(C, _VEC[dt])
+    C = _rowmajor(C, _VEC[C.dtype])
     a = _dev(a, "a").to(dt).contiguous()
     b = _dev(b, "b").to(dt).contiguous()
     if a.numel() != n or b.numel() != m:
@@ -204,7 +247,7 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
                           check_every=int(check_every),
                           flavor=L.OTF_FLAVOR_OTT if flavor == "ott" else L.OTF_FLAVOR_POT,
                           err_squared=int(err_squared), sync_every=int(sync_every),
-                          engine=L.ENGINES[engine])
+                          engine=L.ENGINES[engine], cost_f16=int(cost_f16))
     L.check(L.lib().otf_sinkhorn(
         a.data_ptr(), b.data_ptr(), C.data_ptr(), n, m, C.stride(0), _DT[dt], L.ptr(cost_scale),
         ctypes.byref(opts), u.data_ptr(), v.data_ptr(), L.ptr(P), P.stride(0) if P is not None else 0,
@@ -216,9 +259,10 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
 def sinkhorn_profile(a, b, C, reg, iters, cost_scale=None, flavor="pot", workspace=None) -> float:
     """Runs exactly ``iters`` iterations with a HIP event pair around every pass;
     returns the mean pass duration in ms (bench.py's roofline probe)."""
-    dt = C.dtype
+    cost_f16 = C.dtype == torch.float16
+    dt = torch.float32 if cost_f16 else C.dtype
     n, m = C.shape
-    C = _rowmajor(C, _VEC[dt])
+    C = _rowmajor(C, _VEC[C.dtype])
     a = a.to(dt).contiguous()
     b = b.to(dt).contiguous()
     if cost_scale is not None:
@@ -230,7 +274,8 @@ def sinkhorn_profile(a, b, C, reg, iters, cost_scale=None, flavor="pot", workspa
         workspace = sinkhorn_workspace(n, m, dt, iters, C.device)
     opts = L.SinkhornOpts(reg=float(reg), stop_thr=-1.0, max_iter=int(iters), check_every=10,
                           flavor=L.OTF_FLAVOR_OTT if flavor == "ott" else L.OTF_FLAVOR_POT,
-                          err_squared=0, sync_every=0, engine=L.ENGINE_STREAM)
+                          err_squared=0, sync_every=0, engine=L.ENGINE_STREAM,
+                          cost_f16=int(cost_f16))
     avg = ctypes.c_float(0.0)
     L.check(L.lib().otf_sinkhorn_profile(
         a.data_ptr(), b.data_ptr(), C.data_ptr(), n, m, C.stride(0), _DT[dt], L.ptr(cost_scale),

@@ -34,9 +34,10 @@ def test_version_and_workspace_queries_are_host_only():
 def test_abi_structs_and_enums_match_header():
     from otfuse import _lib as L
     src = open(L.HEADER_PATH).read()
-    assert ctypes.sizeof(L.SinkhornOpts) == 40
+    assert ctypes.sizeof(L.SinkhornOpts) == 48
     assert L.INFO_INT32S * 4 == 32
-    for name, val in [("OTF_F32", 0), ("OTF_F64", 1), ("OTF_FLAVOR_POT", 0), ("OTF_FLAVOR_OTT", 1),
+    for name, val in [("OTF_F32", 0), ("OTF_F64", 1), ("OTF_F16", 2), ("OTF_FLAVOR_POT", 0),
+                      ("OTF_FLAVOR_OTT", 1),
                       ("OTF_SK_CONVERGED", 1), ("OTF_SK_MAX_ITER", 2),
                       ("OTF_SK_NUMERICAL_BREAK", 3)]:
         m = re.search(rf"\b{name}\s*=\s*(-?\d+)", src)
@@ -54,6 +55,15 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert rc == L.OTF_EINVAL
     assert lib.otf_cost_pairwise(None, 0, None, 0, 4, 4, 4, 0, 0, None, 4, None, None) == L.OTF_EINVAL
     assert lib.otf_gemm_f32(None, 1, 1, None, 1, 1, None, 1, 1, 1, 1, 1.0, 0.0, None) == L.OTF_EINVAL
+    # fp16 cost entry point: bad dtypes and an undersized workspace are argument errors
+    ws = lib.otf_cost_ex_workspace_size(64, 64, 32, L.OTF_F16)
+    assert ws < lib.otf_cost_ex_workspace_size(64, 64, 32, L.OTF_F32)  # no lo images
+    buf = ctypes.create_string_buffer(16)
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    assert lib.otf_cost_pairwise_ex(p, 32, p, 32, L.OTF_F64, 64, 64, 32, 0, 0, p, 64, L.OTF_F16,
+                                    None, None, p, ws, None) == L.OTF_EINVAL
+    assert lib.otf_cost_pairwise_ex(p, 32, p, 32, L.OTF_F16, 64, 64, 32, 0, 0, p, 64, L.OTF_F16,
+                                    None, None, p, ws - 1, None) == L.OTF_EINVAL
 
 
 def test_group_features_by_label_mirrors_reference():
