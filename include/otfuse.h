@@ -88,7 +88,8 @@ typedef struct {
                            iterations; 0 = never (finished passes no-op)             */
     int32_t engine;     /* otf_engine                                                  */
     int32_t cost_f16;   /* 1: C is stored as fp16 (dtype must be OTF_F32; compute fp32)  */
-    int32_t reserved;   /* 0                                                           */
+    int32_t n_total;    /* row-sharded solve: rows of the whole problem (u0 = 1/n_total);
+                           0 = n                                                      */
 } otf_sinkhorn_opts;
 
 /* Written on the device by otf_sinkhorn (read it after the stream completes). */
@@ -195,6 +196,30 @@ int otf_sinkhorn_profile(const void* a, const void* b, const void* C, int64_t n,
                          const otf_sinkhorn_opts* opts, void* u_out, void* v_out,
                          otf_sinkhorn_info* info, void* workspace, size_t ws_bytes,
                          float* avg_pass_ms, otf_stream_t stream);
+
+/* Row-sharded streaming solve (POT flavour), one pass at a time — the multi-GPU
+ * form of one large coupled problem: each rank owns rows R_r of C
+ * (n = |R_r| rows, a = a[R_r], b and m global, opts->n_total = total rows) and
+ * runs, on its stream,
+ *     for pass in 0 .. max_iter:
+ *         otf_sinkhorn_pass(..., pass, &colsum, &len)   -> pass 0 also initialises
+ *         all-reduce(sum) of colsum[0 .. len)            (len = m_pad + 1 values of
+ *                                                          dtype: the shard's K^T u
+ *                                                          partials + break count)
+ *     otf_sinkhorn_finish(...)                           -> u (local rows), v, P rows
+ * Every rank then takes the same stop / break decisions (they depend only on the
+ * reduced sums), so the result equals otf_sinkhorn on the whole problem.  The
+ * arguments and workspace must be identical in every call of one solve.         */
+int otf_sinkhorn_pass(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                      int64_t ldc, int32_t dtype, const void* cost_scale,
+                      const otf_sinkhorn_opts* opts, int32_t pass, otf_sinkhorn_info* info,
+                      double* errlog, void* workspace, size_t ws_bytes, void** colsum,
+                      int64_t* colsum_len, otf_stream_t stream);
+int otf_sinkhorn_finish(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                        int64_t ldc, int32_t dtype, const void* cost_scale,
+                        const otf_sinkhorn_opts* opts, void* u_out, void* v_out, void* P_out,
+                        int64_t ldp, int32_t P_dtype, otf_sinkhorn_info* info, double* errlog,
+                        void* workspace, size_t ws_bytes, otf_stream_t stream);
 
 /* Plan post-processing (MRI_PET_OT_nojax.py:702-715): T (d x d2, ldt, dtype
  * float32/64) -> Tn float32 (ldtn): NaN -> nan_fill, row sums (0 -> 1e-8),

@@ -37,13 +37,17 @@ template <typename T> struct SkArgs {
     const void* C;         // cost, element type CT (T, or fp16 storage with fp32 compute)
     int64_t ldc;
     int n, m;
+    int n_total;           // rows of the whole problem (u0 = 1/n_total; > n when row-sharded)
     const T* a;            // padded copy (workspace)
     const T* b;            // padded copy, zero beyond m (workspace)
     const T* cost_scale;   // device scalar; cost is C / cost_scale (nullable)
     double reg;
     int it;                // iteration index ii; -1 = prologue pass
-    const T* cs_src;       // column sums accumulated by the previous pass
-    T* cs_dst;             // column sums accumulated by this pass
+    // column-sum buffers, m_pad + 1 wide: [0, m) sums K^T u, [m_pad] number of rows
+    // whose scaling in that iteration is not finite (one buffer = one all-reduce in
+    // the row-sharded solve)
+    const T* cs_src;       // accumulated by the previous pass
+    T* cs_dst;             // accumulated by this pass
     T* cs_zero;            // zeroed by this pass (accumulated by the next)
     T* u_cur;              // u (POT) / f (OTT) of iteration it
     T* v_cur;              // v / g of iteration it
@@ -51,7 +55,6 @@ template <typename T> struct SkArgs {
     const T* v_prev;       // v / g of iteration it-1
     const int* cmin_key;   // OTT prologue: ordered-int column minima of C
     otf_sinkhorn_info* info;
-    int* bad;              // bad[it] = 1 if the row scaling of iteration it is not finite
     double* errlog;
     double stop_thr;
     int check_every;
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
     // ---- decisions about iteration it-1 (identical in every workgroup)
     if (p.it >= 1) {
         const int prev = p.it - 1;
-        if (p.bad[prev]) {  // row scaling of prev not finite: revert to prev-1, stop
+        if (p.cs_src[p.m_pad] != (T)0) {  // row scaling of prev not finite: revert to prev-1, stop
             if (lead) sk_stop(p.info, prev - 1, prev, OTF_SK_NUMERICAL_BREAK, prev);
             return;
         }
@@ -317,11 +320,11 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
                 const int row = r0 + tid;
                 if (row < p.n) {
                     p.u_cur[row] = mine;
-                    if (!finite_val(mine) || !finite_val(wmine)) p.bad[p.it] = 1;
+                    if (!finite_val(mine) || !finite_val(wmine)) atomicAdd(p.cs_dst + p.m_pad, (T)1);
                 }
             }
         } else {
-            const T u0 = LOG ? (T)1 : (T)1 / (T)p.n;
+            const T u0 = LOG ? (T)1 : (T)1 / (T)p.n_total;
 #pragma unroll
             for (int r = 0; r < R; ++r) ur[r] = u0;
         }
@@ -350,18 +353,18 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
     for (int j = tid; j < p.m; j += NT) atomicAdd(p.cs_dst + j, colbuf[j]);
 
     // ---- zero the column-sum buffer of the next pass (nobody touches it now)
-    for (int j = blockIdx.x * NT + tid; j < p.m_pad; j += gridDim.x * NT) p.cs_zero[j] = 0;
+    for (int j = blockIdx.x * NT + tid; j <= p.m_pad; j += gridDim.x * NT) p.cs_zero[j] = 0;
 }
 
 template <typename T>
 __global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, T* a_pad, T* b_pad,
-                               T* cs, T* u2, T* v2, int* bad, int nbad, int* cmin_key,
+                               T* cs, int cs_stride, T* u2, T* v2, int* cmin_key,
                                otf_sinkhorn_info* info) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int stride = gridDim.x * blockDim.x;
     for (int j = t; j < m_pad; j += stride) {
         b_pad[j] = j < m ? b[j] : (T)0;
-        cs[j] = cs[m_pad + j] = cs[2 * m_pad + j] = 0;
+        cs[j] = cs[cs_stride + j] = cs[2 * cs_stride + j] = 0;
         v2[j] = v2[m_pad + j] = 0;
         cmin_key[j] = 0x7fffffff;
     }
@@ -369,7 +372,7 @@ __global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, 
         a_pad[i] = a[i];
         u2[i] = u2[n + i] = 0;
     }
-    for (int j = t; j < nbad; j += stride) bad[j] = 0;
+    if (t < 3) cs[t * cs_stride + m_pad] = 0;
     if (t == 0) {
         info->stop = 0;
         info->last_good = -1;
@@ -410,7 +413,7 @@ __global__ __launch_bounds__(512) void sk_finalize_kernel(SkArgs<T> p, int max_i
         return;
     }
     const int it = max_iter - 1;
-    if (p.bad[it]) {
+    if (p.cs_src[p.m_pad] != (T)0) {
         if (lead) sk_stop(p.info, it - 1, it, OTF_SK_NUMERICAL_BREAK, it);
         return;
     }
@@ -441,12 +444,12 @@ __global__ __launch_bounds__(512) void sk_finalize_kernel(SkArgs<T> p, int max_i
 
 // Copies the scalings of info->last_good (or the initial ones) to the outputs.
 template <typename T, bool LOG>
-__global__ void sk_output_kernel(const T* u2, const T* v2, int n, int m, int m_pad,
+__global__ void sk_output_kernel(const T* u2, const T* v2, int n, int n_total, int m, int m_pad,
                                  const otf_sinkhorn_info* info, T* u_out, T* v_out) {
     const int lg = info->last_good;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int stride = gridDim.x * blockDim.x;
-    const T u0 = LOG ? (T)0 : (T)1 / (T)n;
+    const T u0 = LOG ? (T)0 : (T)1 / (T)n_total;
     const T v0 = LOG ? (T)0 : (T)1 / (T)m;
     for (int i = t; i < n; i += stride) u_out[i] = lg >= 0 ? u2[(lg & 1) * n + i] : u0;
     for (int j = t; j < m; j += stride) v_out[j] = lg >= 0 ? v2[(lg & 1) * m_pad + j] : v0;
@@ -1062,7 +1065,7 @@ struct Workspace {
     void* cs;
     void* u2;
     void* v2;
-    int* bad;
+    int64_t cs_stride;  // m_pad + 64: the break-count slot and alignment
     int* cmin_key;
     double* errlog;
     void* res;        // resident engine: sums (max_iter+1) x m_pad | bad_cnt | barrier
@@ -1094,11 +1097,11 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.m_pad = (int64_t)align_up((size_t)m, 64);
     w.a_pad = take(n * esz);
     w.b_pad = take(w.m_pad * esz);
-    w.cs = take(3 * w.m_pad * esz);
+    w.cs_stride = w.m_pad + 64;
+    w.cs = take(3 * w.cs_stride * esz);
     w.u2 = take(2 * n * esz);
     w.v2 = take(2 * w.m_pad * esz);
     w.cmin_key = (int*)take(sizeof(int) * (size_t)w.m_pad);
-    w.bad = (int*)take(sizeof(int) * (size_t)(max_iter + 2));
     w.errlog = (double*)take(sizeof(double) * (size_t)(max_iter + 2));
     w.nrep = res_replicas(nrb);
     w.res_bytes = align_up((size_t)(max_iter + 1) * w.nrep * w.m_pad * esz, 256) +
@@ -1180,41 +1183,140 @@ hipError_t run_resident(const PassCfg& cfg, int grid, const CT* C, int64_t ldc, 
     return launch_resident<T, CT, float>(cfg, grid, p, s);
 }
 
+// Validated shape / workspace of one solve (deterministic in n, m, max_iter).
+template <typename T> struct SkSetup {
+    PassCfg cfg;
+    int nrb, grid, m_pad;
+    Workspace w;
+};
+
+template <typename T, typename CT>
+int sk_prepare(const void* a, const void* b, const CT* C, int64_t n, int64_t m, int64_t ldc,
+               const otf_sinkhorn_opts& o, const otf_sinkhorn_info* info, void* ws,
+               size_t ws_bytes, SkSetup<T>& su) {
+    constexpr int VEC = Vec<T>::N;
+    if (n <= 0 || m <= 0 || !a || !b || !C || !info || !ws) return OTF_EINVAL;
+    if (ldc < m || ldc % VEC != 0 || ((uintptr_t)C % 16) != 0) return OTF_EINVAL;
+    if (!(o.reg > 0.0) || o.max_iter < 0 || o.check_every <= 0) return OTF_EINVAL;
+    if (n > INT32_MAX || m > (int64_t)kPassThreads * kMaxG * VEC) return OTF_EUNSUPPORTED;
+    su.cfg = pick_cfg<T>((int)m);
+    su.nrb = (int)((n + su.cfg.R - 1) / su.cfg.R);
+    su.w = carve(ws, n, m, sizeof(T), o.max_iter, su.nrb);
+    if (ws_bytes < su.w.bytes) return OTF_EINVAL;
+    su.m_pad = (int)su.w.m_pad;
+    su.grid = su.nrb < device_cu_count() ? su.nrb : device_cu_count();
+    return OTF_OK;
+}
+
+template <typename T, typename CT, bool LOG>
+SkArgs<T> sk_args(const SkSetup<T>& su, const CT* C, int64_t ldc, int64_t n, int64_t m,
+                  const T* cost_scale, const otf_sinkhorn_opts& o, otf_sinkhorn_info* info,
+                  double* errlog, bool profile) {
+    SkArgs<T> p{};
+    p.C = C;
+    p.ldc = ldc;
+    p.n = (int)n;
+    p.n_total = o.n_total > 0 ? o.n_total : (int)n;
+    p.m = (int)m;
+    p.a = (const T*)su.w.a_pad;
+    p.b = (const T*)su.w.b_pad;
+    p.cost_scale = cost_scale;
+    p.reg = o.reg;
+    p.cmin_key = su.w.cmin_key;
+    p.info = info;
+    p.errlog = errlog ? errlog : su.w.errlog;
+    p.stop_thr = profile ? -1.0 : o.stop_thr;
+    p.check_every = o.check_every;
+    p.check_off = LOG ? 1 : 0;
+    p.err_squared = LOG ? 0 : o.err_squared;
+    p.m_pad = su.m_pad;
+    return p;
+}
+
+// Buffers of pass `pass` (iteration it = pass - 1; pass 0 is the prologue).
+template <typename T>
+void sk_set_pass(SkArgs<T>& p, const SkSetup<T>& su, int pass) {
+    T* cs = (T*)su.w.cs;
+    T* u2 = (T*)su.w.u2;
+    T* v2 = (T*)su.w.v2;
+    const size_t st = (size_t)su.w.cs_stride;
+    const int it = pass - 1;
+    p.it = it;
+    p.cs_src = pass >= 1 ? cs + (size_t)((pass - 1) % 3) * st : nullptr;
+    p.cs_dst = cs + (size_t)(pass % 3) * st;
+    p.cs_zero = cs + (size_t)((pass + 1) % 3) * st;
+    // iteration it writes slot (it & 1); the prologue (it = -1) writes slot 1 (OTT g_{-1})
+    p.u_cur = u2 + (size_t)(it & 1) * p.n;
+    p.v_cur = v2 + (size_t)(it & 1) * su.m_pad;
+    p.u_prev = u2 + (size_t)((it - 1) & 1) * p.n;
+    p.v_prev = v2 + (size_t)((it - 1) & 1) * su.m_pad;
+}
+
+template <typename T>
+int sk_init(const SkSetup<T>& su, const T* a, const T* b, int64_t n, int64_t m,
+            otf_sinkhorn_info* info, hipStream_t s) {
+    sk_init_kernel<T><<<64, 256, 0, s>>>(a, b, (int)n, (int)m, su.m_pad, (T*)su.w.a_pad,
+                                         (T*)su.w.b_pad, (T*)su.w.cs, (int)su.w.cs_stride,
+                                         (T*)su.w.u2, (T*)su.w.v2, su.w.cmin_key, info);
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+// After the last pass: decide the last iteration, write (u, v) and the plan.
+template <typename T, typename CT, bool LOG>
+int sk_finish(SkArgs<T>& p, const SkSetup<T>& su, const CT* C, int64_t ldc, int64_t n, int64_t m,
+              const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out, void* P_out,
+              int64_t ldp, int P_dtype, otf_sinkhorn_info* info, hipStream_t s) {
+    // pass max_iter (iteration max_iter-1) accumulated into cs[max_iter % 3]
+    sk_set_pass(p, su, o.max_iter + 1);
+    p.it = o.max_iter - 1;
+    p.v_cur = (T*)su.w.v2 + (size_t)(p.it & 1) * su.m_pad;
+    sk_finalize_kernel<T, LOG><<<1, 512, 0, s>>>(p, o.max_iter);
+    OTF_HIP(hipGetLastError());
+    sk_output_kernel<T, LOG><<<64, 256, 0, s>>>((const T*)su.w.u2, (const T*)su.w.v2, (int)n,
+                                                p.n_total, (int)m, su.m_pad, info, u_out, v_out);
+    OTF_HIP(hipGetLastError());
+    if (P_out) {
+        const int pgrid = n < 4096 ? (int)n : 4096;
+        if (P_dtype == OTF_F32)
+            sk_plan_kernel<T, CT, float, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
+                                                                   cost_scale, o.reg, (float*)P_out, ldp);
+        else
+            sk_plan_kernel<T, CT, double, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out,
+                                                                    v_out, cost_scale, o.reg,
+                                                                    (double*)P_out, ldp);
+        OTF_HIP(hipGetLastError());
+    }
+    return OTF_OK;
+}
+
 template <typename T, typename CT, bool LOG>
 int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_t ldc,
                  const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out, void* P_out,
                  int64_t ldp, int P_dtype, otf_sinkhorn_info* info, double* errlog_user,
                  void* ws, size_t ws_bytes, hipStream_t s, float* avg_pass_ms) {
     constexpr int VEC = Vec<T>::N;
-    if (n <= 0 || m <= 0 || !a || !b || !C || !u_out || !v_out || !info || !ws) return OTF_EINVAL;
-    if (ldc < m || ldc % VEC != 0 || ((uintptr_t)C % 16) != 0) return OTF_EINVAL;
-    if (!(o.reg > 0.0) || o.max_iter < 0 || o.check_every <= 0) return OTF_EINVAL;
+    if (!u_out || !v_out) return OTF_EINVAL;
     if (P_out && (ldp < m || ldp % VEC != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
-    if (n > INT32_MAX || m > (int64_t)kPassThreads * kMaxG * VEC) return OTF_EUNSUPPORTED;
-    const PassCfg cfg = pick_cfg<T>((int)m);
-    const int nrb = (int)((n + cfg.R - 1) / cfg.R);
-    Workspace w = carve(ws, n, m, sizeof(T), o.max_iter, nrb);
-    if (ws_bytes < w.bytes) return OTF_EINVAL;
-    double* errlog = errlog_user ? errlog_user : w.errlog;
-    const int m_pad = (int)w.m_pad;
-    const int grid = nrb < device_cu_count() ? nrb : device_cu_count();
-    T* cs = (T*)w.cs;
-    T* u2 = (T*)w.u2;
-    T* v2 = (T*)w.v2;
-
-    sk_init_kernel<T><<<64, 256, 0, s>>>(a, b, (int)n, (int)m, m_pad, (T*)w.a_pad, (T*)w.b_pad, cs,
-                                         u2, v2, w.bad, o.max_iter + 2, w.cmin_key, info);
-    OTF_HIP(hipGetLastError());
+    SkSetup<T> su;
+    int rc = sk_prepare<T, CT>(a, b, C, n, m, ldc, o, info, ws, ws_bytes, su);
+    if (rc != OTF_OK) return rc;
+    double* errlog = errlog_user ? errlog_user : su.w.errlog;
+    rc = sk_init<T>(su, a, b, n, m, info, s);
+    if (rc != OTF_OK) return rc;
 
     // resident engine: the whole solve in one persistent launch when every row block
     // gets its own CU (POT flavour, no per-pass profiling requested)
-    const bool fits = nrb <= device_cu_count() && cfg.G <= 4;
+    const bool fits = su.nrb <= device_cu_count() && su.cfg.G <= 4 &&
+                      (o.n_total <= 0 || o.n_total == n);
     const bool want_res = !LOG && !avg_pass_ms && fits && o.max_iter >= 1 &&
                           (o.engine == OTF_ENGINE_RESIDENT || o.engine == OTF_ENGINE_AUTO);
     if (o.engine == OTF_ENGINE_RESIDENT && (LOG || !fits)) return OTF_EUNSUPPORTED;
     if (want_res) {
-        const hipError_t e = run_resident<T, CT>(cfg, nrb, C, ldc, (int)n, (int)m, cost_scale, o, w,
-                                             u_out, v_out, P_out, ldp, P_dtype, info, errlog, s);
+        Workspace w = su.w;
+        const hipError_t e = run_resident<T, CT>(su.cfg, su.nrb, C, ldc, (int)n, (int)m, cost_scale,
+                                                 o, w, u_out, v_out, P_out, ldp, P_dtype, info,
+                                                 errlog, s);
         if (e == hipSuccess) return OTF_OK;
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_RESIDENT) return check_hip(e);
@@ -1222,28 +1324,10 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     }
     if (LOG) {
         dim3 g((unsigned)((m + 255) / 256), (unsigned)(n < 64 ? n : 64));
-        sk_colmin_kernel<CT><<<g, 256, 0, s>>>(C, ldc, (int)n, (int)m, w.cmin_key);
+        sk_colmin_kernel<CT><<<g, 256, 0, s>>>(C, ldc, (int)n, (int)m, su.w.cmin_key);
         OTF_HIP(hipGetLastError());
     }
-
-    SkArgs<T> p{};
-    p.C = C;
-    p.ldc = ldc;
-    p.n = (int)n;
-    p.m = (int)m;
-    p.a = (const T*)w.a_pad;
-    p.b = (const T*)w.b_pad;
-    p.cost_scale = cost_scale;
-    p.reg = o.reg;
-    p.cmin_key = w.cmin_key;
-    p.info = info;
-    p.bad = w.bad;
-    p.errlog = errlog;
-    p.stop_thr = avg_pass_ms ? -1.0 : o.stop_thr;
-    p.check_every = o.check_every;
-    p.check_off = LOG ? 1 : 0;
-    p.err_squared = LOG ? 0 : o.err_squared;
-    p.m_pad = m_pad;
+    SkArgs<T> p = sk_args<T, CT, LOG>(su, C, ldc, n, m, cost_scale, o, info, errlog, avg_pass_ms);
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double total_ms = 0.0;
@@ -1256,18 +1340,9 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     if (o.sync_every > 0) OTF_HIP(hipHostMalloc((void**)&host_stop, sizeof(int), hipHostMallocDefault));
 
     for (int pass = 0; pass <= o.max_iter; ++pass) {
-        const int it = pass - 1;
-        p.it = it;
-        p.cs_src = pass >= 1 ? cs + (size_t)((pass - 1) % 3) * m_pad : nullptr;
-        p.cs_dst = cs + (size_t)(pass % 3) * m_pad;
-        p.cs_zero = cs + (size_t)((pass + 1) % 3) * m_pad;
-        // iteration it writes slot (it & 1); the prologue (it = -1) writes slot 1 (OTT g_{-1})
-        p.u_cur = u2 + (size_t)(it & 1) * n;
-        p.v_cur = v2 + (size_t)(it & 1) * m_pad;
-        p.u_prev = u2 + (size_t)((it - 1) & 1) * n;
-        p.v_prev = v2 + (size_t)((it - 1) & 1) * m_pad;
+        sk_set_pass(p, su, pass);
         if (avg_pass_ms && pass >= 1) OTF_HIP(hipEventRecord(ev0, s));
-        OTF_HIP((launch_pass<T, CT, LOG>(cfg, grid, p, s)));
+        OTF_HIP((launch_pass<T, CT, LOG>(su.cfg, su.grid, p, s)));
         if (avg_pass_ms && pass >= 1) {
             OTF_HIP(hipEventRecord(ev1, s));
             OTF_HIP(hipEventSynchronize(ev1));
@@ -1283,28 +1358,9 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         }
     }
     if (host_stop) OTF_HIP(hipHostFree(host_stop));
-
-    // finalize: pass max_iter (iteration max_iter-1) accumulated into cs[max_iter % 3]
-    {
-        const int it = o.max_iter - 1;
-        p.it = it;
-        p.cs_src = cs + (size_t)(o.max_iter % 3) * m_pad;
-        p.v_cur = v2 + (size_t)(it & 1) * m_pad;
-        sk_finalize_kernel<T, LOG><<<1, 512, 0, s>>>(p, o.max_iter);
-        OTF_HIP(hipGetLastError());
-    }
-    sk_output_kernel<T, LOG><<<64, 256, 0, s>>>(u2, v2, (int)n, (int)m, m_pad, info, u_out, v_out);
-    OTF_HIP(hipGetLastError());
-    if (P_out) {
-        const int pgrid = n < 4096 ? (int)n : 4096;
-        if (P_dtype == OTF_F32)
-            sk_plan_kernel<T, CT, float, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
-                                                               cost_scale, o.reg, (float*)P_out, ldp);
-        else
-            sk_plan_kernel<T, CT, double, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
-                                                                cost_scale, o.reg, (double*)P_out, ldp);
-        OTF_HIP(hipGetLastError());
-    }
+    rc = sk_finish<T, CT, LOG>(p, su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype,
+                               info, s);
+    if (rc != OTF_OK) return rc;
     if (avg_pass_ms) {
         OTF_HIP(hipStreamSynchronize(s));
         *avg_pass_ms = timed ? (float)(total_ms / timed) : 0.f;
@@ -1312,6 +1368,49 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         (void)hipEventDestroy(ev1);
     }
     return OTF_OK;
+}
+
+// One pass of the row-sharded streaming solve (POT flavour).  Pass 0 also runs the
+// init kernel.  *colsum receives this pass's column-sum buffer (m_pad + 1 values of
+// dtype: the partial K^T u of this shard's rows and the break count), which the
+// caller all-reduces (sum) across the shards before the next pass.
+template <typename T, typename CT>
+int sk_pass_api(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_t ldc,
+                const T* cost_scale, const otf_sinkhorn_opts& o, int pass,
+                otf_sinkhorn_info* info, double* errlog, void* ws, size_t ws_bytes, void** colsum,
+                int64_t* colsum_len, hipStream_t s) {
+    if (o.flavor != OTF_FLAVOR_POT) return OTF_EUNSUPPORTED;
+    if (pass < 0 || pass > o.max_iter) return OTF_EINVAL;
+    SkSetup<T> su;
+    int rc = sk_prepare<T, CT>(a, b, C, n, m, ldc, o, info, ws, ws_bytes, su);
+    if (rc != OTF_OK) return rc;
+    if (pass == 0) {
+        rc = sk_init<T>(su, a, b, n, m, info, s);
+        if (rc != OTF_OK) return rc;
+    }
+    SkArgs<T> p = sk_args<T, CT, false>(su, C, ldc, n, m, cost_scale, o, info, errlog, false);
+    sk_set_pass(p, su, pass);
+    OTF_HIP((launch_pass<T, CT, false>(su.cfg, su.grid, p, s)));
+    if (colsum) *colsum = p.cs_dst;
+    if (colsum_len) *colsum_len = su.m_pad + 1;
+    return OTF_OK;
+}
+
+template <typename T, typename CT>
+int sk_finish_api(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_t ldc,
+                  const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out, void* P_out,
+                  int64_t ldp, int P_dtype, otf_sinkhorn_info* info, double* errlog, void* ws,
+                  size_t ws_bytes, hipStream_t s) {
+    constexpr int VEC = Vec<T>::N;
+    if (o.flavor != OTF_FLAVOR_POT) return OTF_EUNSUPPORTED;
+    if (!u_out || !v_out) return OTF_EINVAL;
+    if (P_out && (ldp < m || ldp % VEC != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
+    SkSetup<T> su;
+    int rc = sk_prepare<T, CT>(a, b, C, n, m, ldc, o, info, ws, ws_bytes, su);
+    if (rc != OTF_OK) return rc;
+    SkArgs<T> p = sk_args<T, CT, false>(su, C, ldc, n, m, cost_scale, o, info, errlog, false);
+    return sk_finish<T, CT, false>(p, su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp,
+                                   P_dtype, info, s);
 }
 
 template <typename T, typename CT>
@@ -1387,6 +1486,56 @@ int otf_sinkhorn_profile(const void* a, const void* b, const void* C, int64_t n,
     if (dtype == OTF_F64)
         return otf::dispatch<double>(a, b, C, n, m, ldc, cost_scale, o, u_out, v_out, nullptr, 0,
                                      OTF_F64, info, nullptr, workspace, ws_bytes, s, avg_pass_ms);
+    return OTF_EINVAL;
+}
+
+int otf_sinkhorn_pass(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                      int64_t ldc, int32_t dtype, const void* cost_scale,
+                      const otf_sinkhorn_opts* opts, int32_t pass, otf_sinkhorn_info* info,
+                      double* errlog, void* workspace, size_t ws_bytes, void** colsum,
+                      int64_t* colsum_len, otf_stream_t stream) {
+    if (!opts) return OTF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const otf_sinkhorn_opts& o = *opts;
+    if (dtype == OTF_F32 && o.cost_f16)
+        return otf::sk_pass_api<float, _Float16>((const float*)a, (const float*)b, (const _Float16*)C,
+                                                 n, m, ldc, (const float*)cost_scale, o, pass, info,
+                                                 errlog, workspace, ws_bytes, colsum, colsum_len, s);
+    if (dtype == OTF_F32)
+        return otf::sk_pass_api<float, float>((const float*)a, (const float*)b, (const float*)C, n, m,
+                                              ldc, (const float*)cost_scale, o, pass, info, errlog,
+                                              workspace, ws_bytes, colsum, colsum_len, s);
+    if (dtype == OTF_F64 && !o.cost_f16)
+        return otf::sk_pass_api<double, double>((const double*)a, (const double*)b, (const double*)C,
+                                                n, m, ldc, (const double*)cost_scale, o, pass, info,
+                                                errlog, workspace, ws_bytes, colsum, colsum_len, s);
+    return OTF_EINVAL;
+}
+
+int otf_sinkhorn_finish(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                        int64_t ldc, int32_t dtype, const void* cost_scale,
+                        const otf_sinkhorn_opts* opts, void* u_out, void* v_out, void* P_out,
+                        int64_t ldp, int32_t P_dtype, otf_sinkhorn_info* info, double* errlog,
+                        void* workspace, size_t ws_bytes, otf_stream_t stream) {
+    if (!opts) return OTF_EINVAL;
+    if (P_out && P_dtype != OTF_F32 && P_dtype != OTF_F64) return OTF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const otf_sinkhorn_opts& o = *opts;
+    if (dtype == OTF_F32 && o.cost_f16)
+        return otf::sk_finish_api<float, _Float16>((const float*)a, (const float*)b, (const _Float16*)C,
+                                                   n, m, ldc, (const float*)cost_scale, o, (float*)u_out,
+                                                   (float*)v_out, P_out, ldp, P_dtype, info, errlog,
+                                                   workspace, ws_bytes, s);
+    if (dtype == OTF_F32)
+        return otf::sk_finish_api<float, float>((const float*)a, (const float*)b, (const float*)C, n, m,
+                                                ldc, (const float*)cost_scale, o, (float*)u_out,
+                                                (float*)v_out, P_out, ldp, P_dtype, info, errlog,
+                                                workspace, ws_bytes, s);
+    if (dtype == OTF_F64 && !o.cost_f16)
+        return otf::sk_finish_api<double, double>((const double*)a, (const double*)b, (const double*)C,
+                                                  n, m, ldc, (const double*)cost_scale, o,
+                                                  (double*)u_out, (double*)v_out, P_out, ldp, P_dtype,
+                                                  info, errlog, workspace, ws_bytes, s);
     return OTF_EINVAL;
 }
 

@@ -38,7 +38,7 @@ class SinkhornOpts(ctypes.Structure):
                 ("max_iter", ctypes.c_int32), ("check_every", ctypes.c_int32),
                 ("flavor", ctypes.c_int32), ("err_squared", ctypes.c_int32),
                 ("sync_every", ctypes.c_int32), ("engine", ctypes.c_int32),
-                ("cost_f16", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("cost_f16", ctypes.c_int32), ("n_total", ctypes.c_int32)]
 
 
 INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "engine", "pad")
@@ -68,6 +68,13 @@ _SIGS = {
     "otf_sinkhorn_profile": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
                                             ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _vp,
                                             ctypes.c_size_t, ctypes.POINTER(ctypes.c_float), _vp]),
+    "otf_sinkhorn_pass": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
+                                         ctypes.POINTER(SinkhornOpts), _i32, _vp, _vp, _vp,
+                                         ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+                                         ctypes.POINTER(ctypes.c_int64), _vp]),
+    "otf_sinkhorn_finish": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
+                                           ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _i64, _i32,
+                                           _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "otf_plan_postprocess": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i32, ctypes.c_float, _i32,
                                             _vp, _i64, _vp]),
     "otf_gemm_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64,

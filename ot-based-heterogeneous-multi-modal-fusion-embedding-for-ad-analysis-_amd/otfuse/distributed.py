@@ -12,14 +12,24 @@ the path actually needs:
   of the d x d2 float64 partials (1 MiB at d = 512... 32 MiB at d = 2048) replaces
   gathering the embeddings.  The Sinkhorn solve is then replicated (it is tiny).
 
+* ``sinkhorn_row_sharded`` — ONE large coupled problem (BASELINE config 5) with the
+  cost rows split over the ranks: per iteration the only exchange is an
+  all-reduce(SUM) of the column sums K^T u (m + 1 values incl. the break count);
+  every rank then takes the same stop / break decisions.  ``coupled_solve_sharded``
+  is the whole per-epoch pipeline: all-gather the PET embedding shards, build this
+  rank's cost rows, agree on the global max, solve.
+
 Independent problems (per-rank minibatches / labels) need no collective at all;
 bench.py scales that way ("weak", replicas).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.distributed as dist
 
+from . import _lib as L
 from . import ops
 
 
@@ -76,3 +86,123 @@ def gather_epoch_features(mri_local: torch.Tensor, pet_local: torch.Tensor,
     (feature_extract, MRI_PET_OT_OT_per_epoch_attn.py:889-912, run data-parallel)."""
     return (all_gather_rows(mri_local, group), all_gather_rows(pet_local, group),
             all_gather_rows(labels_local, group))
+
+
+# --------------------------------------------------------------------------- row-sharded solve
+class DevicePasses:
+    """HIP backend of ``sinkhorn_row_sharded``: otf_sinkhorn_pass / otf_sinkhorn_finish
+    on this rank's rows (include/otfuse.h)."""
+
+    def __init__(self, a_local, b, C_local, reg, max_iter, stop_thr, cost_scale, n_total,
+                 check_every=10, err_squared=False):
+        ops._dev(C_local, "C_local")
+        if C_local.dtype not in ops._VEC:
+            raise TypeError("C_local must be float16, float32 or float64")
+        self.cost_f16 = C_local.dtype == torch.float16
+        self.dt = torch.float32 if self.cost_f16 else C_local.dtype
+        self.n, self.m = C_local.shape
+        self.C = ops._rowmajor(C_local, ops._VEC[C_local.dtype])
+        self.a = a_local.to(self.C.device, self.dt).contiguous()
+        self.b = b.to(self.C.device, self.dt).contiguous()
+        if self.a.numel() != self.n or self.b.numel() != self.m:
+            raise ValueError("a_local / b do not match C_local")
+        self.cost_scale = None if cost_scale is None else cost_scale.to(self.dt).contiguous()
+        dev = self.C.device
+        self.ws = ops.sinkhorn_workspace(self.n, self.m, self.dt, max_iter, dev)
+        self.info = torch.empty(L.INFO_INT32S, dtype=torch.int32, device=dev)
+        self.errlog = torch.zeros(max_iter // max(check_every, 1) + 2, dtype=torch.float64, device=dev)
+        self.opts = L.SinkhornOpts(reg=float(reg), stop_thr=float(stop_thr), max_iter=int(max_iter),
+                                   check_every=int(check_every), flavor=L.OTF_FLAVOR_POT,
+                                   err_squared=int(err_squared), sync_every=0,
+                                   engine=L.ENGINE_STREAM, cost_f16=int(self.cost_f16),
+                                   n_total=int(n_total))
+        self._esz = torch.empty((), dtype=self.dt).element_size()
+
+    def _common(self):
+        return (self.a.data_ptr(), self.b.data_ptr(), self.C.data_ptr(), self.n, self.m,
+                self.C.stride(0), ops._DT[self.dt], L.ptr(self.cost_scale))
+
+    def run_pass(self, p: int) -> torch.Tensor:
+        """Enqueue pass p; returns the (m_pad + 1) column-sum buffer to all-reduce."""
+        ptr = ctypes.c_void_p()
+        ln = ctypes.c_int64()
+        L.check(L.lib().otf_sinkhorn_pass(
+            *self._common(), ctypes.byref(self.opts), int(p), self.info.data_ptr(),
+            self.errlog.data_ptr(), self.ws.data_ptr(), self.ws.numel(), ctypes.byref(ptr),
+            ctypes.byref(ln), L.stream_handle(self.C.device)), "otf_sinkhorn_pass")
+        off = ptr.value - self.ws.data_ptr()
+        return self.ws[off: off + ln.value * self._esz].view(self.dt)
+
+    def stopped(self) -> bool:
+        return bool(self.info[0].item())
+
+    def finish(self, want_plan=True, plan_dtype=None) -> ops.SinkhornResult:
+        dev = self.C.device
+        u = torch.empty(self.n, dtype=self.dt, device=dev)
+        v = torch.empty(self.m, dtype=self.dt, device=dev)
+        P = None
+        if want_plan:
+            P = ops._alloc_rowmajor(self.n, self.m, plan_dtype or self.dt, dev, 4)
+        L.check(L.lib().otf_sinkhorn_finish(
+            *self._common(), ctypes.byref(self.opts), u.data_ptr(), v.data_ptr(), L.ptr(P),
+            P.stride(0) if P is not None else 0, ops._DT[P.dtype] if P is not None else 0,
+            self.info.data_ptr(), self.errlog.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+            L.stream_handle(dev)), "otf_sinkhorn_finish")
+        return ops.SinkhornResult(u=u, v=v, plan=P, info_dev=self.info, errlog_dev=self.errlog)
+
+
+def sinkhorn_row_sharded(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.Tensor, reg: float,
+                         max_iter: int = 1000, stop_thr: float = 1e-9,
+                         cost_scale: torch.Tensor | None = None, n_total: int | None = None,
+                         check_every: int = 10, err_squared: bool = False, sync_every: int = 0,
+                         want_plan: bool = True, plan_dtype=None, group=None, backend=None):
+    """POT ``sinkhorn_knopp`` on a problem whose cost rows are split over the ranks.
+
+    Rank r passes its rows ``C_local`` (n_r x m), ``a_local = a[R_r]`` and the full
+    ``b``; the result holds this rank's rows of u and of the plan, and the full v.
+    One all-reduce(SUM) of m + 1 values per iteration.  With
+    ``sync_every`` > 0 the host polls the (rank-identical) stop flag to end early.
+    """
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if n_total is None:
+        n_total = C_local.shape[0]
+        if world > 1:
+            t = torch.tensor([n_total], dtype=torch.int64, device=C_local.device)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+            n_total = int(t.item())
+    be = (backend or DevicePasses)(a_local, b, C_local, reg, max_iter, stop_thr, cost_scale,
+                                   n_total, check_every, err_squared)
+    for p in range(max_iter + 1):
+        cs = be.run_pass(p)
+        if world > 1:
+            dist.all_reduce(cs, op=dist.ReduceOp.SUM, group=group)
+        if sync_every > 0 and p >= 1 and p % sync_every == 0 and p < max_iter and be.stopped():
+            break
+    return be.finish(want_plan, plan_dtype)
+
+
+def coupled_solve_sharded(X_local: torch.Tensor, Y_local: torch.Tensor, reg: float,
+                          max_iter: int = 200, stop_thr: float = 0.0, cost_dtype=torch.float16,
+                          want_plan: bool = True, sync_every: int = 0, group=None):
+    """The per-epoch global OT of one large problem over the data-parallel ranks:
+    all-gather the PET embedding shards (RCCL), cost rows of this rank's MRI shard
+    against every PET embedding (fp16 storage by default, BASELINE config 5), one
+    all-reduce(MAX) for scale_cost="max_cost", then the row-sharded Sinkhorn with
+    uniform marginals.  Returns (SinkhornResult of this rank's rows, n_total)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    Y_all = all_gather_rows(Y_local, group) if world > 1 else Y_local
+    C, cmax, unit = ops.pairwise_cost_ex(X_local, Y_all, zero_diag=False, out_dtype=cost_dtype)
+    # the max in true cost units, agreed over ranks; each rank's stored unit may differ
+    gmax = cmax * unit
+    n = torch.tensor([X_local.shape[0]], dtype=torch.int64, device=X_local.device)
+    if world > 1:
+        dist.all_reduce(gmax, op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
+    n_total = int(n.item())
+    m = Y_all.shape[0]
+    a = torch.full((X_local.shape[0],), 1.0 / n_total, dtype=torch.float32, device=X_local.device)
+    b = torch.full((m,), 1.0 / m, dtype=torch.float32, device=X_local.device)
+    res = sinkhorn_row_sharded(a, b, C, reg, max_iter=max_iter, stop_thr=stop_thr,
+                               cost_scale=gmax / unit, n_total=n_total, sync_every=sync_every,
+                               want_plan=want_plan, group=group)
+    return res, n_total

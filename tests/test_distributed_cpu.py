@@ -68,3 +68,72 @@ def test_sharded_feature_cost_and_gather_world2(tmp_path):
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     assert all((tmp_path / f"ok{r}").exists() for r in range(world))
+
+
+class NumpyPasses:
+    """Per-pass restatement of POT sinkhorn_knopp on this rank's rows (test backend for
+    the protocol of otfuse.distributed.sinkhorn_row_sharded; the product backend is
+    DevicePasses over otf_sinkhorn_pass)."""
+
+    def __init__(self, a_local, b, C_local, reg, max_iter, stop_thr, cost_scale, n_total,
+                 check_every=10, err_squared=False):
+        self.K = np.exp(-C_local.numpy() / reg)
+        self.a = a_local.numpy()
+        self.b = b.numpy()
+        self.n_total = n_total
+        self.m = self.K.shape[1]
+        self.u = np.full(self.K.shape[0], 1.0 / n_total)
+        self.v = np.full(self.m, 1.0 / self.m)
+        self.cs = None
+
+    def run_pass(self, p):
+        if p >= 1:
+            self.v = self.b / self.cs[: self.m].numpy()
+            self.u = self.a / (self.K @ self.v)
+        out = np.zeros(self.m + 1)
+        out[: self.m] = self.K.T @ self.u
+        out[self.m] = np.count_nonzero(~np.isfinite(self.u))
+        self.cs = torch.from_numpy(out)
+        return self.cs
+
+    def stopped(self):
+        return False
+
+    def finish(self, want_plan=True, plan_dtype=None):
+        return self.u[:, None] * self.K * self.v[None, :]
+
+
+def _sharded_worker(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as orc
+    import otfuse.distributed as D
+    rng = np.random.default_rng(7)
+    rows = [5, 8]                      # ragged shards: u0 must be 1/n_total on every rank
+    n, m = sum(rows), 11
+    C = rng.random((n, m))
+    a = rng.random(n) + 0.5
+    a /= a.sum()
+    b = rng.random(m) + 0.5
+    b /= b.sum()
+    r0 = sum(rows[:rank])
+    sl = slice(r0, r0 + rows[rank])
+    P_local = D.sinkhorn_row_sharded(torch.from_numpy(a[sl]), torch.from_numpy(b),
+                                     torch.from_numpy(C[sl]), 0.2, max_iter=25, stop_thr=0.0,
+                                     backend=NumpyPasses)
+    P_ref, *_ = orc.sinkhorn_knopp(a, b, C, 0.2, 25, 0.0)
+    np.testing.assert_allclose(P_local, P_ref[sl], rtol=1e-12, atol=1e-15)
+    open(os.path.join(out_dir, f"sharded{rank}"), "w").write("ok")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_row_sharded_sinkhorn_protocol_world2(tmp_path):
+    world = 2
+    mp.spawn(_sharded_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert all((tmp_path / f"sharded{r}").exists() for r in range(world))
