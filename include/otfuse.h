@@ -235,6 +235,93 @@ int otf_gemm_f32(const float* A, int64_t sa0, int64_t sa1, const float* B, int64
                  int64_t sb1, float* out, int64_t ldo, int64_t M, int64_t N, int64_t K,
                  float alpha, float beta, otf_stream_t stream);
 
+/* ------------------------------------------------------------------------
+ * Sample-level costs and Gromov-Wasserstein couplings.
+ * ---------------------------------------------------------------------- */
+
+/* float64 pairwise cost between float32 rows, POT euclidean_distances order
+ * (C = -2 X Y^T + |x|^2 + |y|^2, clamped at 0, sqrt for OTF_EUCLIDEAN, zero
+ * diagonal if zero_diag) — ot.dist(x, x, metric) at MRI_PET_OT_nojax.py:70-71
+ * and PointCloud(x, x) at MRI_PET_OT_OT_per_epoch_attn.py:155-156.  *cmax
+ * (device double, nullable) receives max C; scale_max = 1 also divides C by it
+ * ("C1 /= C1.max()", :74-75; scale_cost="max_cost").
+ * Workspace: otf_cost_pairwise_f64_workspace_size() bytes.                      */
+size_t otf_cost_pairwise_f64_workspace_size(int64_t n, int64_t m);
+int otf_cost_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
+                          int64_t m, int64_t d, int32_t metric, int32_t zero_diag,
+                          int32_t scale_max, double* C, int64_t ldc, double* cmax,
+                          void* workspace, size_t ws_bytes, otf_stream_t stream);
+
+/* GW solvers (square loss, symmetric C1 / C2):
+ * OTF_GW_CG: POT 0.9.6 ot.gromov.gromov_wasserstein(C1, C2, p, q, 'square_loss')
+ *   (conditional gradient, exact EMD inner solve, closed-form line search), as
+ *   called by get_coupling_gromov_pot, MRI_PET_OT_nojax.py:52-88.  Requires
+ *   p = q = uniform (pass NULL) and n == m — the callers' paired per-label groups
+ *   — where the exact EMD is an optimal assignment (solved on the device).
+ * OTF_GW_ENTROPIC: OTT-jax 0.6.0 GromovWasserstein(epsilon, linear_solver=
+ *   Sinkhorn(...)) as called by get_coupling_egw_ott_fixed,
+ *   MRI_PET_OT_OT_per_epoch_attn.py:129-186, and perturbot ott_egwl.py:25-296
+ *   (labels_a / labels_b != NULL: coupling restricted to equal labels).        */
+typedef enum { OTF_GW_CG = 0, OTF_GW_ENTROPIC = 1 } otf_gw_solver;
+enum {
+    OTF_GW_RUNNING = 0,
+    OTF_GW_CONVERGED = 1,
+    OTF_GW_MAX_ITER = 2,
+    OTF_GW_NUMERICAL = 3,  /* non-finite cost / failed assignment                   */
+    OTF_GW_TIMEOUT = 4     /* device-side wall-clock bound (20 s) reached            */
+};
+
+typedef struct {
+    int32_t solver;       /* otf_gw_solver                                              */
+    int32_t max_iter;     /* POT max_iter (1e4) / OTT max_iterations                     */
+    int32_t min_iter;     /* OTT min_iterations (5); CG ignores it                       */
+    int32_t sk_max_iter;  /* OTT inner Sinkhorn max_iterations (2000)                    */
+    int32_t sk_inner;     /* OTT inner_iterations (10)                                   */
+    int32_t warm_start;   /* OTT warm_start (1: inner solves start from the previous f, g) */
+    double tol_rel;       /* POT tol_rel (1e-9)                                          */
+    double tol_abs;       /* POT tol_abs (1e-9)                                          */
+    double threshold;     /* OTT outer threshold (1e-3, rtol of isclose on the costs)    */
+    double sk_threshold;  /* OTT Sinkhorn threshold (1e-3, L1 column-marginal error)     */
+    double eps;           /* OTT epsilon (absolute, on the max-scaled costs)              */
+} otf_gw_opts;
+
+/* One problem; all pointers are device pointers.  T (n x m, ldt) receives the
+ * coupling.  p, q: marginals (float64) or NULL for uniform.                    */
+typedef struct {
+    const double* C1;
+    int64_t ldc1;
+    const double* C2;
+    int64_t ldc2;
+    const double* p;
+    const double* q;
+    const int32_t* labels_a;
+    const int32_t* labels_b;
+    double* T;
+    int64_t ldt;
+    int64_t n;  /* <= 1024 */
+    int64_t m;  /* <= 1024 */
+} otf_gw_problem;
+
+/* Written on the device, one per problem. */
+typedef struct {
+    int32_t n_iter;          /* outer iterations (POT CG iterations / OTT n_iters)       */
+    int32_t converged;       /* outer convergence (POT tolerance hit / OTT out.converged) */
+    int32_t inner_converged; /* OTT: last linear solve converged                          */
+    int32_t status;          /* OTF_GW_*                                                  */
+    int32_t inner_iters;     /* OTT: total Sinkhorn updates                               */
+    int32_t pad;
+    double cost;             /* POT: final GW loss (log['gw_dist']); OTT: reg_gw_cost     */
+} otf_gw_info;
+
+/* Solves nprob independent problems (one workgroup each, concurrently).
+ * probs: HOST array of descriptors; info: device array of nprob; costlog
+ * (device, nullable): nprob rows of costlog_len doubles — POT log['loss'] /
+ * OTT out.costs.  Workspace: otf_gw_workspace_size() bytes.                    */
+size_t otf_gw_workspace_size(int32_t nprob, const otf_gw_problem* probs);
+int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* opts,
+                 otf_gw_info* info, double* costlog, int32_t costlog_len, void* workspace,
+                 size_t ws_bytes, otf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,11 @@ Both follow the reference (file:line into /root/reference):
 * log-domain       perturbot/perturbot/match/fot.py:128-134 -> OTT-jax 0.6.0
                    (absent here: parity unpinned)
 * plan apply       MRI_PET_OT_nojax.py:701-721
+* GW (CG, POT)     MRI_PET_OT_nojax.py:80-82 -> POT ``ot.gromov.gromov_wasserstein``
+                   (absent: parity unpinned; the inner exact EMD / assignment is
+                   cross-checked against scipy's ``linear_sum_assignment``)
+* GW (entropic)    MRI_PET_OT_OT_per_epoch_attn.py:161-174, ott_egwl.py -> OTT
+                   ``GromovWasserstein`` (absent: parity unpinned)
 
 Pinning: the Sinkhorn, feature-cost and plan-apply restatements are checked
 against golden vectors produced by the reference's own code in the survey
@@ -75,6 +80,18 @@ def lib():
         L.oro_plan_apply.argtypes = [_dp, ctypes.c_int64, ctypes.c_int64, _fp, ctypes.c_int64,
                                      _fp, _fp]
         L.oro_plan_apply.restype = None
+        _ii = ctypes.POINTER(ctypes.c_int)
+        L.oro_lap.argtypes = [_dp, ctypes.c_int64, _ii]
+        L.oro_lap.restype = ctypes.c_int
+        L.oro_gw_cg.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                                ctypes.c_double, _dp, _dp, ctypes.c_int, _ip, _dp]
+        L.oro_gw_cg.restype = ctypes.c_int
+        L.oro_gw_entropic.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int64, _dp, _dp, _ii,
+                                      _ii, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_double, ctypes.c_int, _dp, _dp, ctypes.c_int,
+                                      _ip, _dp]
+        L.oro_gw_entropic.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -162,7 +179,107 @@ def plan_apply(T, Z=None):
     return Tn, out
 
 
+def lap(A):
+    """Minimum-cost assignment (serial shortest augmenting paths).  Returns sigma."""
+    A = _d(A)
+    n = A.shape[0]
+    sigma = np.empty(n, np.int32)
+    rc = lib().oro_lap(_ptr(A), n, sigma.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    if rc:
+        raise FloatingPointError("oro_lap: non-finite cost")
+    return sigma
+
+
+def gw_cg(C1, C2, max_iter=10000, tol_rel=1e-9, tol_abs=1e-9, log_len=64):
+    """POT CG-GW (uniform marginals, n x n).  Returns ``(G, info)``."""
+    C1, C2 = _d(C1), _d(C2)
+    n = C1.shape[0]
+    G = np.empty((n, n))
+    clog = np.zeros(log_len)
+    info = np.zeros(3, np.int64)
+    cost = ctypes.c_double()
+    lib().oro_gw_cg(_ptr(C1), _ptr(C2), n, int(max_iter), float(tol_rel), float(tol_abs),
+                    _ptr(G), _ptr(clog), log_len, _ptr(info, _ip), ctypes.byref(cost))
+    it = int(info[0])
+    return G, {"n_iter": it, "converged": bool(info[1]), "status": int(info[2]),
+               "loss": clog[: min(it + 1, log_len)].tolist(), "gw_dist": cost.value}
+
+
+def gw_entropic(C1, C2, eps, a=None, b=None, labels_a=None, labels_b=None, max_iter=2000,
+                min_iter=5, threshold=1e-3, sk_max=2000, sk_inner=10, sk_thr=1e-3, warm=True,
+                log_len=256):
+    """OTT entropic GW.  Returns ``(P, info)``."""
+    C1, C2 = _d(C1), _d(C2)
+    n, m = C1.shape[0], C2.shape[0]
+    P = np.empty((n, m))
+    clog = np.zeros(log_len)
+    info = np.zeros(5, np.int64)
+    cost = ctypes.c_double()
+    ip = ctypes.POINTER(ctypes.c_int)
+    la = None if labels_a is None else np.ascontiguousarray(labels_a, np.int32)
+    lb = None if labels_b is None else np.ascontiguousarray(labels_b, np.int32)
+    a = None if a is None else _d(a)
+    b = None if b is None else _d(b)
+    lib().oro_gw_entropic(_ptr(C1), _ptr(C2), n, m, _ptr(a) if a is not None else None,
+                          _ptr(b) if b is not None else None,
+                          la.ctypes.data_as(ip) if la is not None else None,
+                          lb.ctypes.data_as(ip) if lb is not None else None, float(eps),
+                          int(max_iter), int(min_iter), float(threshold), int(sk_max),
+                          int(sk_inner), float(sk_thr), int(bool(warm)), _ptr(P), _ptr(clog),
+                          log_len, _ptr(info, _ip), ctypes.byref(cost))
+    it = int(info[0])
+    return P, {"n_iters": it, "converged": bool(info[1]), "converged_inner": bool(info[2]),
+               "inner_iters": int(info[3]), "status": int(info[4]),
+               "costs": clog[: min(it, log_len)].tolist(), "reg_gw_cost": cost.value}
+
+
 # --------------------------------------------------------------------------- NumPy
+def gw_cg_np(C1, C2, max_iter=10000, tol_rel=1e-9, tol_abs=1e-9):
+    """POT 0.9.6 ``gromov_wasserstein(C1, C2, unif, unif, 'square_loss')`` in NumPy, with
+    scipy's ``linear_sum_assignment`` as the exact EMD (uniform marginals, n x n) — an
+    independent LAP implementation for cross-checking ``oro_lap`` / the device solver."""
+    from scipy.optimize import linear_sum_assignment
+
+    C1, C2 = _d(C1), _d(C2)
+    n = C1.shape[0]
+    p = np.full(n, 1.0 / n)
+    q = np.full(n, 1.0 / n)
+    constC = ((C1 ** 2) @ p)[:, None] + ((C2 ** 2) @ q)[None, :]
+    hC1, hC2 = C1, 2.0 * C2
+
+    def tens(G):
+        return constC - hC1 @ G @ hC2.T
+
+    G = np.outer(p, q)
+    cost = float(np.sum(tens(G) * G))
+    losses = [cost]
+    it = 0
+    while True:
+        it += 1
+        old = cost
+        df = 2.0 * tens(G)
+        Mi = df + df.min()
+        rows, cols = linear_sum_assignment(Mi)
+        Gc = np.zeros_like(G)
+        Gc[rows, cols] = 1.0 / n
+        dG = Gc - G
+        dot = hC1 @ dG @ hC2.T
+        a = -np.sum(dot * dG)
+        b = -2.0 * np.sum(dot * G)
+        if a > 0:
+            alpha = min(1.0, max(0.0, -b / (2.0 * a)))
+        else:
+            alpha = 1.0 if a + b < 0 else 0.0
+        cost = cost + a * alpha ** 2 + b * alpha
+        G = G + alpha * dG
+        losses.append(cost)
+        absd = abs(cost - old)
+        reld = absd / abs(cost) if cost != 0 else np.nan
+        if reld < tol_rel or absd < tol_abs or it >= max_iter:
+            break
+    return G, {"n_iter": it, "loss": losses, "gw_dist": cost}
+
+
 def pairwise_cost_np(X, Y, metric="sqeuclidean", zero_diag=False):
     """POT ``euclidean_distances`` (via ``ot.dist``) in float64."""
     X, Y = _d(X), _d(Y)

@@ -152,6 +152,23 @@ __global__ __launch_bounds__(256) void postprocess_kernel(const T* Tm, int d, in
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace
+
+// Host launcher for the tiled GEMM, shared with the other translation units.
+template <typename TA, typename TB, typename TACC, typename TOUT>
+int launch_gemm(const TA* A, int64_t sa0, int64_t sa1, const TB* B, int64_t sb0, int64_t sb1,
+                TOUT* out, int64_t ldo, int M, int N, int K, TACC alpha, TACC beta,
+                const TACC* rowadd, const TACC* coladd, hipStream_t s) {
+    if (M > 65535 * GT) return OTF_EUNSUPPORTED;
+    dim3 grid((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT));
+    gemm_kernel<TA, TB, TACC, TOUT><<<grid, 256, 0, s>>>(A, sa0, sa1, B, sb0, sb1, out, ldo, M, N,
+                                                         K, alpha, beta, rowadd, coladd);
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+template int launch_gemm<float, float, double, double>(const float*, int64_t, int64_t,
+                                                       const float*, int64_t, int64_t, double*,
+                                                       int64_t, int, int, int, double, double,
+                                                       const double*, const double*, hipStream_t);
 }  // namespace otf
 
 extern "C" {

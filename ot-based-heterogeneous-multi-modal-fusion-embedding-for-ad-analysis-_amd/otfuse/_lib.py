@@ -41,6 +41,24 @@ class SinkhornOpts(ctypes.Structure):
                 ("cost_f16", ctypes.c_int32), ("n_total", ctypes.c_int32)]
 
 
+class GwOpts(ctypes.Structure):
+    _fields_ = [("solver", ctypes.c_int32), ("max_iter", ctypes.c_int32),
+                ("min_iter", ctypes.c_int32), ("sk_max_iter", ctypes.c_int32),
+                ("sk_inner", ctypes.c_int32), ("warm_start", ctypes.c_int32),
+                ("tol_rel", ctypes.c_double), ("tol_abs", ctypes.c_double),
+                ("threshold", ctypes.c_double), ("sk_threshold", ctypes.c_double),
+                ("eps", ctypes.c_double)]
+
+
+class GwProblem(ctypes.Structure):
+    _fields_ = [("C1", ctypes.c_void_p), ("ldc1", ctypes.c_int64),
+                ("C2", ctypes.c_void_p), ("ldc2", ctypes.c_int64),
+                ("p", ctypes.c_void_p), ("q", ctypes.c_void_p),
+                ("labels_a", ctypes.c_void_p), ("labels_b", ctypes.c_void_p),
+                ("T", ctypes.c_void_p), ("ldt", ctypes.c_int64),
+                ("n", ctypes.c_int64), ("m", ctypes.c_int64)]
+
+
 INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "engine", "pad")
 INFO_INT32S = len(INFO_FIELDS)  # otf_sinkhorn_info is 8 x int32
 
@@ -79,6 +97,18 @@ _SIGS = {
                                             _vp, _i64, _vp]),
     "otf_gemm_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
                                     ctypes.c_float, ctypes.c_float, _vp]),
+    "otf_cost_pairwise_f64_workspace_size": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64]),
+    "otf_cost_pairwise_f64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                             ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.c_void_p]),
+    "otf_gw_workspace_size": (ctypes.c_size_t, [ctypes.c_int32, ctypes.POINTER(GwProblem)]),
+    "otf_gw_solve": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(GwProblem),
+                                    ctypes.POINTER(GwOpts), ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_void_p]),
 }
 
 _lib = None

@@ -168,3 +168,99 @@ def get_coupling_leot_ott(data, eps: float = 5e-3):
     for l in X_dict.keys():
         Ts[l], logs[l] = _eot(X_dict[l], Y_dict[l], eps)
     return Ts, logs
+
+
+# ----------------------------------------------------------------------- entropic GW
+def _egw_solve(pairs, eps, max_iterations, sinkhorn_max_iterations, labels=None):
+    """Entropic GW (OTT GromovWasserstein) on PointCloud(x, x, scale_cost="max_cost")
+    geometries, one device launch for every (X, Y) pair.  Returns plans + logs."""
+    from . import gw
+
+    dev = _device()
+    t0 = time.time()
+    C1s, C2s = [], []
+    for X, Y in pairs:
+        x = torch.nan_to_num(torch.as_tensor(np.asarray(X), device=dev).float())
+        y = torch.nan_to_num(torch.as_tensor(np.asarray(Y), device=dev).float())
+        C1, _ = gw.pairwise_cost_f64(x, None, metric="sqeuclidean", zero_diag=False, scale_max=True)
+        C2, _ = gw.pairwise_cost_f64(y, None, metric="sqeuclidean", zero_diag=False, scale_max=True)
+        C1s.append(C1)
+        C2s.append(C2)
+    torch.cuda.current_stream(dev).synchronize()
+    cost_time = time.time() - t0
+    t0 = time.time()
+    res = gw.solve_batched(C1s, C2s, gw.GW_ENTROPIC, labels=labels, max_iter=max_iterations,
+                           min_iter=5, threshold=1e-3, eps=float(eps),
+                           sk_max_iter=sinkhorn_max_iterations, sk_inner=OTT_INNER,
+                           sk_threshold=OTT_THRESHOLD, warm_start=True,
+                           log_len=max(1, min(max_iterations, 4096)))
+    plans = [T.cpu().numpy() for T in res.plans]
+    infos = res.infos()
+    elapsed = time.time() - t0
+    logs = []
+    for info in infos:
+        if info["status"] == "timeout":
+            raise RuntimeError("entropic GW: device time limit reached")
+        logs.append({"n_iters_outer": info["n_iter"], "converged_inner": info["converged_inner"],
+                     "converged_outer": info["converged"], "GW cost": info["cost"],
+                     "time": elapsed, "cost_time": cost_time})
+    return plans, logs
+
+
+def get_coupling_egw_ott_fixed(
+    data: Tuple[Dict[Number, np.ndarray], Dict[Number, np.ndarray]],
+    eps: float = 5e-3,
+    gw_max_iterations: int = 2000,
+    sinkhorn_max_iterations: int = 2000,
+) -> Tuple[Dict[Number, np.ndarray], Dict]:
+    """Per-label entropic GW (MRI_PET_OT_OT_per_epoch_attn.py:129-186): NaN features
+    are zeroed, ``PointCloud(x, x, scale_cost="max_cost")`` geometries, OTT
+    ``GromovWasserstein(epsilon=eps, max_iterations=gw_max_iterations,
+    linear_solver=Sinkhorn(max_iterations=sinkhorn_max_iterations))``.  All labels in
+    one launch.  Returns ``({label: plan}, {label: log})``."""
+    X_dict, Y_dict = data
+    labels = list(X_dict.keys())
+    plans, logs = _egw_solve([(X_dict[l], Y_dict[l]) for l in labels], eps, gw_max_iterations,
+                             sinkhorn_max_iterations)
+    return dict(zip(labels, plans)), dict(zip(labels, logs))
+
+
+def get_coupling_egw_ott(data, eps: float = 5e-3):
+    """Per-label entropic GW, OTT defaults for the inner Sinkhorn, max_iterations=1000
+    (perturbot ott_egwl.py:129-206)."""
+    return get_coupling_egw_ott_fixed(data, eps, gw_max_iterations=1000,
+                                      sinkhorn_max_iterations=OTT_MAX_ITER)
+
+
+def _concat(data):
+    X_dict, Y_dict = data
+    keys = list(X_dict.keys())
+    Xs = np.concatenate([X_dict[l] for l in keys], axis=0)
+    Xt = np.concatenate([Y_dict[l] for l in keys], axis=0)
+    la = np.concatenate([np.repeat(l, X_dict[l].shape[0]) for l in keys])
+    lb = np.concatenate([np.repeat(l, Y_dict[l].shape[0]) for l in keys])
+    return Xs, Xt, la, lb
+
+
+def get_coupling_egw_all_ott(data, eps: float = 5e-3):
+    """Entropic GW on all samples, labels ignored (perturbot ott_egwl.py:209-296).
+    Returns ``(T, log)``."""
+    Xs, Xt, _, _ = _concat(data)
+    plans, logs = _egw_solve([(Xs, Xt)], eps, 1000, OTT_MAX_ITER)
+    return plans[0], logs[0]
+
+
+def get_coupling_egw_labels_ott(data, eps: float = 5e-3):
+    """Label-restricted entropic GW on all samples (perturbot ott_egwl.py:25-126): the
+    coupling may only join samples with equal labels (the reference's patched OTT
+    ``QuadraticProblem(labels_a, labels_b, block_diag_mat)``; here the linearised
+    cost is +inf off the label blocks).  Returns ``({label: block}, log)``."""
+    Xs, Xt, la, lb = _concat(data)
+    uniq = np.unique(la)
+    code = {v: i for i, v in enumerate(uniq)}
+    ia = np.array([code[v] for v in la], np.int32)
+    ib = np.array([code.get(v, -1 - i) for i, v in enumerate(lb)], np.int32)
+    plans, logs = _egw_solve([(Xs, Xt)], eps, 2000, 2000, labels=[(ia, ib)])
+    T = plans[0]
+    T_dict = {l: T[la == l, :][:, lb == l] for l in uniq}
+    return T_dict, logs[0]

@@ -1,0 +1,184 @@
+"""Device GW solvers (csrc/otf_gw.hip) vs the oracle's GW restatements.
+
+POT / OTT are absent, so the oracle itself is parity-UNPINNED against the reference's
+outputs (its exact-EMD step is pinned to scipy in tests/test_oracle_gw.py).  Bars:
+CG-GW is a vertex / short convex path — plans must agree to 1e-12 absolute and the
+iteration counts exactly; entropic GW in float64 — plans within 1e-4 normwise relative
+(the north star's tolerance), identical outer iteration counts.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def nrel(x, ref):
+    return np.abs(np.asarray(x) - ref).max() / np.abs(ref).max()
+
+
+def _emb(n, d, seed):
+    from otfuse.synthetic import paired_embeddings
+    return paired_embeddings(n, d, seed=seed)
+
+
+@pytest.mark.parametrize("metric,zero_diag,n,m,d", [("euclidean", True, 64, 64, 512),
+                                                    ("sqeuclidean", False, 130, 77, 33),
+                                                    ("euclidean", False, 1, 5, 3)])
+def test_pairwise_cost_f64_vs_oracle(orc, dev, metric, zero_diag, n, m, d):
+    from otfuse import gw
+    X, _, _ = _emb(n, d, 1)
+    _, Y, _ = _emb(m, d, 2)
+    same = n == m and zero_diag
+    Xd = torch.as_tensor(X, device=dev)
+    Yd = Xd if same else torch.as_tensor(Y, device=dev)
+    C, cmax = gw.pairwise_cost_f64(Xd, None if same else Yd, metric=metric, zero_diag=zero_diag,
+                                   scale_max=True)
+    Cr, mr = orc.pairwise_cost(X, X if same else Y, metric=metric, zero_diag=zero_diag,
+                               scale_max=True)
+    assert float(cmax) == pytest.approx(mr, rel=1e-12)
+    assert np.abs(C.cpu().numpy() - Cr).max() < 1e-12
+
+
+def _label_costs(orc, sizes, d, seed, metric="euclidean"):
+    out = []
+    for k, n in enumerate(sizes):
+        X, Y, _ = _emb(n, d, seed + k)
+        zd = metric == "euclidean"
+        C1, _ = orc.pairwise_cost(X, X, metric=metric, zero_diag=zd, scale_max=True)
+        C2, _ = orc.pairwise_cost(Y, Y, metric=metric, zero_diag=zd, scale_max=True)
+        out.append((C1, C2))
+    return out
+
+
+def test_gw_cg_batched_vs_oracle(orc, dev):
+    """Every label problem of one launch (sizes 1..200) against the C restatement."""
+    from otfuse import gw
+    sizes = [1, 2, 3, 17, 64, 64, 100, 130, 200]
+    probs = _label_costs(orc, sizes, 48, 10)
+    res = gw.solve_batched([torch.as_tensor(c1, device=dev) for c1, _ in probs],
+                           [torch.as_tensor(c2, device=dev) for _, c2 in probs], gw.GW_CG,
+                           max_iter=10000, log_len=64)
+    infos = res.infos()
+    for (C1, C2), T, info in zip(probs, res.plans, infos):
+        G, ref = orc.gw_cg(C1, C2)
+        assert info["status"] == "converged", info
+        assert info["n_iter"] == ref["n_iter"]
+        assert np.abs(T.cpu().numpy() - G).max() < 1e-12
+        assert info["cost"] == pytest.approx(ref["gw_dist"], rel=1e-9, abs=1e-13)
+        np.testing.assert_allclose(info["costs"], ref["loss"], rtol=1e-9, atol=1e-13)
+
+
+def test_gw_cg_random_metric_spaces_many_seeds(orc, dev):
+    """Random point clouds (not the structured embeddings): 16 problems in one launch,
+    each checked against the NumPy + scipy restatement (independent LAP)."""
+    from otfuse import gw
+    rng = np.random.default_rng(123)
+    C1s, C2s = [], []
+    for k in range(16):
+        n = int(rng.integers(5, 90))
+        A = rng.standard_normal((n, 3))
+        B = rng.standard_normal((n, 4))
+        C1s.append(orc.pairwise_cost(A, A, metric="euclidean", zero_diag=True, scale_max=True)[0])
+        C2s.append(orc.pairwise_cost(B, B, metric="euclidean", zero_diag=True, scale_max=True)[0])
+    res = gw.solve_batched([torch.as_tensor(c, device=dev) for c in C1s],
+                           [torch.as_tensor(c, device=dev) for c in C2s], gw.GW_CG, max_iter=10000)
+    for C1, C2, T, info in zip(C1s, C2s, res.plans, res.infos()):
+        G, ref = orc.gw_cg_np(C1, C2)
+        assert info["n_iter"] == ref["n_iter"]
+        assert np.abs(T.cpu().numpy() - G).max() < 1e-12
+        assert info["cost"] == pytest.approx(ref["gw_dist"], rel=1e-9, abs=1e-13)
+
+
+def test_gw_cg_isometry(orc, dev):
+    from otfuse import gw
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((50, 5))
+    perm = rng.permutation(50)
+    C1, _ = orc.pairwise_cost(X, X, metric="euclidean", zero_diag=True, scale_max=True)
+    C2 = np.ascontiguousarray(C1[np.ix_(perm, perm)])
+    G, log = gw.gromov_wasserstein(torch.as_tensor(C1, device=dev), torch.as_tensor(C2, device=dev),
+                                   log=True)
+    assert log["gw_dist"] == pytest.approx(0.0, abs=1e-12)
+    assert (G.cpu().numpy().argmax(1) == np.argsort(perm)).all()
+
+
+@pytest.mark.parametrize("n,m,eps", [(64, 64, 5e-3), (30, 50, 5e-3), (128, 100, 1e-2), (1, 4, 5e-3)])
+def test_gw_entropic_vs_oracle(orc, dev, n, m, eps):
+    from otfuse import gw
+    (C1, _), = _label_costs(orc, [n], 24, 30, "sqeuclidean")
+    (_, C2), = _label_costs(orc, [m], 24, 40, "sqeuclidean")
+    P, info = gw.entropic_gromov_wasserstein_ott(torch.as_tensor(C1, device=dev),
+                                                 torch.as_tensor(C2, device=dev), eps,
+                                                 max_iterations=2000)
+    Pr, ref = orc.gw_entropic(C1, C2, eps)
+    assert info["n_iter"] == ref["n_iters"]
+    assert info["converged"] == ref["converged"]
+    assert info["converged_inner"] == ref["converged_inner"]
+    assert nrel(P.cpu().numpy(), Pr) < 1e-4
+    assert info["cost"] == pytest.approx(ref["reg_gw_cost"], rel=1e-6, abs=1e-9)
+
+
+def test_gw_entropic_labelled_vs_oracle(orc, dev):
+    from otfuse import gw
+    (C1, C2), = _label_costs(orc, [60], 24, 50, "sqeuclidean")
+    la = np.array([0] * 35 + [1] * 25, np.int32)
+    lb = np.array([1] * 25 + [0] * 35, np.int32)
+    P, info = gw.entropic_gromov_wasserstein_ott(torch.as_tensor(C1, device=dev),
+                                                 torch.as_tensor(C2, device=dev), 1e-2,
+                                                 labels_a=la, labels_b=lb, max_iterations=2000)
+    Pr, ref = orc.gw_entropic(C1, C2, 1e-2, labels_a=la, labels_b=lb)
+    Pn = P.cpu().numpy()
+    assert Pn[np.not_equal.outer(la, lb)].max() == 0.0
+    assert info["n_iter"] == ref["n_iters"]
+    assert nrel(Pn, Pr) < 1e-4
+
+
+def test_get_coupling_gromov_pot_dropin(orc, dev):
+    """nojax per-epoch flow: grouped features -> GW per label -> feature coupling."""
+    from otfuse import pot
+    from otfuse.fusion import group_features_by_label
+    X, Y, lab = _emb(120, 64, 77)
+    gm = group_features_by_label(lab, X, max_samples_per_label=48)
+    gp = group_features_by_label(lab, Y, max_samples_per_label=48)
+    Ts, log = pot.get_coupling_gromov_pot((gp, gm))
+    assert list(Ts) == list(gp)
+    for l in gp:
+        C1, _ = orc.pairwise_cost(gp[l], gp[l], metric="euclidean", zero_diag=True, scale_max=True)
+        C2, _ = orc.pairwise_cost(gm[l], gm[l], metric="euclidean", zero_diag=True, scale_max=True)
+        G, _ = orc.gw_cg(C1, C2)
+        assert Ts[l].dtype == np.float32 and "time" in log[l]
+        assert np.abs(Ts[l] - G).max() < 1e-7
+    Tf, _ = pot.get_feature_coupling_pot((gp, gm), Ts)
+    assert Tf.shape == (64, 64) and np.isfinite(Tf).all()
+
+
+def test_get_coupling_egw_ott_fixed_dropin(orc, dev):
+    from otfuse import perturbot
+    from otfuse.fusion import group_features_by_label
+    X, Y, lab = _emb(100, 32, 78)
+    gm = group_features_by_label(lab, X, max_samples_per_label=40)
+    gp = group_features_by_label(lab, Y, max_samples_per_label=40)
+    T, log = perturbot.get_coupling_egw_ott_fixed((gp, gm), eps=5e-3)
+    for l in gp:
+        C1, _ = orc.pairwise_cost(gp[l], gp[l], scale_max=True)
+        C2, _ = orc.pairwise_cost(gm[l], gm[l], scale_max=True)
+        Pr, ref = orc.gw_entropic(C1, C2, 5e-3)
+        assert log[l]["n_iters_outer"] == ref["n_iters"]
+        assert set(log[l]) >= {"n_iters_outer", "converged_inner", "converged_outer", "GW cost",
+                               "time", "cost_time"}
+        assert nrel(T[l], Pr) < 1e-4
+    Tf, flog = perturbot.get_coupling_fot((gp, gm), T, eps=5e-3)
+    assert Tf.shape == (32, 32) and np.isfinite(Tf).all()
+
+
+def test_egw_labels_and_all_dropins(dev):
+    from otfuse import perturbot
+    X, Y, lab = _emb(80, 16, 79)
+    Xd = {0: X[lab == 0][:30], 1: X[lab == 1][:30]}
+    Yd = {0: Y[lab == 0][:30], 1: Y[lab == 1][:30]}
+    T_dict, log = perturbot.get_coupling_egw_labels_ott((Xd, Yd), eps=1e-2)
+    assert set(T_dict) == {0, 1} and T_dict[0].shape == (30, 30)
+    assert abs(sum(t.sum() for t in T_dict.values()) - 1.0) < 1e-6
+    T, log2 = perturbot.get_coupling_egw_all_ott((Xd, Yd), eps=1e-2)
+    assert T.shape == (60, 60) and abs(T.sum() - 1.0) < 1e-6
