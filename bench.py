@@ -57,6 +57,7 @@ def parse():
     p.add_argument("--hbm-probe-n", type=int, default=16384)
     p.add_argument("--profile-only", action="store_true",
                    help="run warmup + steps only (for rocprofv3 runs); no probes, no JSON")
+    p.add_argument("--no-gw", action="store_true", help="skip the per-epoch GW latency leg")
     p.add_argument("--engine", default="auto", choices=("auto", "stream", "resident"),
                    help="Sinkhorn engine (auto = resident when the cost fits the register file)")
     return p.parse_args()
@@ -204,6 +205,8 @@ def main():
     }
     if not args.no_hbm_probe:
         out["hbm_probe"] = hbm_probe(ops, paired_embeddings, args.hbm_probe_n, d, eps, dev)
+    if rank == 0 and not args.no_gw:
+        out["gw_per_epoch"] = gw_leg(dev, world == 1 and not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(X_np, Y_np, N, iters, eps, args.cpu_threads)
         out["vs_cpu"] = value / out["cpu_baseline"]["value"]
@@ -211,6 +214,62 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def gw_leg(dev, with_cpu, labels=2, per_label=64, d=512, eps=5e-3):
+    """Per-epoch sample coupling: `labels` label groups of
+    `per_label` paired samples (the reference's --max-jax-samples 64), d = 512.
+    Device: both GW solvers, all labels in one launch (float64 costs built on the
+    device first, inside the timing); latency-bound, so reported as ms per epoch
+    call.  CPU: the oracle's float64 C restatements, one core, same problems."""
+    from otfuse import gw
+    from otfuse.synthetic import paired_embeddings
+    Xs, Ys = [], []
+    for k in range(labels):
+        X, Y, _ = paired_embeddings(per_label, d, seed=500 + k)
+        Xs.append(torch.from_numpy(X).to(dev))
+        Ys.append(torch.from_numpy(Y).to(dev))
+
+    def run(solver):
+        metric = "euclidean" if solver == gw.GW_CG else "sqeuclidean"
+        C1s = [gw.pairwise_cost_f64(x, None, metric=metric, zero_diag=solver == gw.GW_CG,
+                                    scale_max=True)[0] for x in Xs]
+        C2s = [gw.pairwise_cost_f64(y, None, metric=metric, zero_diag=solver == gw.GW_CG,
+                                    scale_max=True)[0] for y in Ys]
+        if solver == gw.GW_CG:
+            return gw.solve_batched(C1s, C2s, gw.GW_CG, max_iter=10000, log_len=1), C1s, C2s
+        return gw.solve_batched(C1s, C2s, gw.GW_ENTROPIC, max_iter=2000, eps=eps,
+                                sk_max_iter=2000, log_len=1), C1s, C2s
+
+    out = {"labels": labels, "samples_per_label": per_label, "d": d, "eps": eps,
+           "unit": "ms per epoch call (all labels)"}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for name, solver in (("pot_cg", gw.GW_CG), ("ott_entropic", gw.GW_ENTROPIC)):
+        run(solver)
+        ts = []
+        for _ in range(5):
+            e0.record()
+            res, C1s, C2s = run(solver)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        info = res.infos()
+        out[name] = {"device_ms": sorted(ts)[2], "outer_iters": [i["n_iter"] for i in info],
+                     "inner_iters": [i["inner_iters"] for i in info]}
+        if with_cpu:
+            from oracle import oracle as orc
+            c1 = [c.cpu().numpy() for c in C1s]
+            c2 = [c.cpu().numpy() for c in C2s]
+            t0 = time.perf_counter()
+            for a_, b_ in zip(c1, c2):
+                if solver == gw.GW_CG:
+                    orc.gw_cg(a_, b_)
+                else:
+                    orc.gw_entropic(a_, b_, eps)
+            cpu_ms = (time.perf_counter() - t0) * 1e3
+            out[name]["cpu_ms"] = cpu_ms
+            out[name]["cpu_note"] = "oracle C restatement, 1 core, solve only (costs given)"
+    return out
 
 
 def hbm_probe(ops, paired_embeddings, n, d, eps, dev):

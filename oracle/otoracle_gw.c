@@ -40,7 +40,29 @@ ORO_EXPORT int oro_lap(const double* A, int64_t n, int* sigma) {
     int* way = (int*)calloc((size_t)n + 1, sizeof(int));
     char* used = (char*)malloc((size_t)n + 1);
     int rc = 0;
+    /* column reduction v_j = min_i a_ij, then a greedy pass: row i takes its cheapest
+     * reduced column (lowest index on ties) with u_i = that reduced cost when the
+     * column is still free.  Potentials stay feasible (a_ij - u_i - v_j >= 0) and the
+     * taken edges tight, so the shortest-path phase below completes an optimum. */
+    char* done = (char*)calloc((size_t)n + 1, 1);
+    for (int64_t j = 1; j <= n; ++j) {
+        double mn = LAP_INF;
+        for (int64_t i = 1; i <= n; ++i) if (A[(i - 1) * n + (j - 1)] < mn) mn = A[(i - 1) * n + (j - 1)];
+        v[j] = mn;
+    }
+    for (int64_t i = 1; i <= n; ++i) {
+        double mn = LAP_INF;
+        int64_t jb = -1;
+        for (int64_t j = 1; j <= n; ++j) {
+            const double r = A[(i - 1) * n + (j - 1)] - v[j];
+            if (r < mn) { mn = r; jb = j; }
+        }
+        if (jb < 0) { rc = 1; break; }
+        u[i] = mn;
+        if (p[jb] == 0) { p[jb] = (int)i; done[i] = 1; }
+    }
     for (int64_t i = 1; i <= n && !rc; ++i) {
+        if (done[i]) continue;
         p[0] = (int)i;
         int64_t j0 = 0;
         for (int64_t j = 0; j <= n; ++j) { minv[j] = LAP_INF; used[j] = 0; }
@@ -72,7 +94,7 @@ ORO_EXPORT int oro_lap(const double* A, int64_t n, int* sigma) {
     }
     if (!rc)
         for (int64_t j = 1; j <= n; ++j) sigma[p[j] - 1] = (int)(j - 1);
-    free(u); free(v); free(minv); free(p); free(way); free(used);
+    free(u); free(v); free(minv); free(p); free(way); free(used); free(done);
     return rc;
 }
 

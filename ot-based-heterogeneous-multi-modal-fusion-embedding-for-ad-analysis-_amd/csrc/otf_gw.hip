@@ -38,11 +38,22 @@
 namespace otf {
 namespace {
 
-constexpr int GW_NT = 256;
-constexpr int GW_NW = GW_NT / kWave;
 constexpr int GW_MAXN = 1024;
 constexpr int GW_MAXP = 16;
 constexpr double GW_INF = 1e300;
+constexpr int GW_SMALLN = 64;  // problems with n, m <= this run with all matrices in LDS
+
+// Kernel variants: SMALL keeps C1, C2, the linearised cost and the plan in LDS
+// (the reference's per-label groups are <= 64 samples); the general variant keeps
+// them in the (L2-resident) workspace.
+template <int NT_, int MAXV_, bool SMALL_> struct GwCfg {
+    static constexpr int NT = NT_;
+    static constexpr int NW = NT_ / kWave;
+    static constexpr int MAXV = MAXV_;
+    static constexpr bool SMALL = SMALL_;
+};
+using GwBig = GwCfg<256, GW_MAXN, false>;
+using GwSmall = GwCfg<512, GW_SMALLN, true>;
 
 struct GwLaunch {
     otf_gw_problem prob[GW_MAXP];
@@ -51,37 +62,98 @@ struct GwLaunch {
     int nprob;
 };
 
-struct GwLap {
-    double minv[GW_MAXN + 1];
-    int pc[GW_MAXN + 1];   // pc[j]: row (1-based) assigned to column j, 0 = free
-    int way[GW_MAXN + 1];  // predecessor column on the shortest path
-    int sigma[GW_MAXN];    // sigma[i]: column of row i (0-based)
-    unsigned char used[GW_MAXN + 1];
+template <int MAXV> struct GwLap {
+    double minv[MAXV + 1];
+    int pc[MAXV + 1];   // pc[j]: row (1-based) assigned to column j, 0 = free
+    int way[MAXV + 1];  // predecessor column on the shortest path
+    int sigma[MAXV];    // sigma[i]: column of row i (0-based)
+    unsigned char used[MAXV + 1];
 };
 
-struct GwMarg {
-    double r[GW_MAXN];  // row marginal of the current plan
-    double c[GW_MAXN];  // column marginal
+template <int MAXV> struct GwMarg {
+    double r[MAXV];  // row marginal of the current plan
+    double c[MAXV];  // column marginal
 };
 
-struct GwShared {
-    double f[GW_MAXN + 1];  // OTT: potential f; CG: LAP row duals u (1-based)
-    double g[GW_MAXN + 1];  // OTT: potential g; CG: LAP column duals v (1-based)
-    double x[GW_MAXN];      // marginal-dependent cost, rows:    (C1^2 r)_i
-    double y[GW_MAXN];      // marginal-dependent cost, columns: (C2^2 c)_j
+template <int S> struct GwMats {
+    double C1[S * S], C2[S * S], L[S * (S + 1)], G[S * S];  // L rows padded: conflict-free column AND row sweeps
+};
+template <> struct GwMats<0> {};
+
+template <class Cfg> struct GwShared {
+    static constexpr int MV = Cfg::MAXV;
+    double f[MV + 1];  // OTT: potential f; CG: LAP row duals u (1-based)
+    double g[MV + 1];  // OTT: potential g; CG: LAP column duals v (1-based)
+    double x[MV];      // marginal-dependent cost, rows:    (C1^2 r)_i
+    double y[MV];      // marginal-dependent cost, columns: (C2^2 c)_j
     union {
-        GwLap lap;
-        GwMarg mg;
+        GwLap<MV> lap;
+        GwMarg<MV> mg;
     };
-    double pm[GW_NT];  // per-thread partials (max / sum)
-    double ps[GW_NT];
+    double pm[Cfg::NT];  // per-thread partials (max / sum)
+    double ps[Cfg::NT];
     double red[32];
     int flag;
+    GwMats<Cfg::SMALL ? GW_SMALLN : 0> mat;
 };
+
+// Diagnostic build only (-DOTF_GW_STAMPS, tools/stamps_gw.hip): per-phase wall-clock
+// totals of workgroup 0..15 (s_memrealtime ticks, 10 ns); compiled out of the library.
+#ifdef OTF_GW_STAMPS
+__device__ unsigned long long g_gw_stamps[16 * 8];
+__device__ unsigned long long g_gw_sk[4];
+#define GW_TBEG() unsigned long long gw_t0_ = __builtin_amdgcn_s_memrealtime()
+#define GW_TEND(k) gw_acc[k] += __builtin_amdgcn_s_memrealtime() - gw_t0_
+#else
+#define GW_TBEG() do {} while (0)
+#define GW_TEND(k) do {} while (0)
+#endif
 
 // --------------------------------------------------------------------- block helpers
 __device__ __forceinline__ double blk_sum(double v, double* red) { return block_sum<double>(v, red); }
 
+// Wave reductions of doubles over DPP (row-local exchanges + row broadcasts), result
+// read from lane 63 with s_readlane: no LDS round trips (the __shfl forms are
+// ds_bpermute, ~6x slower per step, and dominated the per-row LSE updates).
+template <int CTRL, int RM, bool ID_ZERO>
+__device__ __forceinline__ double dpp_f64(double x, double ident) {
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    const int olo = __double2loint(ident), ohi = __double2hiint(ident);
+    const int rlo = __builtin_amdgcn_update_dpp(olo, lo, CTRL, RM, 0xf, false);
+    const int rhi = __builtin_amdgcn_update_dpp(ohi, hi, CTRL, RM, 0xf, false);
+    return __hiloint2double(rhi, rlo);
+}
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+    return __hiloint2double(hi, lo);
+}
+template <int OP>  // 0 sum, 1 max, 2 min
+__device__ __forceinline__ double dpp_op(double a, double b) {
+    return OP == 0 ? a + b : (OP == 1 ? fmax(a, b) : fmin(a, b));
+}
+template <int OP>
+__device__ __forceinline__ double wave_reduce_f64(double x) {
+    const double id = OP == 0 ? 0.0 : (OP == 1 ? -INFINITY : INFINITY);
+    x = dpp_op<OP>(x, dpp_f64<0xB1, 0xf, false>(x, id));   // quad_perm [1,0,3,2]
+    x = dpp_op<OP>(x, dpp_f64<0x4E, 0xf, false>(x, id));   // quad_perm [2,3,0,1]
+    x = dpp_op<OP>(x, dpp_f64<0x141, 0xf, false>(x, id));  // row_half_mirror
+    x = dpp_op<OP>(x, dpp_f64<0x140, 0xf, false>(x, id));  // row_mirror
+    x = dpp_op<OP>(x, dpp_f64<0x142, 0xa, false>(x, id));  // row_bcast:15 -> rows 1, 3
+    x = dpp_op<OP>(x, dpp_f64<0x143, 0xc, false>(x, id));  // row_bcast:31 -> rows 2, 3
+    return readlane_f64(x, 63);
+}
+__device__ __forceinline__ int wave_min_i32(int x) {
+    x = min(x, __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xf, 0xf, false));
+    x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x4E, 0xf, 0xf, false));
+    x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x141, 0xf, 0xf, false));
+    x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x140, 0xf, 0xf, false));
+    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x142, 0xa, 0xf, false));
+    x = min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(x, 63);
+}
+
+template <class Cfg>
 __device__ double blk_minmax(double v, double* red, bool want_max) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -92,51 +164,51 @@ __device__ double blk_minmax(double v, double* red, bool want_max) {
     if (lane == 0) red[w] = v;
     __syncthreads();
     double r = red[0];
-    for (int i = 1; i < GW_NW; ++i) r = want_max ? fmax(r, red[i]) : fmin(r, red[i]);
+    for (int i = 1; i < Cfg::NW; ++i) r = want_max ? fmax(r, red[i]) : fmin(r, red[i]);
     __syncthreads();
     return r;
 }
 
-// out (n x m, ld ldo) = alpha * A (n x k, lda) . B~, B~(kk, j) = B[row(kk) * ldb + j],
-// row(kk) = perm ? perm[kk] : kk.  Each thread owns 4 consecutive columns of a row.
-template <bool PERM>
-__device__ void blk_gemm(double* out, int64_t ldo, const double* A, int64_t lda, const double* B,
-                         int64_t ldb, int n, int m, int k, const int* perm, double alpha) {
-    const int mq = (m + 3) >> 2;
-    for (int o = threadIdx.x; o < n * mq; o += GW_NT) {
-        const int i = o / mq, j = (o - i * mq) * 4;
-        const double* a = A + (int64_t)i * lda;
-        double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        if (j + 3 < m) {
-            for (int kk = 0; kk < k; ++kk) {
-                const double av = a[kk];
-                const double* b = B + (int64_t)(PERM ? perm[kk] : kk) * ldb + j;
-                s0 = fma(av, b[0], s0);
-                s1 = fma(av, b[1], s1);
-                s2 = fma(av, b[2], s2);
-                s3 = fma(av, b[3], s3);
-            }
-        } else {
-            for (int kk = 0; kk < k; ++kk) {
-                const double av = a[kk];
-                const double* b = B + (int64_t)(PERM ? perm[kk] : kk) * ldb + j;
-                s0 = fma(av, b[0], s0);
-                if (j + 1 < m) s1 = fma(av, b[1], s1);
-                if (j + 2 < m) s2 = fma(av, b[2], s2);
-            }
+// out(i, j) = alpha * sum_k A(i, k) B(k, j) on v_mfma_f64_16x16x4_f64, one 16 x 16
+// output tile per wave at a time:  A(i, k) = A[i * sai + k * sak],
+// B(k, j) = B[row(k) * sbk + j * sbj] with row(k) = perm ? perm[k] : k,
+// out(i, j) -> out[i * soi + j * soj].  Operand lanes: A[i0 + (l & 15)][k0 + (l >> 4)],
+// B[k0 + (l >> 4)][j0 + (l & 15)]; result: col l & 15, rows (l >> 4) + 4 r.
+// Callers pick strides so that the 16 lanes of a row group read consecutive doubles.
+typedef double gw_f64x4 __attribute__((ext_vector_type(4)));
+template <class Cfg, bool PERM>
+__device__ void blk_gemm(double* out, int64_t soi, int64_t soj, const double* A, int64_t sai,
+                         int64_t sak, const double* B, int64_t sbk, int64_t sbj, int n, int m,
+                         int k, const int* perm, double alpha) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int tn = (n + 15) >> 4, tm = (m + 15) >> 4;
+    const int li = lane & 15, lk = lane >> 4;
+    for (int tile = w; tile < tn * tm; tile += Cfg::NW) {
+        const int i0 = (tile / tm) * 16, j0 = (tile % tm) * 16;
+        const int ia = i0 + li, jb = j0 + li;
+        gw_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int k0 = 0; k0 < k; k0 += 4) {
+            const int kk = k0 + lk;
+            const bool kin = kk < k;
+            const double av = (ia < n && kin) ? A[ia * sai + kk * sak] : 0.0;
+            const double bv = (jb < m && kin) ? B[(int64_t)(PERM ? perm[kk] : kk) * sbk + jb * sbj] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
         }
-        double* d = out + (int64_t)i * ldo + j;
-        d[0] = alpha * s0;
-        if (j + 1 < m) d[1] = alpha * s1;
-        if (j + 2 < m) d[2] = alpha * s2;
-        if (j + 3 < m) d[3] = alpha * s3;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + lk + 4 * r;
+            if (i < n && jb < m) out[i * soi + jb * soj] = alpha * acc[r];
+        }
     }
 }
 
 // v[i] = sum_k C[k][i]^2 w[k]  (C symmetric, so this is (C^2 w)_i; column reads coalesce)
+template <class Cfg>
 __device__ void blk_sq_matvec(double* v, const double* C, int64_t ldc, int n, const double* w) {
-    for (int i = threadIdx.x; i < n; i += GW_NT) {
+    for (int i = threadIdx.x; i < n; i += Cfg::NT) {
         double s = 0;
+#pragma unroll 8
         for (int k = 0; k < n; ++k) {
             const double c = C[(int64_t)k * ldc + i];
             s = fma(c * c, w[k], s);
@@ -150,82 +222,70 @@ __device__ __forceinline__ double marg(const double* p, int i, int n) {
 }
 
 // Thread-to-(column, row-segment) map for column reductions: CW threads span the
-// columns, S = GW_NT / CW segments split the rows.
-struct ColMap {
+// columns, S = Cfg::NT / CW segments split the rows.
+template <class Cfg> struct ColMap {
     int CW, S, seg, jj;
     __device__ ColMap(int m) {
-        CW = m <= 64 ? 64 : (m <= 128 ? 128 : GW_NT);
-        S = GW_NT / CW;
+        CW = kWave;
+        while (CW < m && CW < Cfg::NT) CW <<= 1;
+        S = Cfg::NT / CW;
         seg = threadIdx.x / CW;
         jj = threadIdx.x - seg * CW;
     }
 };
 
-// Online log-sum-exp accumulator (running max, rescaled sum).
-__device__ __forceinline__ void lse_add(double z, double& mx, double& s) {
-    if (z > mx) {
-        s = (mx == -INFINITY) ? 0.0 : s * exp(mx - z);
-        mx = z;
-    }
-    if (z != -INFINITY) s += exp(z - mx);
-}
-__device__ __forceinline__ void lse_merge(double& mx, double& s, double m2, double s2) {
-    if (m2 == -INFINITY) return;
-    if (mx == -INFINITY) { mx = m2; s = s2; return; }
-    if (m2 > mx) { s = s * exp(mx - m2) + s2; mx = m2; }
-    else s += s2 * exp(m2 - mx);
-}
-
-// g_j = eps log b_j - eps LSE_i((f_i - L_ij) / eps)
-__device__ void lse_col_update(const double* Lm, int64_t ldl, int n, int m, const double* b,
-                               double eps, GwShared& sh) {
-    const ColMap cm(m);
-    for (int j0 = 0; j0 < m; j0 += cm.CW) {
-        const int j = j0 + cm.jj;
-        double mx = -INFINITY, s = 0;
-        if (j < m)
-            for (int i = cm.seg; i < n; i += cm.S) lse_add((sh.f[i] - Lm[(int64_t)i * ldl + j]) / eps, mx, s);
+// Log-sum-exp updates, two passes over the (LDS- or L2-resident) cost: a max pass and
+// a sum-of-exp pass, one exp per element; potentials in absolute units, exponents
+// scaled by ieps = 1 / eps.
+// One LSE sweep: for every output o < nout,
+//     out[o] = eps log w_o - eps LSE_k((pot[k] - L(o, k)) / eps),  L(o, k) = Lm[o*so + k*sk],
+// CW threads across the outputs, S segments across k, each thread a strided run of k
+// (independent loads and exps); a max pass and a sum pass merged over the segments
+// in LDS in a fixed order.  Column update: (o, k) = (j, i); row update: (i, j).
+template <class Cfg>
+__device__ void lse_sweep(const double* Lm, int64_t so, int64_t sk, int nout, int nk,
+                          const double* pot, double* out, const double* w, double eps,
+                          double ieps, GwShared<Cfg>& sh) {
+    const ColMap<Cfg> cm(nout);
+    for (int o0 = 0; o0 < nout; o0 += cm.CW) {
+        const int o = o0 + cm.jj;
+        const double* lo = Lm + (int64_t)o * so;
+        double mx = -INFINITY;
+        if (o < nout) {
+#pragma unroll 4
+            for (int k = cm.seg; k < nk; k += cm.S) mx = fmax(mx, (pot[k] - lo[k * sk]) * ieps);
+        }
         sh.pm[threadIdx.x] = mx;
+        __syncthreads();
+        double s = 0;
+        if (o < nout) {
+            for (int q = 0; q < cm.S; ++q) mx = fmax(mx, sh.pm[cm.jj + q * cm.CW]);
+#pragma unroll 4
+            for (int k = cm.seg; k < nk; k += cm.S) s += exp((pot[k] - lo[k * sk]) * ieps - mx);
+        }
         sh.ps[threadIdx.x] = s;
         __syncthreads();
-        if (cm.seg == 0 && j < m) {
-            for (int q = 1; q < cm.S; ++q) lse_merge(mx, s, sh.pm[threadIdx.x + q * cm.CW], sh.ps[threadIdx.x + q * cm.CW]);
-            const double lse = mx + log(s);
-            sh.g[j] = eps * log(marg(b, j, m)) - eps * lse;
+        if (cm.seg == 0 && o < nout) {
+            s = sh.ps[cm.jj];
+            for (int q = 1; q < cm.S; ++q) s += sh.ps[cm.jj + q * cm.CW];
+            out[o] = eps * log(marg(w, o, nout)) - eps * (mx + log(s));
         }
         __syncthreads();
     }
-}
-
-// f_i = eps log a_i - eps LSE_j((g_j - L_ij) / eps): one wave per row, lanes over j.
-__device__ void lse_row_update(const double* Lm, int64_t ldl, int n, int m, const double* a,
-                               double eps, GwShared& sh) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int i = w; i < n; i += GW_NW) {
-        const double* row = Lm + (int64_t)i * ldl;
-        double mx = -INFINITY, s = 0;
-        for (int j = lane; j < m; j += kWave) lse_add((sh.g[j] - row[j]) / eps, mx, s);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const double m2 = __shfl_xor(mx, o, kWave), s2 = __shfl_xor(s, o, kWave);
-            lse_merge(mx, s, m2, s2);
-        }
-        if (lane == 0) sh.f[i] = eps * log(marg(a, i, n)) - eps * (mx + log(s));
-    }
-    __syncthreads();
 }
 
 // L1 error of the column marginal: sum_j |sum_i exp((f_i + g_j - L_ij)/eps) - b_j|
+template <class Cfg>
 __device__ double lse_col_error(const double* Lm, int64_t ldl, int n, int m, const double* b,
-                                double eps, GwShared& sh) {
-    const ColMap cm(m);
+                                double ieps, GwShared<Cfg>& sh) {
+    const ColMap<Cfg> cm(m);
     double err = 0;
     for (int j0 = 0; j0 < m; j0 += cm.CW) {
         const int j = j0 + cm.jj;
         double s = 0;
         if (j < m)
             for (int i = cm.seg; i < n; i += cm.S)
-                s += exp((sh.f[i] + sh.g[j] - Lm[(int64_t)i * ldl + j]) / eps);
+                s += exp((sh.f[i] + sh.g[j] - Lm[(int64_t)i * ldl + j]) * ieps);
         sh.ps[threadIdx.x] = s;
         __syncthreads();
         if (cm.seg == 0 && j < m) {
@@ -237,7 +297,8 @@ __device__ double lse_col_error(const double* Lm, int64_t ldl, int n, int m, con
     return blk_sum(err, sh.red);
 }
 
-__device__ bool blk_timed_out(unsigned long long deadline, GwShared& sh) {
+template <class Cfg>
+__device__ bool blk_timed_out(unsigned long long deadline, GwShared<Cfg>& sh) {
     if (threadIdx.x == 0) sh.flag = __builtin_amdgcn_s_memrealtime() > deadline;
     __syncthreads();
     const bool t = sh.flag != 0;
@@ -247,18 +308,35 @@ __device__ bool blk_timed_out(unsigned long long deadline, GwShared& sh) {
 
 // OTT lse-mode Sinkhorn on L (n x m) from the potentials in sh.f / sh.g:
 // chunks of `inner` (g, f) updates, L1 column error after each chunk.
+template <class Cfg>
 __device__ int blk_sinkhorn_lse(const double* Lm, int64_t ldl, int n, int m, const double* a,
                                 const double* b, double eps, double thr, int inner, int maxit,
-                                GwShared& sh, bool& conv, unsigned long long deadline,
+                                GwShared<Cfg>& sh, bool& conv, unsigned long long deadline,
                                 bool& timeout) {
+    const double ieps = 1.0 / eps;
     int it = 0;
     conv = false;
     while (it < maxit && !conv) {
         for (int k = 0; k < inner && it < maxit; ++k, ++it) {
-            lse_col_update(Lm, ldl, n, m, b, eps, sh);
-            lse_row_update(Lm, ldl, n, m, a, eps, sh);
+#ifdef OTF_GW_STAMPS
+            unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            lse_sweep(Lm, 1, ldl, m, n, sh.f, sh.g, b, eps, ieps, sh);
+            unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            lse_sweep(Lm, ldl, 1, n, m, sh.g, sh.f, a, eps, ieps, sh);
+            unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+            if (threadIdx.x == 0 && blockIdx.x == 0) { g_gw_sk[0] += t1 - t0; g_gw_sk[1] += t2 - t1; }
+#else
+            lse_sweep(Lm, 1, ldl, m, n, sh.f, sh.g, b, eps, ieps, sh);  // g from f
+            lse_sweep(Lm, ldl, 1, n, m, sh.g, sh.f, a, eps, ieps, sh);  // f from g
+#endif
         }
-        const double err = lse_col_error(Lm, ldl, n, m, b, eps, sh);
+#ifdef OTF_GW_STAMPS
+        unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+#endif
+        const double err = lse_col_error(Lm, ldl, n, m, b, ieps, sh);
+#ifdef OTF_GW_STAMPS
+        if (threadIdx.x == 0 && blockIdx.x == 0) g_gw_sk[2] += __builtin_amdgcn_s_memrealtime() - t3;
+#endif
         if (!(err == err)) break;  // diverged
         conv = err < thr;
         if (blk_timed_out(deadline, sh)) { timeout = true; break; }
@@ -266,86 +344,198 @@ __device__ int blk_sinkhorn_lse(const double* Lm, int64_t ldl, int n, int m, con
     return it;
 }
 
-// Minimum-cost assignment of the n x n matrix A (row stride lda), one wavefront:
-// shortest augmenting paths with dual potentials, lanes over columns, ties to the
-// lowest column (the serial scan's order).  Wave-synchronous LDS (volatile, one
-// wave in program order).  Writes sh.lap.sigma; returns false on a non-finite cost.
-__device__ bool wave_lap(const double* A, int64_t lda, int n, GwShared& sh) {
-    const int lane = threadIdx.x;
-    typedef volatile __attribute__((address_space(3))) double lds_d;
-    typedef volatile __attribute__((address_space(3))) int lds_i;
-    typedef volatile __attribute__((address_space(3))) unsigned char lds_u8;
-    lds_d* u = (lds_d*)sh.f;
-    lds_d* v = (lds_d*)sh.g;
-    lds_d* minv = (lds_d*)sh.lap.minv;
-    lds_i* pc = (lds_i*)sh.lap.pc;
-    lds_i* way = (lds_i*)sh.lap.way;
-    lds_u8* used = (lds_u8*)sh.lap.used;
-    for (int j = lane; j <= n; j += kWave) { u[j] = 0; v[j] = 0; pc[j] = 0; way[j] = 0; }
+// Minimum-cost assignment of the n x n matrix A (row stride lda), ONE wavefront:
+// shortest augmenting paths with dual potentials (the serial form in the oracle's
+// oro_lap), lanes over columns.  Column j (1-based) lives in lane (j-1) % 64, slot
+// (j-1) / 64; every per-column quantity -- v, minv, used, the predecessor column
+// and the row assigned to the column together with that row's dual u -- stays in
+// its owner's registers, so a search step costs one load of the active row, a wave
+// arg-min (ties to the lowest column, the serial scan's choice) and register
+// updates; values of one column are fetched with a shuffle from its owner.
+// Arithmetic and decisions are those of the serial form step by step.  Writes
+// sigma (LDS, row -> column, 0-based); returns false on a non-finite cost.
+template <int CPL>
+__device__ bool wave_lap(const double* A, int64_t lda, int n, int* sigma, double* urow,
+                         unsigned char* done) {
+    const int lane = threadIdx.x & 63;
+    double v[CPL], minv[CPL], ucol[CPL];
+    int pc[CPL], way[CPL];
+    bool used[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) { v[c] = 0; ucol[c] = 0; pc[c] = 0; way[c] = 0; }
+    // j is wave-uniform: pick the slot, then s_readlane from the owner lane
+    auto geti = [&](const int (&arr)[CPL], int j) {
+        const int sl = (j - 1) >> 6;
+        int x = arr[0];
+#pragma unroll
+        for (int c = 1; c < CPL; ++c) if (sl == c) x = arr[c];
+        return __builtin_amdgcn_readlane(x, (j - 1) & 63);
+    };
+    auto getd = [&](const double (&arr)[CPL], int j) {
+        const int sl = (j - 1) >> 6;
+        double x = arr[0];
+#pragma unroll
+        for (int c = 1; c < CPL; ++c) if (sl == c) x = arr[c];
+        return readlane_f64(x, (j - 1) & 63);
+    };
+    // column reduction v_j = min_i a_ij, then a greedy pass in row order: row i takes
+    // its cheapest reduced column (lowest on ties) with u_i = that reduced cost when
+    // the column is free (the oracle's oro_lap, step for step).  urow / done are
+    // written with the same (wave-uniform) value by every lane and read back by each
+    // lane itself, so no cross-lane ordering is involved.
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+        const int j = 1 + lane + kWave * c;
+        double mn = GW_INF;
+        if (j <= n)
+            for (int i = 0; i < n; ++i) {
+                const double a = A[(int64_t)i * lda + (j - 1)];
+                if (a < mn) mn = a;
+            }
+        v[c] = mn;
+    }
     for (int i = 1; i <= n; ++i) {
-        if (lane == 0) pc[0] = i;
+        const double* arow = A + (int64_t)(i - 1) * lda;
+        double mn = GW_INF;
+        int jb = 0x7fffffff;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int j = 1 + lane + kWave * c;
+            if (j <= n) {
+                const double r = arow[j - 1] - v[c];
+                if (r < mn) { mn = r; jb = j; }
+            }
+        }
+        const double rmin = wave_reduce_f64<2>(mn);
+        jb = wave_min_i32(mn == rmin ? jb : 0x7fffffff);
+        if (jb > n || !(rmin < GW_INF)) return false;
+        urow[i] = rmin;
+        const bool take = geti(pc, jb) == 0;
+        done[i] = take ? 1 : 0;
+        if (take && lane == ((jb - 1) & 63)) {
+            const int sl = (jb - 1) >> 6;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+                if (sl == c) { pc[c] = i; ucol[c] = rmin; }
+        }
+    }
+    for (int i = 1; i <= n; ++i) {
+        if (done[i]) continue;
+        double ucur = urow[i];  // dual of row i, which sits at the virtual column 0
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) { minv[c] = GW_INF; used[c] = false; }
         int j0 = 0;
-        for (int j = lane; j <= n; j += kWave) { minv[j] = GW_INF; used[j] = 0; }
         while (true) {
-            if (lane == 0) used[j0] = 1;
-            const int i0 = pc[j0];
-            const double ui0 = u[i0];
+            int i0;
+            double ui0;
+            if (j0 == 0) { i0 = i; ui0 = ucur; }
+            else { i0 = geti(pc, j0); ui0 = getd(ucol, j0); }
             const double* arow = A + (int64_t)(i0 - 1) * lda;
             double delta = GW_INF;
             int j1 = 0x7fffffff;
-            for (int j = 1 + lane; j <= n; j += kWave) {
-                if (!used[j]) {
-                    const double cur = arow[j - 1] - ui0 - v[j];
-                    if (cur < minv[j]) { minv[j] = cur; way[j] = j0; }
-                    if (minv[j] < delta) { delta = minv[j]; j1 = j; }
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int j = 1 + lane + kWave * c;
+                if (j <= n && !used[c]) {
+                    const double cur = arow[j - 1] - ui0 - v[c];
+                    if (cur < minv[c]) { minv[c] = cur; way[c] = j0; }
+                    if (minv[c] < delta) { delta = minv[c]; j1 = j; }
                 }
             }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const double od = __shfl_xor(delta, o, kWave);
-                const int oj = __shfl_xor(j1, o, kWave);
-                if (od < delta || (od == delta && oj < j1)) { delta = od; j1 = oj; }
-            }
+            // wave arg-min, ties to the lowest column
+            const double dmin = wave_reduce_f64<2>(delta);
+            j1 = wave_min_i32(delta == dmin ? j1 : 0x7fffffff);
+            delta = dmin;
             if (j1 > n || !(delta < GW_INF)) return false;
-            for (int j = lane; j <= n; j += kWave) {
-                if (used[j]) { u[pc[j]] += delta; v[j] -= delta; }
-                else minv[j] -= delta;
+            ucur += delta;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                if (1 + lane + kWave * c > n) continue;
+                if (used[c]) { ucol[c] += delta; v[c] -= delta; }
+                else minv[c] -= delta;
             }
             j0 = j1;
-            if (pc[j0] == 0) break;
+            if (geti(pc, j0) == 0) break;
+            const int sl = (j0 - 1) >> 6;
+            if (lane == ((j0 - 1) & 63)) {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) if (sl == c) used[c] = true;
+            }
         }
-        if (lane == 0) {
-            do {
-                const int jp = way[j0];
-                pc[j0] = pc[jp];
-                j0 = jp;
-            } while (j0 != 0);
+        // augment along the predecessor chain; each row carries its dual along
+        while (j0 != 0) {
+            const int jp = geti(way, j0);
+            int nr;
+            double nu;
+            if (jp == 0) { nr = i; nu = ucur; }
+            else { nr = geti(pc, jp); nu = getd(ucol, jp); }
+            const int sl = (j0 - 1) >> 6;
+            if (lane == ((j0 - 1) & 63)) {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c)
+                    if (sl == c) { pc[c] = nr; ucol[c] = nu; }
+            }
+            j0 = jp;
         }
     }
-    for (int j = 1 + lane; j <= n; j += kWave) sh.lap.sigma[pc[j] - 1] = j - 1;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+        const int j = 1 + lane + kWave * c;
+        if (j <= n) sigma[pc[c] - 1] = j - 1;
+    }
     return true;
 }
 
 // ---------------------------------------------------------------------- the kernel
-__global__ __launch_bounds__(GW_NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, otf_gw_info* infos,
+template <class Cfg>
+__global__ __launch_bounds__(Cfg::NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, otf_gw_info* infos,
                                                    double* costlog, int costlog_len,
                                                    unsigned long long timeout_ticks) {
-    __shared__ GwShared sh;
+    __shared__ GwShared<Cfg> sh;
     if ((int)blockIdx.x >= Lz.nprob) return;
     const otf_gw_problem P = Lz.prob[blockIdx.x];
     const int pid = Lz.first + blockIdx.x;
     otf_gw_info* info = infos + pid;
     double* clog = costlog ? costlog + (int64_t)pid * costlog_len : nullptr;
     const int n = (int)P.n, m = (int)P.m;
-    const int64_t ldt = P.ldt;
     const int64_t nm = (int64_t)n * m;
-    double* D = Lz.ws[blockIdx.x];  // C1 . G          (n x m, ld m)
+    double* D = Lz.ws[blockIdx.x];  // (C1 . G)^T      (m x n, ld n)
     double* R = D + nm;             // C1 . G . C2     (n x m, ld m)
-    double* Lm = R + nm;            // df / linearised cost (n x m, ld m)
-    double* S = Lm + nm;            // CG: C1 . Gc . C2
-    double* G = P.T;                // the plan, in place in the output
+    double* S = R + 2 * nm;         // CG: C1 . Gc . C2
+    double* Lm;                     // df / linearised cost (n x m, ld ldl)
+    int64_t ldl;
+    double* G;                      // the plan
+    int64_t ldt, ldc1, ldc2;
+    const double* C1;
+    const double* C2;
+    if constexpr (Cfg::SMALL) {
+        for (int e = threadIdx.x; e < n * n; e += Cfg::NT) sh.mat.C1[e] = P.C1[(e / n) * P.ldc1 + e % n];
+        for (int e = threadIdx.x; e < m * m; e += Cfg::NT) sh.mat.C2[e] = P.C2[(e / m) * P.ldc2 + e % m];
+        C1 = sh.mat.C1;
+        C2 = sh.mat.C2;
+        ldc1 = n;
+        ldc2 = m;
+        Lm = sh.mat.L;
+        ldl = m + 1;
+        G = sh.mat.G;
+        ldt = m;
+        __syncthreads();
+    } else {
+        C1 = P.C1;
+        C2 = P.C2;
+        ldc1 = P.ldc1;
+        ldc2 = P.ldc2;
+        Lm = R + nm;
+        ldl = m;
+        G = P.T;
+        ldt = P.ldt;
+    }
     const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
     const int t = threadIdx.x;
+#ifdef OTF_GW_STAMPS
+    unsigned long long gw_acc[4] = {0, 0, 0, 0};
+    const unsigned long long gw_start = __builtin_amdgcn_s_memrealtime();
+#endif
 
     int status = OTF_GW_MAX_ITER, it = 0, inner_total = 0;
     bool converged = false, inner_conv = false;
@@ -354,20 +544,22 @@ __global__ __launch_bounds__(GW_NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, o
     if (o.solver == OTF_GW_CG) {
         // G0 = p q^T (uniform), constC terms from p, q
         const double g0 = 1.0 / ((double)n * (double)m);
-        for (int64_t e = t; e < nm; e += GW_NT) G[(e / m) * ldt + (e % m)] = g0;
-        for (int i = t; i < n; i += GW_NT) sh.mg.r[i] = 1.0 / n;
-        for (int j = t; j < m; j += GW_NT) sh.mg.c[j] = 1.0 / m;
+        for (int64_t e = t; e < nm; e += Cfg::NT) G[(e / m) * ldt + (e % m)] = g0;
+        for (int i = t; i < n; i += Cfg::NT) sh.mg.r[i] = 1.0 / n;
+        for (int j = t; j < m; j += Cfg::NT) sh.mg.c[j] = 1.0 / m;
         __syncthreads();
-        blk_sq_matvec(sh.x, P.C1, P.ldc1, n, sh.mg.r);
-        blk_sq_matvec(sh.y, P.C2, P.ldc2, m, sh.mg.c);
+        { GW_TBEG();
+        blk_sq_matvec<Cfg>(sh.x, C1, ldc1, n, sh.mg.r);
+        blk_sq_matvec<Cfg>(sh.y, C2, ldc2, m, sh.mg.c);
         __syncthreads();
-        blk_gemm<false>(D, m, P.C1, P.ldc1, G, ldt, n, m, n, nullptr, 1.0);
+        blk_gemm<Cfg, false>(D, 1, n, C1, 1, ldc1, G, ldt, 1, n, m, n, nullptr, 1.0);
         __syncthreads();
-        blk_gemm<false>(R, m, D, m, P.C2, P.ldc2, n, m, m, nullptr, 1.0);
+        blk_gemm<Cfg, false>(R, m, 1, D, 1, n, C2, ldc2, 1, n, m, m, nullptr, 1.0);
         __syncthreads();
+        GW_TEND(0); }
         // cost(G) = <constC - 2 R, G>
         double acc = 0;
-        for (int64_t e = t; e < nm; e += GW_NT) {
+        for (int64_t e = t; e < nm; e += Cfg::NT) {
             const int i = (int)(e / m), j = (int)(e % m);
             acc += (sh.x[i] + sh.y[j] - 2.0 * R[e]) * G[i * ldt + j];
         }
@@ -378,17 +570,18 @@ __global__ __launch_bounds__(GW_NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, o
             const double old = cost;
             // df = 2 (constC - 2 R);  Mi = df + min(df)
             double mn = INFINITY;
-            for (int64_t e = t; e < nm; e += GW_NT) {
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
                 const int i = (int)(e / m), j = (int)(e % m);
                 const double df = 2.0 * (sh.x[i] + sh.y[j] - 2.0 * R[e]);
-                Lm[e] = df;
+                Lm[i * ldl + j] = df;
                 mn = fmin(mn, df);
             }
-            mn = blk_minmax(mn, sh.red, false);
+            mn = blk_minmax<Cfg>(mn, sh.red, false);
             bool finite = true;
-            for (int64_t e = t; e < nm; e += GW_NT) {
-                const double v = Lm[e] + mn;
-                Lm[e] = v;
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
+                const int64_t le = (e / m) * ldl + e % m;
+                const double v = Lm[le] + mn;
+                Lm[le] = v;
                 if (!finite_val(v)) finite = false;
             }
             sh.flag = 0;
@@ -398,19 +591,23 @@ __global__ __launch_bounds__(GW_NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, o
             if (sh.flag) { status = OTF_GW_NUMERICAL; break; }
             __syncthreads();
             // Gc = assignment(Mi) / n
+{ GW_TBEG();
             if (t < kWave) {
-                const bool ok = wave_lap(Lm, m, n, sh);
+                const bool ok = wave_lap<(Cfg::MAXV + kWave - 1) / kWave>(Lm, ldl, n, sh.lap.sigma, sh.f, sh.lap.used);
                 if (t == 0) sh.flag = ok ? 0 : 1;
             }
             __syncthreads();
+GW_TEND(1); }
             if (sh.flag) { status = OTF_GW_NUMERICAL; break; }
             // S = C1 Gc C2:  S_ij = (1/n) sum_k C1[i][k] C2[sigma(k)][j]
-            blk_gemm<true>(S, m, P.C1, P.ldc1, P.C2, P.ldc2, n, m, n, sh.lap.sigma, 1.0 / n);
+{ GW_TBEG();
+            blk_gemm<Cfg, true>(S, m, 1, C1, 1, ldc1, C2, ldc2, 1, n, m, n, sh.lap.sigma, 1.0 / n);
             __syncthreads();
+GW_TEND(0); }
             // dot = 2 (S - R); a = -<dot, Gc - G>; b = -2 <dot, G>
             double ta = 0, tb = 0;
             const double gc = 1.0 / n;
-            for (int64_t e = t; e < nm; e += GW_NT) {
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
                 const int i = (int)(e / m), j = (int)(e % m);
                 const double dot = 2.0 * (S[e] - R[e]);
                 const double gv = G[i * ldt + j];
@@ -425,7 +622,7 @@ __global__ __launch_bounds__(GW_NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, o
             else alpha = (a + b < 0) ? 1.0 : 0.0;
             cost = cost + a * (alpha * alpha) + b * alpha;
             // G += alpha (Gc - G)
-            for (int64_t e = t; e < nm; e += GW_NT) {
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
                 const int i = (int)(e / m), j = (int)(e % m);
                 const double gv = G[i * ldt + j];
                 const double gcv = (sh.lap.sigma[i] == j) ? gc : 0.0;
@@ -434,10 +631,12 @@ __global__ __launch_bounds__(GW_NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, o
             __syncthreads();
             if (clog && t == 0 && it < costlog_len) clog[it] = cost;
             // df(G) for the next iteration (POT recomputes it from G)
-            blk_gemm<false>(D, m, P.C1, P.ldc1, G, ldt, n, m, n, nullptr, 1.0);
+            { GW_TBEG();
+            blk_gemm<Cfg, false>(D, 1, n, C1, 1, ldc1, G, ldt, 1, n, m, n, nullptr, 1.0);
             __syncthreads();
-            blk_gemm<false>(R, m, D, m, P.C2, P.ldc2, n, m, m, nullptr, 1.0);
+            blk_gemm<Cfg, false>(R, m, 1, D, 1, n, C2, ldc2, 1, n, m, m, nullptr, 1.0);
             __syncthreads();
+            GW_TEND(0); }
             const double absd = fabs(cost - old);
             const double reld = cost != 0.0 ? absd / fabs(cost) : NAN;
             if (reld < o.tol_rel || absd < o.tol_abs) { converged = true; status = OTF_GW_CONVERGED; break; }
@@ -448,59 +647,65 @@ __global__ __launch_bounds__(GW_NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, o
         // Entropic GW (OTT).  P0 = a b^T; f = g = 0.
         const double* pa = P.p;
         const double* pb = P.q;
-        for (int64_t e = t; e < nm; e += GW_NT) {
+        for (int64_t e = t; e < nm; e += Cfg::NT) {
             const int i = (int)(e / m), j = (int)(e % m);
             G[i * ldt + j] = marg(pa, i, n) * marg(pb, j, m);
         }
-        for (int i = t; i < n; i += GW_NT) { sh.mg.r[i] = marg(pa, i, n); sh.f[i] = 0; }
-        for (int j = t; j < m; j += GW_NT) { sh.mg.c[j] = marg(pb, j, m); sh.g[j] = 0; }
+        for (int i = t; i < n; i += Cfg::NT) { sh.mg.r[i] = marg(pa, i, n); sh.f[i] = 0; }
+        for (int j = t; j < m; j += Cfg::NT) { sh.mg.c[j] = marg(pb, j, m); sh.g[j] = 0; }
         __syncthreads();
         double cprev = 0, cprev2 = 0;
         bool timeout = false;
         while (true) {
             // linearisation at the current plan
-            blk_sq_matvec(sh.x, P.C1, P.ldc1, n, sh.mg.r);
-            blk_sq_matvec(sh.y, P.C2, P.ldc2, m, sh.mg.c);
-            blk_gemm<false>(D, m, P.C1, P.ldc1, G, ldt, n, m, n, nullptr, 1.0);
+            { GW_TBEG();
+            blk_sq_matvec<Cfg>(sh.x, C1, ldc1, n, sh.mg.r);
+            blk_sq_matvec<Cfg>(sh.y, C2, ldc2, m, sh.mg.c);
+            blk_gemm<Cfg, false>(D, 1, n, C1, 1, ldc1, G, ldt, 1, n, m, n, nullptr, 1.0);
             __syncthreads();
-            blk_gemm<false>(R, m, D, m, P.C2, P.ldc2, n, m, m, nullptr, 1.0);
+            blk_gemm<Cfg, false>(R, m, 1, D, 1, n, C2, ldc2, 1, n, m, m, nullptr, 1.0);
             __syncthreads();
-            for (int64_t e = t; e < nm; e += GW_NT) {
+            GW_TEND(0); }
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
                 const int i = (int)(e / m), j = (int)(e % m);
                 double l = sh.x[i] + sh.y[j] - 2.0 * R[e];
                 if (P.labels_a && P.labels_a[i] != P.labels_b[j]) l = INFINITY;
-                Lm[e] = l;
+                Lm[i * ldl + j] = l;
             }
             if (!o.warm_start) {
-                for (int i = t; i < n; i += GW_NT) sh.f[i] = 0;
-                for (int j = t; j < m; j += GW_NT) sh.g[j] = 0;
+                for (int i = t; i < n; i += Cfg::NT) sh.f[i] = 0;
+                for (int j = t; j < m; j += Cfg::NT) sh.g[j] = 0;
             }
             __syncthreads();
-            int sk_it = blk_sinkhorn_lse(Lm, m, n, m, pa, pb, o.eps, o.sk_threshold, o.sk_inner,
+#ifdef OTF_GW_STAMPS
+            unsigned long long gw_t0_ = __builtin_amdgcn_s_memrealtime();
+#endif
+            int sk_it = blk_sinkhorn_lse(Lm, ldl, n, m, pa, pb, o.eps, o.sk_threshold, o.sk_inner,
                                          o.sk_max_iter, sh, inner_conv, deadline, timeout);
+            GW_TEND(2);
             inner_total += sk_it;
             // plan, its marginals and mass; reg_ot_cost
             double mass = 0;
-            for (int64_t e = t; e < nm; e += GW_NT) {
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
                 const int i = (int)(e / m), j = (int)(e % m);
-                const double pv = exp((sh.f[i] + sh.g[j] - Lm[e]) / o.eps);
+                const double pv = exp((sh.f[i] + sh.g[j] - Lm[i * ldl + j]) / o.eps);
                 G[i * ldt + j] = pv;
                 mass += pv;
             }
             mass = blk_sum(mass, sh.red);  // (barrier inside: plan visible)
-            for (int i = t; i < n; i += GW_NT) {
+            for (int i = t; i < n; i += Cfg::NT) {
                 double s = 0;
                 for (int j = 0; j < m; ++j) s += G[i * ldt + j];
                 sh.mg.r[i] = s;
             }
-            for (int j = t; j < m; j += GW_NT) {
+            for (int j = t; j < m; j += Cfg::NT) {
                 double s = 0;
                 for (int i = 0; i < n; ++i) s += G[i * ldt + j];
                 sh.mg.c[j] = s;
             }
             double fa = 0, sa = 0, sb = 0;
-            for (int i = t; i < n; i += GW_NT) { fa += marg(pa, i, n) * sh.f[i]; sa += marg(pa, i, n); }
-            for (int j = t; j < m; j += GW_NT) { fa += marg(pb, j, m) * sh.g[j]; sb += marg(pb, j, m); }
+            for (int i = t; i < n; i += Cfg::NT) { fa += marg(pa, i, n) * sh.f[i]; sa += marg(pa, i, n); }
+            for (int j = t; j < m; j += Cfg::NT) { fa += marg(pb, j, m) * sh.g[j]; sb += marg(pb, j, m); }
             fa = blk_sum(fa, sh.red);
             sa = blk_sum(sa, sh.red);
             sb = blk_sum(sb, sh.red);
@@ -519,6 +724,15 @@ __global__ __launch_bounds__(GW_NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, o
             if (blk_timed_out(deadline, sh)) { status = OTF_GW_TIMEOUT; break; }
         }
     }
+    if constexpr (Cfg::SMALL) {
+        __syncthreads();
+        for (int e = t; e < (int)nm; e += Cfg::NT) P.T[(e / m) * P.ldt + e % m] = G[e];
+    }
+#ifdef OTF_GW_STAMPS
+    gw_acc[3] = __builtin_amdgcn_s_memrealtime() - gw_start;
+    if (t == 0 && blockIdx.x < 16)
+        for (int k = 0; k < 4; ++k) g_gw_stamps[blockIdx.x * 8 + k] = gw_acc[k];
+#endif
     if (t == 0) {
         info->n_iter = it;
         info->converged = converged ? 1 : 0;
@@ -684,7 +898,13 @@ int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* 
             L.ws[b] = (double*)wsp;
             wsp += align256(4 * 8 * (size_t)(probs[first + b].n * probs[first + b].m));
         }
-        gw_kernel<<<L.nprob, GW_NT, 0, s>>>(L, o, info, costlog, costlog_len, ticks);
+        bool small = true;
+        for (int b = 0; b < L.nprob; ++b)
+            if (L.prob[b].n > GW_SMALLN || L.prob[b].m > GW_SMALLN) small = false;
+        if (small)
+            gw_kernel<GwSmall><<<L.nprob, GwSmall::NT, 0, s>>>(L, o, info, costlog, costlog_len, ticks);
+        else
+            gw_kernel<GwBig><<<L.nprob, GwBig::NT, 0, s>>>(L, o, info, costlog, costlog_len, ticks);
         OTF_HIP(hipGetLastError());
     }
     return OTF_OK;
