@@ -58,7 +58,7 @@ def parse():
     p.add_argument("--profile-only", action="store_true",
                    help="run warmup + steps only (for rocprofv3 runs); no probes, no JSON")
     p.add_argument("--no-gw", action="store_true", help="skip the per-epoch GW latency leg")
-    p.add_argument("--engine", default="auto", choices=("auto", "stream", "resident"),
+    p.add_argument("--engine", default="auto", choices=("auto", "stream", "resident", "tiled"),
                    help="Sinkhorn engine (auto = resident when the cost fits the register file)")
     return p.parse_args()
 
@@ -142,7 +142,7 @@ def main():
     # does all iterations (+ the plan write) with the cost held in registers, so its
     # algorithmic rate can exceed the HBM peak — the PMC traffic shows the real bytes.
     iter_bytes = N * N * 4
-    kernel_name = "sk_resident_kernel" if engine == "resident" else "sk_pass_kernel"
+    kernel_name = {"resident": "sk_resident_kernel", "tiled": "sk_tiled_kernel"}.get(engine, "sk_pass_kernel")
 
     def pmc_traffic(kname):
         try:
@@ -155,7 +155,7 @@ def main():
     traffic = pmc_traffic(kernel_name)
     # streaming engine for reference: HIP event pair around every fused pass
     pass_ms = ops.sinkhorn_profile(a, a, C, eps, iters, cost_scale=cmax, workspace=ws)
-    if engine == "resident":
+    if engine in ("resident", "tiled"):
         launch_bytes = iter_bytes * iters
         achieved = launch_bytes / (sk_ms * 1e-3) / 1e9
     else:
@@ -192,7 +192,7 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "algorithmic_bytes_per_launch": launch_bytes,
                      "note": ("resident: all iterations in one launch, cost held in registers; "
-                              "algorithmic bytes = iters x N*N*4" if engine == "resident" else
+                              "algorithmic bytes = iters x N*N*4" if engine in ("resident", "tiled") else
                               "one launch per iteration; C (64 MiB) fits the 256 MiB Infinity Cache")},
         "cost_roofline": {"bound": "mfma", "kernel": "cost_split16_kernel", "achieved": cost_tflops,
                           "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -74,8 +74,17 @@ enum {
  * OTF_ENGINE_STREAM: one launch per iteration, C re-read from HBM every iteration.
  * OTF_ENGINE_RESIDENT: one persistent launch for the whole solve; every workgroup
  *   keeps its rows of K = exp(-C/reg) in registers; iterations are separated by a
- *   device-wide barrier.  POT flavour only.                                      */
-typedef enum { OTF_ENGINE_AUTO = 0, OTF_ENGINE_STREAM = 1, OTF_ENGINE_RESIDENT = 2 } otf_engine;
+ *   device-wide barrier.  POT flavour only.
+ * OTF_ENGINE_TILED: resident like OTF_ENGINE_RESIDENT, float32, but every workgroup
+ *   keeps a 128-row x 512-column TILE of K; the row sums are combined within groups
+ *   of column tiles, the column sums across the grid (8x fewer atomics).  AUTO picks
+ *   it first when ceil(n/128) * ceil(m/512) <= #CUs.                              */
+typedef enum {
+    OTF_ENGINE_AUTO = 0,
+    OTF_ENGINE_STREAM = 1,
+    OTF_ENGINE_RESIDENT = 2,
+    OTF_ENGINE_TILED = 3
+} otf_engine;
 
 typedef struct {
     double reg;         /* entropic regularisation (absolute, on the scaled cost)      */

@@ -175,8 +175,10 @@ __global__ void scale_inplace_kernel(T* C, int64_t n, int64_t m, int64_t ldc, co
 // accumulator) instead of eight v_mfma_f32_32x32x2_f32: ~5x the MFMA rate.
 // ============================================================================
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
-constexpr int SBK = 32;        // K per LDS stage
-constexpr int SLD = SBK + 8;   // padded LDS row (80 B): conflict-free ds_read_b128
+constexpr int SBK = 64;        // K per LDS stage
+constexpr int SLD = SBK + 8;   // padded LDS row (144 B): conflict-free ds_read_b128
+constexpr int SCPR = SBK / 8;  // 16-B chunks per row per stage
+constexpr int SCPT = BM * SCPR / 256;  // chunks per thread per image
 
 // One 256-thread workgroup per row: squared norm (fp32, same expansion as the fp32
 // path) and the fp16 image(s) of the row, zero-padded to ldh.
@@ -282,12 +284,12 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
     // staging: a 128-row x 32-half tile is 512 16-B chunks; 256 threads x 2 chunks,
     // for each of {A hi, A lo, B hi, B lo} (lo only when NS == 3)
     using u4 = __attribute__((ext_vector_type(4))) unsigned int;
-    u4 st[2][2 * NI];
+    u4 st[SCPT][2 * NI];
     auto gload = [&](int k0) {
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
+        for (int c = 0; c < SCPT; ++c) {
             const int chunk = tid + 256 * c;
-            const int row = chunk >> 2, kc = (chunk & 3) * 8;
+            const int row = chunk / SCPR, kc = (chunk % SCPR) * 8;
             const int gi = i0 + row < n ? i0 + row : n - 1;
             const int gj = j0 + row < m ? j0 + row : m - 1;
             st[c][0] = *reinterpret_cast<const u4*>(Xh + (int64_t)gi * ldh + k0 + kc);
@@ -300,9 +302,9 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
     };
     auto lstore = [&]() {
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
+        for (int c = 0; c < SCPT; ++c) {
             const int chunk = tid + 256 * c;
-            const int row = chunk >> 2, kc = (chunk & 3) * 8;
+            const int row = chunk / SCPR, kc = (chunk % SCPR) * 8;
 #pragma unroll
             for (int h = 0; h < NI; ++h) {
                 *reinterpret_cast<u4*>(&As[h][row][kc]) = st[c][h];

@@ -1013,6 +1013,424 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     }
 }
 
+// ============================================================================
+// Tiled resident engine (OTF_ENGINE_TILED, float): the whole solve in one launch like
+// sk_resident_kernel, but each workgroup owns a 2-D TILE of K -- TL_R = 128 rows x
+// TL_C = 512 columns (8 waves x 16 rows, 64 lanes x 8 columns) -- instead of 16
+// full rows.  Per iteration it therefore adds only 512 column partials to the sums
+// (8x fewer float atomics: they execute at the memory side at ~1.3 TB/s chip-wide,
+// and 4096 per workgroup were the single largest term of an iteration), and the
+// row sums K v become a two-level reduction: within the wave (butterfly), then over
+// the ncb column tiles of the row block -- a GROUP of workgroups that exchange 128
+// partials each through write-through (sc1) stores and a per-group arrival counter
+// (placed on one XCD when the shape allows; speed only).  Every member gathers the
+// ncb partials in the same fixed order, so all members compute the same u.
+//
+// Control differs from sk_resident_kernel only in WHEN a numerical break in v is
+// seen: a workgroup sees only its own columns, so a zero / non-finite v counts into
+// bad_cnt[it] (as a non-finite u always did) and every workgroup takes the break at
+// the top of iteration it+1 -- the same (last_good, niter, break_iter) as POT.  The
+// marginal error of iterate it-1 (every check_every) is computed by every workgroup
+// from the FULL sum vectors cs[it] and cs[it-1] (v(it-1) = b / cs[it-1] is recomputed
+// bit-identically), so every workgroup takes the same stop decision at once.
+// ============================================================================
+constexpr int TL_RW = 16;                 // rows per wave (per thread)
+constexpr int TL_NW = 8;                  // waves per workgroup
+constexpr int TL_R = TL_RW * TL_NW;       // 128 rows per tile
+constexpr int TL_G = 2, TL_VEC = 4;       // 8 columns per lane
+constexpr int TL_C = kWave * TL_G * TL_VEC;  // 512 columns per tile
+
+template <typename T> struct SkTileArgs {
+    const void* C;
+    int64_t ldc;
+    int n, m, m_pad;
+    const T* a;
+    const T* b;
+    const T* cost_scale;
+    double reg;
+    int max_iter, check_every, err_squared;
+    double stop_thr;
+    T* cs;            // (max_iter + 1) x nrep x m_pad column sums, zeroed before launch
+    int nrep;
+    int* bad_cnt;     // max_iter + 1 counters, zeroed
+    int* bar;         // flat barrier counter, zeroed
+    SkSync sync;      // hierarchical barrier words, zeroed
+    T* xch;           // 2 x nrb x ncb x TL_R row partials (write-through hand-off)
+    int* grp;         // nrb counters, one 256-B line each, zeroed
+    int nrb, ncb;
+    otf_sinkhorn_info* info;
+    double* errlog;
+    T* u_out;
+    T* v_out;
+    void* P;
+    int64_t ldp;
+    unsigned long long timeout_ticks;
+};
+
+template <typename T>
+__device__ __forceinline__ void store_wt(T* p, T v) {  // write-through (sc1) store
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename CT, typename TP, int NREP>
+__global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
+    using T = float;
+    constexpr int G = TL_G, VEC = TL_VEC, R = TL_RW;
+    using V = typename Vec<T>::type;
+    using VP = __attribute__((ext_vector_type(VEC))) TP;
+    __shared__ __attribute__((aligned(16))) T colbuf[TL_NW][TL_C];
+    __shared__ T urow[TL_NW][R];          // u of each wave's rows (wave-private)
+    __shared__ T uhist[2][TL_R];          // u history (slot = iteration & 1)
+    __shared__ __attribute__((aligned(16))) T vhist[2][TL_C];  // v history
+    __shared__ T red[17 + 17];
+    __shared__ int s_flag;
+    __shared__ int s_pop[3];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nwg = gridDim.x;
+    const bool lead = (blockIdx.x == 0 && tid == 0);
+    const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+
+    // tile of this workgroup; groups (row blocks) on one XCD when nrb % 8 == 0
+    int rb, cb;
+    {
+        const int b = blockIdx.x;
+        if ((p.nrb & 7) == 0) {
+            const int x = b & 7, q = b >> 3;
+            rb = (q / p.ncb) * 8 + x;
+            cb = q % p.ncb;
+        } else {
+            rb = b / p.ncb;
+            cb = b % p.ncb;
+        }
+    }
+    const int row0 = rb * TL_R + w * R;   // this wave's first row
+    const int col0 = cb * TL_C;           // this tile's first column
+
+    const double unit = exp_unit<T>();
+    double cinv = 1.0;
+    if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
+    const T ks = (T)(-unit / p.reg * cinv);
+
+    int colc[G];
+    bool cok[G][VEC];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int c0 = col0 + (lane + kWave * g) * VEC;
+        colc[g] = c0 < p.m ? c0 : 0;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) cok[g][k] = c0 + k < p.m;
+    }
+    // ---- K for this wave's 16 rows x this lane's 8 columns, once
+    T kv[R][G][VEC];
+    {
+        const CT* crow = (const CT*)p.C + (int64_t)row0 * p.ldc;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const CT* src = (row0 + r < p.n) ? crow : (const CT*)p.C;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const V c = load_cost<T>(src + colc[g]);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
+            }
+            crow += p.ldc;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool rok = row0 + r < p.n;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k)
+                    kv[r][g][k] = (rok && cok[g][k]) ? fast_exp(kv[r][g][k] * ks) : (T)0;
+        }
+    }
+    // 1 / a of the row whose total this lane finishes (lanes 0..15 of each wave)
+    const T ia_mine = (T)1 / p.a[row0 + (lane & (R - 1)) < p.n ? row0 + (lane & (R - 1)) : p.n - 1];
+    const T u0 = (T)1 / (T)p.n, v0 = (T)1 / (T)p.m;
+    for (int q = tid; q < TL_C; q += blockDim.x) vhist[0][q] = vhist[1][q] = v0;
+    if (tid < TL_R) uhist[0][tid] = uhist[1][tid] = u0;
+
+    const size_t it_stride = (size_t)NREP * p.m_pad;
+    const int xcd = xcc_id();
+    const int my_rep = xcd % NREP;
+    const __amdgpu_buffer_rsrc_t rs = sums_rsrc(p.cs);
+    // this lane's 8 column sums of one buffer (all replicas), unmasked 16-B sc1 loads
+    auto load_sums = [&](const T* base, T (&out)[G][VEC], T fill) {
+        const uint32_t boff = (uint32_t)((base - p.cs) * sizeof(T));
+        V acc[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] = load_sum_vec<T>(rs, boff + colc[g] * (uint32_t)sizeof(T));
+#pragma unroll
+        for (int q = 1; q < NREP; ++q)
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const V t = load_sum_vec<T>(rs, boff + (uint32_t)((q * p.m_pad + colc[g]) * sizeof(T)));
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) acc[g][k] += t[k];
+            }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) out[g][k] = cok[g][k] ? acc[g][k] : fill;
+    };
+    // full-vector L2 marginal error of iterate `itp` (needs cs[itp + 1] and cs[itp])
+    auto full_error = [&](int itp) -> double {
+        const uint32_t bs = (uint32_t)((size_t)(itp + 1) * it_stride * sizeof(T));
+        const uint32_t bp = (uint32_t)((size_t)itp * it_stride * sizeof(T));
+        T e = 0;
+        for (int c0 = tid * VEC; c0 < p.m_pad; c0 += blockDim.x * VEC) {
+            V sc = load_sum_vec<T>(rs, bs + c0 * (uint32_t)sizeof(T));
+            V sp = load_sum_vec<T>(rs, bp + c0 * (uint32_t)sizeof(T));
+#pragma unroll
+            for (int q = 1; q < NREP; ++q) {
+                const V t1 = load_sum_vec<T>(rs, bs + (uint32_t)((q * p.m_pad + c0) * sizeof(T)));
+                const V t2 = load_sum_vec<T>(rs, bp + (uint32_t)((q * p.m_pad + c0) * sizeof(T)));
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) { sc[k] += t1[k]; sp[k] += t2[k]; }
+            }
+            const V bv = *reinterpret_cast<const V*>(p.b + c0);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const T vb = bv[k] / sp[k];
+                const T rr = vb * sc[k] - bv[k];
+                e += (c0 + k < p.m) ? rr * rr : (T)0;
+            }
+        }
+        e = block_sum<T>(e, red);
+        return p.err_squared ? (double)e : sqrt((double)e);
+    };
+    // column partials K_tile^T w -> atomics into sums buffer dst (this tile's columns)
+    auto flush = [&](const T (&wr)[R], T* dst) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            V acc;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                T sacc = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) sacc += kv[r][g][k] * wr[r];
+                acc[k] = sacc;
+            }
+            *reinterpret_cast<V*>(&colbuf[w][(lane + kWave * g) * VEC]) = acc;
+        }
+        __syncthreads();
+        for (int q = tid; q < TL_C; q += blockDim.x) {
+            T sacc = colbuf[0][q];
+#pragma unroll
+            for (int ww = 1; ww < TL_NW; ++ww) sacc += colbuf[ww][q];
+            if (col0 + q < p.m) atomicAdd(dst + (size_t)my_rep * p.m_pad + col0 + q, sacc);
+        }
+    };
+
+    // ---- prologue: K^T u0 into sums[0]
+    {
+        T wr[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) wr[r] = (row0 + r < p.n) ? u0 : (T)0;
+        flush(wr, p.cs);
+    }
+    int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
+    bool done = false;
+    if (tid == 0)
+        __hip_atomic_fetch_add(p.sync.reg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!grid_barrier(p.bar, nwg, deadline, &s_flag)) {
+        status = OTF_SK_TIMEOUT;
+        done = true;
+    }
+    if (tid == 0) {
+        int nact = 0;
+        unsigned mask = 0;
+        for (int x = 0; x < 8; ++x) {
+            const int c = __hip_atomic_load(p.sync.reg + x * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c > 0) { ++nact; mask |= 1u << x; }
+        }
+        s_pop[0] = __hip_atomic_load(p.sync.reg + xcd * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_pop[1] = nact;
+        s_pop[2] = (int)mask;
+    }
+    __syncthreads();
+    const int nx = s_pop[0], nact = s_pop[1];
+    const unsigned act_mask = (unsigned)s_pop[2];
+    int* gcnt = p.grp + rb * 64;
+    const int rowl = butterfly_row<R>(lane);  // row whose wave total this lane holds
+
+    for (int it = 0; it < p.max_iter && !done; ++it) {
+        OTF_STAMP(it, 0);
+        // a numerical break in iteration it-1 (v or u, any tile) -> revert to it-2
+        if (it >= 1 && load_agent(p.bad_cnt + it - 1) > 0) {
+            last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
+            break;
+        }
+        T s[G][VEC], vn[G][VEC];
+        load_sums(p.cs + (size_t)it * it_stride, s, (T)1);
+        int badv = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const V bv = *reinterpret_cast<const V*>(p.b + colc[g]);  // target marginal (L1/L2)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const T val = bv[k] / s[g][k];
+                badv |= (cok[g][k] && ((s[g][k] == (T)0) || !finite_val(val))) ? 1 : 0;
+                vn[g][k] = cok[g][k] ? val : (T)0;
+            }
+        }
+        // marginal error of iterate it-1 from the full sum vectors (same in every tile)
+        if (it >= 1 && ((it - 1) % p.check_every) == 0) {
+            const double err = full_error(it - 1);
+            if (lead) p.errlog[(it - 1) / p.check_every] = err;
+            n_err = (it - 1) / p.check_every + 1;
+            if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) {
+                last_good = it - 1; niter = it - 1; status = OTF_SK_CONVERGED;
+                break;
+            }
+        }
+        if (__any(badv) && lane == 0) atomicAdd(p.bad_cnt + it, 1);
+        OTF_STAMP(it, 1);
+        // row partials over this tile's columns, wave totals, publish to the group
+        T rp[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            T acc = 0;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) acc += kv[r][g][k] * vn[g][k];
+            rp[r] = acc;
+        }
+        wave_sum_multi<T, R>(rp, lane);
+        const int slot = it & 1;
+        T* xg = p.xch + ((size_t)slot * p.nrb + rb) * (size_t)p.ncb * TL_R;
+        if (lane < R) store_wt(xg + (size_t)cb * TL_R + w * R + rowl, rp[0]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            int ok = 1;
+            __hip_atomic_fetch_add(gcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int target = p.ncb * (it + 1);
+            while (load_agent(gcnt) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = 0; break; }
+            }
+            s_flag = ok;
+        }
+        __syncthreads();
+        if (!s_flag) { status = OTF_SK_TIMEOUT; done = true; break; }
+        OTF_STAMP(it, 2);
+        // gather the ncb partials of this wave's rows (fixed order), u(it)
+        T tot = 0;
+        {
+            const int rr = lane & (R - 1);
+            for (int mb = lane >> 4; mb < p.ncb; mb += 4)
+                tot += __hip_atomic_load(xg + (size_t)mb * TL_R + w * R + rr, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            tot += __shfl_xor(tot, 16, kWave);
+            tot += __shfl_xor(tot, 32, kWave);
+        }
+        if (lane < R) {
+            const int rr = lane;
+            const bool rok = row0 + rr < p.n;
+            T un = (T)1 / (tot * ia_mine);
+            if (!rok) un = 0;
+            urow[w][rr] = un;
+            uhist[slot][w * R + rr] = un;
+        }
+        __builtin_amdgcn_wave_barrier();  // wave-private LDS hand-off (in-order LDS queue)
+        T un[R];
+        int badu = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            un[r] = urow[w][r];
+            badu |= (row0 + r < p.n && !finite_val(un[r])) ? 1 : 0;
+        }
+        if (badu && lane == 0) atomicAdd(p.bad_cnt + it, 1);
+        if (w == 0) {
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                *reinterpret_cast<V*>(&vhist[slot][(lane + kWave * g) * VEC]) =
+                    V{vn[g][0], vn[g][1], vn[g][2], vn[g][3]};
+        }
+        OTF_STAMP(it, 3);
+        flush(un, p.cs + (size_t)(it + 1) * it_stride);
+        if (!xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 1, deadline, &s_flag)) {
+            status = OTF_SK_TIMEOUT;
+            done = true;
+        }
+        OTF_STAMP(it, 5);
+    }
+    if (status == OTF_SK_MAX_ITER && p.max_iter > 0) {
+        const int it = p.max_iter - 1;
+        if (load_agent(p.bad_cnt + it) > 0) {
+            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
+        } else {
+            last_good = it; niter = it;
+            if ((it % p.check_every) == 0) {
+                const double err = full_error(it);
+                if (lead) p.errlog[it / p.check_every] = err;
+                n_err = it / p.check_every + 1;
+                if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) status = OTF_SK_CONVERGED;
+            }
+        }
+    }
+
+    // ---- outputs: (u, v) of last_good from the histories, plan from registers
+    __syncthreads();
+    const int hs = last_good & 1;
+    T uo[R], vo[G][VEC];
+#pragma unroll
+    for (int r = 0; r < R; ++r) uo[r] = last_good < 0 ? u0 : uhist[hs][w * R + r];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+            vo[g][k] = last_good < 0 ? v0 : vhist[hs][(lane + kWave * g) * VEC + k];
+    if (cb == 0 && lane < R && row0 + lane < p.n) {
+        T mine = uo[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) if (lane == r) mine = uo[r];
+        p.u_out[row0 + lane] = mine;
+    }
+    if (rb == 0 && w == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k)
+                if (cok[g][k]) p.v_out[colc[g] + k] = vo[g][k];
+    }
+    if (p.P) {
+        TP* P = (TP*)p.P;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (row0 + r >= p.n) break;
+            TP* prow = P + (int64_t)(row0 + r) * p.ldp;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int c0 = col0 + (lane + kWave * g) * VEC;
+                if (c0 >= p.m) continue;
+                VP o;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) o[k] = (TP)(uo[r] * kv[r][g][k] * vo[g][k]);
+                if (c0 + VEC <= p.m) {
+                    *reinterpret_cast<VP*>(prow + c0) = o;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k)
+                        if (c0 + k < p.m) prow[c0 + k] = o[k];
+                }
+            }
+        }
+    }
+    if (lead) {
+        p.info->last_good = last_good;
+        p.info->niter = niter;
+        p.info->status = status;
+        p.info->break_iter = brk;
+        p.info->n_err = n_err;
+        p.info->engine = OTF_ENGINE_TILED;
+        p.info->stop = 1;
+    }
+}
+
 struct PassCfg {
     int G, R, NT;
 };
@@ -1073,6 +1491,8 @@ struct Workspace {
     int nrep;
     size_t bytes;
     int64_t m_pad;
+    int64_t t_nrb, t_ncb;  // tiled engine: row / column tiles
+    size_t t_xch_off;      // tiled engine: exchange region offset inside res
 };
 
 // hierarchical barrier words: reg[8], xcnt[8], top, gen[8], each on a 256-B line
@@ -1106,6 +1526,12 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.nrep = res_replicas(nrb);
     w.res_bytes = align_up((size_t)(max_iter + 1) * w.nrep * w.m_pad * esz, 256) +
                   align_up(sizeof(int) * (size_t)(max_iter + 1), 256) + 256 + kSyncBytes;
+    // tiled engine: row-partial exchange (2 slots x nrb x ncb x TL_R) + group counters
+    w.t_nrb = (n + TL_R - 1) / TL_R;
+    w.t_ncb = (m + TL_C - 1) / TL_C;
+    w.t_xch_off = w.res_bytes;
+    w.res_bytes += align_up(2 * (size_t)w.t_nrb * w.t_ncb * TL_R * esz, 256) +
+                   (size_t)w.t_nrb * 256;
     w.res = take(w.res_bytes);
     w.bytes = off;
     return w;
@@ -1181,6 +1607,78 @@ hipError_t run_resident(const PassCfg& cfg, int grid, const CT* C, int64_t ldc, 
     if (e != hipSuccess) return e;
     if (P_out && P_dtype == OTF_F64) return launch_resident<T, CT, double>(cfg, grid, p, s);
     return launch_resident<T, CT, float>(cfg, grid, p, s);
+}
+
+// Tiled resident solve (float).  Same contract as run_resident.
+template <typename CT, typename TP, int NREP>
+hipError_t launch_tiled_g(int grid, SkTileArgs<float>& p, hipStream_t s) {
+    void* args[] = {&p};
+    const void* k = (const void*)sk_tiled_kernel<CT, TP, NREP>;
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1 || grid > per_cu * device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
+    return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
+}
+
+inline int tiled_nrep(const Workspace& w) {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("OTF_TILED_NREP");
+        env = e ? atoi(e) : 1;
+    }
+    int r = env == 2 || env == 4 ? env : 1;
+    return r <= w.nrep ? r : 1;
+}
+
+template <typename CT>
+hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const float* cost_scale,
+                     const otf_sinkhorn_opts& o, Workspace& w, float* u_out, float* v_out,
+                     void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
+                     double* errlog, hipStream_t s) {
+    SkTileArgs<float> p{};
+    const int nrep = tiled_nrep(w);
+    p.C = C;
+    p.ldc = ldc;
+    p.n = n;
+    p.m = m;
+    p.m_pad = (int)w.m_pad;
+    p.a = (const float*)w.a_pad;
+    p.b = (const float*)w.b_pad;
+    p.cost_scale = cost_scale;
+    p.reg = o.reg;
+    p.max_iter = o.max_iter;
+    p.check_every = o.check_every;
+    p.err_squared = o.err_squared;
+    p.stop_thr = o.stop_thr;
+    p.cs = (float*)w.res;
+    p.nrep = nrep;
+    p.bad_cnt = (int*)((char*)w.res +
+                       align_up((size_t)(o.max_iter + 1) * w.nrep * w.m_pad * sizeof(float), 256));
+    p.bar = (int*)((char*)p.bad_cnt + align_up(sizeof(int) * (size_t)(o.max_iter + 1), 256));
+    int* sw = (int*)((char*)p.bar + 256);
+    p.sync.reg = sw;
+    p.sync.xcnt = sw + 8 * 64;
+    p.sync.top = sw + 16 * 64;
+    p.sync.gen = sw + 17 * 64;
+    p.xch = (float*)((char*)w.res + w.t_xch_off);
+    p.grp = (int*)((char*)p.xch + align_up(2 * (size_t)w.t_nrb * w.t_ncb * TL_R * sizeof(float), 256));
+    p.nrb = (int)w.t_nrb;
+    p.ncb = (int)w.t_ncb;
+    p.info = info;
+    p.errlog = errlog;
+    p.u_out = u_out;
+    p.v_out = v_out;
+    p.P = P_out;
+    p.ldp = ldp;
+    p.timeout_ticks = 500000000ull;
+    hipError_t e = hipMemsetAsync(w.res, 0, w.res_bytes, s);
+    if (e != hipSuccess) return e;
+    const int grid = (int)(w.t_nrb * w.t_ncb);
+    const bool f64p = P_out && P_dtype == OTF_F64;
+    if (nrep == 4) return f64p ? launch_tiled_g<CT, double, 4>(grid, p, s) : launch_tiled_g<CT, float, 4>(grid, p, s);
+    if (nrep == 2) return f64p ? launch_tiled_g<CT, double, 2>(grid, p, s) : launch_tiled_g<CT, float, 2>(grid, p, s);
+    return f64p ? launch_tiled_g<CT, double, 1>(grid, p, s) : launch_tiled_g<CT, float, 1>(grid, p, s);
 }
 
 // Validated shape / workspace of one solve (deterministic in n, m, max_iter).
@@ -1307,8 +1805,26 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
 
     // resident engine: the whole solve in one persistent launch when every row block
     // gets its own CU (POT flavour, no per-pass profiling requested)
-    const bool fits = su.nrb <= device_cu_count() && su.cfg.G <= 4 &&
-                      (o.n_total <= 0 || o.n_total == n);
+    const bool whole = o.n_total <= 0 || o.n_total == n;
+    const bool fits = su.nrb <= device_cu_count() && su.cfg.G <= 4 && whole;
+    // tiled engine: float, every (128 x 512) tile on its own CU
+    const bool tfits = sizeof(T) == 4 && whole && su.w.t_nrb * su.w.t_ncb <= device_cu_count();
+    const bool want_tiled = !LOG && !avg_pass_ms && tfits && o.max_iter >= 1 &&
+                            (o.engine == OTF_ENGINE_TILED || o.engine == OTF_ENGINE_AUTO);
+    if (o.engine == OTF_ENGINE_TILED && (LOG || !tfits)) return OTF_EUNSUPPORTED;
+    if constexpr (sizeof(T) == 4) {
+        if (want_tiled) {
+            Workspace w = su.w;
+            const hipError_t e = run_tiled<CT>(C, ldc, (int)n, (int)m, (const float*)cost_scale, o, w,
+                                               (float*)u_out, (float*)v_out, P_out, ldp, P_dtype,
+                                               info, errlog, s);
+            if (e == hipSuccess) return OTF_OK;
+            (void)hipGetLastError();
+            if (o.engine == OTF_ENGINE_TILED) return check_hip(e);
+        }
+    }
+    // AUTO reaches here only when the tiled engine did not take the solve (shape, dtype
+    // or co-residency refused), so the row-block resident engine is the next choice
     const bool want_res = !LOG && !avg_pass_ms && fits && o.max_iter >= 1 &&
                           (o.engine == OTF_ENGINE_RESIDENT || o.engine == OTF_ENGINE_AUTO);
     if (o.engine == OTF_ENGINE_RESIDENT && (LOG || !fits)) return OTF_EUNSUPPORTED;

@@ -28,8 +28,9 @@ OTF_FLAVOR_POT, OTF_FLAVOR_OTT = 0, 1
 SK_RUNNING, SK_CONVERGED, SK_MAX_ITER, SK_NUMERICAL_BREAK, SK_TIMEOUT = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "running", 1: "converged", 2: "max_iter", 3: "numerical_break",
                 4: "timeout"}
-ENGINE_AUTO, ENGINE_STREAM, ENGINE_RESIDENT = 0, 1, 2
-ENGINES = {"auto": ENGINE_AUTO, "stream": ENGINE_STREAM, "resident": ENGINE_RESIDENT}
+ENGINE_AUTO, ENGINE_STREAM, ENGINE_RESIDENT, ENGINE_TILED = 0, 1, 2, 3
+ENGINES = {"auto": ENGINE_AUTO, "stream": ENGINE_STREAM, "resident": ENGINE_RESIDENT,
+           "tiled": ENGINE_TILED}
 ENGINE_NAMES = {v: k for k, v in ENGINES.items()}
 
 

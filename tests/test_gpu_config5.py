@@ -67,7 +67,7 @@ def test_fp16_cost_storage_is_scaled_and_rounded_once(ops, orc, dev, in_dtype):
     assert (np.abs(Cs - ref) <= tol).all()
 
 
-@pytest.mark.parametrize("engine", ["stream", "resident"])
+@pytest.mark.parametrize("engine", ["stream", "resident", "tiled"])
 @pytest.mark.parametrize("n,m", [(2048, 2048), (300, 1001)])
 def test_sinkhorn_on_fp16_cost_vs_oracle(ops, orc, dev, engine, n, m):
     X, _ = _emb16(n, 128, seed=7)

@@ -162,7 +162,7 @@ def test_feature_cost_dense_ts_vs_oracle(ops, orc, dev):
     assert nrel(M2, orc.feature_cost(X, Y2, Tsq, weights="fot")) < 1e-13
 
 
-@pytest.mark.parametrize("engine", ["stream", "resident"])
+@pytest.mark.parametrize("engine", ["stream", "resident", "tiled"])
 @pytest.mark.parametrize("n,m,dt", [(300, 200, torch.float32), (64, 4099, torch.float32),
                                     (1000, 8191, torch.float32), (513, 2049, torch.float64),
                                     (3, 7, torch.float64), (1, 1, torch.float32),
@@ -178,9 +178,9 @@ def test_sinkhorn_ragged_shapes_vs_oracle(ops, orc, dev, n, m, dt, engine):
     try:
         res = ops.sinkhorn(_t(a, dev, dt), _t(b, dev, dt), _t(C, dev, dt), 0.1, max_iter=60,
                            stop_thr=0.0, engine=engine)
-    except Exception as e:  # resident needs one row block per CU
-        if engine == "resident" and "unsupported" in str(e):
-            pytest.skip("problem does not fit the resident engine")
+    except Exception as e:  # resident / tiled need one row block / tile per CU; tiled is fp32
+        if engine in ("resident", "tiled") and "unsupported" in str(e):
+            pytest.skip(f"problem does not fit the {engine} engine")
         raise
     tol = 1e-4 if dt == torch.float32 else 1e-10
     assert nrel(res.plan.cpu().numpy(), P_r) < tol
@@ -191,7 +191,38 @@ def test_sinkhorn_ragged_shapes_vs_oracle(ops, orc, dev, n, m, dt, engine):
                                u_r * v_r.mean(), rtol=tol * 10)
 
 
-@pytest.mark.parametrize("engine", ["stream", "resident"])
+@pytest.mark.parametrize("engine", ["stream", "resident", "tiled"])
+def test_float32_stop_and_break_all_engines(ops, orc, dev, engine):
+    """float32 inputs: the convergence stop lands on the oracle's check (every 10) and a
+    zero column of K (K^T u = 0 at iteration 0) reverts to (u0, v0) in every engine."""
+    rng = np.random.default_rng(22)
+    n, m = 700, 300
+    C = rng.random((n, m)).astype(np.float32)
+    a = np.full(n, 1.0 / n)
+    b = np.full(m, 1.0 / m)
+    P_r, *_, info_r = orc.sinkhorn_knopp(a, b, C.astype(np.float64), 0.05, 2000, 1e-5)
+    assert info_r["niter"] < 1999
+    res = ops.sinkhorn(_t(a, dev, torch.float32), _t(b, dev, torch.float32), _t(C, dev), 0.05,
+                       max_iter=2000, stop_thr=1e-5, engine=engine)
+    info = res.info()
+    assert info["engine_name"] == engine
+    assert info["status_name"] == "converged"
+    assert abs(info["niter"] - info_r["niter"]) <= 10   # float32 error vs float64 at a check
+    assert nrel(res.plan.cpu().numpy(), P_r) < 1e-3
+    # a column of cost 1e3 at reg 1: exp(-1000) = 0 in float32 and float64
+    C2 = rng.random((n, m)).astype(np.float32)
+    C2[:, 17] = 1e3
+    P2, *_, info2 = orc.sinkhorn_knopp(a, b, C2.astype(np.float64), 1.0, 100, 0.0)
+    assert info2["break_iter"] == 0
+    res = ops.sinkhorn(_t(a, dev, torch.float32), _t(b, dev, torch.float32), _t(C2, dev), 1.0,
+                       max_iter=100, stop_thr=0.0, engine=engine)
+    info = res.info()
+    assert info["status_name"] == "numerical_break" and info["break_iter"] == 0
+    assert info["niter"] == info2["niter"]
+    assert nrel(res.plan.cpu().numpy(), P2) < 1e-5
+
+
+@pytest.mark.parametrize("engine", ["stream", "resident"])   # float64 (tiled: fp32 test above)
 def test_engines_agree_on_early_stop_and_break(ops, orc, golden, dev, engine):
     """Convergence stop and the numerical break behave identically in both engines."""
     rng = np.random.default_rng(21)
