@@ -1300,26 +1300,26 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
         }
         wave_sum_multi<T, R>(rp, lane);
         const int slot = it & 1;
-        T* xg = p.xch + ((size_t)slot * p.nrb + rb) * (size_t)p.ncb * TL_R;
-        if (lane < R) store_wt(xg + (size_t)cb * TL_R + w * R + rowl, rp[0]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            int ok = 1;
-            __hip_atomic_fetch_add(gcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int target = p.ncb * (it + 1);
-            while (load_agent(gcnt) < target) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = 0; break; }
-            }
-            s_flag = ok;
-        }
-        __syncthreads();
-        if (!s_flag) { status = OTF_SK_TIMEOUT; done = true; break; }
-        OTF_STAMP(it, 2);
-        // gather the ncb partials of this wave's rows (fixed order), u(it)
         T tot = 0;
         {
+            T* xg = p.xch + ((size_t)slot * p.nrb + rb) * (size_t)p.ncb * TL_R;
+            if (lane < R) store_wt(xg + (size_t)cb * TL_R + w * R + rowl, rp[0]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                int ok = 1;
+                __hip_atomic_fetch_add(gcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int target = p.ncb * (it + 1);
+                while (load_agent(gcnt) < target) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = 0; break; }
+                }
+                s_flag = ok;
+            }
+            __syncthreads();
+            if (!s_flag) { status = OTF_SK_TIMEOUT; done = true; break; }
+            OTF_STAMP(it, 2);
+            // gather the ncb partials of this wave's rows (fixed order)
             const int rr = lane & (R - 1);
             for (int mb = lane >> 4; mb < p.ncb; mb += 4)
                 tot += __hip_atomic_load(xg + (size_t)mb * TL_R + w * R + rr, __ATOMIC_RELAXED,
@@ -1352,6 +1352,11 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
         }
         OTF_STAMP(it, 3);
         flush(un, p.cs + (size_t)(it + 1) * it_stride);
+#ifdef OTF_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        OTF_STAMP(it, 4);
+#endif
         if (!xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 1, deadline, &s_flag)) {
             status = OTF_SK_TIMEOUT;
             done = true;
@@ -1495,6 +1500,11 @@ struct Workspace {
     size_t t_xch_off;      // tiled engine: exchange region offset inside res
 };
 
+// tiled engine row exchange: two slots (iteration parity) of nrb x ncb x TL_R partials
+size_t tiled_xch_bytes(int64_t nrb, int64_t ncb) {
+    return align_up(2 * (size_t)nrb * ncb * TL_R * sizeof(float), 256);
+}
+
 // hierarchical barrier words: reg[8], xcnt[8], top, gen[8], each on a 256-B line
 constexpr size_t kSyncBytes = 25 * 64 * sizeof(int);
 
@@ -1530,8 +1540,7 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.t_nrb = (n + TL_R - 1) / TL_R;
     w.t_ncb = (m + TL_C - 1) / TL_C;
     w.t_xch_off = w.res_bytes;
-    w.res_bytes += align_up(2 * (size_t)w.t_nrb * w.t_ncb * TL_R * esz, 256) +
-                   (size_t)w.t_nrb * 256;
+    w.res_bytes += tiled_xch_bytes(w.t_nrb, w.t_ncb) + (size_t)w.t_nrb * 256;
     w.res = take(w.res_bytes);
     w.bytes = off;
     return w;
@@ -1662,7 +1671,7 @@ hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const float* cost_s
     p.sync.top = sw + 16 * 64;
     p.sync.gen = sw + 17 * 64;
     p.xch = (float*)((char*)w.res + w.t_xch_off);
-    p.grp = (int*)((char*)p.xch + align_up(2 * (size_t)w.t_nrb * w.t_ncb * TL_R * sizeof(float), 256));
+    p.grp = (int*)((char*)p.xch + tiled_xch_bytes(w.t_nrb, w.t_ncb));
     p.nrb = (int)w.t_nrb;
     p.ncb = (int)w.t_ncb;
     p.info = info;

@@ -16,6 +16,7 @@
 
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 4096;
+    const bool tiled = argc > 2 && argv[2][0] == 't';  // second argument "tiled": OTF_ENGINE_TILED
     const int iters = 100;
     float *C, *a, *u, *v, *P;
     otf_sinkhorn_info* info;
@@ -36,7 +37,7 @@ int main(int argc, char** argv) {
     (void)hipMalloc(&ws, wsb);
     otf_sinkhorn_opts o{};
     o.reg = 0.1; o.stop_thr = 0; o.max_iter = iters; o.check_every = 10;
-    o.flavor = OTF_FLAVOR_POT; o.engine = OTF_ENGINE_RESIDENT;
+    o.flavor = OTF_FLAVOR_POT; o.engine = tiled ? OTF_ENGINE_TILED : OTF_ENGINE_RESIDENT;
     for (int rep = 0; rep < 3; ++rep) {
         hipEvent_t e0, e1;
         (void)hipEventCreate(&e0);
@@ -79,7 +80,8 @@ int main(int argc, char** argv) {
     }
     std::vector<unsigned long long> st(256 * 16 * 8);
     (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(otf::g_stamps), st.size() * 8);
-    const int nwg = (N + 15) / 16 < 256 ? (N + 15) / 16 : 256;
+    int nwg = (N + 15) / 16 < 256 ? (N + 15) / 16 : 256;
+    if (tiled) nwg = ((N + 127) / 128) * ((N + 511) / 512) < 256 ? ((N + 127) / 128) * ((N + 511) / 512) : 256;
     double span[6] = {0};
     int cnt = 0;
     double arrive_spread = 0;
@@ -96,8 +98,11 @@ int main(int argc, char** argv) {
         }
         arrive_spread += (double)(amax - amin);
     }
-    const char* names[6] = {"sums+v+decide", "row dots+reduce", "u+partials+atomics issue",
-                            "atomics performed", "grid barrier", "loop back"};
+    const char* rnames[6] = {"sums+v+decide", "row dots+reduce", "u+partials+atomics issue",
+                             "atomics performed", "grid barrier", "loop back"};
+    const char* tnames[6] = {"sums+v+decide", "row partials+group wait", "gather+u",
+                             "col partials+atomics done", "grid barrier", "loop back"};
+    const char* const* names = tiled ? tnames : rnames;
     for (int ph = 0; ph < 6; ++ph) printf("%-26s %8.2f us\n", names[ph], span[ph] / cnt / 100.0);
     printf("barrier arrival spread     %8.2f us\n", arrive_spread / 13 / 100.0);
     return 0;
