@@ -219,7 +219,7 @@ def main():
 def gw_leg(dev, with_cpu, labels=2, per_label=64, d=512, eps=5e-3):
     """Per-epoch sample coupling: `labels` label groups of
     `per_label` paired samples (the reference's --max-jax-samples 64), d = 512.
-    Device: both GW solvers, all labels in one launch (float64 costs built on the
+    Device: the three GW solvers, all labels in one launch (float64 costs built on the
     device first, inside the timing); latency-bound, so reported as ms per epoch
     call.  CPU: the oracle's float64 C restatements, one core, same problems."""
     from otfuse import gw
@@ -231,20 +231,27 @@ def gw_leg(dev, with_cpu, labels=2, per_label=64, d=512, eps=5e-3):
         Ys.append(torch.from_numpy(Y).to(dev))
 
     def run(solver):
-        metric = "euclidean" if solver == gw.GW_CG else "sqeuclidean"
-        C1s = [gw.pairwise_cost_f64(x, None, metric=metric, zero_diag=solver == gw.GW_CG,
+        # POT callers use cdist / max (Euclidean), OTT PointCloud the squared distance
+        euc = solver in (gw.GW_CG, gw.GW_PGD)
+        metric = "euclidean" if euc else "sqeuclidean"
+        C1s = [gw.pairwise_cost_f64(x, None, metric=metric, zero_diag=euc,
                                     scale_max=True)[0] for x in Xs]
-        C2s = [gw.pairwise_cost_f64(y, None, metric=metric, zero_diag=solver == gw.GW_CG,
+        C2s = [gw.pairwise_cost_f64(y, None, metric=metric, zero_diag=euc,
                                     scale_max=True)[0] for y in Ys]
         if solver == gw.GW_CG:
             return gw.solve_batched(C1s, C2s, gw.GW_CG, max_iter=10000, log_len=1), C1s, C2s
+        if solver == gw.GW_PGD:
+            return gw.solve_batched(C1s, C2s, gw.GW_PGD, max_iter=1000, tol_abs=1e-9, eps=eps,
+                                    sk_max_iter=1000, sk_inner=10, sk_threshold=1e-9,
+                                    log_len=1), C1s, C2s
         return gw.solve_batched(C1s, C2s, gw.GW_ENTROPIC, max_iter=2000, eps=eps,
                                 sk_max_iter=2000, log_len=1), C1s, C2s
 
     out = {"labels": labels, "samples_per_label": per_label, "d": d, "eps": eps,
            "unit": "ms per epoch call (all labels)"}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for name, solver in (("pot_cg", gw.GW_CG), ("ott_entropic", gw.GW_ENTROPIC)):
+    for name, solver in (("pot_cg", gw.GW_CG), ("ott_entropic", gw.GW_ENTROPIC),
+                         ("pot_entropic_pgd", gw.GW_PGD)):
         run(solver)
         ts = []
         for _ in range(5):
@@ -264,6 +271,8 @@ def gw_leg(dev, with_cpu, labels=2, per_label=64, d=512, eps=5e-3):
             for a_, b_ in zip(c1, c2):
                 if solver == gw.GW_CG:
                     orc.gw_cg(a_, b_)
+                elif solver == gw.GW_PGD:
+                    orc.gw_pgd(a_, b_, eps)
                 else:
                     orc.gw_entropic(a_, b_, eps)
             cpu_ms = (time.perf_counter() - t0) * 1e3

@@ -270,8 +270,15 @@ int otf_cost_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64_t l
  * OTF_GW_ENTROPIC: OTT-jax 0.6.0 GromovWasserstein(epsilon, linear_solver=
  *   Sinkhorn(...)) as called by get_coupling_egw_ott_fixed,
  *   MRI_PET_OT_OT_per_epoch_attn.py:129-186, and perturbot ott_egwl.py:25-296
- *   (labels_a / labels_b != NULL: coupling restricted to equal labels).        */
-typedef enum { OTF_GW_CG = 0, OTF_GW_ENTROPIC = 1 } otf_gw_solver;
+ *   (labels_a / labels_b != NULL: coupling restricted to equal labels).
+ * OTF_GW_PGD: POT 0.9.6 ot.gromov.entropic_gromov_wasserstein(C1, C2, p, q,
+ *   'square_loss', epsilon, solver='PGD') as called by perturbot/perturbot/match/
+ *   gw.py:31-59 (egw_pgd) and :80-102 (egw_all): sinkhorn_knopp inner solves on the
+ *   gradient 2 (constC - 2 C1 T C2); opts: max_iter (1000), tol_abs = tol (1e-9),
+ *   eps, sk_max_iter = numItermax (1000), sk_threshold = stopThr (1e-9), sk_inner =
+ *   the inner error-check period (10); costlog = log['err'] (every 10th iteration),
+ *   info.cost = log['gw_dist'].                                                   */
+typedef enum { OTF_GW_CG = 0, OTF_GW_ENTROPIC = 1, OTF_GW_PGD = 2 } otf_gw_solver;
 enum {
     OTF_GW_RUNNING = 0,
     OTF_GW_CONVERGED = 1,

@@ -92,6 +92,10 @@ def lib():
                                       ctypes.c_double, ctypes.c_int, _dp, _dp, ctypes.c_int,
                                       _ip, _dp]
         L.oro_gw_entropic.restype = ctypes.c_int
+        L.oro_gw_pgd.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int64, _dp, _dp,
+                                 ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                 ctypes.c_double, _dp, _dp, ctypes.c_int, _ip, _dp]
+        L.oro_gw_pgd.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -233,6 +237,25 @@ def gw_entropic(C1, C2, eps, a=None, b=None, labels_a=None, labels_b=None, max_i
                "costs": clog[: min(it, log_len)].tolist(), "reg_gw_cost": cost.value}
 
 
+def gw_pgd(C1, C2, eps, a=None, b=None, max_iter=1000, tol=1e-9, sk_max=1000, sk_thr=1e-9,
+           log_len=128):
+    """POT entropic GW, solver='PGD' (perturbot gw.py:31-59).  Returns ``(T, info)``."""
+    C1, C2 = _d(C1), _d(C2)
+    n, m = C1.shape[0], C2.shape[0]
+    T = np.empty((n, m))
+    elog = np.zeros(log_len)
+    info = np.zeros(4, np.int64)
+    cost = ctypes.c_double()
+    a = None if a is None else _d(a)
+    b = None if b is None else _d(b)
+    lib().oro_gw_pgd(_ptr(C1), _ptr(C2), n, m, _ptr(a) if a is not None else None,
+                     _ptr(b) if b is not None else None, float(eps), int(max_iter), float(tol),
+                     int(sk_max), float(sk_thr), _ptr(T), _ptr(elog), log_len, _ptr(info, _ip),
+                     ctypes.byref(cost))
+    return T, {"n_iter": int(info[0]), "converged": bool(info[1]), "inner_iters": int(info[2]),
+               "err": elog[: min(int(info[3]), log_len)].tolist(), "gw_dist": cost.value}
+
+
 # --------------------------------------------------------------------------- NumPy
 def gw_cg_np(C1, C2, max_iter=10000, tol_rel=1e-9, tol_abs=1e-9):
     """POT 0.9.6 ``gromov_wasserstein(C1, C2, unif, unif, 'square_loss')`` in NumPy, with
@@ -278,6 +301,30 @@ def gw_cg_np(C1, C2, max_iter=10000, tol_rel=1e-9, tol_abs=1e-9):
         if reld < tol_rel or absd < tol_abs or it >= max_iter:
             break
     return G, {"n_iter": it, "loss": losses, "gw_dist": cost}
+
+
+def gw_pgd_np(C1, C2, eps, p=None, q=None, max_iter=1000, tol=1e-9, sk_max=1000, sk_thr=1e-9):
+    """POT 0.9.6 ``entropic_gromov_wasserstein(C1, C2, p, q, 'square_loss', epsilon,
+    solver='PGD')`` in NumPy (symmetric C1, C2; the inner solve is ``sinkhorn_knopp_np``)."""
+    C1, C2 = _d(C1), _d(C2)
+    n, m = C1.shape[0], C2.shape[0]
+    p = np.full(n, 1.0 / n) if p is None else _d(p)
+    q = np.full(m, 1.0 / m) if q is None else _d(q)
+    constC = ((C1 ** 2) @ p)[:, None] + ((C2 ** 2) @ q)[None, :]
+
+    def tens(T):
+        return constC - C1 @ T @ (2.0 * C2).T
+
+    T = np.outer(p, q)
+    cpt, err, errs = 0, 1.0, []
+    while err > tol and cpt < max_iter:
+        Tprev = T
+        T, _, _, _ = sinkhorn_knopp_np(p, q, 2.0 * tens(T), eps, sk_max, sk_thr)
+        if cpt % 10 == 0:
+            err = np.linalg.norm(T - Tprev)
+            errs.append(err)
+        cpt += 1
+    return T, {"n_iter": cpt, "err": errs, "gw_dist": float(np.sum(tens(T) * T))}
 
 
 def pairwise_cost_np(X, Y, metric="sqeuclidean", zero_diag=False):

@@ -310,3 +310,113 @@ ORO_EXPORT int oro_gw_entropic(const double* C1, const double* C2, int64_t n, in
     free(tmp); free(R); free(L); free(f); free(g); free(r); free(c); free(x); free(y);
     return 0;
 }
+
+/* POT 0.9.6 ot.gromov.entropic_gromov_wasserstein(C1, C2, p, q, 'square_loss', epsilon,
+ * solver='PGD') on symmetric C1, C2, as called by perturbot/perturbot/match/gw.py:31-59
+ * (egw_pgd) and :80-102 (egw_all).  T0 = p q^T; per iteration
+ *     tens = gwggrad = 2 tensor_product(constC, C1, 2 C2, T) = 2 (constC - 2 C1 T C2)
+ *     T    = sinkhorn_knopp(p, q, tens, eps, numItermax = sk_max, stopThr = sk_thr)
+ * (ot.bregman.sinkhorn_knopp: K = exp(tens / -eps), Kp = K / p, u = 1/n, v = 1/m,
+ * v = q / K^T u, u = 1 / (Kp v); a zero K^T u or non-finite u / v keeps the previous
+ * pair and stops; every 10th update err = || sum_i u_i K_ij v_j - q ||_2 < stopThr
+ * stops); every 10th outer iteration err = ||T - Tprev||_F; loop while err > tol and
+ * it < max_iter.  info: [n_iter, converged, inner_total, n_err]; errlog = log['err'];
+ * cost_out = log['gw_dist'] = sum(tensor_product(T) * T). */
+ORO_EXPORT int oro_gw_pgd(const double* C1, const double* C2, int64_t n, int64_t m,
+                          const double* a, const double* b, double eps, int max_iter, double tol,
+                          int sk_max, double sk_thr, double* T, double* errlog, int errlog_len,
+                          int64_t* info, double* cost_out) {
+    const int64_t nm = n * m;
+    double* constC = (double*)malloc(sizeof(double) * (size_t)nm);
+    double* tmp = (double*)malloc(sizeof(double) * (size_t)nm);
+    double* tens = (double*)malloc(sizeof(double) * (size_t)nm);
+    double* K = (double*)malloc(sizeof(double) * (size_t)nm);
+    double* Kp = (double*)malloc(sizeof(double) * (size_t)nm);
+    double* u = (double*)malloc(sizeof(double) * (size_t)n);
+    double* v = (double*)malloc(sizeof(double) * (size_t)m);
+    double* up = (double*)malloc(sizeof(double) * (size_t)n);
+    double* vp = (double*)malloc(sizeof(double) * (size_t)m);
+    /* init_matrix (square loss): constC = (C1^2 p) 1^T + 1 (C2^2 q)^T */
+    for (int64_t i = 0; i < n; ++i) {
+        double s = 0.0;
+        for (int64_t k = 0; k < n; ++k) s += C1[i * n + k] * C1[i * n + k] * marg(a, k, n);
+        up[i] = s;
+    }
+    for (int64_t j = 0; j < m; ++j) {
+        double s = 0.0;
+        for (int64_t k = 0; k < m; ++k) s += C2[j * m + k] * C2[j * m + k] * marg(b, k, m);
+        vp[j] = s;
+    }
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t j = 0; j < m; ++j) {
+            constC[i * m + j] = up[i] + vp[j];
+            T[i * m + j] = marg(a, i, n) * marg(b, j, m);
+        }
+    double err = 1.0;
+    int it = 0, nerr = 0, inner_total = 0;
+    while (err > tol && it < max_iter) {
+        tensor_product(constC, C1, C2, T, n, m, tmp, tens);
+        for (int64_t e = 0; e < nm; ++e) K[e] = exp(2.0 * tens[e] / -eps);
+        for (int64_t i = 0; i < n; ++i) {
+            const double ia = 1.0 / marg(a, i, n);
+            for (int64_t j = 0; j < m; ++j) Kp[i * m + j] = ia * K[i * m + j];
+        }
+        for (int64_t i = 0; i < n; ++i) u[i] = 1.0 / (double)n;
+        for (int64_t j = 0; j < m; ++j) v[j] = 1.0 / (double)m;
+        int ii;
+        for (ii = 0; ii < sk_max; ++ii) {
+            memcpy(up, u, sizeof(double) * (size_t)n);
+            memcpy(vp, v, sizeof(double) * (size_t)m);
+            int bad = 0;
+            for (int64_t j = 0; j < m; ++j) {
+                double s = 0.0;
+                for (int64_t i = 0; i < n; ++i) s += K[i * m + j] * u[i];
+                v[j] = marg(b, j, m) / s;
+                if (s == 0.0 || !isfinite(v[j])) bad = 1;
+            }
+            for (int64_t i = 0; i < n; ++i) {
+                double s = 0.0;
+                for (int64_t j = 0; j < m; ++j) s += Kp[i * m + j] * v[j];
+                u[i] = 1.0 / s;
+                if (!isfinite(u[i])) bad = 1;
+            }
+            if (bad) {
+                memcpy(u, up, sizeof(double) * (size_t)n);
+                memcpy(v, vp, sizeof(double) * (size_t)m);
+                break;
+            }
+            if (ii % 10 == 0) {
+                double e2 = 0.0;
+                for (int64_t j = 0; j < m; ++j) {
+                    double s = 0.0;
+                    for (int64_t i = 0; i < n; ++i) s += u[i] * K[i * m + j] * v[j];
+                    const double d = s - marg(b, j, m);
+                    e2 += d * d;
+                }
+                if (sqrt(e2) < sk_thr) break;
+            }
+        }
+        inner_total += ii < sk_max ? ii + 1 : sk_max;
+        double d2 = 0.0;
+        for (int64_t i = 0; i < n; ++i)
+            for (int64_t j = 0; j < m; ++j) {
+                const double tv = u[i] * K[i * m + j] * v[j];
+                const double d = tv - T[i * m + j];
+                d2 += d * d;
+                T[i * m + j] = tv;
+            }
+        if (it % 10 == 0) {
+            err = sqrt(d2);
+            if (errlog && nerr < errlog_len) errlog[nerr] = err;
+            ++nerr;
+        }
+        ++it;
+    }
+    tensor_product(constC, C1, C2, T, n, m, tmp, tens);
+    double cost = 0.0;
+    for (int64_t e = 0; e < nm; ++e) cost += tens[e] * T[e];
+    if (info) { info[0] = it; info[1] = err <= tol; info[2] = inner_total; info[3] = nerr; }
+    if (cost_out) *cost_out = cost;
+    free(constC); free(tmp); free(tens); free(K); free(Kp); free(u); free(v); free(up); free(vp);
+    return 0;
+}

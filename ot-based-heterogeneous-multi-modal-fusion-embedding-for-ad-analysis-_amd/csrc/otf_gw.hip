@@ -29,6 +29,14 @@
 //    max(3, min_iter) iterations.  Optional labels restrict the coupling to
 //    same-label pairs (L = +inf elsewhere): the labelled variant of ott_egwl.py:25-126.
 //
+//  OTF_GW_PGD — POT 0.9.6 ot.gromov.entropic_gromov_wasserstein(C1, C2, p, q,
+//    'square_loss', epsilon, solver='PGD') as called by perturbot/perturbot/match/
+//    gw.py:31-59 (egw_pgd) and :80-102 (egw_all): T0 = p q^T, constC from (p, q);
+//    per iteration T = sinkhorn_knopp(p, q, 2 (constC - 2 C1 T C2), epsilon) with
+//    POT's defaults (1000 updates, stopThr 1e-9); every 10th iteration
+//    err = ||T - Tprev||_F; stop when err <= tol or at max_iter; gw_dist =
+//    <constC - 2 C1 T C2, T>.
+//
 // Everything is float64 like the reference.  Matrices live in a caller workspace
 // (L2-resident at the reference's sizes, <= 1024 per side), vectors in LDS.
 #include <float.h>
@@ -94,6 +102,7 @@ template <class Cfg> struct GwShared {
     double ps[Cfg::NT];
     double red[32];
     int flag;
+    int kflag[2];  // PGD inner Sinkhorn: numerical-error flags by update parity
     GwMats<Cfg::SMALL ? GW_SMALLN : 0> mat;
 };
 
@@ -342,6 +351,95 @@ __device__ int blk_sinkhorn_lse(const double* Lm, int64_t ldl, int n, int m, con
         if (blk_timed_out(deadline, sh)) { timeout = true; break; }
     }
     return it;
+}
+
+// POT sinkhorn_knopp (ot.bregman, POT 0.9.6), the inner solver of POT's entropic GW
+// (solver='PGD'), on K = exp(M / -eps) (n x m, row stride ldk, LDS- or L2-resident):
+//   u = 1/n, v = 1/m;  per update  v = b / K^T u,  u = 1 / (Kp v),  Kp = K / a (rows);
+//   a zero in K^T u or a non-finite u / v keeps the previous (u, v) and stops; every
+//   `every` updates err = || sum_i u_i K_ij v_j - b ||_2 < thr stops.
+// (u, v) alternate between two LDS slots: slot 0 = (f, g), slot 1 = (mg.r, mg.c).
+// Returns the slot holding the result; iters = update passes run (POT's loop count).
+template <class Cfg>
+__device__ int blk_sinkhorn_knopp(const double* K, int64_t ldk, int n, int m, const double* a,
+                                  const double* b, double thr, int maxit, int every,
+                                  GwShared<Cfg>& sh, bool& conv, int& iters) {
+    const int t = threadIdx.x;
+    for (int i = t; i < n; i += Cfg::NT) sh.f[i] = 1.0 / (double)n;
+    for (int j = t; j < m; j += Cfg::NT) sh.g[j] = 1.0 / (double)m;
+    if (t == 0) { sh.kflag[0] = 0; sh.kflag[1] = 0; }
+    __syncthreads();
+    const ColMap<Cfg> cc(m), rc(n);
+    int cur = 0;
+    conv = false;
+    iters = maxit;
+    for (int ii = 0; ii < maxit; ++ii) {
+        const double* u = cur ? sh.mg.r : sh.f;
+        double* un = cur ? sh.f : sh.mg.r;
+        double* vn = cur ? sh.g : sh.mg.c;
+        int* flag = &sh.kflag[ii & 1];
+        // v = b / K^T u: threads across columns, segments across rows
+        for (int j0 = 0; j0 < m; j0 += cc.CW) {
+            const int j = j0 + cc.jj;
+            double s = 0;
+            if (j < m)
+                for (int i = cc.seg; i < n; i += cc.S) s += K[(int64_t)i * ldk + j] * u[i];
+            sh.ps[t] = s;
+            __syncthreads();
+            // the other parity's flag: every reader of it (previous update) is past this barrier
+            if (t == 0) sh.kflag[(ii + 1) & 1] = 0;
+            if (cc.seg == 0 && j < m) {
+                for (int q = 1; q < cc.S; ++q) s += sh.ps[t + q * cc.CW];
+                const double vv = marg(b, j, m) / s;
+                vn[j] = vv;
+                if (s == 0.0 || !finite_val(vv)) *flag = 1;
+            }
+            __syncthreads();
+        }
+        // u = 1 / (Kp v): threads across rows, segments across columns
+        for (int i0 = 0; i0 < n; i0 += rc.CW) {
+            const int i = i0 + rc.jj;
+            double s = 0;
+            if (i < n) {
+                const double ia = 1.0 / marg(a, i, n);
+                const double* kr = K + (int64_t)i * ldk;
+                for (int j = rc.seg; j < m; j += rc.S) s += (ia * kr[j]) * vn[j];
+            }
+            sh.ps[t] = s;
+            __syncthreads();
+            if (rc.seg == 0 && i < n) {
+                for (int q = 1; q < rc.S; ++q) s += sh.ps[t + q * rc.CW];
+                const double uu = 1.0 / s;
+                un[i] = uu;
+                if (!finite_val(uu)) *flag = 1;
+            }
+            __syncthreads();
+        }
+        if (*flag) { iters = ii + 1; return cur; }  // numerical error: keep the previous pair
+        cur ^= 1;
+        if (ii % every == 0) {
+            const double* uc = cur ? sh.mg.r : sh.f;
+            const double* vc = cur ? sh.mg.c : sh.g;
+            double e2 = 0;
+            for (int j0 = 0; j0 < m; j0 += cc.CW) {
+                const int j = j0 + cc.jj;
+                double s = 0;
+                if (j < m)
+                    for (int i = cc.seg; i < n; i += cc.S) s += uc[i] * K[(int64_t)i * ldk + j] * vc[j];
+                sh.ps[t] = s;
+                __syncthreads();
+                if (cc.seg == 0 && j < m) {
+                    for (int q = 1; q < cc.S; ++q) s += sh.ps[t + q * cc.CW];
+                    const double d = s - marg(b, j, m);
+                    e2 += d * d;
+                }
+                __syncthreads();
+            }
+            e2 = blk_sum(e2, sh.red);
+            if (sqrt(e2) < thr) { conv = true; iters = ii + 1; return cur; }
+        }
+    }
+    return cur;
 }
 
 // Minimum-cost assignment of the n x n matrix A (row stride lda), ONE wavefront:
@@ -643,6 +741,79 @@ GW_TEND(0); }
             if (it >= o.max_iter) break;
             if (blk_timed_out(deadline, sh)) { status = OTF_GW_TIMEOUT; break; }
         }
+    } else if (o.solver == OTF_GW_PGD) {
+        // POT entropic GW, solver='PGD'.  T0 = p q^T; constC from (p, q), fixed.
+        const double* pa = P.p;
+        const double* pb = P.q;
+        for (int64_t e = t; e < nm; e += Cfg::NT) {
+            const int i = (int)(e / m), j = (int)(e % m);
+            G[i * ldt + j] = marg(pa, i, n) * marg(pb, j, m);
+        }
+        for (int i = t; i < n; i += Cfg::NT) sh.mg.r[i] = marg(pa, i, n);
+        for (int j = t; j < m; j += Cfg::NT) sh.mg.c[j] = marg(pb, j, m);
+        __syncthreads();
+        blk_sq_matvec<Cfg>(sh.x, C1, ldc1, n, sh.mg.r);
+        blk_sq_matvec<Cfg>(sh.y, C2, ldc2, m, sh.mg.c);
+        __syncthreads();
+        double err = 1.0;
+        int nerr = 0;
+        const double neps = -o.eps;
+        while (err > o.tol_abs && it < o.max_iter) {
+            { GW_TBEG();
+            blk_gemm<Cfg, false>(D, 1, n, C1, 1, ldc1, G, ldt, 1, n, m, n, nullptr, 1.0);
+            __syncthreads();
+            blk_gemm<Cfg, false>(R, m, 1, D, 1, n, C2, ldc2, 1, n, m, m, nullptr, 1.0);
+            __syncthreads();
+            GW_TEND(0); }
+            // K = exp(gwggrad / -eps), gwggrad = 2 (constC - 2 C1 T C2)
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
+                const int i = (int)(e / m), j = (int)(e % m);
+                const double tens = 2.0 * (sh.x[i] + sh.y[j] - 2.0 * R[e]);
+                Lm[i * ldl + j] = exp(tens / neps);
+            }
+            __syncthreads();
+            int sk_it = 0;
+#ifdef OTF_GW_STAMPS
+            unsigned long long gw_t0_ = __builtin_amdgcn_s_memrealtime();
+#endif
+            const int slot = blk_sinkhorn_knopp<Cfg>(Lm, ldl, n, m, pa, pb, o.sk_threshold,
+                                                     o.sk_max_iter, o.sk_inner, sh, inner_conv, sk_it);
+            GW_TEND(2);
+            inner_total += sk_it;
+            // T = diag(u) K diag(v) (POT: u[:, None] * K * v[None, :]); ||T - Tprev||_F
+            const double* uf = slot ? sh.mg.r : sh.f;
+            const double* vf = slot ? sh.mg.c : sh.g;
+            double d2 = 0;
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
+                const int i = (int)(e / m), j = (int)(e % m);
+                const double tv = uf[i] * Lm[i * ldl + j] * vf[j];
+                const double d = tv - G[i * ldt + j];
+                d2 += d * d;
+                G[i * ldt + j] = tv;
+            }
+            d2 = blk_sum(d2, sh.red);  // (barrier inside: plan visible)
+            if (it % 10 == 0) {
+                err = sqrt(d2);
+                if (clog && t == 0 && nerr < costlog_len) clog[nerr] = err;
+                ++nerr;
+            }
+            ++it;
+            if (blk_timed_out(deadline, sh)) { status = OTF_GW_TIMEOUT; break; }
+        }
+        converged = err <= o.tol_abs;
+        if (status != OTF_GW_TIMEOUT)
+            status = converged ? OTF_GW_CONVERGED : (err == err ? OTF_GW_MAX_ITER : OTF_GW_NUMERICAL);
+        // log['gw_dist'] = <constC - 2 C1 T C2, T>
+        blk_gemm<Cfg, false>(D, 1, n, C1, 1, ldc1, G, ldt, 1, n, m, n, nullptr, 1.0);
+        __syncthreads();
+        blk_gemm<Cfg, false>(R, m, 1, D, 1, n, C2, ldc2, 1, n, m, m, nullptr, 1.0);
+        __syncthreads();
+        double acc = 0;
+        for (int64_t e = t; e < nm; e += Cfg::NT) {
+            const int i = (int)(e / m), j = (int)(e % m);
+            acc += (sh.x[i] + sh.y[j] - 2.0 * R[e]) * G[i * ldt + j];
+        }
+        cost = blk_sum(acc, sh.red);
     } else {
         // Entropic GW (OTT).  P0 = a b^T; f = g = 0.
         const double* pa = P.p;
@@ -869,9 +1040,10 @@ int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* 
     using namespace otf;
     if (nprob <= 0 || !probs || !opts || !info || !workspace) return OTF_EINVAL;
     const otf_gw_opts o = *opts;
-    if (o.solver != OTF_GW_CG && o.solver != OTF_GW_ENTROPIC) return OTF_EINVAL;
+    if (o.solver != OTF_GW_CG && o.solver != OTF_GW_ENTROPIC && o.solver != OTF_GW_PGD)
+        return OTF_EINVAL;
     if (o.max_iter < 1) return OTF_EINVAL;
-    if (o.solver == OTF_GW_ENTROPIC && (!(o.eps > 0) || o.sk_inner < 1 || o.sk_max_iter < 1))
+    if (o.solver != OTF_GW_CG && (!(o.eps > 0) || o.sk_inner < 1 || o.sk_max_iter < 1))
         return OTF_EINVAL;
     if (costlog && costlog_len < 1) return OTF_EINVAL;
     if (ws_bytes < otf_gw_workspace_size(nprob, probs)) return OTF_EINVAL;
@@ -885,6 +1057,7 @@ int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* 
             // exact EMD as an assignment: uniform marginals on equal sizes
             if (P.n != P.m || P.p || P.q || P.labels_a) return OTF_EUNSUPPORTED;
         }
+        if (o.solver == OTF_GW_PGD && P.labels_a) return OTF_EUNSUPPORTED;
     }
     hipStream_t s = (hipStream_t)stream;
     char* wsp = (char*)workspace;

@@ -8,6 +8,9 @@ problem, all problems of a call in one launch:
   closed-form line search, as called by ``get_coupling_gromov_pot``
   (MRI_PET_OT_nojax.py:52-88).  The exact EMD for the callers' uniform, equal-size
   marginals is an optimal assignment / n, solved on the device.
+* ``entropic_gromov_wasserstein`` — POT 0.9.6 ``ot.gromov.entropic_gromov_wasserstein(
+  C1, C2, p, q, 'square_loss', epsilon, solver='PGD')``: sinkhorn_knopp inner solves on
+  the gradient, as called by perturbot ``match/gw.py`` (egw_pgd, egw_all).
 * ``entropic_gromov_wasserstein_ott`` — OTT-jax 0.6.0 ``GromovWasserstein(epsilon,
   linear_solver=Sinkhorn(max_iterations))``, as called by
   ``get_coupling_egw_ott_fixed`` (MRI_PET_OT_OT_per_epoch_attn.py:129-186) and
@@ -26,7 +29,7 @@ import torch
 
 from . import _lib as L
 
-GW_CG, GW_ENTROPIC = 0, 1
+GW_CG, GW_ENTROPIC, GW_PGD = 0, 1, 2
 GW_STATUS = {0: "running", 1: "converged", 2: "max_iter", 3: "numerical", 4: "timeout"}
 GW_MAXN = 1024
 
@@ -99,7 +102,7 @@ class GwResult:
                  "status": GW_STATUS.get(int(ints[b, 3]), str(int(ints[b, 3]))),
                  "inner_iters": int(ints[b, 4]), "cost": float(cost[b])}
             if logs is not None:
-                k = it + 1 if self.solver == GW_CG else it
+                k = it + 1 if self.solver == GW_CG else ((it + 9) // 10 if self.solver == GW_PGD else it)
                 d["costs"] = logs[b, :min(k, logs.shape[1])].tolist()
             out.append(d)
         return out
@@ -190,6 +193,49 @@ def gromov_wasserstein(C1, C2, p=None, q=None, loss_fun: str = "square_loss", sy
         info = res.infos()[0]
         return G, {"loss": info["costs"], "gw_dist": info["cost"], "n_iter": info["n_iter"]}
     return G
+
+
+def entropic_gromov_wasserstein(C1, C2, p=None, q=None, loss_fun: str = "square_loss",
+                                epsilon: float = 0.1, symmetric=None, G0=None,
+                                max_iter: int = 1000, tol: float = 1e-9, solver: str = "PGD",
+                                warmstart: bool = False, verbose: bool = False, log: bool = False,
+                                **kwargs):
+    """``ot.gromov.entropic_gromov_wasserstein`` (POT 0.9.6) on device tensors, as called
+    by perturbot/perturbot/match/gw.py:47-57 and :90-99.
+
+    Supported: square loss, symmetric C1 / C2, solver='PGD', G0 = p q^T, no warm start;
+    p / q may be any histograms (None: uniform).  Keywords for the inner
+    ``ot.sinkhorn`` (numItermax, stopThr) are honoured, as POT forwards **kwargs.
+    Returns T (and log with 'err' every 10th iteration and 'gw_dist').
+    """
+    if loss_fun != "square_loss":
+        raise NotImplementedError(f"loss_fun={loss_fun!r}: only 'square_loss'")
+    if solver != "PGD":
+        raise NotImplementedError(f"solver={solver!r}: only 'PGD'")
+    if G0 is not None or warmstart:
+        raise NotImplementedError("G0 / warmstart are not supported")
+    sk_max = int(kwargs.pop("numItermax", 1000))
+    sk_thr = float(kwargs.pop("stopThr", 1e-9))
+    kwargs.pop("method", None)
+    if kwargs:
+        raise TypeError(f"unsupported keywords: {sorted(kwargs)}")
+    if symmetric is None:
+        symmetric = _symmetric(C1) and _symmetric(C2)
+    if not symmetric:
+        raise NotImplementedError("asymmetric C1 / C2 are not supported")
+    dev = C1.device
+    pq = [None if w is None else torch.as_tensor(w, dtype=torch.float64, device=dev) for w in (p, q)]
+    res = solve_batched([C1], [C2], GW_PGD, ps=[pq[0]], qs=[pq[1]], max_iter=int(max_iter),
+                        tol_abs=float(tol), eps=float(epsilon), sk_max_iter=sk_max, sk_inner=10,
+                        sk_threshold=sk_thr, log_len=max(1, (int(max_iter) + 9) // 10))
+    T = res.plans[0]
+    if log:
+        info = res.infos()[0]
+        if info["status"] == "timeout":
+            raise RuntimeError("entropic GW (PGD): device time limit reached")
+        return T, {"err": info["costs"], "gw_dist": info["cost"], "n_iter": info["n_iter"],
+                   "inner_iters": info["inner_iters"]}
+    return T
 
 
 def entropic_gromov_wasserstein_ott(C1, C2, epsilon: float, a=None, b=None, labels_a=None,

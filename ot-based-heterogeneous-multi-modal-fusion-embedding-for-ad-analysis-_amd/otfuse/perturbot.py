@@ -6,6 +6,10 @@ Mirrors (names, arguments, return conventions):
   (called per batch at MRI_PET_OT.py:677-681 and per epoch at
   MRI_PET_OT_OT_per_epoch_attn.py:959, baseline_models_fusion.py:167);
 * ``get_coupling_eot_ott`` / ``get_coupling_leot_ott`` -> perturbot/perturbot/match/ott_egwl.py:299-454;
+* ``gw_cg`` / ``egw_pgd`` / ``gw_all`` / ``egw_all`` and their ``get_coupling_gw_cg`` /
+  ``get_coupling_egw`` / ``get_coupling_gw_all`` / ``get_coupling_egw_all`` wrappers ->
+  perturbot/perturbot/match/gw.py:7-137 (POT GW: exact CG and entropic PGD; the costs
+  are cdist / max, every label problem of a call in one device launch);
 * ``mdict_to_matrix`` -> semantics of baseline_models_fusion.py:233-239 (the module
   ``perturbot.utils`` it stands in for is missing from the reference tree).
 
@@ -264,3 +268,103 @@ def get_coupling_egw_labels_ott(data, eps: float = 5e-3):
     T = plans[0]
     T_dict = {l: T[la == l, :][:, lb == l] for l in uniq}
     return T_dict, logs[0]
+
+
+# ---------------------------------------------------------------- POT GW (match/gw.py)
+def _cdist_max(x, dev):
+    """scipy ``cdist(x, x)`` (Euclidean) ``/ max`` in float64 on the device."""
+    from . import gw
+    t = torch.as_tensor(np.asarray(x), device=dev).float()
+    C, _ = gw.pairwise_cost_f64(t, None, metric="euclidean", zero_diag=True, scale_max=True)
+    return C
+
+
+def _gw_labels(X_dict, Y_dict, solver, eps=None, max_iter=None):
+    from . import gw
+    dev = _device()
+    labels = list(X_dict.keys())
+    log = {"cost_time": {}, "time": {}}
+    t0 = time.time()
+    C1s = [_cdist_max(X_dict[l], dev) for l in labels]
+    C2s = [_cdist_max(Y_dict[l], dev) for l in labels]
+    torch.cuda.current_stream(dev).synchronize()
+    ct = (time.time() - t0) / max(len(labels), 1)
+    t0 = time.time()
+    if solver == gw.GW_CG:
+        res = gw.solve_batched(C1s, C2s, gw.GW_CG, max_iter=int(max_iter or 1e4), log_len=4096)
+    else:
+        res = gw.solve_batched(C1s, C2s, gw.GW_PGD, max_iter=int(max_iter or 1000), tol_abs=1e-9,
+                               eps=float(eps), sk_max_iter=1000, sk_inner=10, sk_threshold=1e-9,
+                               log_len=1024)
+    Ts = [T.cpu().numpy() for T in res.plans]
+    infos = res.infos()
+    el = (time.time() - t0) / max(len(labels), 1)
+    out = {}
+    for l, T, info in zip(labels, Ts, infos):
+        if info["status"] == "timeout":
+            raise RuntimeError("GW: device time limit reached")
+        out[l] = T
+        log["cost_time"][l] = ct
+        log["time"][l] = el
+        if solver == gw.GW_CG:
+            log[l] = {"loss": info["costs"], "gw_dist": info["cost"]}
+        else:
+            log[l] = {"err": info["costs"], "gw_dist": info["cost"]}
+    return out, log
+
+
+def gw_cg(X_dict, Y_dict):
+    """Per-label POT CG-GW on cdist / max costs (perturbot match/gw.py:7-28).  The exact
+    EMD is the device assignment solver: equal-size label groups (uniform marginals)."""
+    from . import gw
+    return _gw_labels(X_dict, Y_dict, gw.GW_CG)
+
+
+def egw_pgd(X_dict, Y_dict, epsilon=5e-3):
+    """Per-label POT entropic GW, solver='PGD' (perturbot match/gw.py:31-59)."""
+    from . import gw
+    return _gw_labels(X_dict, Y_dict, gw.GW_PGD, eps=epsilon)
+
+
+def _all(Xtot, Ytot, solver, eps=None, max_iter=None):
+    Ts, log = _gw_labels({0: Xtot}, {0: Ytot}, solver, eps=eps, max_iter=max_iter)
+    out = dict(log[0])
+    out["time"] = log["time"][0]
+    out["cost_time"] = log["cost_time"][0]
+    return Ts[0], out
+
+
+def gw_all(Xtot, Ytot):
+    """POT CG-GW on all samples (perturbot match/gw.py:62-77, max_iter=1e8)."""
+    from . import gw
+    return _all(Xtot, Ytot, gw.GW_CG, max_iter=10 ** 8)
+
+
+def egw_all(Xtot, Ytot, epsilon=5e-3):
+    """POT entropic GW (PGD) on all samples (perturbot match/gw.py:80-102)."""
+    from . import gw
+    return _all(Xtot, Ytot, gw.GW_PGD, eps=epsilon)
+
+
+def get_coupling_gw_cg(data):
+    return gw_cg(data[0], data[1])
+
+
+def get_coupling_egw(data, eps=5e-3):
+    return egw_pgd(data[0], data[1], epsilon=eps)
+
+
+def get_coupling_gw_all(data):
+    """GW all-to-all, labels ignored (perturbot match/gw.py:119-126)."""
+    X_dict, Y_dict = data
+    Xtot = np.concatenate([X_dict[l] for l in X_dict.keys()], axis=0)
+    Ytot = np.concatenate([Y_dict[l] for l in X_dict.keys()], axis=0)
+    return gw_all(Xtot, Ytot)
+
+
+def get_coupling_egw_all(data, eps=5e-3):
+    """Entropic GW all-to-all, labels ignored (perturbot match/gw.py:129-137)."""
+    X_dict, Y_dict = data
+    Xtot = np.concatenate([X_dict[l] for l in X_dict.keys()], axis=0)
+    Ytot = np.concatenate([Y_dict[l] for l in X_dict.keys()], axis=0)
+    return egw_all(Xtot, Ytot, eps)

@@ -182,3 +182,67 @@ def test_egw_labels_and_all_dropins(dev):
     assert abs(sum(t.sum() for t in T_dict.values()) - 1.0) < 1e-6
     T, log2 = perturbot.get_coupling_egw_all_ott((Xd, Yd), eps=1e-2)
     assert T.shape == (60, 60) and abs(T.sum() - 1.0) < 1e-6
+
+
+@pytest.mark.parametrize("n,m,eps", [(64, 64, 5e-3), (30, 45, 1e-2), (1, 4, 5e-2), (100, 90, 2e-2)])
+def test_gw_pgd_vs_oracle(orc, dev, n, m, eps):
+    """POT entropic GW, solver='PGD' (perturbot match/gw.py:47-57): float64 device solve
+    against the C restatement -- same outer iteration count and err log, plans to 1e-9."""
+    from otfuse import gw
+    (C1, _), = _label_costs(orc, [n], 24, 60)
+    (_, C2), = _label_costs(orc, [m], 24, 70)
+    T, log = gw.entropic_gromov_wasserstein(torch.as_tensor(C1, device=dev),
+                                            torch.as_tensor(C2, device=dev), epsilon=eps,
+                                            log=True)
+    Tr, ref = orc.gw_pgd(C1, C2, eps)
+    assert log["n_iter"] == ref["n_iter"]
+    assert log["inner_iters"] == ref["inner_iters"]
+    np.testing.assert_allclose(log["err"], ref["err"], rtol=1e-6, atol=1e-14)
+    assert nrel(T.cpu().numpy(), Tr) < 1e-9
+    assert log["gw_dist"] == pytest.approx(ref["gw_dist"], rel=1e-9, abs=1e-14)
+
+
+def test_gw_pgd_batched_weighted(orc, dev):
+    """Several problems in one launch, with non-uniform marginals."""
+    from otfuse import gw
+    rng = np.random.default_rng(9)
+    probs = _label_costs(orc, [20, 33, 48], 16, 80)
+    ps = [rng.random(c1.shape[0]) + 0.5 for c1, _ in probs]
+    qs = [rng.random(c2.shape[0]) + 0.5 for _, c2 in probs]
+    ps = [p / p.sum() for p in ps]
+    qs = [q / q.sum() for q in qs]
+    res = gw.solve_batched([torch.as_tensor(c1, device=dev) for c1, _ in probs],
+                           [torch.as_tensor(c2, device=dev) for _, c2 in probs], gw.GW_PGD,
+                           ps=[torch.as_tensor(p, device=dev) for p in ps],
+                           qs=[torch.as_tensor(q, device=dev) for q in qs], max_iter=1000,
+                           tol_abs=1e-9, eps=2e-2, sk_max_iter=1000, sk_inner=10,
+                           sk_threshold=1e-9, log_len=128)
+    for (C1, C2), p, q, T, info in zip(probs, ps, qs, res.plans, res.infos()):
+        Tr, ref = orc.gw_pgd(C1, C2, 2e-2, a=p, b=q)
+        assert info["n_iter"] == ref["n_iter"]
+        assert nrel(T.cpu().numpy(), Tr) < 1e-9
+
+
+def test_perturbot_pot_gw_dropins(orc, dev):
+    """perturbot match/gw.py: get_coupling_gw_cg / get_coupling_egw per label, and the
+    all-to-all forms (labels ignored), against the oracle on cdist / max costs."""
+    from otfuse import perturbot
+    X, Y, lab = _emb(90, 24, 81)
+    Xd = {0: X[lab == 0][:30], 1: X[lab == 1][:30]}
+    Yd = {0: Y[lab == 0][:30], 1: Y[lab == 1][:30]}
+    Ts, log = perturbot.get_coupling_gw_cg((Xd, Yd))
+    Te, loge = perturbot.get_coupling_egw((Xd, Yd), eps=1e-2)
+    assert set(log) >= {"cost_time", "time", 0, 1} and set(loge) >= {"cost_time", "time", 0, 1}
+    for l in (0, 1):
+        C1, _ = orc.pairwise_cost(Xd[l], Xd[l], metric="euclidean", zero_diag=True, scale_max=True)
+        C2, _ = orc.pairwise_cost(Yd[l], Yd[l], metric="euclidean", zero_diag=True, scale_max=True)
+        G, ref = orc.gw_cg(C1, C2)
+        assert np.abs(Ts[l] - G).max() < 1e-12
+        assert log[l]["gw_dist"] == pytest.approx(ref["gw_dist"], rel=1e-9, abs=1e-13)
+        Tr, refe = orc.gw_pgd(C1, C2, 1e-2)
+        assert nrel(Te[l], Tr) < 1e-9
+        assert len(loge[l]["err"]) == len(refe["err"])
+    T, loga = perturbot.get_coupling_gw_all((Xd, Yd))
+    assert T.shape == (60, 60) and abs(T.sum() - 1.0) < 1e-9 and "time" in loga
+    T2, loga2 = perturbot.get_coupling_egw_all((Xd, Yd), eps=1e-2)
+    assert T2.shape == (60, 60) and abs(T2.sum() - 1.0) < 1e-6 and "gw_dist" in loga2

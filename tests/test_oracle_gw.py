@@ -87,3 +87,35 @@ def test_gw_entropic_labels_block_structure(orc):
     assert info["status"] == 1
     assert P[np.not_equal.outer(la, lb)].max() == 0.0
     np.testing.assert_allclose(P[la == 0].sum(), 25 / 40, rtol=1e-6)
+
+
+@pytest.mark.parametrize("n,m,eps", [(20, 20, 5e-2), (30, 45, 1e-2), (40, 40, 5e-3)])
+def test_gw_pgd_c_matches_numpy(orc, n, m, eps):
+    """POT entropic GW (solver='PGD'): the C restatement against the NumPy one, which
+    follows POT's code line by line on top of ``sinkhorn_knopp_np``."""
+    C1, _ = _costs(n, 16, 11)
+    _, C2 = _costs(m, 16, 12)
+    T, info = orc.gw_pgd(C1, C2, eps)
+    T2, info2 = orc.gw_pgd_np(C1, C2, eps)
+    assert info["n_iter"] == info2["n_iter"]
+    assert np.abs(T - T2).max() < 1e-12 * np.abs(T2).max()
+    np.testing.assert_allclose(info["err"], info2["err"], rtol=1e-6, atol=1e-14)
+    assert info["gw_dist"] == pytest.approx(info2["gw_dist"], rel=1e-10)
+    assert info["converged"] and abs(T.sum() - 1.0) < 1e-9
+
+
+def test_gw_pgd_weighted_marginals(orc):
+    """Non-uniform p, q: the plan's marginals are the histograms (inner Sinkhorn)."""
+    rng = np.random.default_rng(3)
+    C1, _ = _costs(25, 8, 21)
+    _, C2 = _costs(35, 8, 22)
+    p = rng.random(25) + 0.5
+    p /= p.sum()
+    q = rng.random(35) + 0.5
+    q /= q.sum()
+    T, info = orc.gw_pgd(C1, C2, 2e-2, a=p, b=q)
+    T2, info2 = orc.gw_pgd_np(C1, C2, 2e-2, p=p, q=q)
+    assert info["n_iter"] == info2["n_iter"]
+    assert np.abs(T - T2).max() < 1e-12 * np.abs(T2).max()
+    np.testing.assert_allclose(T.sum(1), p, rtol=1e-9)
+    np.testing.assert_allclose(T.sum(0), q, atol=1e-8)
