@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--profile-only", action="store_true",
                    help="run warmup + steps only (for rocprofv3 runs); no probes, no JSON")
     p.add_argument("--no-gw", action="store_true", help="skip the per-epoch GW latency leg")
+    p.add_argument("--no-batch-ot", action="store_true",
+                   help="skip the per-training-step OT block leg (config 2)")
     p.add_argument("--engine", default="auto", choices=("auto", "stream", "resident", "tiled"),
                    help="Sinkhorn engine (auto = resident when the cost fits the register file)")
     return p.parse_args()
@@ -207,6 +209,8 @@ def main():
         out["hbm_probe"] = hbm_probe(ops, paired_embeddings, args.hbm_probe_n, d, eps, dev)
     if rank == 0 and not args.no_gw:
         out["gw_per_epoch"] = gw_leg(dev, world == 1 and not args.no_cpu_baseline)
+    if rank == 0 and not args.no_batch_ot:
+        out["batch_ot_per_step"] = batch_ot_leg(dev, world == 1 and not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(X_np, Y_np, N, iters, eps, args.cpu_threads)
         out["vs_cpu"] = value / out["cpu_baseline"]["value"]
@@ -214,6 +218,60 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def batch_ot_leg(dev, with_cpu, B=8, d=512, eps=1e-2):
+    """Config 2: the OT block of forward in every training
+    step (MRI_PET_OT_nojax.py:679-725) -- feature cost with Ts = I/B, POT Sinkhorn in
+    float64 to stopThr 1e-9 (<= 2000 iterations), NaN guard + row normalisation,
+    pet_fused @ T^T, cosine loss -- forward AND backward through the plan apply, all
+    on the device (the reference: D2H copy, POT on the host, H2D copy).  Latency-bound,
+    reported as ms per step.  CPU: the oracle's float64 C restatement of the same
+    forward (feature cost + sinkhorn_knopp + post-processing + apply), host cores."""
+    import numpy as np
+    from otfuse import fusion
+    from otfuse.synthetic import paired_embeddings
+    X, Y, _ = paired_embeddings(B, d, seed=321)
+    mri = torch.from_numpy(X).to(dev).requires_grad_(True)
+    pet = torch.from_numpy(Y).to(dev).requires_grad_(True)
+
+    def step():
+        loss, _, T = fusion.ot_alignment_loss(mri, pet, eps=eps)
+        loss.backward()
+        return loss
+
+    step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(7):
+        e0.record()
+        loss = step()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    _, res = fusion.batch_feature_plan(mri, pet, eps)
+    info = res.info()
+    out = {"B": B, "d": d, "eps": eps, "unit": "ms per training step (OT block forward + backward)",
+           "device_ms": sorted(ts)[3], "sinkhorn_iters": info["niter"],
+           "status": info["status_name"], "engine": info["engine_name"], "loss": float(loss.detach())}
+    if with_cpu:
+        from oracle import oracle as orc
+        t0 = time.perf_counter()
+        for _ in range(3):
+            M = orc.feature_cost(X, Y, np.eye(B) / B)
+            u = np.full(d, 1.0 / d)
+            P, *_ = orc.sinkhorn_knopp(u, u, M, eps, 2000, 1e-9)
+            T = np.nan_to_num(P.astype(np.float32), nan=1e-8)
+            rs = T.sum(1, keepdims=True)
+            T = T / np.where(rs == 0, 1e-8, rs)
+            Z = Y @ T.T
+            cos = (X * Z).sum(1) / (np.linalg.norm(X, axis=1) * np.linalg.norm(Z, axis=1))
+            _ = 1.0 - cos.mean()
+        out["cpu_ms"] = (time.perf_counter() - t0) * 1e3 / 3
+        out["cpu_note"] = ("oracle C/OpenMP restatement of the forward only (no backward), "
+                           f"{os.environ.get('OMP_NUM_THREADS', 'default')} OpenMP threads")
+    return out
 
 
 def gw_leg(dev, with_cpu, labels=2, per_label=64, d=512, eps=5e-3):
