@@ -176,6 +176,21 @@ int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, i
                      const double* ts_diag, int32_t weights_mode, double* M, int64_t ldm,
                      void* workspace, size_t ws_bytes, otf_stream_t stream);
 
+/* COOT cost (perturbot/perturbot/match/utils.py:125-184 init_matrix_np and its uses in
+ * cot_labels.py:155-160, 173, 192):
+ *   M (p x q, ldm) = t1[:, None] + t2[None, :] - 2 A T B^T,
+ *   t1 = (A*A) w1, t2 = (B*B) w2   (squares in float32, as X**2 on float32 data)
+ * A (p x r) and B (q x s) float32 addressed by element strides (a0, a1) / (b0, b1),
+ * so a transposed view is free: the sample cost of label k is (A, B, T) = (X_k, Y_k,
+ * Tv) with w = (v1, v2); the feature cost is (X^T, Y^T, Ts) with w = (w1, w2).
+ * T (r x s, ldt), w1 (r), w2 (s), M: float64 device.
+ * Workspace: otf_coupled_cost_workspace_size(p, q, r) bytes.                    */
+size_t otf_coupled_cost_workspace_size(int64_t p, int64_t q, int64_t r);
+int otf_coupled_cost(const float* A, int64_t a0, int64_t a1, const float* B, int64_t b0,
+                     int64_t b1, int64_t p, int64_t q, int64_t r, int64_t s, const double* T,
+                     int64_t ldt, const double* w1, const double* w2, double* M, int64_t ldm,
+                     void* workspace, size_t ws_bytes, otf_stream_t stream);
+
 /* Entropic OT between histograms a (n) and b (m) with cost C (n x m, ldc), all
  * of `dtype` (float32 or float64), on the device:
  *   K = exp(-C * cscale / reg)      (cscale = 1/(*cost_scale) if cost_scale != NULL)

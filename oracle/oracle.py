@@ -327,6 +327,62 @@ def gw_pgd_np(C1, C2, eps, p=None, q=None, max_iter=1000, tol=1e-9, sk_max=1000,
     return T, {"n_iter": cpt, "err": errs, "gw_dist": float(np.sum(tens(T) * T))}
 
 
+def coupled_cost_np(A, B, T, w1, w2):
+    """perturbot utils.py:125-184 init_matrix_np + ``constC - hC1 T hC2^T``: squares of
+    the float32 data in float32 (X**2), everything else in float64."""
+    A = np.asarray(A, np.float32)
+    B = np.asarray(B, np.float32)
+    t1 = (A * A).astype(np.float64) @ _d(w1)
+    t2 = (B * B).astype(np.float64) @ _d(w2)
+    return t1[:, None] + t2[None, :] - (A.astype(np.float64) @ _d(T)) @ (2.0 * B.astype(np.float64)).T
+
+
+def cotl_sinkhorn_np(X_dict, Y_dict, eps, niter=100):
+    """cot_labels.py:14-225 with algo = algo2 = 'sinkhorn': OTT solves restated by the
+    C log-domain Sinkhorn on max-scaled costs (uniform marginals), the BCD loop and its
+    reference quirks (feature solve at eps, Tv-only delta, Tv renormalisation)."""
+    labels = list(X_dict.keys())
+
+    def hist(D):
+        Xc = np.concatenate([np.asarray(D[k]) for k in labels], axis=0)
+        if (Xc >= 0).all():
+            return np.asarray(Xc.sum(axis=0) / Xc.sum(), dtype=np.float64)
+        return np.ones(Xc.shape[1]) / Xc.shape[1]
+
+    v1, v2 = hist(X_dict), hist(Y_dict)
+    X = {k: np.asarray(X_dict[k], np.float32) for k in labels}
+    Y = {k: np.asarray(Y_dict[k], np.float32) for k in labels}
+    w1 = {k: np.ones(len(X[k])) / len(X[k]) for k in labels}
+    w2 = {k: np.ones(len(Y[k])) / len(Y[k]) for k in labels}
+    d, d2 = X[labels[0]].shape[1], Y[labels[0]].shape[1]
+    Ts = {k: np.ones((len(X[k]), len(Y[k]))) / (len(X[k]) * len(Y[k])) for k in labels}
+    Tv = np.ones((d, d2)) / (d * d2)
+
+    def ott(M):
+        n, m = M.shape
+        P, *_ = sinkhorn_log(np.ones(n) / n, np.ones(m) / m, M, eps, max_iter=2000,
+                             threshold=1e-3, cscale=1.0 / M.max())
+        return P
+
+    cost, costs = np.inf, []
+    for _ in range(niter):
+        Tvold, costold = Tv, cost
+        for k in labels:
+            Ts[k] = ott(coupled_cost_np(X[k], Y[k], Tv, v1, v2))
+        M = 0
+        for k in labels:
+            M = M + coupled_cost_np(X[k].T, Y[k].T, Ts[k], w1[k], w2[k])
+        Tv = ott(M)
+        if not np.abs(Tv.sum() - 1.0) < 1e-8:
+            Tv = Tv / Tv.sum()
+        delta = np.linalg.norm(Tv - Tvold)
+        cost = np.sum(M * Tv)
+        costs.append(cost)
+        if delta < 1e-16 or np.abs(costold - cost) < 1e-7:
+            break
+    return Ts, Tv, cost, {"cost": costs}
+
+
 def pairwise_cost_np(X, Y, metric="sqeuclidean", zero_diag=False):
     """POT ``euclidean_distances`` (via ``ot.dist``) in float64."""
     X, Y = _d(X), _d(Y)

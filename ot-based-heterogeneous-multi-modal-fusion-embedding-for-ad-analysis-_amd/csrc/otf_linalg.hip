@@ -115,6 +115,20 @@ __global__ void weighted_sq_colsum_kernel(const float* X, int64_t ldx, int n, in
     t[k] = s;
 }
 
+// t[o] = sum_k A(o, k)^2 w[k], A(o, k) = A[o * so + k * sk]; the square in float32
+// as the reference's X**2 on float32 data, the weighted sum in float64.
+__global__ void weighted_sq_strided_kernel(const float* A, int64_t so, int64_t sk, int nout, int nk,
+                                           const double* w, double* t) {
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= nout) return;
+    double s = 0.0;
+    for (int k = 0; k < nk; ++k) {
+        const float x = A[(int64_t)o * so + (int64_t)k * sk];
+        s += (double)(x * x) * w[k];
+    }
+    t[o] = s;
+}
+
 // Z[i][l] = diag[i] * Y[i][l]   (Ts diagonal, e.g. np.eye(B)/B)
 __global__ void diag_scale_kernel(const float* Y, int64_t ldy, int n, int d2, const double* diag,
                                   double* Z) {
@@ -220,6 +234,46 @@ int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, i
     dim3 grid((unsigned)((d2 + otf::GT - 1) / otf::GT), (unsigned)((d + otf::GT - 1) / otf::GT));
     otf::gemm_kernel<float, double, double, double><<<grid, 256, 0, s>>>(
         X, 1, ldx, Z, d2, 1, M, ldm, (int)d, (int)d2, (int)n, -2.0, 0.0, t1, t2);
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+size_t otf_coupled_cost_workspace_size(int64_t p, int64_t q, int64_t r) {
+    using otf::align_up;
+    return align_up(8 * (size_t)p, 256) + align_up(8 * (size_t)q, 256) +
+           align_up(8 * (size_t)(r * q), 256);
+}
+
+int otf_coupled_cost(const float* A, int64_t a0, int64_t a1, const float* B, int64_t b0,
+                     int64_t b1, int64_t p, int64_t q, int64_t r, int64_t s_, const double* T,
+                     int64_t ldt, const double* w1, const double* w2, double* M, int64_t ldm,
+                     void* workspace, size_t ws_bytes, otf_stream_t stream) {
+    using otf::align_up;
+    if (!A || !B || !T || !w1 || !w2 || !M || !workspace) return OTF_EINVAL;
+    if (p <= 0 || q <= 0 || r <= 0 || s_ <= 0 || ldt < s_ || ldm < q) return OTF_EINVAL;
+    if (ws_bytes < otf_coupled_cost_workspace_size(p, q, r)) return OTF_EINVAL;
+    if (p > 65535LL * otf::GT || r > 65535LL * otf::GT || q > 2147483647LL || s_ > 2147483647LL)
+        return OTF_EUNSUPPORTED;
+    hipStream_t st = (hipStream_t)stream;
+    char* w = (char*)workspace;
+    double* t1 = (double*)w; w += align_up(8 * (size_t)p, 256);
+    double* t2 = (double*)w; w += align_up(8 * (size_t)q, 256);
+    double* Z = (double*)w;
+    otf::weighted_sq_strided_kernel<<<(int)((p + 255) / 256), 256, 0, st>>>(A, a0, a1, (int)p, (int)r, w1, t1);
+    otf::weighted_sq_strided_kernel<<<(int)((q + 255) / 256), 256, 0, st>>>(B, b0, b1, (int)q, (int)s_, w2, t2);
+    OTF_HIP(hipGetLastError());
+    // Z = T B^T  (r x q)
+    {
+        dim3 grid((unsigned)((q + otf::GT - 1) / otf::GT), (unsigned)((r + otf::GT - 1) / otf::GT));
+        otf::gemm_kernel<double, float, double, double><<<grid, 256, 0, st>>>(
+            T, ldt, 1, B, b1, b0, Z, q, (int)r, (int)q, (int)s_, 1.0, 0.0, nullptr, nullptr);
+    }
+    // M = -2 A Z + t1[:, None] + t2[None, :]
+    {
+        dim3 grid((unsigned)((q + otf::GT - 1) / otf::GT), (unsigned)((p + otf::GT - 1) / otf::GT));
+        otf::gemm_kernel<float, double, double, double><<<grid, 256, 0, st>>>(
+            A, a0, a1, Z, q, 1, M, ldm, (int)p, (int)q, (int)r, -2.0, 0.0, t1, t2);
+    }
     OTF_HIP(hipGetLastError());
     return OTF_OK;
 }

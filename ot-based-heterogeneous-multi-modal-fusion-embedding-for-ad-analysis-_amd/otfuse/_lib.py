@@ -80,6 +80,10 @@ _SIGS = {
     "otf_feature_cost_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i64]),
     "otf_feature_cost": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64,
                                         _vp, _i32, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
+    "otf_coupled_cost_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64]),
+    "otf_coupled_cost": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
+                                        _vp, _i64, _vp, _vp, _vp, _i64, _vp, ctypes.c_size_t,
+                                        _vp]),
     "otf_sinkhorn_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i32, _i32]),
     "otf_sinkhorn": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
                                     ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _i64, _i32, _vp,

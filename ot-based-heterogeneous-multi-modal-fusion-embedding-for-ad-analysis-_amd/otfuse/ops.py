@@ -174,6 +174,40 @@ def feature_cost(X: torch.Tensor, Y: torch.Tensor, Ts: torch.Tensor | None = Non
     return M
 
 
+def coupled_cost(A: torch.Tensor, B: torch.Tensor, T: torch.Tensor, w1: torch.Tensor,
+                 w2: torch.Tensor) -> torch.Tensor:
+    """COOT cost ``M = (A*A) w1 [:, None] + (B*B) w2 [None, :] - 2 A T B^T`` in float64
+    (perturbot utils.py:125-184 ``init_matrix_np`` + ``constC - hC1 T hC2^T``).
+
+    A (p, r), B (q, s) are float32 and may be strided views (``X.T`` costs nothing);
+    T (r, s), w1 (r,), w2 (s,) float64.
+    """
+    for t, nm in ((A, "A"), (B, "B"), (T, "T"), (w1, "w1"), (w2, "w2")):
+        _dev(t, nm)
+    if A.dtype != torch.float32:
+        A = A.float()
+    if B.dtype != torch.float32:
+        B = B.float()
+    p, r = A.shape
+    q, s = B.shape
+    T = _rowmajor(T.to(torch.float64))
+    if tuple(T.shape) != (r, s):
+        raise ValueError(f"T {tuple(T.shape)} must be ({r}, {s})")
+    w1 = w1.to(torch.float64).contiguous()
+    w2 = w2.to(torch.float64).contiguous()
+    if w1.numel() != r or w2.numel() != s:
+        raise ValueError("w1 / w2 must have len r / s")
+    M = torch.empty((p, q), dtype=torch.float64, device=A.device)
+    lib = L.lib()
+    wsb = lib.otf_coupled_cost_workspace_size(p, q, r)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=A.device)
+    L.check(lib.otf_coupled_cost(A.data_ptr(), A.stride(0), A.stride(1), B.data_ptr(), B.stride(0),
+                                 B.stride(1), p, q, r, s, T.data_ptr(), T.stride(0), w1.data_ptr(),
+                                 w2.data_ptr(), M.data_ptr(), M.stride(0), ws.data_ptr(), wsb,
+                                 L.stream_handle(A.device)), "otf_coupled_cost")
+    return M
+
+
 # --------------------------------------------------------------------------- Sinkhorn
 @dataclass
 class SinkhornResult:

@@ -368,3 +368,100 @@ def get_coupling_egw_all(data, eps=5e-3):
     Xtot = np.concatenate([X_dict[l] for l in X_dict.keys()], axis=0)
     Ytot = np.concatenate([Y_dict[l] for l in X_dict.keys()], axis=0)
     return egw_all(Xtot, Ytot, eps)
+
+
+# ---------------------------------------------------------------- COOT-L (cot_labels.py)
+def _feature_hist(D, labels):
+    """cot_labels.py:110-122: column mass of the concatenated data when it is
+    non-negative, else uniform (computed in the data's dtype, as the reference)."""
+    Xc = np.concatenate([np.asarray(D[k]) for k in labels], axis=0)
+    if (Xc >= 0).all():
+        return np.asarray(Xc.sum(axis=0) / Xc.sum(), dtype=np.float64)
+    return np.ones(Xc.shape[1]) / Xc.shape[1]
+
+
+def cotl_sinkhorn(X_dict, Y_dict, eps: float = 5e-3, eps2: float | None = None,
+                  niter: int = 100, v1=None, v2=None, w1=None, w2=None, log: bool = False):
+    """``cotl_numpy(X_dict, Y_dict, algo="sinkhorn", algo2="sinkhorn", reg=eps,
+    reg2=eps2)`` (perturbot/perturbot/match/cot_labels.py:14-225) on the device.
+
+    Block-coordinate descent over per-label sample couplings Ts[k] and one feature
+    coupling Tv: the sample costs ``constC_s - X_k Tv (2 Y_k)^T`` and the feature cost
+    ``sum_k constC_v,k - X_k^T Ts[k] (2 Y_k)`` come from ``otf_coupled_cost`` (float64,
+    float32 squares), every linear problem is OTT ``linear.solve(Geometry(M, epsilon,
+    scale_cost="max_cost"), max_iterations=2000)`` -- uniform marginals, as the
+    reference's Sinkhorn branch -- on the device Sinkhorn (float64, lse mode).
+    Reference behaviour kept: the feature solve uses ``eps`` (reg), not eps2 (:200);
+    ``delta`` counts only Tv (``Tsold = Ts`` aliases the dict that is updated in place,
+    :167-172, so the Ts terms are 0); Tv is renormalised when its mass is off by 1e-8;
+    stop when delta < 1e-16 or |cost change| < 1e-7.
+    Returns ``(Ts dict of numpy, Tv, cost[, {"cost": [...]}])``.
+    """
+    assert sorted(X_dict.keys()) == sorted(Y_dict.keys()), "Labels don't match in y1 & y2."
+    dev = _device()
+    labels = list(X_dict.keys())
+    if v1 is None:
+        v1 = _feature_hist(X_dict, labels)
+    if v2 is None:
+        v2 = _feature_hist(Y_dict, labels)
+    Xs = {k: torch.as_tensor(np.asarray(X_dict[k]), device=dev).float() for k in labels}
+    Ys = {k: torch.as_tensor(np.asarray(Y_dict[k]), device=dev).float() for k in labels}
+    v1t = torch.as_tensor(np.asarray(v1, dtype=np.float64), device=dev)
+    v2t = torch.as_tensor(np.asarray(v2, dtype=np.float64), device=dev)
+    f64 = dict(dtype=torch.float64, device=dev)
+    w1t = {k: (torch.full((Xs[k].shape[0],), 1.0 / Xs[k].shape[0], **f64) if w1 is None
+               else torch.as_tensor(np.asarray(w1[k], dtype=np.float64), device=dev)) for k in labels}
+    w2t = {k: (torch.full((Ys[k].shape[0],), 1.0 / Ys[k].shape[0], **f64) if w2 is None
+               else torch.as_tensor(np.asarray(w2[k], dtype=np.float64), device=dev)) for k in labels}
+    d, d2 = Xs[labels[0]].shape[1], Ys[labels[0]].shape[1]
+    Ts = {k: torch.full((Xs[k].shape[0], Ys[k].shape[0]),
+                        1.0 / (Xs[k].shape[0] * Ys[k].shape[0]), **f64) for k in labels}
+    Tv = torch.full((d, d2), 1.0 / (d * d2), **f64)
+    cost = np.inf
+    costs = []
+    for _ in range(niter):
+        Tvold, costold = Tv, cost
+        for k in labels:  # sample OT per label
+            Mk = ops.coupled_cost(Xs[k], Ys[k], Tv, v1t, v2t)
+            res, _ = solve_ott(Mk, eps, "max_cost", max_iterations=OTT_MAX_ITER)
+            Ts[k] = res.plan
+        M = None  # global feature OT
+        for k in labels:
+            Mv = ops.coupled_cost(Xs[k].T, Ys[k].T, Ts[k], w1t[k], w2t[k])
+            M = Mv if M is None else M + Mv
+        res, _ = solve_ott(M, eps, "max_cost", max_iterations=OTT_MAX_ITER)
+        Tv = res.plan
+        tot = float(Tv.sum())
+        if not abs(tot - 1.0) < 1e-8:
+            Tv = Tv / tot
+        delta = float(torch.linalg.norm(Tv - Tvold))
+        cost = float((M * Tv).sum())
+        costs.append(cost)
+        if delta < 1e-16 or abs(costold - cost) < 1e-7:
+            break
+    Ts_np = {k: Ts[k].cpu().numpy() for k in labels}
+    if log:
+        return Ts_np, Tv.cpu().numpy(), cost, {"cost": costs}
+    return Ts_np, Tv.cpu().numpy(), cost
+
+
+def get_coupling_cotl_sinkhorn(data, eps: float = 5e-3, eps2: float | None = None):
+    """perturbot cot_labels.py:279-340: COOT-L with Sinkhorn solves, niter=2000.
+    Returns ``(Ts dict, log)`` (``(-1, -1)`` on a FloatingPointError, as the reference)."""
+    X_dict, Y_dict = data
+    start = time.time()
+    try:
+        Ts, Tv, cost, log = cotl_sinkhorn(X_dict, Y_dict, eps=eps, eps2=eps if eps2 is None else eps2,
+                                          niter=2000, log=True)
+    except FloatingPointError:
+        return -1, -1
+    log["time"] = time.time() - start
+    return Ts, log
+
+
+def get_coupling_cotl(data):
+    """perturbot cot_labels.py:228-276 (COOT-L with exact EMD on non-uniform marginals).
+    Not provided: it needs a general-marginal network simplex; use
+    ``get_coupling_cotl_sinkhorn``."""
+    raise NotImplementedError("COOT-L with exact EMD (general marginals) is not implemented; "
+                              "get_coupling_cotl_sinkhorn is the device COOT-L")
