@@ -1014,10 +1014,10 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
 }
 
 // ============================================================================
-// Tiled resident engine (OTF_ENGINE_TILED, float): the whole solve in one launch like
-// sk_resident_kernel, but each workgroup owns a 2-D TILE of K -- TL_R = 128 rows x
-// TL_C = 512 columns (8 waves x 16 rows, 64 lanes x 8 columns) -- instead of 16
-// full rows.  Per iteration it therefore adds only 512 column partials to the sums
+// Tiled resident engine (OTF_ENGINE_TILED): the whole solve in one launch like
+// sk_resident_kernel, but each workgroup owns a 2-D TILE of K -- 512 columns x
+// 128 rows for float (8 waves x 16 rows, 64 lanes x 8 columns) or 64 rows for double
+// (8 waves x 8 rows) -- instead of a few full rows.  Per iteration it therefore adds only 512 column partials to the sums
 // (8x fewer float atomics: they execute at the memory side at ~1.3 TB/s chip-wide,
 // and 4096 per workgroup were the single largest term of an iteration), and the
 // row sums K v become a two-level reduction: within the wave (butterfly), then over
@@ -1034,11 +1034,16 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
 // from the FULL sum vectors cs[it] and cs[it-1] (v(it-1) = b / cs[it-1] is recomputed
 // bit-identically), so every workgroup takes the same stop decision at once.
 // ============================================================================
-constexpr int TL_RW = 16;                 // rows per wave (per thread)
-constexpr int TL_NW = 8;                  // waves per workgroup
-constexpr int TL_R = TL_RW * TL_NW;       // 128 rows per tile
-constexpr int TL_G = 2, TL_VEC = 4;       // 8 columns per lane
-constexpr int TL_C = kWave * TL_G * TL_VEC;  // 512 columns per tile
+template <typename T> struct TileCfg {
+    static constexpr int NW = 8;                        // waves per workgroup
+    static constexpr int RW = sizeof(T) == 4 ? 16 : 8;  // rows per wave (per thread)
+    static constexpr int VEC = Vec<T>::N;
+    static constexpr int G = sizeof(T) == 4 ? 2 : 4;    // VEC-vectors per lane: 8 columns
+    static constexpr int R = RW * NW;                   // rows per tile: 128 / 64
+    static constexpr int C = kWave * G * VEC;           // 512 columns per tile
+};
+constexpr int TL_C = 512;
+inline int64_t tile_rows(size_t esz) { return esz == 4 ? TileCfg<float>::R : TileCfg<double>::R; }
 
 template <typename T> struct SkTileArgs {
     const void* C;
@@ -1055,7 +1060,7 @@ template <typename T> struct SkTileArgs {
     int* bad_cnt;     // max_iter + 1 counters, zeroed
     int* bar;         // flat barrier counter, zeroed
     SkSync sync;      // hierarchical barrier words, zeroed
-    T* xch;           // 2 x nrb x ncb x TL_R row partials (write-through hand-off)
+    T* xch;           // 2 x nrb x ncb x tile rows row partials (write-through hand-off)
     int* grp;         // nrb counters, one 256-B line each, zeroed
     int nrb, ncb;
     otf_sinkhorn_info* info;
@@ -1072,15 +1077,16 @@ __device__ __forceinline__ void store_wt(T* p, T v) {  // write-through (sc1) st
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename CT, typename TP, int NREP>
-__global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
-    using T = float;
-    constexpr int G = TL_G, VEC = TL_VEC, R = TL_RW;
+template <typename T, typename CT, typename TP, int NREP>
+__global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
+    using Cf = TileCfg<T>;
+    constexpr int G = Cf::G, VEC = Cf::VEC, R = Cf::RW, NW = Cf::NW, TR = Cf::R;
+    static_assert(Cf::C == TL_C, "tile width");
     using V = typename Vec<T>::type;
     using VP = __attribute__((ext_vector_type(VEC))) TP;
-    __shared__ __attribute__((aligned(16))) T colbuf[TL_NW][TL_C];
-    __shared__ T urow[TL_NW][R];          // u of each wave's rows (wave-private)
-    __shared__ T uhist[2][TL_R];          // u history (slot = iteration & 1)
+    __shared__ __attribute__((aligned(16))) T colbuf[NW][TL_C];
+    __shared__ T urow[NW][R];          // u of each wave's rows (wave-private)
+    __shared__ T uhist[2][TR];          // u history (slot = iteration & 1)
     __shared__ __attribute__((aligned(16))) T vhist[2][TL_C];  // v history
     __shared__ T red[17 + 17];
     __shared__ int s_flag;
@@ -1103,7 +1109,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
             cb = b % p.ncb;
         }
     }
-    const int row0 = rb * TL_R + w * R;   // this wave's first row
+    const int row0 = rb * TR + w * R;   // this wave's first row
     const int col0 = cb * TL_C;           // this tile's first column
 
     const double unit = exp_unit<T>();
@@ -1149,7 +1155,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
     const T ia_mine = (T)1 / p.a[row0 + (lane & (R - 1)) < p.n ? row0 + (lane & (R - 1)) : p.n - 1];
     const T u0 = (T)1 / (T)p.n, v0 = (T)1 / (T)p.m;
     for (int q = tid; q < TL_C; q += blockDim.x) vhist[0][q] = vhist[1][q] = v0;
-    if (tid < TL_R) uhist[0][tid] = uhist[1][tid] = u0;
+    if (tid < TR) uhist[0][tid] = uhist[1][tid] = u0;
 
     const size_t it_stride = (size_t)NREP * p.m_pad;
     const int xcd = xcc_id();
@@ -1218,7 +1224,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
         for (int q = tid; q < TL_C; q += blockDim.x) {
             T sacc = colbuf[0][q];
 #pragma unroll
-            for (int ww = 1; ww < TL_NW; ++ww) sacc += colbuf[ww][q];
+            for (int ww = 1; ww < NW; ++ww) sacc += colbuf[ww][q];
             if (col0 + q < p.m) atomicAdd(dst + (size_t)my_rep * p.m_pad + col0 + q, sacc);
         }
     };
@@ -1301,9 +1307,15 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
         wave_sum_multi<T, R>(rp, lane);
         const int slot = it & 1;
         T tot = 0;
-        {
-            T* xg = p.xch + ((size_t)slot * p.nrb + rb) * (size_t)p.ncb * TL_R;
-            if (lane < R) store_wt(xg + (size_t)cb * TL_R + w * R + rowl, rp[0]);
+        if (p.ncb == 1) {  // the tile spans whole rows: the wave totals are the row sums
+            if (lane < R) urow[w][rowl] = rp[0];
+            __builtin_amdgcn_wave_barrier();
+            tot = urow[w][lane & (R - 1)];
+            __builtin_amdgcn_wave_barrier();
+            OTF_STAMP(it, 2);
+        } else {
+            T* xg = p.xch + ((size_t)slot * p.nrb + rb) * (size_t)p.ncb * TR;
+            if (lane < R) store_wt(xg + (size_t)cb * TR + w * R + rowl, rp[0]);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) {
@@ -1321,11 +1333,11 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
             OTF_STAMP(it, 2);
             // gather the ncb partials of this wave's rows (fixed order)
             const int rr = lane & (R - 1);
-            for (int mb = lane >> 4; mb < p.ncb; mb += 4)
-                tot += __hip_atomic_load(xg + (size_t)mb * TL_R + w * R + rr, __ATOMIC_RELAXED,
+            for (int mb = lane / R; mb < p.ncb; mb += kWave / R)
+                tot += __hip_atomic_load(xg + (size_t)mb * TR + w * R + rr, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
-            tot += __shfl_xor(tot, 16, kWave);
-            tot += __shfl_xor(tot, 32, kWave);
+#pragma unroll
+            for (int o = R; o < kWave; o <<= 1) tot += __shfl_xor(tot, o, kWave);
         }
         if (lane < R) {
             const int rr = lane;
@@ -1346,9 +1358,12 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<float> p) {
         if (badu && lane == 0) atomicAdd(p.bad_cnt + it, 1);
         if (w == 0) {
 #pragma unroll
-            for (int g = 0; g < G; ++g)
-                *reinterpret_cast<V*>(&vhist[slot][(lane + kWave * g) * VEC]) =
-                    V{vn[g][0], vn[g][1], vn[g][2], vn[g][3]};
+            for (int g = 0; g < G; ++g) {
+                V vv;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) vv[q] = vn[g][q];
+                *reinterpret_cast<V*>(&vhist[slot][(lane + kWave * g) * VEC]) = vv;
+            }
         }
         OTF_STAMP(it, 3);
         flush(un, p.cs + (size_t)(it + 1) * it_stride);
@@ -1500,9 +1515,9 @@ struct Workspace {
     size_t t_xch_off;      // tiled engine: exchange region offset inside res
 };
 
-// tiled engine row exchange: two slots (iteration parity) of nrb x ncb x TL_R partials
-size_t tiled_xch_bytes(int64_t nrb, int64_t ncb) {
-    return align_up(2 * (size_t)nrb * ncb * TL_R * sizeof(float), 256);
+// tiled engine row exchange: two slots (iteration parity) of nrb x ncb x tile-rows partials
+size_t tiled_xch_bytes(int64_t nrb, int64_t ncb, size_t esz) {
+    return align_up(2 * (size_t)nrb * ncb * tile_rows(esz) * esz, 256);
 }
 
 // hierarchical barrier words: reg[8], xcnt[8], top, gen[8], each on a 256-B line
@@ -1536,11 +1551,11 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.nrep = res_replicas(nrb);
     w.res_bytes = align_up((size_t)(max_iter + 1) * w.nrep * w.m_pad * esz, 256) +
                   align_up(sizeof(int) * (size_t)(max_iter + 1), 256) + 256 + kSyncBytes;
-    // tiled engine: row-partial exchange (2 slots x nrb x ncb x TL_R) + group counters
-    w.t_nrb = (n + TL_R - 1) / TL_R;
+    // tiled engine: row-partial exchange (2 slots x nrb x ncb x tile rows) + group counters
+    w.t_nrb = (n + tile_rows(esz) - 1) / tile_rows(esz);
     w.t_ncb = (m + TL_C - 1) / TL_C;
     w.t_xch_off = w.res_bytes;
-    w.res_bytes += tiled_xch_bytes(w.t_nrb, w.t_ncb) + (size_t)w.t_nrb * 256;
+    w.res_bytes += tiled_xch_bytes(w.t_nrb, w.t_ncb, esz) + (size_t)w.t_nrb * 256;
     w.res = take(w.res_bytes);
     w.bytes = off;
     return w;
@@ -1618,11 +1633,11 @@ hipError_t run_resident(const PassCfg& cfg, int grid, const CT* C, int64_t ldc, 
     return launch_resident<T, CT, float>(cfg, grid, p, s);
 }
 
-// Tiled resident solve (float).  Same contract as run_resident.
-template <typename CT, typename TP, int NREP>
-hipError_t launch_tiled_g(int grid, SkTileArgs<float>& p, hipStream_t s) {
+// Tiled resident solve.  Same contract as run_resident.
+template <typename T, typename CT, typename TP, int NREP>
+hipError_t launch_tiled_g(int grid, SkTileArgs<T>& p, hipStream_t s) {
     void* args[] = {&p};
-    const void* k = (const void*)sk_tiled_kernel<CT, TP, NREP>;
+    const void* k = (const void*)sk_tiled_kernel<T, CT, TP, NREP>;
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
     if (e != hipSuccess) return e;
@@ -1640,38 +1655,38 @@ inline int tiled_nrep(const Workspace& w) {
     return r <= w.nrep ? r : 1;
 }
 
-template <typename CT>
-hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const float* cost_scale,
-                     const otf_sinkhorn_opts& o, Workspace& w, float* u_out, float* v_out,
+template <typename T, typename CT>
+hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const T* cost_scale,
+                     const otf_sinkhorn_opts& o, Workspace& w, T* u_out, T* v_out,
                      void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                      double* errlog, hipStream_t s) {
-    SkTileArgs<float> p{};
+    SkTileArgs<T> p{};
     const int nrep = tiled_nrep(w);
     p.C = C;
     p.ldc = ldc;
     p.n = n;
     p.m = m;
     p.m_pad = (int)w.m_pad;
-    p.a = (const float*)w.a_pad;
-    p.b = (const float*)w.b_pad;
+    p.a = (const T*)w.a_pad;
+    p.b = (const T*)w.b_pad;
     p.cost_scale = cost_scale;
     p.reg = o.reg;
     p.max_iter = o.max_iter;
     p.check_every = o.check_every;
     p.err_squared = o.err_squared;
     p.stop_thr = o.stop_thr;
-    p.cs = (float*)w.res;
+    p.cs = (T*)w.res;
     p.nrep = nrep;
     p.bad_cnt = (int*)((char*)w.res +
-                       align_up((size_t)(o.max_iter + 1) * w.nrep * w.m_pad * sizeof(float), 256));
+                       align_up((size_t)(o.max_iter + 1) * w.nrep * w.m_pad * sizeof(T), 256));
     p.bar = (int*)((char*)p.bad_cnt + align_up(sizeof(int) * (size_t)(o.max_iter + 1), 256));
     int* sw = (int*)((char*)p.bar + 256);
     p.sync.reg = sw;
     p.sync.xcnt = sw + 8 * 64;
     p.sync.top = sw + 16 * 64;
     p.sync.gen = sw + 17 * 64;
-    p.xch = (float*)((char*)w.res + w.t_xch_off);
-    p.grp = (int*)((char*)p.xch + tiled_xch_bytes(w.t_nrb, w.t_ncb));
+    p.xch = (T*)((char*)w.res + w.t_xch_off);
+    p.grp = (int*)((char*)p.xch + tiled_xch_bytes(w.t_nrb, w.t_ncb, sizeof(T)));
     p.nrb = (int)w.t_nrb;
     p.ncb = (int)w.t_ncb;
     p.info = info;
@@ -1685,9 +1700,11 @@ hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const float* cost_s
     if (e != hipSuccess) return e;
     const int grid = (int)(w.t_nrb * w.t_ncb);
     const bool f64p = P_out && P_dtype == OTF_F64;
-    if (nrep == 4) return f64p ? launch_tiled_g<CT, double, 4>(grid, p, s) : launch_tiled_g<CT, float, 4>(grid, p, s);
-    if (nrep == 2) return f64p ? launch_tiled_g<CT, double, 2>(grid, p, s) : launch_tiled_g<CT, float, 2>(grid, p, s);
-    return f64p ? launch_tiled_g<CT, double, 1>(grid, p, s) : launch_tiled_g<CT, float, 1>(grid, p, s);
+    if constexpr (sizeof(T) == 4) {
+        if (nrep == 4) return f64p ? launch_tiled_g<T, CT, double, 4>(grid, p, s) : launch_tiled_g<T, CT, float, 4>(grid, p, s);
+        if (nrep == 2) return f64p ? launch_tiled_g<T, CT, double, 2>(grid, p, s) : launch_tiled_g<T, CT, float, 2>(grid, p, s);
+    }
+    return f64p ? launch_tiled_g<T, CT, double, 1>(grid, p, s) : launch_tiled_g<T, CT, float, 1>(grid, p, s);
 }
 
 // Validated shape / workspace of one solve (deterministic in n, m, max_iter).
@@ -1816,21 +1833,22 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     // gets its own CU (POT flavour, no per-pass profiling requested)
     const bool whole = o.n_total <= 0 || o.n_total == n;
     const bool fits = su.nrb <= device_cu_count() && su.cfg.G <= 4 && whole;
-    // tiled engine: float, every (128 x 512) tile on its own CU
-    const bool tfits = sizeof(T) == 4 && whole && su.w.t_nrb * su.w.t_ncb <= device_cu_count();
+    // tiled engine: every (128 x 512 float / 64 x 512 double) tile on its own CU
+    const bool tfits = whole && su.w.t_nrb * su.w.t_ncb <= device_cu_count();
+    // AUTO takes it for float only: for float64 (64-row tiles) it measured no faster
+    // than the row-block resident engine (config 2, d = 512: 12.8 vs 12.3 ms per step --
+    // both sit on the ~5 us grid-sync round trip per iteration); TILED forces it
     const bool want_tiled = !LOG && !avg_pass_ms && tfits && o.max_iter >= 1 &&
-                            (o.engine == OTF_ENGINE_TILED || o.engine == OTF_ENGINE_AUTO);
+                            (o.engine == OTF_ENGINE_TILED ||
+                             (o.engine == OTF_ENGINE_AUTO && sizeof(T) == 4));
     if (o.engine == OTF_ENGINE_TILED && (LOG || !tfits)) return OTF_EUNSUPPORTED;
-    if constexpr (sizeof(T) == 4) {
-        if (want_tiled) {
-            Workspace w = su.w;
-            const hipError_t e = run_tiled<CT>(C, ldc, (int)n, (int)m, (const float*)cost_scale, o, w,
-                                               (float*)u_out, (float*)v_out, P_out, ldp, P_dtype,
-                                               info, errlog, s);
-            if (e == hipSuccess) return OTF_OK;
-            (void)hipGetLastError();
-            if (o.engine == OTF_ENGINE_TILED) return check_hip(e);
-        }
+    if (want_tiled) {
+        Workspace w = su.w;
+        const hipError_t e = run_tiled<T, CT>(C, ldc, (int)n, (int)m, cost_scale, o, w, u_out, v_out,
+                                              P_out, ldp, P_dtype, info, errlog, s);
+        if (e == hipSuccess) return OTF_OK;
+        (void)hipGetLastError();
+        if (o.engine == OTF_ENGINE_TILED) return check_hip(e);
     }
     // AUTO reaches here only when the tiled engine did not take the solve (shape, dtype
     // or co-residency refused), so the row-block resident engine is the next choice
