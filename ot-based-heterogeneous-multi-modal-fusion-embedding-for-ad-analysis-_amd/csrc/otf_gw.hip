@@ -442,6 +442,85 @@ __device__ int blk_sinkhorn_knopp(const double* K, int64_t ldk, int n, int m, co
     return cur;
 }
 
+// The same sinkhorn_knopp for n, m <= 64 with two workgroup barriers per update (the
+// block version above spends four, plus LDS round trips for u and v; at <= 64 points
+// the barriers dominate).  K is a zero-padded 64 x 65 LDS image (entries outside
+// n x m are 0).  Every wavefront holds the whole u (lane i) and v (lane j) in
+// registers: wavefront w forms the partial column sums of K^T u over its RPW rows
+// and, after a barrier, every wavefront sums the NW partials of its lane's column in
+// the same order, so all of them compute the same v; the row sums (Kp v) go the same
+// way over column slices.  Identical values in every wavefront make the numerical-
+// error ballot and the stop test uniform, so the barrier counts always agree.  The
+// previous pair stays in registers for the revert-on-error rule.  u ends in sh.f,
+// v in sh.g (slot 0); conv / iters are uniform.
+constexpr int GW_WLD = GW_SMALLN + 1;
+
+template <class Cfg>
+__device__ void small_sinkhorn_knopp(const double* K, int n, int m, const double* a, const double* b,
+                                     double thr, int maxit, int every, GwShared<Cfg>& sh,
+                                     bool& conv, int& iters) {
+    static_assert(GW_SMALLN % Cfg::NW == 0 && Cfg::NT <= 8 * GW_SMALLN, "row slices");
+    constexpr int RPW = GW_SMALLN / Cfg::NW;
+    const int l = threadIdx.x & (kWave - 1);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const bool rl = l < n, cl = l < m;
+    const double ia = rl ? 1.0 / marg(a, l, n) : 0.0;
+    const double bj = cl ? marg(b, l, m) : 0.0;
+    const double* kcol = K + (w * RPW) * GW_WLD + l;  // rows w*RPW.., column l
+    const double* krow = K + l * GW_WLD + w * RPW;    // row l, columns w*RPW..
+    double* pc = sh.ps;                               // NW x 64 column partials
+    double* pr = sh.pm;                               // NW x 64 row partials
+    double u = rl ? 1.0 / (double)n : 0.0, v = cl ? 1.0 / (double)m : 0.0;
+    conv = false;
+    iters = maxit;
+    for (int ii = 0; ii < maxit; ++ii) {
+        // v = b / K^T u
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) s += kcol[r * GW_WLD] * readlane_f64(u, w * RPW + r);
+        pc[w * kWave + l] = s;
+        __syncthreads();
+        s = 0.0;
+#pragma unroll
+        for (int q = 0; q < Cfg::NW; ++q) s += pc[q * kWave + l];
+        const double vn = cl ? bj / s : 0.0;
+        bool bad = cl && (s == 0.0 || !finite_val(vn));
+        // u = 1 / (Kp v)
+        s = 0.0;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) s += (ia * krow[r]) * readlane_f64(vn, w * RPW + r);
+        pr[w * kWave + l] = s;
+        __syncthreads();
+        s = 0.0;
+#pragma unroll
+        for (int q = 0; q < Cfg::NW; ++q) s += pr[q * kWave + l];
+        const double un = rl ? 1.0 / s : 0.0;
+        bad = bad || (rl && !finite_val(un));
+        if (__ballot(bad) != 0) { iters = ii + 1; break; }  // keep the previous pair
+        u = un;
+        v = vn;
+        if (ii % every == 0) {
+            s = 0.0;
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) s += kcol[r * GW_WLD] * readlane_f64(u, w * RPW + r);
+            pc[w * kWave + l] = s;  // every column-partial read of this update is done
+            __syncthreads();
+            s = 0.0;
+#pragma unroll
+            for (int q = 0; q < Cfg::NW; ++q) s += pc[q * kWave + l];
+            const double d = cl ? s * v - bj : 0.0;
+            const double e2 = wave_reduce_f64<0>(d * d);
+            __syncthreads();  // reads done before the next update rewrites pc
+            if (sqrt(e2) < thr) { conv = true; iters = ii + 1; break; }
+        }
+    }
+    if (w == 0) {
+        sh.f[l] = u;
+        sh.g[l] = v;
+    }
+    __syncthreads();
+}
+
 // Minimum-cost assignment of the n x n matrix A (row stride lda), ONE wavefront:
 // shortest augmenting paths with dual potentials (the serial form in the oracle's
 // oro_lap), lanes over columns.  Column j (1-based) lives in lane (j-1) % 64, slot
@@ -758,6 +837,13 @@ GW_TEND(0); }
         double err = 1.0;
         int nerr = 0;
         const double neps = -o.eps;
+        // small problems: K in a zero-padded 64 x 65 LDS image for the wavefront solve
+        const bool wave_sk = Cfg::SMALL && n <= kWave && m <= kWave;
+        const int64_t kld = wave_sk ? GW_WLD : ldl;
+        if (wave_sk) {
+            for (int e = t; e < GW_SMALLN * GW_WLD; e += Cfg::NT) Lm[e] = 0.0;
+            __syncthreads();
+        }
         while (err > o.tol_abs && it < o.max_iter) {
             { GW_TBEG();
             blk_gemm<Cfg, false>(D, 1, n, C1, 1, ldc1, G, ldt, 1, n, m, n, nullptr, 1.0);
@@ -769,15 +855,21 @@ GW_TEND(0); }
             for (int64_t e = t; e < nm; e += Cfg::NT) {
                 const int i = (int)(e / m), j = (int)(e % m);
                 const double tens = 2.0 * (sh.x[i] + sh.y[j] - 2.0 * R[e]);
-                Lm[i * ldl + j] = exp(tens / neps);
+                Lm[i * kld + j] = exp(tens / neps);
             }
             __syncthreads();
             int sk_it = 0;
 #ifdef OTF_GW_STAMPS
             unsigned long long gw_t0_ = __builtin_amdgcn_s_memrealtime();
 #endif
-            const int slot = blk_sinkhorn_knopp<Cfg>(Lm, ldl, n, m, pa, pb, o.sk_threshold,
-                                                     o.sk_max_iter, o.sk_inner, sh, inner_conv, sk_it);
+            int slot = 0;
+            if (wave_sk) {
+                small_sinkhorn_knopp<Cfg>(Lm, n, m, pa, pb, o.sk_threshold, o.sk_max_iter,
+                                          o.sk_inner, sh, inner_conv, sk_it);
+            } else {
+                slot = blk_sinkhorn_knopp<Cfg>(Lm, kld, n, m, pa, pb, o.sk_threshold,
+                                               o.sk_max_iter, o.sk_inner, sh, inner_conv, sk_it);
+            }
             GW_TEND(2);
             inner_total += sk_it;
             // T = diag(u) K diag(v) (POT: u[:, None] * K * v[None, :]); ||T - Tprev||_F
@@ -786,7 +878,7 @@ GW_TEND(0); }
             double d2 = 0;
             for (int64_t e = t; e < nm; e += Cfg::NT) {
                 const int i = (int)(e / m), j = (int)(e % m);
-                const double tv = uf[i] * Lm[i * ldl + j] * vf[j];
+                const double tv = uf[i] * Lm[i * kld + j] * vf[j];
                 const double d = tv - G[i * ldt + j];
                 d2 += d * d;
                 G[i * ldt + j] = tv;
