@@ -21,6 +21,22 @@ namespace {
 
 constexpr int BM = 128, BN = 128, BK = 32, LDSW = BM + 1;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+// Global max of non-negative floats as a uint bit pattern: ONE atomic per 256-thread
+// workgroup at most (a per-wave atomic made every tile's waves queue on one address).
+__device__ __forceinline__ void block_max_publish(unsigned int* cmax, float lmax) {
+    __shared__ float wmx[4];
+    lmax = wave_max(lmax);
+    if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = lmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // cmax only grows: a coherent read at or above this tile's max makes the atomic
+        // redundant, so after the first tiles almost none are issued.
+        const unsigned int v = __float_as_uint(fmaxf(fmaxf(wmx[0], wmx[1]), fmaxf(wmx[2], wmx[3])));
+        if (v > __hip_atomic_load(cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(cmax, v);
+    }
+}
+
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 __device__ __forceinline__ f32x4 load4(const float* base, int64_t ld, int row, int nrows, int k,
@@ -150,10 +166,7 @@ __global__ __launch_bounds__(256) void cost_pairwise_kernel(
                     lmax = fmaxf(lmax, c);
                 }
             }
-    if (cmax) {
-        lmax = wave_max(lmax);
-        if (lane == 0) atomicMax(cmax, __float_as_uint(lmax));
-    }
+    if (cmax) block_max_publish(cmax, lmax);
 }
 
 template <typename T>
@@ -370,10 +383,7 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
                     lmax = fmaxf(lmax, (float)cs);
                 }
             }
-    if (cmax) {
-        lmax = wave_max(lmax);
-        if (lane == 0) atomicMax(cmax, __float_as_uint(lmax));
-    }
+    if (cmax) block_max_publish(cmax, lmax);
 }
 
 }  // namespace
