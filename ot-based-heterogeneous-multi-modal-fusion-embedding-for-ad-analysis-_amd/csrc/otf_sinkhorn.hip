@@ -830,6 +830,8 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
         const T* cs_it = p.cs + (size_t)it * it_stride;   // K^T u(it-1)
         T s[G][VEC], vn[G][VEC];
         int badv = 0;
+        // the break flag of u(it-1) is loaded together with the sums (one round trip)
+        const int prev_bad = it >= 1 ? load_agent(p.bad_cnt + it - 1) : 0;
         load_sums(cs_it, s, (T)1);
 #pragma unroll
         for (int g = 0; g < G; ++g)
@@ -841,7 +843,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
                 vn[g][k] = cok[g][k] ? val : (T)0;
             }
         // numerical break in u(it-1) -> revert to it-2
-        if (it >= 1 && load_agent(p.bad_cnt + it - 1) > 0) {
+        if (prev_bad > 0) {
             last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
             break;
         }
@@ -1263,13 +1265,15 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
 
     for (int it = 0; it < p.max_iter && !done; ++it) {
         OTF_STAMP(it, 0);
-        // a numerical break in iteration it-1 (v or u, any tile) -> revert to it-2
-        if (it >= 1 && load_agent(p.bad_cnt + it - 1) > 0) {
+        // a numerical break in iteration it-1 (v or u, any tile) -> revert to it-2.  The
+        // flag load is issued together with the sum loads (one memory round trip, not two).
+        const int prev_bad = it >= 1 ? load_agent(p.bad_cnt + it - 1) : 0;
+        T s[G][VEC], vn[G][VEC];
+        load_sums(p.cs + (size_t)it * it_stride, s, (T)1);
+        if (prev_bad > 0) {
             last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
             break;
         }
-        T s[G][VEC], vn[G][VEC];
-        load_sums(p.cs + (size_t)it * it_stride, s, (T)1);
         int badv = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
