@@ -246,3 +246,24 @@ def test_perturbot_pot_gw_dropins(orc, dev):
     assert T.shape == (60, 60) and abs(T.sum() - 1.0) < 1e-9 and "time" in loga
     T2, loga2 = perturbot.get_coupling_egw_all((Xd, Yd), eps=1e-2)
     assert T2.shape == (60, 60) and abs(T2.sum() - 1.0) < 1e-6 and "gw_dist" in loga2
+
+
+@pytest.mark.parametrize("n,m,eps", [(40, 50, 1e-4), (64, 17, 2e-3)])
+def test_gw_pgd_small_inner_break_vs_oracle(orc, dev, n, m, eps):
+    """The <= 64-point inner solve (two-barrier small_sinkhorn_knopp) on problems whose
+    kernel underflows (eps = 1e-4: zero columns of K^T u -> POT's revert-and-break) and on
+    a ragged n != m shape: same outer / inner counts as the oracle, plans to 1e-9."""
+    from otfuse import gw
+    (C1, _), = _label_costs(orc, [n], 16, 90)
+    (_, C2), = _label_costs(orc, [m], 16, 91)
+    T, log = gw.entropic_gromov_wasserstein(torch.as_tensor(C1, device=dev),
+                                            torch.as_tensor(C2, device=dev), epsilon=eps,
+                                            log=True)
+    Tr, ref = orc.gw_pgd(C1, C2, eps)
+    assert log["n_iter"] == ref["n_iter"]
+    assert log["inner_iters"] == ref["inner_iters"]
+    Td = T.cpu().numpy()
+    assert np.array_equal(np.isfinite(Td), np.isfinite(Tr))
+    fin = np.isfinite(Tr)
+    if fin.any() and np.abs(Tr[fin]).max() > 0:
+        assert np.abs(Td[fin] - Tr[fin]).max() / np.abs(Tr[fin]).max() < 1e-9
