@@ -22,6 +22,21 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 32, LDSW = BM + 1;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
+// XCD-contiguous tile index wg -> (tile row, tile column) in column bands of
+// TILE_GROUP tile rows: the ~64 tiles an XCD runs at once form an 8 x 8 block, whose
+// X and Y panels (2 + 2 MB in split-fp16) stay in that XCD's 4 MB L2 -- row-major
+// order made them span 2 tile rows x ALL of Y, streamed from the MALL per tile row.
+constexpr int TILE_GROUP = 8;
+__device__ __forceinline__ void grouped_tile(int wg, int nwg, int tiles_n, int& tm, int& tn) {
+    const int tiles_m = nwg / tiles_n;
+    const int per_group = TILE_GROUP * tiles_n;
+    const int first_m = (wg / per_group) * TILE_GROUP;
+    const int gsize = min(tiles_m - first_m, TILE_GROUP);
+    const int li = wg % per_group;
+    tm = first_m + li % gsize;
+    tn = li / gsize;
+}
+
 // Global max of non-negative floats as a uint bit pattern: ONE atomic per 256-thread
 // workgroup at most (a per-wave atomic made every tile's waves queue on one address).
 __device__ __forceinline__ void block_max_publish(unsigned int* cmax, float lmax) {
@@ -68,7 +83,8 @@ __global__ __launch_bounds__(256) void cost_pairwise_kernel(
     const int bid = blockIdx.x;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    const int tm = wg / tiles_n, tn = wg % tiles_n;
+    int tm, tn;
+    grouped_tile(wg, nwg, tiles_n, tm, tn);
     const int i0 = tm * BM, j0 = tn * BN;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -281,7 +297,8 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    const int tm = wg / tiles_n, tn = wg % tiles_n;
+    int tm, tn;
+    grouped_tile(wg, nwg, tiles_n, tm, tn);
     const int i0 = tm * BM, j0 = tn * BN;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
