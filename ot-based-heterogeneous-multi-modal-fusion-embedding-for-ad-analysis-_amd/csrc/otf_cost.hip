@@ -209,59 +209,67 @@ constexpr int SLD = SBK + 8;   // padded LDS row (144 B): conflict-free ds_read_
 constexpr int SCPR = SBK / 8;  // 16-B chunks per row per stage
 constexpr int SCPT = BM * SCPR / 256;  // chunks per thread per image
 
-// One 256-thread workgroup per row: squared norm (fp32, same expansion as the fp32
-// path) and the fp16 image(s) of the row, zero-padded to ldh.
+// Split-fp16 images of both operands in ONE launch, one wavefront per row (4 rows per
+// 256-thread workgroup, wave reductions, no workgroup barriers): squared norm (fp32)
+// and the fp16 image(s) of the row, zero-padded to ldh.
 //   SPLIT (fp32 input): power-of-two scale s, hi = fp16(x s), lo = fp16(x s - hi);
 //   !SPLIT (fp16 input): hi = x, inv_scale = 1.
 // max_norm (nullable): running max of the squared norms (bit pattern, >= 0).
+// (Was one 256-thread workgroup per row and one launch per operand: 2 x 9 us at
+// 4096 x 512.)
+template <typename TI> struct PrepSide {
+    const TI* X;
+    int64_t ldx;
+    int n;
+    _Float16* hi;
+    _Float16* lo;
+    float* inv_scale;
+    float* norm;
+    unsigned int* max_norm;  // nullable
+};
+
 template <typename TI, bool SPLIT>
-__global__ __launch_bounds__(256) void split16_prep_kernel(const TI* __restrict__ X, int64_t ldx,
-                                                          int n, int d, _Float16* hi, _Float16* lo,
-                                                          int ldh, float* inv_scale, float* norm,
-                                                          unsigned int* max_norm) {
-    __shared__ float red[17];
-    __shared__ float wm[16];
-    float nmax = 0.f;
-    for (int row = blockIdx.x; row < n; row += gridDim.x) {
-        const TI* x = X + (int64_t)row * ldx;
+__global__ __launch_bounds__(256) void split16_prep2_kernel(PrepSide<TI> A, PrepSide<TI> B, int d,
+                                                           int ldh) {
+    const int lane = threadIdx.x & 63;
+    const int total = A.n + B.n;
+    float nmax[2] = {0.f, 0.f};
+    for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < total; row += gridDim.x * 4) {
+        const bool sb = row >= A.n;
+        const PrepSide<TI>& P = sb ? B : A;
+        const int r = sb ? row - A.n : row;
+        const TI* x = P.X + (int64_t)r * P.ldx;
         float mx = 0.f, s2 = 0.f;
-        for (int k = threadIdx.x; k < d; k += blockDim.x) {
+        for (int k = lane; k < d; k += 64) {
             const float v = (float)x[k];
             mx = fmaxf(mx, fabsf(v));
             s2 = fmaf(v, v, s2);
         }
-        s2 = block_sum<float>(s2, red);
+        s2 = wave_sum(s2);
         int e = 0;
         if (SPLIT) {
             mx = wave_max(mx);
-            if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                float m2 = 0.f;
-                for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m2 = fmaxf(m2, wm[w]);
-                wm[0] = m2;
-            }
-            __syncthreads();
-            mx = wm[0];
             e = mx > 0.f ? ilogbf(mx) : 0;
         }
         const float sc = SPLIT ? ldexpf(1.0f, 14 - e) : 1.0f;
-        _Float16* h = hi + (int64_t)row * ldh;
-        _Float16* l = SPLIT ? lo + (int64_t)row * ldh : nullptr;
-        for (int k = threadIdx.x; k < ldh; k += blockDim.x) {
+        _Float16* h = P.hi + (int64_t)r * ldh;
+        _Float16* l = SPLIT ? P.lo + (int64_t)r * ldh : nullptr;
+        for (int k = lane; k < ldh; k += 64) {
             const float v = k < d ? (float)x[k] * sc : 0.f;
             const _Float16 vh = (_Float16)v;
             h[k] = vh;
             if (SPLIT) l[k] = (_Float16)(v - (float)vh);
         }
-        if (threadIdx.x == 0) {
-            inv_scale[row] = SPLIT ? ldexpf(1.0f, e - 14) : 1.0f;
-            norm[row] = s2;
-            nmax = fmaxf(nmax, s2);
+        if (lane == 0) {
+            P.inv_scale[r] = SPLIT ? ldexpf(1.0f, e - 14) : 1.0f;
+            P.norm[r] = s2;
+            nmax[sb ? 1 : 0] = fmaxf(nmax[sb ? 1 : 0], s2);
         }
-        __syncthreads();
     }
-    if (max_norm && threadIdx.x == 0) atomicMax(max_norm, __float_as_uint(nmax));
+    if (lane == 0) {
+        if (A.max_norm && nmax[0] > 0.f) atomicMax(A.max_norm, __float_as_uint(nmax[0]));
+        if (B.max_norm && nmax[1] > 0.f) atomicMax(B.max_norm, __float_as_uint(nmax[1]));
+    }
 }
 
 // fp16 cost storage scale: 2^-k with 2^k >= the largest possible cost given the row
@@ -472,19 +480,20 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     unsigned int* mn = f16out ? (unsigned int*)small : nullptr;
     if (f16out) OTF_HIP(hipMemsetAsync(small, 0, 2 * sizeof(float), s));
     const bool same = (X == Y && n == m && ldx == ldy);
-    const int gx = (int)(n < 4096 ? n : 4096), gy = (int)(m < 4096 ? m : 4096);
-    if (split) {
-        otf::split16_prep_kernel<float, true><<<gx, 256, 0, s>>>((const float*)X, ldx, (int)n, (int)d,
-                                                                Xh, Xl, ldh, xs, xx, mn);
-        if (!same)
-            otf::split16_prep_kernel<float, true><<<gy, 256, 0, s>>>((const float*)Y, ldy, (int)m, (int)d,
-                                                                    Yh, Yl, ldh, ys, yy, mn ? mn + 1 : nullptr);
-    } else {
-        otf::split16_prep_kernel<_Float16, false><<<gx, 256, 0, s>>>((const _Float16*)X, ldx, (int)n,
-                                                                    (int)d, Xh, nullptr, ldh, xs, xx, mn);
-        if (!same)
-            otf::split16_prep_kernel<_Float16, false><<<gy, 256, 0, s>>>(
-                (const _Float16*)Y, ldy, (int)m, (int)d, Yh, nullptr, ldh, ys, yy, mn ? mn + 1 : nullptr);
+    {
+        const int rows = (int)n + (same ? 0 : (int)m);
+        const int nblk = (rows + 3) / 4 < 4096 ? (rows + 3) / 4 : 4096;
+        if (split) {
+            const otf::PrepSide<float> A{(const float*)X, ldx, (int)n, Xh, Xl, xs, xx, mn};
+            const otf::PrepSide<float> B{(const float*)Y, ldy, same ? 0 : (int)m, Yh, Yl, ys, yy,
+                                         mn ? mn + 1 : nullptr};
+            otf::split16_prep2_kernel<float, true><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh);
+        } else {
+            const otf::PrepSide<_Float16> A{(const _Float16*)X, ldx, (int)n, Xh, nullptr, xs, xx, mn};
+            const otf::PrepSide<_Float16> B{(const _Float16*)Y, ldy, same ? 0 : (int)m, Yh, nullptr,
+                                            ys, yy, mn ? mn + 1 : nullptr};
+            otf::split16_prep2_kernel<_Float16, false><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh);
+        }
     }
     OTF_HIP(hipGetLastError());
     if (same) {

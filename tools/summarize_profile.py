@@ -21,7 +21,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 PROF = os.path.join(REPO, "profiles")
-HOT = ("sk_resident_kernel", "sk_tiled_kernel", "sk_pass_kernel", "cost_split16_kernel", "split16_prep_kernel",
+HOT = ("sk_resident_kernel", "sk_tiled_kernel", "sk_pass_kernel", "cost_split16_kernel", "split16_prep2_kernel",
        "sk_init_kernel", "sk_plan_kernel")
 
 
