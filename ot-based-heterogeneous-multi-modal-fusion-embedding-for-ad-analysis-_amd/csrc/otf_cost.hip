@@ -301,6 +301,7 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
     constexpr int NI = NS == 3 ? 2 : 1;  // fp16 images per operand
     __shared__ __attribute__((aligned(16))) _Float16 As[NI][BM][SLD];  // [hi|lo][row][k]
     __shared__ __attribute__((aligned(16))) _Float16 Bs[NI][BN][SLD];
+    __shared__ float sxs[BM], sxx[BM];  // row scale / squared norm of this tile's rows
 
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
@@ -351,6 +352,22 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
         }
     };
 
+    // epilogue operands, fetched up front (their latency hides under the main loop):
+    // the tile's 128 row factors to LDS, this lane's 2 column factors to registers
+    if (tid < BM) {
+        const int gi = i0 + tid < n ? i0 + tid : n - 1;
+        sxs[tid] = xs[gi];
+        sxx[tid] = xx[gi];
+    }
+    float cys[2], cyy[2];
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) {
+        const int gj0 = j0 + wn * 64 + nj * 32 + (lane & 31);
+        const int gj = gj0 < m ? gj0 : m - 1;
+        cys[nj] = ys[gj];
+        cyy[nj] = yy[gj];
+    }
+
     const int nk = kpad / SBK;
     gload(0);
     for (int kt = 0; kt < nk; ++kt) {
@@ -398,8 +415,8 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
                 const int cl = wn * 64 + nj * 32 + (lane & 31);
                 const int gi = i0 + rl, gj = j0 + cl;
                 if (gi < n && gj < m) {
-                    const float dot = acc[mi][nj][e] * xs[gi] * ys[gj];
-                    float c = xx[gi] + yy[gj] - 2.f * dot;
+                    const float dot = acc[mi][nj][e] * sxs[rl] * cys[nj];
+                    float c = sxx[rl] + cyy[nj] - 2.f * dot;
                     c = c > 0.f ? c : 0.f;
                     if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
                     if (zero_diag && gi == gj) c = 0.f;
