@@ -65,12 +65,13 @@ enum {
     OTF_SK_CONVERGED = 1,
     OTF_SK_MAX_ITER = 2,
     OTF_SK_NUMERICAL_BREAK = 3,
-    OTF_SK_TIMEOUT = 4  /* resident solver: a device-wide barrier did not complete */
+    OTF_SK_TIMEOUT = 4  /* persistent engine: a device-wide barrier made no progress for
+                           5 s (grid not co-resident); outputs are invalid            */
 };
 
 /* Solver engines (otf_sinkhorn_opts.engine).
- * OTF_ENGINE_AUTO: resident when the problem fits the register files of the chip
- *   (one row block per CU), streaming otherwise.
+ * OTF_ENGINE_AUTO: tiled (float32) or resident when the problem fits the register
+ *   files of the chip (one tile / row block per CU), else sweep, else streaming.
  * OTF_ENGINE_STREAM: one launch per iteration, C re-read from HBM every iteration.
  * OTF_ENGINE_RESIDENT: one persistent launch for the whole solve; every workgroup
  *   keeps its rows of K = exp(-C/reg) in registers; iterations are separated by a
@@ -78,12 +79,18 @@ enum {
  * OTF_ENGINE_TILED: resident like OTF_ENGINE_RESIDENT, float32, but every workgroup
  *   keeps a 128-row x 512-column TILE of K; the row sums are combined within groups
  *   of column tiles, the column sums across the grid (8x fewer atomics).  AUTO picks
- *   it first when ceil(n/128) * ceil(m/512) <= #CUs.                              */
+ *   it first when ceil(n/128) * ceil(m/512) <= #CUs.
+ * OTF_ENGINE_SWEEP: one persistent launch for the whole solve that streams C from
+ *   HBM / the Infinity Cache once per iteration (costs too large for the register
+ *   files, e.g. N = 8192 fp16 or N = 16384 fp32); one workgroup per CU owns row
+ *   blocks, the column sums go through a 4-slot ring of per-iteration buffers and an
+ *   XCD-hierarchical barrier.  POT flavour, m <= 16384 (float) / 8192 (double).      */
 typedef enum {
     OTF_ENGINE_AUTO = 0,
     OTF_ENGINE_STREAM = 1,
     OTF_ENGINE_RESIDENT = 2,
-    OTF_ENGINE_TILED = 3
+    OTF_ENGINE_TILED = 3,
+    OTF_ENGINE_SWEEP = 4
 } otf_engine;
 
 typedef struct {
@@ -109,8 +116,8 @@ typedef struct {
     int32_t status;     /* OTF_SK_*                                                    */
     int32_t n_err;      /* number of entries written to the err log                    */
     int32_t break_iter; /* iteration of the numerical break, or -1                     */
-    int32_t engine;     /* engine that ran (OTF_ENGINE_STREAM / OTF_ENGINE_RESIDENT)     */
-    int32_t pad;
+    int32_t engine;     /* engine that ran (otf_engine)                                */
+    int32_t stalled;    /* persistent engines: 1 if any workgroup hit the stall timeout */
 } otf_sinkhorn_info;
 
 /* Library identification; returns a static string ("otfuse <ver> gfx950"). */

@@ -1,0 +1,168 @@
+// otf_persist.h — in-launch synchronisation for the persistent Sinkhorn engines
+// (resident, tiled, sweep): XCD-hierarchical grid barrier, write-through stores and
+// sc1 loads of the column sums, and the shared hand-off of per-iteration sum buffers.
+//
+// Hand-off form (MI355X microarch guide, inter-workgroup visibility, valid forms):
+// producers add with agent-scope float atomics (performed at the memory side) or store
+// write-through (sc1); every producing wave drains (s_waitcnt vmcnt(0)) before its
+// workgroup arrives on a counter; EVERY consumer load of the handed-off words is a
+// 16-B sc1 buffer load to registers (bypasses this CU's L1).  Every spin is bounded by
+// s_memrealtime (100 MHz): a barrier that makes no progress for `timeout_ticks` ends
+// the solve with OTF_SK_TIMEOUT instead of hanging.  The deadline is re-armed after
+// every completed barrier, so only a stall times out, never a long healthy solve.
+#pragma once
+#include "otf_device.h"
+
+namespace otf {
+
+struct SkSync {
+    int* reg;   // [8 * 64]  workgroups per XCD (registration, before the first barrier)
+    int* xcnt;  // [8 * 64]  arrivals per XCD
+    int* top;   // [64]      XCD arrivals
+    int* gen;   // [8 * 64]  published epoch per XCD
+};
+
+// hierarchical barrier words: reg[8], xcnt[8], top, gen[8], each on a 256-B line
+constexpr size_t kSyncBytes = 25 * 64 * sizeof(int);
+
+inline SkSync sync_words(int* base) {
+    SkSync s;
+    s.reg = base;
+    s.xcnt = base + 8 * 64;
+    s.top = base + 16 * 64;
+    s.gen = base + 17 * 64;
+    return s;
+}
+
+// 5 s of no progress at the 100 MHz s_memrealtime clock
+constexpr unsigned long long kStallTicks = 500000000ull;
+
+// XCD this wave runs on (0..7).  Only speed depends on it (replica choice, grouping).
+__device__ __forceinline__ int xcc_id() {
+    int v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+    return v;
+}
+
+template <typename T> __device__ __forceinline__ T load_agent(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T>
+__device__ __forceinline__ void store_wt(T* p, T v) {  // write-through (sc1) store
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sums_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ typename Vec<T>::type load_sum_vec(__amdgpu_buffer_rsrc_t rs,
+                                                              uint32_t byte_off) {
+    const auto raw = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16 /* sc1 */);
+    return __builtin_bit_cast(typename Vec<T>::type, raw);
+}
+
+// Device-wide flat barrier: every wave drains its own memory operations, one lane per
+// workgroup arrives on the counter and polls it.  Returns false on a stall (flag
+// broadcast via LDS); re-arms `deadline` on success.
+__device__ __forceinline__ bool grid_barrier(int* bar, int target, unsigned long long& deadline,
+                                             unsigned long long stall, int* s_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (load_agent(bar) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() > deadline) {
+                ok = 0;
+                break;
+            }
+        }
+        *s_flag = ok;
+    }
+    __syncthreads();
+    deadline = __builtin_amdgcn_s_memrealtime() + stall;
+    return *s_flag != 0;
+}
+
+// XCD-hierarchical grid barrier for epoch e >= 1 (all counters zeroed per call):
+// each workgroup arrives on its XCD's counter (~32 adders instead of 256 on one
+// word); the last arriver of an XCD (told by the value its add returned) arrives
+// on the top counter; the last of those publishes e to every XCD's generation
+// word, which only that XCD's workgroups poll.  Placement affects speed only: the
+// per-XCD populations are counted in the launch (sync.reg), not assumed.
+__device__ __forceinline__ bool xcd_barrier(const SkSync& sy, int xcd, int nx, int nact,
+                                            unsigned act_mask, int e,
+                                            unsigned long long& deadline,
+                                            unsigned long long stall, int* s_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        const int old = __hip_atomic_fetch_add(sy.xcnt + xcd * 64, 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        if (old == e * nx - 1) {
+            const int o2 = __hip_atomic_fetch_add(sy.top, 1, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            if (o2 == e * nact - 1) {
+                for (int x = 0; x < 8; ++x)
+                    if (act_mask & (1u << x))
+                        __hip_atomic_store(sy.gen + x * 64, e, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        while (__hip_atomic_load(sy.gen + xcd * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() > deadline) {
+                ok = 0;
+                break;
+            }
+        }
+        *s_flag = ok;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    deadline = __builtin_amdgcn_s_memrealtime() + stall;
+    return *s_flag != 0;
+}
+
+// Registration on the XCD population + the one flat barrier of a launch; returns
+// this XCD's population, the number of active XCDs and their mask in s_pop[0..2].
+__device__ __forceinline__ bool register_grid(const SkSync& sy, int* bar, int xcd,
+                                              unsigned long long& deadline,
+                                              unsigned long long stall, int* s_flag,
+                                              int* s_pop) {
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(sy.reg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool ok = grid_barrier(bar, gridDim.x, deadline, stall, s_flag);
+    if (threadIdx.x == 0) {
+        int nact = 0;
+        unsigned mask = 0;
+        for (int x = 0; x < 8; ++x) {
+            const int c = __hip_atomic_load(sy.reg + x * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c > 0) {
+                ++nact;
+                mask |= 1u << x;
+            }
+        }
+        s_pop[0] = __hip_atomic_load(sy.reg + xcd * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_pop[1] = nact;
+        s_pop[2] = (int)mask;
+    }
+    __syncthreads();
+    return ok;
+}
+
+// Sweep engine (otf_sweep.hip): persistent streaming solve for costs that do not fit
+// the register files.  Host entry points; `region` is zeroed by the launcher.
+template <typename T> size_t sweep_region_bytes(int64_t m_pad);
+template <typename T, typename CT> bool sweep_supported(int64_t n, int64_t m, int64_t ldc);
+template <typename T, typename CT>
+hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T* a_pad,
+                     const T* b_pad, const T* cost_scale, const otf_sinkhorn_opts& o, void* region,
+                     T* u_out, T* v_out, void* P_out, int64_t ldp, int P_dtype,
+                     otf_sinkhorn_info* info, double* errlog, hipStream_t s);
+
+}  // namespace otf

@@ -28,7 +28,7 @@
 // (read p-1, accumulate p, zero p+1) so a pass never races the zeroing.
 #include <stdlib.h>
 
-#include "otf_device.h"
+#include "otf_persist.h"
 
 namespace otf {
 namespace {
@@ -381,7 +381,7 @@ __global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, 
         info->n_err = 0;
         info->break_iter = -1;
         info->engine = OTF_ENGINE_STREAM;
-        info->pad = 0;
+        info->stalled = 0;
     }
 }
 
@@ -511,12 +511,6 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const CT* C, int64_t ldc, 
 // complete sets OTF_SK_TIMEOUT instead of hanging.  Co-residency of the grid
 // (<= one workgroup per CU) is checked before the launch (launch_resident_g).
 // ============================================================================
-struct SkSync {
-    int* reg;   // [8 * 64]  workgroups per XCD (registration, before the first barrier)
-    int* xcnt;  // [8 * 64]  arrivals per XCD
-    int* top;   // [64]      XCD arrivals
-    int* gen;   // [8 * 64]  published epoch per XCD
-};
 
 template <typename T> struct SkResArgs {
     const void* C;    // cost, element type CT
@@ -528,10 +522,10 @@ template <typename T> struct SkResArgs {
     double reg;
     int max_iter, check_every, err_squared;
     double stop_thr;
-    T* cs;            // (max_iter + 1) x nrep x m_pad column-sum buffers, zeroed before launch
+    T* cs;            // ring of 4 slots (slot k % 4 = K^T u(k-1)), nrep x m_pad each, zeroed
     SkSync sync;      // hierarchical barrier words, zeroed before launch
     int nrep;         // replicas per iteration (= the kernel's NREP)
-    int* bad_cnt;     // max_iter + 1 counters, zeroed
+    int* bad_cnt;     // ring of 4 counters (one 256-B line each), zeroed
     int* bar;         // barrier counter, zeroed
     otf_sinkhorn_info* info;
     double* errlog;
@@ -558,97 +552,6 @@ __device__ unsigned long long g_stamps[256 * 16 * 8];
     } while (0)
 #endif
 
-// XCD this wave runs on (0..7): selects the column-sum replica so that the ~32
-// workgroups of one XCD share a replica (32 adders per address instead of 256, and
-// the replica readers of one XCD hit the same L2 lines).  Only speed depends on it.
-__device__ __forceinline__ int xcc_id() {
-    int v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
-    return v;
-}
-
-template <typename T> __device__ __forceinline__ T load_agent(const T* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Column sums are handed off inside the launch: producers add with agent-scope
-// atomics (performed past L2, the line is dropped from the adder's L2), every adding
-// wave drains them (s_waitcnt vmcnt(0)) before its workgroup arrives on the barrier,
-// and EVERY consumer load of the sums is a 16-B sc1 buffer load to registers (bypasses
-// this CU's L1, which is never refreshed by other CUs' stores) -- the no-acquire form
-// of the hand-off (MI355X microarch guide, inter-workgroup visibility, valid forms).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sums_rsrc(const void* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
-}
-template <typename T>
-__device__ __forceinline__ typename Vec<T>::type load_sum_vec(__amdgpu_buffer_rsrc_t rs,
-                                                              uint32_t byte_off) {
-    const auto raw = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16 /* sc1 */);
-    return __builtin_bit_cast(typename Vec<T>::type, raw);
-}
-
-// Device-wide barrier: every wave drains its own memory operations (the atomics that
-// carry the payload are then performed at memory), one lane per workgroup arrives
-// on the counter and polls it.  Returns false on timeout (flag broadcast via LDS).
-__device__ __forceinline__ bool grid_barrier(int* bar, int target, unsigned long long deadline,
-                                             int* s_flag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int ok = 1;
-        __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (load_agent(bar) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() > deadline) {
-                ok = 0;
-                break;
-            }
-        }
-        *s_flag = ok;
-    }
-    __syncthreads();
-    return *s_flag != 0;
-}
-
-// XCD-hierarchical grid barrier for epoch e >= 1 (all counters zeroed per call):
-// each workgroup arrives on its XCD's counter (~32 adders instead of 256 on one
-// word); the last arriver of an XCD (told by the value its add returned) arrives
-// on the top counter; the last of those publishes e to every XCD's generation
-// word, which only that XCD's workgroups poll.  Placement affects speed only: the
-// per-XCD populations are counted in the launch (sync.reg), not assumed.
-__device__ __forceinline__ bool xcd_barrier(const SkSync& sy, int xcd, int nx, int nact,
-                                            unsigned act_mask, int e,
-                                            unsigned long long deadline, int* s_flag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int ok = 1;
-        const int old = __hip_atomic_fetch_add(sy.xcnt + xcd * 64, 1, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-        if (old == e * nx - 1) {
-            const int o2 = __hip_atomic_fetch_add(sy.top, 1, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-            if (o2 == e * nact - 1) {
-                for (int x = 0; x < 8; ++x)
-                    if (act_mask & (1u << x))
-                        __hip_atomic_store(sy.gen + x * 64, e, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        while (__hip_atomic_load(sy.gen + xcd * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() > deadline) {
-                ok = 0;
-                break;
-            }
-        }
-        *s_flag = ok;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __syncthreads();
-    return *s_flag != 0;
-}
-
 template <typename T, typename CT, typename TP, int G, int R, int NREP>
 __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     constexpr int VEC = Vec<T>::N;
@@ -665,7 +568,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     const int NT = blockDim.x;
     const int nwg = gridDim.x;
     const bool lead = (blockIdx.x == 0 && tid == 0);
-    const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
 
     const double unit = exp_unit<T>();
     double cinv = 1.0;
@@ -791,6 +694,16 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
         for (int j = tid; j < p.m; j += NT) atomicAdd(dst + j, colbuf[j]);
     };
 
+    // slot k % 4 is free once iteration k - 1 has started (S[k-4] was last read in
+    // iteration k - 3): this workgroup's share of it and its break counter, write-through
+    auto zero_slot = [&](int k) {
+        T* zs = p.cs + (size_t)(k & 3) * it_stride;
+        const int64_t per = ((int64_t)it_stride + nwg - 1) / nwg;
+        const int64_t z0 = (int64_t)blockIdx.x * per;
+        const int64_t z1 = z0 + per < (int64_t)it_stride ? z0 + per : (int64_t)it_stride;
+        for (int64_t j = z0 + tid; j < z1; j += NT) store_wt(zs + j, (T)0);
+        if (blockIdx.x == 0 && tid == 0) store_wt(p.bad_cnt + (k & 3) * 64, 0);
+    };
     // ---- prologue: K^T u0 into sums[0]
     {
         T w[R];
@@ -803,7 +716,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     // register on this XCD's population, then the one flat barrier of the launch
     if (tid == 0)
         __hip_atomic_fetch_add(p.sync.reg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!grid_barrier(p.bar, nwg, deadline, &s_flag)) {
+    if (!grid_barrier(p.bar, nwg, deadline, p.timeout_ticks, &s_flag)) {
         status = OTF_SK_TIMEOUT;
         done = true;
     }
@@ -827,11 +740,11 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
 
     for (int it = 0; it < p.max_iter && !done; ++it) {
         OTF_STAMP(it, 0);
-        const T* cs_it = p.cs + (size_t)it * it_stride;   // K^T u(it-1)
+        const T* cs_it = p.cs + (size_t)(it & 3) * it_stride;   // K^T u(it-1)
         T s[G][VEC], vn[G][VEC];
         int badv = 0;
         // the break flag of u(it-1) is loaded together with the sums (one round trip)
-        const int prev_bad = it >= 1 ? load_agent(p.bad_cnt + it - 1) : 0;
+        const int prev_bad = it >= 1 ? load_agent(p.bad_cnt + ((it - 1) & 3) * 64) : 0;
         load_sums(cs_it, s, (T)1);
 #pragma unroll
         for (int g = 0; g < G; ++g)
@@ -894,7 +807,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
             badu |= (rok && !finite_val(un[r])) ? 1 : 0;
             if (!rok) un[r] = 0;
         }
-        if (badu && tid == 0) atomicAdd(p.bad_cnt + it, 1);
+        if (badu && tid == 0) atomicAdd(p.bad_cnt + (it & 3) * 64, 1);
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -906,7 +819,8 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
                 if (tid == r) mine = un[r];
             uhist[it & 1][tid] = mine;
         }
-        flush(un, p.cs + (size_t)(it + 1) * it_stride);
+        flush(un, p.cs + (size_t)((it + 1) & 3) * it_stride);
+        zero_slot(it + 2);
         idxB = it;
         OTF_STAMP(it, 3);
 #ifdef OTF_STAMPS
@@ -914,7 +828,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
         __syncthreads();
         OTF_STAMP(it, 4);
 #endif
-        if (!xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 1, deadline, &s_flag)) {
+        if (!xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 1, deadline, p.timeout_ticks, &s_flag)) {
             status = OTF_SK_TIMEOUT;
             done = true;
         }
@@ -922,12 +836,12 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     }
     if (status == OTF_SK_MAX_ITER && p.max_iter > 0 && idxB == p.max_iter - 1) {
         const int it = p.max_iter - 1;
-        if (load_agent(p.bad_cnt + it) > 0) {
+        if (load_agent(p.bad_cnt + (it & 3) * 64) > 0) {
             last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
         } else {
             last_good = it; niter = it;
             if ((it % p.check_every) == 0) {
-                const T* cs_last = p.cs + (size_t)p.max_iter * it_stride;
+                const T* cs_last = p.cs + (size_t)(p.max_iter & 3) * it_stride;
                 T e = 0, sl[G][VEC];
                 load_sums(cs_last, sl, (T)0);
 #pragma unroll
@@ -1004,6 +918,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
             }
         }
     }
+    if (status == OTF_SK_TIMEOUT && threadIdx.x == 0) store_wt(&p.info->stalled, 1);
     if (lead) {
         p.info->last_good = last_good;
         p.info->niter = niter;
@@ -1057,9 +972,9 @@ template <typename T> struct SkTileArgs {
     double reg;
     int max_iter, check_every, err_squared;
     double stop_thr;
-    T* cs;            // (max_iter + 1) x nrep x m_pad column sums, zeroed before launch
+    T* cs;            // ring of 4 slots (slot k % 4 = K^T u(k-1)), nrep x m_pad each, zeroed
     int nrep;
-    int* bad_cnt;     // max_iter + 1 counters, zeroed
+    int* bad_cnt;     // ring of 4 counters (one 256-B line each), zeroed
     int* bar;         // flat barrier counter, zeroed
     SkSync sync;      // hierarchical barrier words, zeroed
     T* xch;           // 2 x nrb x ncb x tile rows row partials (write-through hand-off)
@@ -1074,10 +989,6 @@ template <typename T> struct SkTileArgs {
     unsigned long long timeout_ticks;
 };
 
-template <typename T>
-__device__ __forceinline__ void store_wt(T* p, T v) {  // write-through (sc1) store
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 template <typename T, typename CT, typename TP, int NREP>
 __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
@@ -1096,7 +1007,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nwg = gridDim.x;
     const bool lead = (blockIdx.x == 0 && tid == 0);
-    const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
 
     // tile of this workgroup; groups (row blocks) on one XCD when nrb % 8 == 0
     int rb, cb;
@@ -1184,8 +1095,8 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
     };
     // full-vector L2 marginal error of iterate `itp` (needs cs[itp + 1] and cs[itp])
     auto full_error = [&](int itp) -> double {
-        const uint32_t bs = (uint32_t)((size_t)(itp + 1) * it_stride * sizeof(T));
-        const uint32_t bp = (uint32_t)((size_t)itp * it_stride * sizeof(T));
+        const uint32_t bs = (uint32_t)((size_t)((itp + 1) & 3) * it_stride * sizeof(T));
+        const uint32_t bp = (uint32_t)((size_t)(itp & 3) * it_stride * sizeof(T));
         T e = 0;
         for (int c0 = tid * VEC; c0 < p.m_pad; c0 += blockDim.x * VEC) {
             V sc = load_sum_vec<T>(rs, bs + c0 * (uint32_t)sizeof(T));
@@ -1231,6 +1142,16 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
         }
     };
 
+    // slot k % 4 is free once iteration k - 1 has started (S[k-4] was last read in
+    // iteration k - 3): this workgroup's share of it and its break counter, write-through
+    auto zero_slot = [&](int k) {
+        T* zs = p.cs + (size_t)(k & 3) * it_stride;
+        const int64_t per = ((int64_t)it_stride + nwg - 1) / nwg;
+        const int64_t z0 = (int64_t)blockIdx.x * per;
+        const int64_t z1 = z0 + per < (int64_t)it_stride ? z0 + per : (int64_t)it_stride;
+        for (int64_t j = z0 + tid; j < z1; j += (int)blockDim.x) store_wt(zs + j, (T)0);
+        if (blockIdx.x == 0 && tid == 0) store_wt(p.bad_cnt + (k & 3) * 64, 0);
+    };
     // ---- prologue: K^T u0 into sums[0]
     {
         T wr[R];
@@ -1242,7 +1163,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
     bool done = false;
     if (tid == 0)
         __hip_atomic_fetch_add(p.sync.reg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!grid_barrier(p.bar, nwg, deadline, &s_flag)) {
+    if (!grid_barrier(p.bar, nwg, deadline, p.timeout_ticks, &s_flag)) {
         status = OTF_SK_TIMEOUT;
         done = true;
     }
@@ -1267,9 +1188,9 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
         OTF_STAMP(it, 0);
         // a numerical break in iteration it-1 (v or u, any tile) -> revert to it-2.  The
         // flag load is issued together with the sum loads (one memory round trip, not two).
-        const int prev_bad = it >= 1 ? load_agent(p.bad_cnt + it - 1) : 0;
+        const int prev_bad = it >= 1 ? load_agent(p.bad_cnt + ((it - 1) & 3) * 64) : 0;
         T s[G][VEC], vn[G][VEC];
-        load_sums(p.cs + (size_t)it * it_stride, s, (T)1);
+        load_sums(p.cs + (size_t)(it & 3) * it_stride, s, (T)1);
         if (prev_bad > 0) {
             last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
             break;
@@ -1295,7 +1216,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
                 break;
             }
         }
-        if (__any(badv) && lane == 0) atomicAdd(p.bad_cnt + it, 1);
+        if (__any(badv) && lane == 0) atomicAdd(p.bad_cnt + (it & 3) * 64, 1);
         OTF_STAMP(it, 1);
         // row partials over this tile's columns, wave totals, publish to the group
         T rp[R];
@@ -1334,6 +1255,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
             }
             __syncthreads();
             if (!s_flag) { status = OTF_SK_TIMEOUT; done = true; break; }
+            deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
             OTF_STAMP(it, 2);
             // gather the ncb partials of this wave's rows (fixed order)
             const int rr = lane & (R - 1);
@@ -1359,7 +1281,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
             un[r] = urow[w][r];
             badu |= (row0 + r < p.n && !finite_val(un[r])) ? 1 : 0;
         }
-        if (badu && lane == 0) atomicAdd(p.bad_cnt + it, 1);
+        if (badu && lane == 0) atomicAdd(p.bad_cnt + (it & 3) * 64, 1);
         if (w == 0) {
 #pragma unroll
             for (int g = 0; g < G; ++g) {
@@ -1370,13 +1292,14 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
             }
         }
         OTF_STAMP(it, 3);
-        flush(un, p.cs + (size_t)(it + 1) * it_stride);
+        flush(un, p.cs + (size_t)((it + 1) & 3) * it_stride);
+        zero_slot(it + 2);
 #ifdef OTF_STAMPS
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         OTF_STAMP(it, 4);
 #endif
-        if (!xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 1, deadline, &s_flag)) {
+        if (!xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 1, deadline, p.timeout_ticks, &s_flag)) {
             status = OTF_SK_TIMEOUT;
             done = true;
         }
@@ -1384,7 +1307,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
     }
     if (status == OTF_SK_MAX_ITER && p.max_iter > 0) {
         const int it = p.max_iter - 1;
-        if (load_agent(p.bad_cnt + it) > 0) {
+        if (load_agent(p.bad_cnt + (it & 3) * 64) > 0) {
             last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
         } else {
             last_good = it; niter = it;
@@ -1444,6 +1367,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
             }
         }
     }
+    if (status == OTF_SK_TIMEOUT && threadIdx.x == 0) store_wt(&p.info->stalled, 1);
     if (lead) {
         p.info->last_good = last_good;
         p.info->niter = niter;
@@ -1510,8 +1434,10 @@ struct Workspace {
     int64_t cs_stride;  // m_pad + 64: the break-count slot and alignment
     int* cmin_key;
     double* errlog;
-    void* res;        // resident engine: sums (max_iter+1) x m_pad | bad_cnt | barrier
+    void* res;        // resident / tiled engines: 4-slot sums ring | bad_cnt ring | barrier
     size_t res_bytes;
+    void* sweep;      // sweep engine region (otf_sweep.hip)
+    size_t sweep_bytes;
     int nrep;
     size_t bytes;
     int64_t m_pad;
@@ -1524,8 +1450,6 @@ size_t tiled_xch_bytes(int64_t nrb, int64_t ncb, size_t esz) {
     return align_up(2 * (size_t)nrb * ncb * tile_rows(esz) * esz, 256);
 }
 
-// hierarchical barrier words: reg[8], xcnt[8], top, gen[8], each on a 256-B line
-constexpr size_t kSyncBytes = 25 * 64 * sizeof(int);
 
 // Column-sum replicas of the resident engine (grids of >= 128 row blocks; workgroups
 // add into replica xcc_id % NREP, readers load all NREP replicas at once).  A
@@ -1534,6 +1458,10 @@ constexpr size_t kSyncBytes = 25 * 64 * sizeof(int);
 #define OTF_RES_NREP 4
 #endif
 int res_replicas(int64_t nrb) { return nrb >= 128 ? OTF_RES_NREP : 1; }
+
+// Largest grid the resident / tiled engines are sized for (one workgroup per CU; the
+// workspace size is a function of the shape only, so it cannot ask the device).
+constexpr int64_t kMaxResidentWG = 1024;
 
 Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int64_t nrb) {
     Workspace w{};
@@ -1553,14 +1481,18 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.cmin_key = (int*)take(sizeof(int) * (size_t)w.m_pad);
     w.errlog = (double*)take(sizeof(double) * (size_t)(max_iter + 2));
     w.nrep = res_replicas(nrb);
-    w.res_bytes = align_up((size_t)(max_iter + 1) * w.nrep * w.m_pad * esz, 256) +
-                  align_up(sizeof(int) * (size_t)(max_iter + 1), 256) + 256 + kSyncBytes;
-    // tiled engine: row-partial exchange (2 slots x nrb x ncb x tile rows) + group counters
+    // per-iteration sums live in a ring of 4 slots: O(m) whatever max_iter is
+    w.res_bytes = align_up(4 * (size_t)w.nrep * w.m_pad * esz, 256) + 4 * 256 + 256 + kSyncBytes;
+    // tiled engine: row-partial exchange (2 slots x nrb x ncb x tile rows) + group counters,
+    // only for shapes whose tiles can all be resident (<= kMaxResidentWG)
     w.t_nrb = (n + tile_rows(esz) - 1) / tile_rows(esz);
     w.t_ncb = (m + TL_C - 1) / TL_C;
     w.t_xch_off = w.res_bytes;
-    w.res_bytes += tiled_xch_bytes(w.t_nrb, w.t_ncb, esz) + (size_t)w.t_nrb * 256;
+    if (w.t_nrb * w.t_ncb <= kMaxResidentWG)
+        w.res_bytes += tiled_xch_bytes(w.t_nrb, w.t_ncb, esz) + (size_t)w.t_nrb * 256;
     w.res = take(w.res_bytes);
+    w.sweep_bytes = esz == 8 ? sweep_region_bytes<double>(w.m_pad) : sweep_region_bytes<float>(w.m_pad);
+    w.sweep = take(w.sweep_bytes);
     w.bytes = off;
     return w;
 }
@@ -1615,14 +1547,9 @@ hipError_t run_resident(const PassCfg& cfg, int grid, const CT* C, int64_t ldc, 
     p.stop_thr = o.stop_thr;
     p.cs = (T*)w.res;
     p.nrep = w.nrep;
-    p.bad_cnt = (int*)((char*)w.res +
-                       align_up((size_t)(o.max_iter + 1) * w.nrep * w.m_pad * sizeof(T), 256));
-    p.bar = (int*)((char*)p.bad_cnt + align_up(sizeof(int) * (size_t)(o.max_iter + 1), 256));
-    int* sw = (int*)((char*)p.bar + 256);
-    p.sync.reg = sw;
-    p.sync.xcnt = sw + 8 * 64;
-    p.sync.top = sw + 16 * 64;
-    p.sync.gen = sw + 17 * 64;
+    p.bad_cnt = (int*)((char*)w.res + align_up(4 * (size_t)w.nrep * w.m_pad * sizeof(T), 256));
+    p.bar = (int*)((char*)p.bad_cnt + 4 * 256);
+    p.sync = sync_words((int*)((char*)p.bar + 256));
     p.info = info;
     p.errlog = errlog;
     p.u_out = u_out;
@@ -1630,7 +1557,7 @@ hipError_t run_resident(const PassCfg& cfg, int grid, const CT* C, int64_t ldc, 
     p.P = P_out;
     p.ldp = ldp;
     p.p_f64 = P_dtype == OTF_F64;
-    p.timeout_ticks = 500000000ull;  // 5 s at the 100 MHz s_memrealtime clock
+    p.timeout_ticks = kStallTicks;
     hipError_t e = hipMemsetAsync(w.res, 0, w.res_bytes, s);
     if (e != hipSuccess) return e;
     if (P_out && P_dtype == OTF_F64) return launch_resident<T, CT, double>(cfg, grid, p, s);
@@ -1681,14 +1608,9 @@ hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const T* cost_scale
     p.stop_thr = o.stop_thr;
     p.cs = (T*)w.res;
     p.nrep = nrep;
-    p.bad_cnt = (int*)((char*)w.res +
-                       align_up((size_t)(o.max_iter + 1) * w.nrep * w.m_pad * sizeof(T), 256));
-    p.bar = (int*)((char*)p.bad_cnt + align_up(sizeof(int) * (size_t)(o.max_iter + 1), 256));
-    int* sw = (int*)((char*)p.bar + 256);
-    p.sync.reg = sw;
-    p.sync.xcnt = sw + 8 * 64;
-    p.sync.top = sw + 16 * 64;
-    p.sync.gen = sw + 17 * 64;
+    p.bad_cnt = (int*)((char*)w.res + align_up(4 * (size_t)w.nrep * w.m_pad * sizeof(T), 256));
+    p.bar = (int*)((char*)p.bad_cnt + 4 * 256);
+    p.sync = sync_words((int*)((char*)p.bar + 256));
     p.xch = (T*)((char*)w.res + w.t_xch_off);
     p.grp = (int*)((char*)p.xch + tiled_xch_bytes(w.t_nrb, w.t_ncb, sizeof(T)));
     p.nrb = (int)w.t_nrb;
@@ -1699,7 +1621,7 @@ hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const T* cost_scale
     p.v_out = v_out;
     p.P = P_out;
     p.ldp = ldp;
-    p.timeout_ticks = 500000000ull;
+    p.timeout_ticks = kStallTicks;
     hipError_t e = hipMemsetAsync(w.res, 0, w.res_bytes, s);
     if (e != hipSuccess) return e;
     const int grid = (int)(w.t_nrb * w.t_ncb);
@@ -1838,7 +1760,8 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     const bool whole = o.n_total <= 0 || o.n_total == n;
     const bool fits = su.nrb <= device_cu_count() && su.cfg.G <= 4 && whole;
     // tiled engine: every (128 x 512 float / 64 x 512 double) tile on its own CU
-    const bool tfits = whole && su.w.t_nrb * su.w.t_ncb <= device_cu_count();
+    const bool tfits = whole && su.w.t_nrb * su.w.t_ncb <= device_cu_count() &&
+                       su.w.t_nrb * su.w.t_ncb <= kMaxResidentWG;
     // AUTO takes it for float only: for float64 (64-row tiles) it measured no faster
     // than the row-block resident engine (config 2, d = 512: 12.8 vs 12.3 ms per step --
     // both sit on the ~5 us grid-sync round trip per iteration); TILED forces it
@@ -1867,7 +1790,20 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         if (e == hipSuccess) return OTF_OK;
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_RESIDENT) return check_hip(e);
-        // co-residency refused (e.g. a smaller device): fall back to streaming
+        // co-residency refused (e.g. a smaller device): fall back to the sweep engine
+    }
+    // sweep engine: one persistent launch that streams C once per iteration (costs
+    // that do not fit the register files; POT flavour, whole problems)
+    const bool sfits = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 &&
+                       sweep_supported<T, CT>(n, m, ldc);
+    if (o.engine == OTF_ENGINE_SWEEP && !sfits) return OTF_EUNSUPPORTED;
+    if (sfits && (o.engine == OTF_ENGINE_SWEEP || o.engine == OTF_ENGINE_AUTO)) {
+        const hipError_t e = run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
+                                              (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
+                                              v_out, P_out, ldp, P_dtype, info, errlog, s);
+        if (e == hipSuccess) return OTF_OK;
+        (void)hipGetLastError();
+        if (o.engine == OTF_ENGINE_SWEEP) return check_hip(e);
     }
     if (LOG) {
         dim3 g((unsigned)((m + 255) / 256), (unsigned)(n < 64 ? n : 64));

@@ -1,0 +1,672 @@
+// otf_sweep.hip — persistent streaming Sinkhorn (OTF_ENGINE_SWEEP), POT flavour.
+//
+// Replaces ot.sinkhorn (POT 0.9.6 sinkhorn_knopp) at MRI_PET_OT_nojax.py:143 /
+// perturbot/perturbot/match/utils.py:6-115 for costs too large to stay in the register
+// files of the chip (BASELINE config 5: N = 8192 fp16, and past the Infinity Cache:
+// N = 16384 fp32).  The whole solve is ONE launch; every iteration streams the
+// materialised cost once.
+//
+// Grid: one 512-thread workgroup per CU.  Workgroup w owns row blocks w, w + grid, ...
+// (R rows x all m columns); thread t owns G chunks of 16 bytes of every row (columns
+// (t + 512 g) * VEC .. + VEC, coalesced 16-B loads).  Per iteration it:
+//   1. reads K^T u(it-1) (the column sums of the previous sweep: NREP replicas of a
+//      ring slot, 16-B sc1 loads) and forms v(it) = b / (K^T u) for its columns, taking
+//      POT's decisions exactly like the resident engines (every workgroup derives the
+//      same decision from the same sums, in a fixed reduction order);
+//   2. sweeps its row blocks, the next block's cost rows in flight (two register
+//      buffers, ping-pong) while the current one is reduced: e = exp(-C/reg) once per
+//      element, row sums K v (wave butterfly + one LDS exchange per block, fixed order)
+//      -> u = 1 / (K/a v) for those rows, then the column partials K^T u with the new u
+//      in registers;
+//   3. adds its m column partials into the next ring slot (memory-side float atomics,
+//      staged through LDS so every wave-instruction covers 256 contiguous bytes; the
+//      slot's replica is picked by the XCD), zeroes its share of the slot after next
+//      (write-through), and meets the grid at the XCD-hierarchical barrier.
+// The first block of the next sweep is put in flight before the barrier, so the
+// barrier and the atomic drain overlap the stream.  The plan is written at the end
+// from the last good (u, v) by a final sweep.
+//
+// Ring of 4 sum slots S[k] = K^T u(k-1) (slot k % 4): iteration it reads S[it] and, on
+// check iterations, S[it-1]; accumulates S[it+1]; zeroes slot (it+2) % 4 (= S[it-2],
+// last read in iteration it-1).  Exits keep S[it-2..it] intact, so the outputs can be
+// recomputed bit-identically from v(k) = b / S[k].  Memory is O(m), not O(max_iter m).
+#include "otf_persist.h"
+
+namespace otf {
+namespace {
+
+constexpr int kSwNT = 512;        // threads per workgroup (8 waves, one workgroup per CU)
+constexpr int kSwRowMax = 1024;   // rows per workgroup kept in the LDS u history
+
+template <typename T> struct SkSweepArgs {
+    const void* C;
+    int64_t ldc;
+    int n, m, m_pad;
+    const T* a;
+    const T* b;
+    const T* cost_scale;
+    double reg;
+    int max_iter, check_every, err_squared;
+    double stop_thr;
+    T* ring;            // 4 slots x slot_stride
+    int64_t slot_stride;
+    int* bad;           // 4 counters of non-finite u rows, one 256-B line each
+    int* bar;
+    SkSync sync;
+    otf_sinkhorn_info* info;
+    double* errlog;
+    T* u_out;
+    T* v_out;
+    void* P;
+    int64_t ldp;
+    unsigned long long stall_ticks;
+};
+
+using Raw = __attribute__((ext_vector_type(4))) unsigned int;  // 16 B of cost
+
+template <typename CT> struct RawN {
+    static constexpr int N = 16 / sizeof(CT);
+};
+
+// 16 B of cost -> compute type
+template <typename T, typename CT>
+__device__ __forceinline__ void widen(const Raw& r, T (&out)[RawN<CT>::N]) {
+    if constexpr (sizeof(CT) == 2) {
+        using H = __attribute__((ext_vector_type(8))) _Float16;
+        const H h = __builtin_bit_cast(H, r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) out[k] = (T)h[k];
+    } else if constexpr (sizeof(CT) == 4) {
+        using F = __attribute__((ext_vector_type(4))) float;
+        const F f = __builtin_bit_cast(F, r);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[k] = (T)f[k];
+    } else {
+        using D = __attribute__((ext_vector_type(2))) double;
+        const D d = __builtin_bit_cast(D, r);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) out[k] = (T)d[k];
+    }
+}
+
+// value of lane r (uniform result)
+__device__ __forceinline__ float bcast_lane(float x, int r) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), r));
+}
+__device__ __forceinline__ double bcast_lane(double x, int r) {
+    const long long b = __builtin_bit_cast(long long, x);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), r);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), r);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+template <typename T, typename CT, typename TP, int G, int R, int NREP>
+__global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
+    constexpr int VC = RawN<CT>::N;            // cost elements per 16-B chunk
+    constexpr int VT = Vec<T>::N;              // compute elements per 16-B sum load
+    constexpr int NW = kSwNT / kWave;
+    static_assert((VC % VT) == 0, "chunk covers whole sum vectors");
+    using V = typename Vec<T>::type;
+    extern __shared__ __attribute__((aligned(16))) unsigned char sw_lds[];
+    // vbuf: v of this iteration for the thread's own columns (only the owning thread
+    // reads it back), then reused to stage the column partials for the atomics
+    T* vbuf = reinterpret_cast<T*>(sw_lds);                         // m_pad
+    T* uhist = vbuf + p.m_pad;                                       // [2][kSwRowMax]
+    T* ialds = uhist + 2 * kSwRowMax;                                // 1 / a of own rows
+    __shared__ T red[2][NW][R];
+    __shared__ T ered[17];
+    __shared__ int s_flag;
+    __shared__ int s_pop[3];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nwg = gridDim.x;
+    const bool lead = (blockIdx.x == 0 && tid == 0);
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.stall_ticks;
+
+    const double unit = exp_unit<T>();
+    double cinv = 1.0;
+    if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
+    const T ks = (T)(-unit / p.reg * cinv);
+
+    // ---- column ownership: chunk g starts at column (tid + 512 g) * VC; cnt[g] of its
+    // VC columns are inside the problem (loads of chunks past m are clamped to 0)
+    int colc[G], cnt[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int c0 = (tid + kSwNT * g) * VC;
+        colc[g] = c0 < p.m ? c0 : 0;
+        const int left = p.m - c0;
+        cnt[g] = left <= 0 ? 0 : (left < VC ? left : VC);
+    }
+    // a chunk that straddles column m: its bytes past m (row padding, any value) are
+    // zeroed on load, so every e is finite; v = 0 there keeps them out of the row sums
+    // and their column partials are never flushed.  A chunk wholly past m re-reads
+    // column 0 (finite) with weight 0.  Rows past n read as 0 (buffer bounds) and get
+    // u = 0.
+    const bool ragged = (p.m % VC) != 0;
+    Raw keep = {~0u, ~0u, ~0u, ~0u};
+    int gk = -1;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+        if (cnt[g] > 0 && cnt[g] < VC) {
+            gk = g;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                // dword q holds elements [q * 4 / sizeof(CT), (q + 1) * 4 / sizeof(CT))
+                unsigned msk = 0;
+                constexpr int per = sizeof(CT) >= 4 ? 1 : 4 / (int)sizeof(CT);
+                for (int s = 0; s < per; ++s) {
+                    const int el = sizeof(CT) == 8 ? q / 2 : q * per + s;
+                    if (el < cnt[g]) msk |= sizeof(CT) >= 4 ? ~0u : (0xffffu << (16 * s));
+                }
+                keep[q] = msk;
+            }
+        }
+    const int nrb = (p.n + R - 1) / R;
+    const int my_nb = nrb > (int)blockIdx.x ? (nrb - 1 - (int)blockIdx.x) / nwg + 1 : 0;
+    const int64_t ld_bytes = p.ldc * (int64_t)sizeof(CT);
+    for (int i = tid; i < my_nb * R; i += kSwNT) {
+        const int row = ((int)blockIdx.x + (i / R) * nwg) * R + i % R;
+        ialds[i] = (T)1 / p.a[row < p.n ? row : 0];
+    }
+
+    // R cost rows of block bi via one SGPR descriptor (rows past n read as 0)
+    auto load_block = [&](int bi, Raw (&buf)[R][G]) {
+        const int r0 = ((int)blockIdx.x + bi * nwg) * R;
+        const int nrow = p.n - r0 < R ? p.n - r0 : R;
+        const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)((const char*)p.C + (int64_t)r0 * ld_bytes), 0, (int)(nrow * ld_bytes), 0x00020000);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                buf[r][g] = __builtin_amdgcn_raw_buffer_load_b128(
+                    cr, (uint32_t)(colc[g] * (int)sizeof(CT)), (uint32_t)(r * ld_bytes), 0);
+    };
+    auto sanitize = [&](Raw (&buf)[R][G]) {
+        if (ragged) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (g == gk) buf[r][g] &= keep;
+        }
+    };
+
+    const __amdgpu_buffer_rsrc_t rs = sums_rsrc(p.ring);
+    // sums of slot k for chunk g (VC columns): all replicas summed in a fixed order
+    auto load_sums_chunk = [&](int k, int g, T (&out)[VC]) {
+        const uint32_t boff = (uint32_t)((size_t)(k & 3) * p.slot_stride * sizeof(T));
+        V acc[VC / VT];
+#pragma unroll
+        for (int h = 0; h < VC / VT; ++h)
+            acc[h] = load_sum_vec<T>(rs, boff + (uint32_t)((colc[g] + h * VT) * sizeof(T)));
+#pragma unroll
+        for (int q = 1; q < NREP; ++q)
+#pragma unroll
+            for (int h = 0; h < VC / VT; ++h) {
+                const V t = load_sum_vec<T>(
+                    rs, boff + (uint32_t)(((size_t)q * p.m_pad + colc[g] + h * VT) * sizeof(T)));
+#pragma unroll
+                for (int k2 = 0; k2 < VT; ++k2) acc[h][k2] += t[k2];
+            }
+#pragma unroll
+        for (int k2 = 0; k2 < VC; ++k2) out[k2] = acc[k2 / VT][k2 % VT];
+    };
+    auto load_b_chunk = [&](int g, T (&bv)[VC]) {
+#pragma unroll
+        for (int h = 0; h < VC / VT; ++h) {
+            const V t = *reinterpret_cast<const V*>(p.b + colc[g] + h * VT);
+#pragma unroll
+            for (int k2 = 0; k2 < VT; ++k2) bv[h * VT + k2] = t[k2];
+        }
+    };
+    // L2 marginal error of iterate k: v(k) = b / S[k] against S[k+1] (all workgroups
+    // compute the same value: same data, same fixed-order block reduction)
+    auto marginal_err = [&](int k) -> double {
+        T e = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            T sk[VC], sk1[VC], bv[VC];
+            load_sums_chunk(k, g, sk);
+            load_sums_chunk(k + 1, g, sk1);
+            load_b_chunk(g, bv);
+#pragma unroll
+            for (int k2 = 0; k2 < VC; ++k2) {
+                const bool ok = k2 < cnt[g];
+                const T vb = bv[k2] / (ok ? sk[k2] : (T)1);
+                const T rr = vb * sk1[k2] - bv[k2];
+                e += ok ? rr * rr : (T)0;
+            }
+        }
+        e = block_sum<T>(e, ered);
+        return p.err_squared ? (double)e : sqrt((double)e);
+    };
+
+    const T u0 = (T)1 / (T)p.n;
+    const int xcd = xcc_id();
+    const int my_rep = xcd % NREP;
+    Raw bufA[R][G], bufB[R][G];
+    T colacc[G][VC];
+
+    // One sweep over this workgroup's row blocks.  it = -1: the prologue (u = u0, no
+    // row sums).  bufA holds block 0's cost on entry (already in flight).
+    int badu = 0;
+    auto sweep = [&](int it) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VC; ++k) colacc[g][k] = 0;
+        auto process = [&](int bi, Raw (&buf)[R][G]) {
+            const int r0 = ((int)blockIdx.x + bi * nwg) * R;
+            const int nrow = p.n - r0 < R ? p.n - r0 : R;
+            sanitize(buf);
+            T e[R][G][VC];
+            T rp[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) rp[r] = 0;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                T vv[VC];
+                if (it >= 0) {
+                    // a chunk past m re-reads column 0's cost: weight it 0
+                    const bool live = cnt[g] > 0;
+#pragma unroll
+                    for (int h = 0; h < VC / VT; ++h) {
+                        const V t = *reinterpret_cast<const V*>(vbuf + colc[g] + h * VT);
+#pragma unroll
+                        for (int k2 = 0; k2 < VT; ++k2) vv[h * VT + k2] = live ? t[k2] : (T)0;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    T c[VC];
+                    widen<T, CT>(buf[r][g], c);
+#pragma unroll
+                    for (int k = 0; k < VC; ++k) {
+                        e[r][g][k] = fast_exp(c[k] * ks);
+                        if (it >= 0) rp[r] += e[r][g][k] * vv[k];
+                    }
+                }
+            }
+            T u[R];
+            if (it >= 0) {
+                // wave totals -> LDS; every wave then finishes the R row sums on lanes
+                // 0..R-1 (same fixed order everywhere) and broadcasts u by readlane
+                wave_sum_multi<T, R>(rp, lane);
+                const int par = bi & 1;
+                if (lane < R) red[par][w][butterfly_row<R>(lane)] = rp[0];
+                __syncthreads();
+                const int rr = lane < R ? lane : 0;
+                T s = red[par][0][rr];
+#pragma unroll
+                for (int ww = 1; ww < NW; ++ww) s += red[par][ww][rr];
+                const T un = (T)1 / (s * ialds[bi * R + rr]);  // POT: u = 1 / (K/a v)
+                const bool rok = rr < nrow;
+                badu |= (lane < R && rok && !finite_val(un)) ? 1 : 0;
+                const T um = rok ? un : (T)0;
+                if (w == 0 && lane < R) uhist[(it & 1) * kSwRowMax + bi * R + lane] = um;
+#pragma unroll
+                for (int r = 0; r < R; ++r) u[r] = bcast_lane(um, r);
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) u[r] = r < nrow ? u0 : (T)0;
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VC; ++k) {
+                    T acc = colacc[g][k];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) acc += e[r][g][k] * u[r];
+                    colacc[g][k] = acc;
+                }
+        };
+        for (int bi = 0; bi < my_nb; bi += 2) {
+            if (bi + 1 < my_nb) load_block(bi + 1, bufB);
+            process(bi, bufA);
+            // the next sweep starts at block 0 again: keep the stream going
+            load_block(bi + 2 < my_nb ? bi + 2 : 0, bufA);
+            if (bi + 1 < my_nb) process(bi + 1, bufB);
+        }
+    };
+
+    // flush the column partials into slot k (replica my_rep), zero slot k + 1's share
+    auto flush = [&](int k) {
+        __syncthreads();  // every thread is done with vbuf (v) before it stages partials
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int c0 = (tid + kSwNT * g) * VC;
+            if (c0 < p.m_pad) {
+#pragma unroll
+                for (int h = 0; h < VC / VT; ++h) {
+                    V wv;
+#pragma unroll
+                    for (int k2 = 0; k2 < VT; ++k2) wv[k2] = colacc[g][h * VT + k2];
+                    *reinterpret_cast<V*>(vbuf + c0 + h * VT) = wv;
+                }
+            }
+        }
+        __syncthreads();
+        T* dst = p.ring + (size_t)(k & 3) * p.slot_stride + (size_t)my_rep * p.m_pad;
+        for (int j = tid; j < p.m; j += kSwNT) atomicAdd(dst + j, vbuf[j]);
+        // slot k + 1 (= S[k - 3]) is free: this workgroup's share of it, write-through
+        T* zs = p.ring + (size_t)((k + 1) & 3) * p.slot_stride;
+        const int64_t per = (p.slot_stride + nwg - 1) / nwg;
+        const int64_t z0 = (int64_t)blockIdx.x * per;
+        const int64_t z1 = z0 + per < p.slot_stride ? z0 + per : p.slot_stride;
+        for (int64_t j = z0 + tid; j < z1; j += kSwNT) store_wt(zs + j, (T)0);
+        if (tid == 0) {
+            if (blockIdx.x == 0) store_wt(p.bad + ((k + 1) & 3) * 64, 0);
+            if (badu) atomicAdd(p.bad + ((k - 1) & 3) * 64, 1);  // u(k-1) not finite
+        }
+        badu = 0;
+    };
+
+    // ---- prologue: S[0] = K^T u0
+    if (my_nb > 0) load_block(0, bufA);
+    sweep(-1);
+    flush(0);
+    int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
+    bool done = false, ran_all = false;
+    if (!register_grid(p.sync, p.bar, xcd, deadline, p.stall_ticks, &s_flag, s_pop)) {
+        status = OTF_SK_TIMEOUT;
+        done = true;
+    }
+    const int nx = s_pop[0], nact = s_pop[1];
+    const unsigned act_mask = (unsigned)s_pop[2];
+
+    for (int it = 0; it < p.max_iter && !done; ++it) {
+        const int prev_bad = it >= 1 ? load_agent(p.bad + ((it - 1) & 3) * 64) : 0;
+        int badv = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            T s[VC], bv[VC];
+            load_sums_chunk(it, g, s);
+            load_b_chunk(g, bv);
+            T vv[VC];
+#pragma unroll
+            for (int k = 0; k < VC; ++k) {
+                const bool ok = k < cnt[g];
+                const T val = bv[k] / (ok ? s[k] : (T)1);
+                badv |= (ok && ((s[k] == (T)0) || !finite_val(val))) ? 1 : 0;
+                vv[k] = ok ? val : (T)0;
+            }
+            const int c0 = (tid + kSwNT * g) * VC;
+            if (c0 < p.m_pad) {
+#pragma unroll
+                for (int h = 0; h < VC / VT; ++h) {
+                    V wv;
+#pragma unroll
+                    for (int k2 = 0; k2 < VT; ++k2) wv[k2] = vv[h * VT + k2];
+                    *reinterpret_cast<V*>(vbuf + c0 + h * VT) = wv;
+                }
+            }
+        }
+        if (prev_bad > 0) {  // u(it-1) not finite: revert to it-2
+            last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
+            break;
+        }
+        if (it >= 1 && ((it - 1) % p.check_every) == 0) {
+            const double err = marginal_err(it - 1);
+            if (lead) p.errlog[(it - 1) / p.check_every] = err;
+            n_err = (it - 1) / p.check_every + 1;
+            if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) {
+                last_good = it - 1; niter = it - 1; status = OTF_SK_CONVERGED;
+                break;
+            }
+        }
+        badv = __syncthreads_or(badv);
+        if (badv) {  // zero in K^T u or non-finite v: revert to it-1
+            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
+            break;
+        }
+        sweep(it);
+        flush(it + 1);
+        if (!xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 1, deadline, p.stall_ticks, &s_flag)) {
+            status = OTF_SK_TIMEOUT;
+            done = true;
+        }
+        if (it == p.max_iter - 1 && !done) ran_all = true;
+    }
+    if (status == OTF_SK_MAX_ITER && ran_all) {
+        const int it = p.max_iter - 1;
+        if (load_agent(p.bad + (it & 3) * 64) > 0) {
+            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
+        } else {
+            last_good = it; niter = it;
+            if ((it % p.check_every) == 0) {
+                const double err = marginal_err(it);
+                if (lead) p.errlog[it / p.check_every] = err;
+                n_err = it / p.check_every + 1;
+                if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) status = OTF_SK_CONVERGED;
+            }
+        }
+    }
+
+    // ---- outputs: (u, v) of last_good, then the plan by one more sweep
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const T v0 = (T)1 / (T)p.m;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        T vo[VC];
+        if (last_good >= 0) {
+            T sl[VC], bv[VC];
+            load_sums_chunk(last_good, g, sl);
+            load_b_chunk(g, bv);
+#pragma unroll
+            for (int k = 0; k < VC; ++k) vo[k] = k < cnt[g] ? bv[k] / sl[k] : (T)0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < VC; ++k) vo[k] = v0;
+        }
+#pragma unroll
+        for (int k = 0; k < VC; ++k) colacc[g][k] = vo[k];  // v(last_good) from here on
+        if (blockIdx.x == 0) {
+#pragma unroll
+            for (int k = 0; k < VC; ++k)
+                if (k < cnt[g]) p.v_out[colc[g] + k] = vo[k];
+        }
+    }
+    const T* uh = uhist + (last_good & 1) * kSwRowMax;
+    for (int bi = 0; bi < my_nb; ++bi) {
+        const int r0 = ((int)blockIdx.x + bi * nwg) * R;
+        if (tid < R && r0 + tid < p.n) p.u_out[r0 + tid] = last_good >= 0 ? uh[bi * R + tid] : u0;
+    }
+    if (p.P) {
+        TP* P = (TP*)p.P;
+        constexpr int VP = Vec<T>::N;
+        using PV = __attribute__((ext_vector_type(VP))) TP;
+        for (int bi = 0; bi < my_nb; ++bi) {
+            const int r0 = ((int)blockIdx.x + bi * nwg) * R;
+            load_block(bi, bufA);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (r0 + r >= p.n) break;
+                const T ur = last_good >= 0 ? uh[bi * R + r] : u0;
+                TP* prow = P + (int64_t)(r0 + r) * p.ldp;
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    if (cnt[g] == 0) continue;
+                    const int c0 = colc[g];
+                    T c[VC];
+                    widen<T, CT>(bufA[r][g], c);
+                    TP o[VC];
+#pragma unroll
+                    for (int k = 0; k < VC; ++k) o[k] = (TP)(ur * fast_exp(c[k] * ks) * colacc[g][k]);
+                    if (cnt[g] == VC) {
+#pragma unroll
+                        for (int h = 0; h < VC / VP; ++h) {
+                            PV pv;
+#pragma unroll
+                            for (int k = 0; k < VP; ++k) pv[k] = o[h * VP + k];
+                            *reinterpret_cast<PV*>(prow + c0 + h * VP) = pv;
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < VC; ++k)
+                            if (k < cnt[g]) prow[c0 + k] = o[k];
+                    }
+                }
+            }
+        }
+    }
+    if (status == OTF_SK_TIMEOUT && tid == 0) store_wt(&p.info->stalled, 1);
+    if (lead) {
+        p.info->last_good = last_good;
+        p.info->niter = niter;
+        p.info->status = status;
+        p.info->break_iter = brk;
+        p.info->n_err = n_err;
+        p.info->engine = OTF_ENGINE_SWEEP;
+        p.info->stop = 1;
+    }
+}
+
+// Columns per thread (G chunks of 16 B) and rows per block R.  Per thread and column:
+// the column partial (sizeof(T) / 4 VGPRs), then per row of a block the e value and two
+// raw cost buffers (the block being reduced and the next one in flight); R is the
+// largest power of two that keeps these under ~150 of the 256 VGPRs a 512-thread
+// workgroup gets at one workgroup per CU (the rest: addresses, masks, reductions).
+constexpr int pow2_floor(int x) { return x >= 16 ? 16 : x >= 8 ? 8 : x >= 4 ? 4 : x >= 2 ? 2 : 1; }
+template <typename T, typename CT> constexpr int sweep_rows(int G) {
+    return pow2_floor((500 / (G * RawN<CT>::N) - (int)sizeof(T)) /
+                      ((int)sizeof(T) + 2 * (int)sizeof(CT)));
+}
+constexpr int kSwMaxG = 8;
+
+template <typename CT> int sweep_g(int64_t m) {
+    int g = 1;
+    while (g < kSwMaxG && (int64_t)kSwNT * g * RawN<CT>::N < m) g *= 2;
+    return (int64_t)kSwNT * g * RawN<CT>::N < m ? 0 : g;
+}
+
+#ifndef OTF_SWEEP_NREP
+#define OTF_SWEEP_NREP 4
+#endif
+
+template <typename T, typename CT, typename TP, int G>
+hipError_t launch_sweep_g(int grid, SkSweepArgs<T>& p, hipStream_t s) {
+    constexpr int R = sweep_rows<T, CT>(G);
+    void* args[] = {&p};
+    const void* k = (const void*)sk_sweep_kernel<T, CT, TP, G, R, OTF_SWEEP_NREP>;
+    const size_t lds = ((size_t)p.m_pad + 3 * kSwRowMax) * sizeof(T);
+    const int nrb = (p.n + R - 1) / R;
+    if ((int64_t)((nrb + grid - 1) / grid) * R > kSwRowMax) return hipErrorInvalidValue;
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kSwNT, lds);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1 || grid > per_cu * device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
+    return hipLaunchKernel(k, dim3(grid), dim3(kSwNT), args, lds, s);
+}
+
+template <typename T, typename CT, typename TP>
+hipError_t launch_sweep(int G, int grid, SkSweepArgs<T>& p, hipStream_t s) {
+    switch (G) {
+        case 1: return launch_sweep_g<T, CT, TP, 1>(grid, p, s);
+        case 2: return launch_sweep_g<T, CT, TP, 2>(grid, p, s);
+        case 4: return launch_sweep_g<T, CT, TP, 4>(grid, p, s);
+        case 8:
+            if constexpr (sizeof(CT) == 2) return hipErrorInvalidValue;  // m <= 16384 at G = 4
+            else return launch_sweep_g<T, CT, TP, 8>(grid, p, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+size_t align256(size_t x) { return (x + 255) / 256 * 256; }
+
+}  // namespace
+
+template <typename T> size_t sweep_region_bytes(int64_t m_pad) {
+    const size_t slot = (size_t)OTF_SWEEP_NREP * m_pad + 64;
+    return align256(4 * slot * sizeof(T)) + 4 * 256 + 256 + kSyncBytes;
+}
+
+template <typename T, typename CT> bool sweep_supported(int64_t n, int64_t m, int64_t ldc) {
+    const int G = sweep_g<CT>(m);
+    if (G == 0 || (sizeof(CT) == 2 && G > 4)) return false;
+    if (ldc % RawN<CT>::N != 0) return false;
+    if (n > INT32_MAX) return false;
+    int R = 1;
+    switch (G) {
+        case 1: R = sweep_rows<T, CT>(1); break;
+        case 2: R = sweep_rows<T, CT>(2); break;
+        case 4: R = sweep_rows<T, CT>(4); break;
+        default: R = sweep_rows<T, CT>(8); break;
+    }
+    const int64_t nrb = (n + R - 1) / R;
+    const int64_t grid = nrb < device_cu_count() ? nrb : device_cu_count();
+    return (nrb + grid - 1) / grid * R <= kSwRowMax;
+}
+
+template <typename T, typename CT>
+hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T* a_pad,
+                     const T* b_pad, const T* cost_scale, const otf_sinkhorn_opts& o, void* region,
+                     T* u_out, T* v_out, void* P_out, int64_t ldp, int P_dtype,
+                     otf_sinkhorn_info* info, double* errlog, hipStream_t s) {
+    const int G = sweep_g<CT>(m);
+    if (G == 0) return hipErrorInvalidValue;
+    SkSweepArgs<T> p{};
+    p.C = C;
+    p.ldc = ldc;
+    p.n = n;
+    p.m = m;
+    p.m_pad = m_pad;
+    p.a = a_pad;
+    p.b = b_pad;
+    p.cost_scale = cost_scale;
+    p.reg = o.reg;
+    p.max_iter = o.max_iter;
+    p.check_every = o.check_every;
+    p.err_squared = o.err_squared;
+    p.stop_thr = o.stop_thr;
+    p.ring = (T*)region;
+    p.slot_stride = (int64_t)OTF_SWEEP_NREP * m_pad + 64;
+    char* q = (char*)region + align256(4 * (size_t)p.slot_stride * sizeof(T));
+    p.bad = (int*)q;
+    p.bar = (int*)(q + 4 * 256);
+    p.sync = sync_words((int*)(q + 4 * 256 + 256));
+    p.info = info;
+    p.errlog = errlog;
+    p.u_out = u_out;
+    p.v_out = v_out;
+    p.P = P_out;
+    p.ldp = ldp;
+    p.stall_ticks = kStallTicks;
+    hipError_t e = hipMemsetAsync(region, 0, sweep_region_bytes<T>(m_pad), s);
+    if (e != hipSuccess) return e;
+    int R = 1;
+    switch (G) {
+        case 1: R = sweep_rows<T, CT>(1); break;
+        case 2: R = sweep_rows<T, CT>(2); break;
+        case 4: R = sweep_rows<T, CT>(4); break;
+        default: R = sweep_rows<T, CT>(8); break;
+    }
+    const int nrb = (n + R - 1) / R;
+    const int grid = nrb < device_cu_count() ? nrb : device_cu_count();
+    if (P_out && P_dtype == OTF_F64) return launch_sweep<T, CT, double>(G, grid, p, s);
+    return launch_sweep<T, CT, float>(G, grid, p, s);
+}
+
+template size_t sweep_region_bytes<float>(int64_t);
+template size_t sweep_region_bytes<double>(int64_t);
+template bool sweep_supported<float, float>(int64_t, int64_t, int64_t);
+template bool sweep_supported<float, _Float16>(int64_t, int64_t, int64_t);
+template bool sweep_supported<double, double>(int64_t, int64_t, int64_t);
+template hipError_t run_sweep<float, float>(const float*, int64_t, int, int, int, const float*,
+                                            const float*, const float*, const otf_sinkhorn_opts&,
+                                            void*, float*, float*, void*, int64_t, int,
+                                            otf_sinkhorn_info*, double*, hipStream_t);
+template hipError_t run_sweep<float, _Float16>(const _Float16*, int64_t, int, int, int, const float*,
+                                               const float*, const float*, const otf_sinkhorn_opts&,
+                                               void*, float*, float*, void*, int64_t, int,
+                                               otf_sinkhorn_info*, double*, hipStream_t);
+template hipError_t run_sweep<double, double>(const double*, int64_t, int, int, int, const double*,
+                                              const double*, const double*, const otf_sinkhorn_opts&,
+                                              void*, double*, double*, void*, int64_t, int,
+                                              otf_sinkhorn_info*, double*, hipStream_t);
+
+}  // namespace otf

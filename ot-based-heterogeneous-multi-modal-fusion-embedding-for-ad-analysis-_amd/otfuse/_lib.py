@@ -28,9 +28,9 @@ OTF_FLAVOR_POT, OTF_FLAVOR_OTT = 0, 1
 SK_RUNNING, SK_CONVERGED, SK_MAX_ITER, SK_NUMERICAL_BREAK, SK_TIMEOUT = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "running", 1: "converged", 2: "max_iter", 3: "numerical_break",
                 4: "timeout"}
-ENGINE_AUTO, ENGINE_STREAM, ENGINE_RESIDENT, ENGINE_TILED = 0, 1, 2, 3
+ENGINE_AUTO, ENGINE_STREAM, ENGINE_RESIDENT, ENGINE_TILED, ENGINE_SWEEP = 0, 1, 2, 3, 4
 ENGINES = {"auto": ENGINE_AUTO, "stream": ENGINE_STREAM, "resident": ENGINE_RESIDENT,
-           "tiled": ENGINE_TILED}
+           "tiled": ENGINE_TILED, "sweep": ENGINE_SWEEP}
 ENGINE_NAMES = {v: k for k, v in ENGINES.items()}
 
 
@@ -60,7 +60,7 @@ class GwProblem(ctypes.Structure):
                 ("n", ctypes.c_int64), ("m", ctypes.c_int64)]
 
 
-INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "engine", "pad")
+INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "engine", "stalled")
 INFO_INT32S = len(INFO_FIELDS)  # otf_sinkhorn_info is 8 x int32
 
 _vp = ctypes.c_void_p

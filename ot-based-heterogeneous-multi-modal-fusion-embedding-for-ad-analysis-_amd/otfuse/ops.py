@@ -226,8 +226,8 @@ class SinkhornResult:
             d = dict(zip(L.INFO_FIELDS, vals))
             d["status_name"] = L.STATUS_NAMES.get(d["status"], "?")
             d["engine_name"] = L.ENGINE_NAMES.get(d["engine"], "?")
-            if d["status"] == L.SK_TIMEOUT:
-                raise L.OtfError("resident Sinkhorn: device-wide barrier timed out "
+            if d["status"] == L.SK_TIMEOUT or d["stalled"]:
+                raise L.OtfError("persistent Sinkhorn: a device-wide barrier made no progress "
                                  "(grid not co-resident?); results are invalid")
             d["err"] = self.errlog_dev[: max(d["n_err"], 0)].cpu().tolist()
             self._info = d

@@ -21,12 +21,15 @@ def test_version_and_workspace_queries_are_host_only():
     lib = L.lib()
     assert lib.otf_version().decode().startswith("otfuse")
     ws = lib.otf_sinkhorn_workspace_size(4096, 4096, L.OTF_F32, 100)
-    # streaming buffers (~9 vectors) + the resident engine's per-iteration sums
-    # (101 iterations x 4 replicas x N: 256 row blocks of 16 rows)
-    assert 4 * 4096 * (9 + 404) < ws < 4 * 4096 * (32 + 404)
+    # streaming buffers (~9 vectors), the persistent engines' 4-slot sum rings (resident
+    # and sweep: 4 slots x 4 replicas x N each) and the tiled engine's row exchange
+    assert 4 * 4096 * (9 + 32) < ws < 4 * 4096 * 80
+    # only the err log grows with max_iter (the ring replaces per-iteration buffers)
+    ws_long = lib.otf_sinkhorn_workspace_size(4096, 4096, L.OTF_F32, 100000)
+    assert ws_long - ws <= 8 * 100000 + 512
     # a small problem (8 row blocks) keeps a single replica
     ws_small = lib.otf_sinkhorn_workspace_size(128, 4096, L.OTF_F32, 100)
-    assert ws_small < 4 * 4096 * (32 + 101)
+    assert ws_small < ws
     assert lib.otf_sinkhorn_workspace_size(8, 512, L.OTF_F64, 2000) > 8 * 512 * 7
     assert lib.otf_feature_cost_workspace_size(8, 8, 512, 512) >= 8 * (8 * 512)
 

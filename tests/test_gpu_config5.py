@@ -67,8 +67,8 @@ def test_fp16_cost_storage_is_scaled_and_rounded_once(ops, orc, dev, in_dtype):
     assert (np.abs(Cs - ref) <= tol).all()
 
 
-@pytest.mark.parametrize("engine", ["stream", "resident", "tiled"])
-@pytest.mark.parametrize("n,m", [(2048, 2048), (300, 1001)])
+@pytest.mark.parametrize("engine", ["stream", "resident", "tiled", "sweep"])
+@pytest.mark.parametrize("n,m", [(2048, 2048), (300, 1001), (1500, 16380)])
 def test_sinkhorn_on_fp16_cost_vs_oracle(ops, orc, dev, engine, n, m):
     X, _ = _emb16(n, 128, seed=7)
     _, Y = _emb16(m, 128, seed=8)
@@ -76,7 +76,12 @@ def test_sinkhorn_on_fp16_cost_vs_oracle(ops, orc, dev, engine, n, m):
                                       out_dtype=torch.float16)
     a = torch.full((n,), 1.0 / n, device=dev)
     b = torch.full((m,), 1.0 / m, device=dev)
-    res = ops.sinkhorn(a, b, C, 0.05, max_iter=80, stop_thr=0.0, cost_scale=cmax, engine=engine)
+    try:
+        res = ops.sinkhorn(a, b, C, 0.05, max_iter=80, stop_thr=0.0, cost_scale=cmax, engine=engine)
+    except Exception as e:  # resident / tiled need one row block / tile per CU
+        if engine in ("resident", "tiled") and "unsupported" in str(e):
+            pytest.skip(f"problem does not fit the {engine} engine")
+        raise
     info = res.info()
     assert info["engine_name"] == engine
     Cin = C.float().cpu().numpy().astype(np.float64) / float(cmax)   # what the solver consumed
@@ -95,8 +100,14 @@ def test_config5_full_size(ops, orc, dev):
                                          torch.as_tensor(Y, device=dev), out_dtype=torch.float16)
     a = torch.full((N,), 1.0 / N, device=dev)
     res = ops.sinkhorn(a, a, C, 0.1, max_iter=iters, stop_thr=0.0, cost_scale=cmax)
-    assert res.info()["engine_name"] == "stream"       # 1024 row blocks > 256 CUs
+    assert res.info()["engine_name"] == "sweep"        # too large for the register files
     P = res.plan.cpu().numpy().astype(np.float64)
+    # the one-launch-per-iteration engine gives the same plan (same arithmetic order
+    # per element; only the column-sum atomics' order differs)
+    res_s = ops.sinkhorn(a, a, C, 0.1, max_iter=iters, stop_thr=0.0, cost_scale=cmax,
+                         engine="stream")
+    assert nrel(res_s.plan.cpu().numpy(), P) < 1e-5
+    del res_s
     np.testing.assert_allclose(P.sum(1), 1.0 / N, rtol=1e-4)
     Cin = C.float().cpu().numpy().astype(np.float64) / float(cmax)
     del C
