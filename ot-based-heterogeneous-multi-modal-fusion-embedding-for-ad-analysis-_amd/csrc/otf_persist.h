@@ -34,6 +34,21 @@ inline SkSync sync_words(int* base) {
     return s;
 }
 
+// Diagnostic build only (-DOTF_STAMPS, tools/stamps_resident.hip, tools/stamps_sweep.hip):
+// per-phase wall-clock stamps of the persistent loops; compiled out of the library.
+#ifdef OTF_STAMPS
+__device__ unsigned long long g_stamps[256 * 16 * 8];
+#define OTF_STAMP(it, ph)                                                                   \
+    do {                                                                                    \
+        if (threadIdx.x == 0 && (it) < 16 && blockIdx.x < 256)                              \
+            g_stamps[(blockIdx.x * 16 + (it)) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define OTF_STAMP(it, ph) \
+    do {                  \
+    } while (0)
+#endif
+
 // 5 s of no progress at the 100 MHz s_memrealtime clock
 constexpr unsigned long long kStallTicks = 500000000ull;
 
@@ -61,6 +76,14 @@ __device__ __forceinline__ typename Vec<T>::type load_sum_vec(__amdgpu_buffer_rs
                                                               uint32_t byte_off) {
     const auto raw = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16 /* sc1 */);
     return __builtin_bit_cast(typename Vec<T>::type, raw);
+}
+
+// 16-B write-through (sc1) store: the producer side of the no-acquire hand-off
+template <typename T>
+__device__ __forceinline__ void store_sum_vec(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off,
+                                              typename Vec<T>::type v) {
+    using I4 = __attribute__((ext_vector_type(4))) int;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(I4, v), rs, byte_off, 0, 16 /* sc1 */);
 }
 
 // Device-wide flat barrier: every wave drains its own memory operations, one lane per

@@ -537,20 +537,6 @@ template <typename T> struct SkResArgs {
     unsigned long long timeout_ticks;
 };
 
-// Diagnostic build only (-DOTF_STAMPS, tools/stamps_resident.hip): per-phase wall-clock
-// stamps of the resident loop; compiled out of the library.
-#ifdef OTF_STAMPS
-__device__ unsigned long long g_stamps[256 * 16 * 8];
-#define OTF_STAMP(it, ph)                                                                   \
-    do {                                                                                    \
-        if (threadIdx.x == 0 && (it) < 16 && blockIdx.x < 256)                              \
-            g_stamps[(blockIdx.x * 16 + (it)) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-#else
-#define OTF_STAMP(it, ph) \
-    do {                  \
-    } while (0)
-#endif
 
 template <typename T, typename CT, typename TP, int G, int R, int NREP>
 __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {

@@ -32,6 +32,7 @@
 // recomputed bit-identically from v(k) = b / S[k].  Memory is O(m), not O(max_iter m).
 #include "otf_persist.h"
 
+
 namespace otf {
 namespace {
 
@@ -53,6 +54,8 @@ template <typename T> struct SkSweepArgs {
     int* bad;           // 4 counters of non-finite u rows, one 256-B line each
     int* bar;
     SkSync sync;
+    int* gcnt;          // per-XCD group arrival counters, one 256-B line each
+    T* slab;            // grid x m_pad column partials (write-through), one row per workgroup
     otf_sinkhorn_info* info;
     double* errlog;
     T* u_out;
@@ -60,6 +63,7 @@ template <typename T> struct SkSweepArgs {
     void* P;
     int64_t ldp;
     unsigned long long stall_ticks;
+    int nt_loads;       // 1: cost larger than the Infinity Cache, stream it non-temporal
 };
 
 using Raw = __attribute__((ext_vector_type(4))) unsigned int;  // 16 B of cost
@@ -113,10 +117,11 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     T* vbuf = reinterpret_cast<T*>(sw_lds);                         // m_pad
     T* uhist = vbuf + p.m_pad;                                       // [2][kSwRowMax]
     T* ialds = uhist + 2 * kSwRowMax;                                // 1 / a of own rows
+    T* gred = ialds + kSwRowMax;                                     // [kSwNT * VT] group reduce
     __shared__ T red[2][NW][R];
     __shared__ T ered[17];
     __shared__ int s_flag;
-    __shared__ int s_pop[3];
+    __shared__ int s_pop[5];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nwg = gridDim.x;
@@ -170,18 +175,30 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         ialds[i] = (T)1 / p.a[row < p.n ? row : 0];
     }
 
-    // R cost rows of block bi via one SGPR descriptor (rows past n read as 0)
+    // R cost rows of block bi via one SGPR descriptor (rows past n read as 0).  A cost
+    // larger than the Infinity Cache is loaded non-temporal (7.3 vs 6.4 TB/s from HBM,
+    // tools/ubench_mall.hip; N = 16384 fp32: 195 -> 184 us per sweep); a cost that fits
+    // keeps the default policy (nt measured 26.2 vs 22.3 us per config-5 sweep).
     auto load_block = [&](int bi, Raw (&buf)[R][G]) {
         const int r0 = ((int)blockIdx.x + bi * nwg) * R;
         const int nrow = p.n - r0 < R ? p.n - r0 : R;
         const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
             (void*)((const char*)p.C + (int64_t)r0 * ld_bytes), 0, (int)(nrow * ld_bytes), 0x00020000);
+        if (p.nt_loads) {
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+            for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int g = 0; g < G; ++g)
-                buf[r][g] = __builtin_amdgcn_raw_buffer_load_b128(
-                    cr, (uint32_t)(colc[g] * (int)sizeof(CT)), (uint32_t)(r * ld_bytes), 0);
+                for (int g = 0; g < G; ++g)
+                    buf[r][g] = __builtin_amdgcn_raw_buffer_load_b128(
+                        cr, (uint32_t)(colc[g] * (int)sizeof(CT)), (uint32_t)(r * ld_bytes), 2 /* nt */);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    buf[r][g] = __builtin_amdgcn_raw_buffer_load_b128(
+                        cr, (uint32_t)(colc[g] * (int)sizeof(CT)), (uint32_t)(r * ld_bytes), 0);
+        }
     };
     auto sanitize = [&](Raw (&buf)[R][G]) {
         if (ragged) {
@@ -245,7 +262,6 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 
     const T u0 = (T)1 / (T)p.n;
     const int xcd = xcc_id();
-    const int my_rep = xcd % NREP;
     Raw bufA[R][G], bufB[R][G];
     T colacc[G][VC];
 
@@ -331,9 +347,45 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         }
     };
 
-    // flush the column partials into slot k (replica my_rep), zero slot k + 1's share
+    // ---- registration: XCD population, this workgroup's slot in its XCD group and the
+    // group's first slab row (placement changes speed only: groups are counted, not assumed)
+    if (tid == 0) {
+        s_pop[3] = __hip_atomic_fetch_add(p.sync.reg + xcd * 64, 1, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    }
+    bool reg_ok = grid_barrier(p.bar, nwg, deadline, p.stall_ticks, &s_flag);
+    if (tid == 0) {
+        int nact = 0, base = 0;
+        unsigned mask = 0;
+        for (int x = 0; x < 8; ++x) {
+            const int c = __hip_atomic_load(p.sync.reg + x * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (x < xcd) base += c;
+            if (c > 0) {
+                ++nact;
+                mask |= 1u << x;
+            }
+        }
+        s_pop[0] = __hip_atomic_load(p.sync.reg + xcd * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_pop[1] = nact;
+        s_pop[2] = (int)mask;
+        s_pop[4] = base;
+    }
+    __syncthreads();
+    const int nx = s_pop[0], nact = s_pop[1], gslot = s_pop[3], gbase = s_pop[4];
+    const unsigned act_mask = (unsigned)s_pop[2];
+    // this workgroup's column slice of the group reduction: [sl0, sl1) of m_pad
+    const int slw = ((p.m_pad + nx * VT - 1) / (nx * VT)) * VT;
+    const int sl0 = gslot * slw < p.m_pad ? gslot * slw : p.m_pad;
+    const int sl1 = sl0 + slw < p.m_pad ? sl0 + slw : p.m_pad;
+
+    // Flush the column partials into ring slot k, zero slot k + 1's share.  Partials go
+    // through the XCD group: every workgroup stores its m partials write-through into its
+    // slab row, the group meets on its counter (epoch k + 1), then each member sums ONE
+    // column slice over the group's rows in a fixed order and adds it to the slot with
+    // memory-side atomics: 8 x m atomics per iteration instead of grid x m.
+    int gep = 0;
+    const __amdgpu_buffer_rsrc_t srow = sums_rsrc(p.slab + (size_t)(gbase + gslot) * p.m_pad);
     auto flush = [&](int k) {
-        __syncthreads();  // every thread is done with vbuf (v) before it stages partials
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int c0 = (tid + kSwNT * g) * VC;
@@ -343,19 +395,66 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                     V wv;
 #pragma unroll
                     for (int k2 = 0; k2 < VT; ++k2) wv[k2] = colacc[g][h * VT + k2];
-                    *reinterpret_cast<V*>(vbuf + c0 + h * VT) = wv;
+                    store_sum_vec<T>(srow, (uint32_t)((c0 + h * VT) * sizeof(T)), wv);
                 }
             }
         }
+        ++gep;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        T* dst = p.ring + (size_t)(k & 3) * p.slot_stride + (size_t)my_rep * p.m_pad;
-        for (int j = tid; j < p.m; j += kSwNT) atomicAdd(dst + j, vbuf[j]);
+        if (tid == 0) {
+            int ok = 1;
+            __hip_atomic_fetch_add(p.gcnt + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (load_agent(p.gcnt + xcd * 64) < gep * nx) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = 0; break; }
+            }
+            s_flag = ok;
+        }
+        __syncthreads();
+        if (!s_flag) gep = -1;  // stalled: the caller reports OTF_SK_TIMEOUT
+        deadline = __builtin_amdgcn_s_memrealtime() + p.stall_ticks;
+        // slice reduce: thread (q, j) sums rows q, q + Q, ... of vector j of the slice
+        const int nv = (sl1 - sl0) / VT;
+        int Q = 1;
+        while (Q * 2 <= nx && kSwNT / (Q * 2) >= nv) Q *= 2;
+        const int W = kSwNT / Q, q = tid / W, j = tid % W;
+        const __amdgpu_buffer_rsrc_t sr = sums_rsrc(p.slab + (size_t)gbase * p.m_pad);
+        for (int jb = 0; jb < nv; jb += W) {
+            const int jv = jb + j;
+            V acc;
+#pragma unroll
+            for (int k2 = 0; k2 < VT; ++k2) acc[k2] = 0;
+            if (jv < nv) {
+#pragma unroll 4
+                for (int r = q; r < nx; r += Q) {
+                    const V t = load_sum_vec<T>(sr, (uint32_t)(((size_t)r * p.m_pad + sl0 + jv * VT) * sizeof(T)));
+#pragma unroll
+                    for (int k2 = 0; k2 < VT; ++k2) acc[k2] += t[k2];
+                }
+            }
+            *reinterpret_cast<V*>(gred + (size_t)tid * VT) = acc;
+            __syncthreads();
+            if (q == 0 && jv < nv) {
+                V tot = *reinterpret_cast<const V*>(gred + (size_t)j * VT);
+                for (int qq = 1; qq < Q; ++qq) {
+                    const V t = *reinterpret_cast<const V*>(gred + (size_t)(qq * W + j) * VT);
+#pragma unroll
+                    for (int k2 = 0; k2 < VT; ++k2) tot[k2] += t[k2];
+                }
+                *reinterpret_cast<V*>(vbuf + jv * VT) = tot;
+            }
+            __syncthreads();
+        }
+        T* dst = p.ring + (size_t)(k & 3) * p.slot_stride;
+        const int send = sl1 < p.m ? sl1 : p.m;
+        for (int c = sl0 + tid; c < send; c += kSwNT) atomicAdd(dst + c, vbuf[c - sl0]);
         // slot k + 1 (= S[k - 3]) is free: this workgroup's share of it, write-through
         T* zs = p.ring + (size_t)((k + 1) & 3) * p.slot_stride;
         const int64_t per = (p.slot_stride + nwg - 1) / nwg;
         const int64_t z0 = (int64_t)blockIdx.x * per;
         const int64_t z1 = z0 + per < p.slot_stride ? z0 + per : p.slot_stride;
-        for (int64_t j = z0 + tid; j < z1; j += kSwNT) store_wt(zs + j, (T)0);
+        for (int64_t jz = z0 + tid; jz < z1; jz += kSwNT) store_wt(zs + jz, (T)0);
         if (tid == 0) {
             if (blockIdx.x == 0) store_wt(p.bad + ((k + 1) & 3) * 64, 0);
             if (badu) atomicAdd(p.bad + ((k - 1) & 3) * 64, 1);  // u(k-1) not finite
@@ -369,14 +468,14 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     flush(0);
     int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
     bool done = false, ran_all = false;
-    if (!register_grid(p.sync, p.bar, xcd, deadline, p.stall_ticks, &s_flag, s_pop)) {
+    if (!reg_ok || gep < 0 ||
+        !xcd_barrier(p.sync, xcd, nx, nact, act_mask, 1, deadline, p.stall_ticks, &s_flag)) {
         status = OTF_SK_TIMEOUT;
         done = true;
     }
-    const int nx = s_pop[0], nact = s_pop[1];
-    const unsigned act_mask = (unsigned)s_pop[2];
 
     for (int it = 0; it < p.max_iter && !done; ++it) {
+        OTF_STAMP(it, 0);
         const int prev_bad = it >= 1 ? load_agent(p.bad + ((it - 1) & 3) * 64) : 0;
         int badv = 0;
 #pragma unroll
@@ -421,12 +520,22 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
             break;
         }
+        OTF_STAMP(it, 1);
         sweep(it);
+        OTF_STAMP(it, 2);
         flush(it + 1);
-        if (!xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 1, deadline, p.stall_ticks, &s_flag)) {
+        OTF_STAMP(it, 3);
+#ifdef OTF_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        OTF_STAMP(it, 4);
+#endif
+        if (gep < 0 ||
+            !xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 2, deadline, p.stall_ticks, &s_flag)) {
             status = OTF_SK_TIMEOUT;
             done = true;
         }
+        OTF_STAMP(it, 5);
         if (it == p.max_iter - 1 && !done) ran_all = true;
     }
     if (status == OTF_SK_MAX_ITER && ran_all) {
@@ -529,9 +638,12 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 // raw cost buffers (the block being reduced and the next one in flight); R is the
 // largest power of two that keeps these under ~150 of the 256 VGPRs a 512-thread
 // workgroup gets at one workgroup per CU (the rest: addresses, masks, reductions).
+#ifndef OTF_SWEEP_RBUDGET
+#define OTF_SWEEP_RBUDGET 500
+#endif
 constexpr int pow2_floor(int x) { return x >= 16 ? 16 : x >= 8 ? 8 : x >= 4 ? 4 : x >= 2 ? 2 : 1; }
 template <typename T, typename CT> constexpr int sweep_rows(int G) {
-    return pow2_floor((500 / (G * RawN<CT>::N) - (int)sizeof(T)) /
+    return pow2_floor((OTF_SWEEP_RBUDGET / (G * RawN<CT>::N) - (int)sizeof(T)) /
                       ((int)sizeof(T) + 2 * (int)sizeof(CT)));
 }
 constexpr int kSwMaxG = 8;
@@ -543,15 +655,16 @@ template <typename CT> int sweep_g(int64_t m) {
 }
 
 #ifndef OTF_SWEEP_NREP
-#define OTF_SWEEP_NREP 4
+#define OTF_SWEEP_NREP 1
 #endif
+constexpr int kSwMaxGrid = 256;  // slab rows in the workspace (one per workgroup)
 
 template <typename T, typename CT, typename TP, int G>
 hipError_t launch_sweep_g(int grid, SkSweepArgs<T>& p, hipStream_t s) {
     constexpr int R = sweep_rows<T, CT>(G);
     void* args[] = {&p};
     const void* k = (const void*)sk_sweep_kernel<T, CT, TP, G, R, OTF_SWEEP_NREP>;
-    const size_t lds = ((size_t)p.m_pad + 3 * kSwRowMax) * sizeof(T);
+    const size_t lds = ((size_t)p.m_pad + 3 * kSwRowMax + (size_t)kSwNT * Vec<T>::N) * sizeof(T);
     const int nrb = (p.n + R - 1) / R;
     if ((int64_t)((nrb + grid - 1) / grid) * R > kSwRowMax) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -578,11 +691,21 @@ hipError_t launch_sweep(int G, int grid, SkSweepArgs<T>& p, hipStream_t s) {
 
 size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 
+// region: ring (4 slots) | bad counters | barrier | sync words | group counters, all
+// zeroed per solve | slab (one row of column partials per workgroup, overwritten)
+size_t sweep_ctrl_bytes(int64_t m_pad, size_t esz) {
+    const size_t slot = (size_t)OTF_SWEEP_NREP * m_pad + 64;
+    return align256(4 * slot * esz) + 4 * 256 + 256 + align256(kSyncBytes) + 8 * 256;
+}
+int sweep_grid(int64_t nrb) {
+    int64_t g = nrb < device_cu_count() ? nrb : device_cu_count();
+    return (int)(g < kSwMaxGrid ? g : kSwMaxGrid);
+}
+
 }  // namespace
 
 template <typename T> size_t sweep_region_bytes(int64_t m_pad) {
-    const size_t slot = (size_t)OTF_SWEEP_NREP * m_pad + 64;
-    return align256(4 * slot * sizeof(T)) + 4 * 256 + 256 + kSyncBytes;
+    return sweep_ctrl_bytes(m_pad, sizeof(T)) + (size_t)kSwMaxGrid * m_pad * sizeof(T);
 }
 
 template <typename T, typename CT> bool sweep_supported(int64_t n, int64_t m, int64_t ldc) {
@@ -598,7 +721,7 @@ template <typename T, typename CT> bool sweep_supported(int64_t n, int64_t m, in
         default: R = sweep_rows<T, CT>(8); break;
     }
     const int64_t nrb = (n + R - 1) / R;
-    const int64_t grid = nrb < device_cu_count() ? nrb : device_cu_count();
+    const int64_t grid = sweep_grid(nrb);
     return (nrb + grid - 1) / grid * R <= kSwRowMax;
 }
 
@@ -629,6 +752,8 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     p.bad = (int*)q;
     p.bar = (int*)(q + 4 * 256);
     p.sync = sync_words((int*)(q + 4 * 256 + 256));
+    p.gcnt = (int*)(q + 4 * 256 + 256 + align256(kSyncBytes));
+    p.slab = (T*)((char*)region + sweep_ctrl_bytes(m_pad, sizeof(T)));
     p.info = info;
     p.errlog = errlog;
     p.u_out = u_out;
@@ -636,7 +761,8 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     p.P = P_out;
     p.ldp = ldp;
     p.stall_ticks = kStallTicks;
-    hipError_t e = hipMemsetAsync(region, 0, sweep_region_bytes<T>(m_pad), s);
+    p.nt_loads = (double)n * ldc * sizeof(CT) > 192.0 * (1 << 20) ? 1 : 0;
+    hipError_t e = hipMemsetAsync(region, 0, sweep_ctrl_bytes(m_pad, sizeof(T)), s);
     if (e != hipSuccess) return e;
     int R = 1;
     switch (G) {
@@ -646,7 +772,7 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
         default: R = sweep_rows<T, CT>(8); break;
     }
     const int nrb = (n + R - 1) / R;
-    const int grid = nrb < device_cu_count() ? nrb : device_cu_count();
+    const int grid = sweep_grid(nrb);
     if (P_out && P_dtype == OTF_F64) return launch_sweep<T, CT, double>(G, grid, p, s);
     return launch_sweep<T, CT, float>(G, grid, p, s);
 }

@@ -21,9 +21,9 @@ def test_version_and_workspace_queries_are_host_only():
     lib = L.lib()
     assert lib.otf_version().decode().startswith("otfuse")
     ws = lib.otf_sinkhorn_workspace_size(4096, 4096, L.OTF_F32, 100)
-    # streaming buffers (~9 vectors), the persistent engines' 4-slot sum rings (resident
-    # and sweep: 4 slots x 4 replicas x N each) and the tiled engine's row exchange
-    assert 4 * 4096 * (9 + 32) < ws < 4 * 4096 * 80
+    # streaming buffers (~9 vectors), the persistent engines' 4-slot sum rings, the tiled
+    # engine's row exchange and the sweep engine's partial slab (256 rows of N)
+    assert 4 * 4096 * (9 + 16 + 256) < ws < 4 * 4096 * (80 + 256)
     # only the err log grows with max_iter (the ring replaces per-iteration buffers)
     ws_long = lib.otf_sinkhorn_workspace_size(4096, 4096, L.OTF_F32, 100000)
     assert ws_long - ws <= 8 * 100000 + 512
