@@ -46,7 +46,7 @@ enum {
     OTF_EHIP = -1
 };
 
-typedef enum { OTF_F32 = 0, OTF_F64 = 1, OTF_F16 = 2 } otf_dtype;
+typedef enum { OTF_F32 = 0, OTF_F64 = 1, OTF_F16 = 2, OTF_BF16 = 3 } otf_dtype;
 typedef enum { OTF_SQEUCLIDEAN = 0, OTF_EUCLIDEAN = 1 } otf_metric;
 
 /* Sinkhorn flavours.
@@ -106,6 +106,9 @@ typedef struct {
     int32_t cost_f16;   /* 1: C is stored as fp16 (dtype must be OTF_F32; compute fp32)  */
     int32_t n_total;    /* row-sharded solve: rows of the whole problem (u0 = 1/n_total);
                            0 = n                                                      */
+    int32_t deterministic; /* 1: bitwise-reproducible column sums (fixed-order reduction,
+                           no float atomics; sweep engine, POT flavour), e.g. for
+                           parity runs; other engines return OTF_EUNSUPPORTED        */
 } otf_sinkhorn_opts;
 
 /* Written on the device by otf_sinkhorn (read it after the stream completes). */
@@ -183,6 +186,15 @@ int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, i
                      const double* ts_diag, int32_t weights_mode, double* M, int64_t ldm,
                      void* workspace, size_t ws_bytes, otf_stream_t stream);
 
+/* otf_feature_cost with the embeddings stored as in_dtype = OTF_F32, OTF_BF16 or
+ * OTF_F16 (BASELINE config 4: bf16 encoder outputs).  Every element is widened
+ * exactly to float32 first, so the result equals otf_feature_cost on the rounded
+ * values upcast to float32 (the reference's arithmetic on such arrays).           */
+int otf_feature_cost_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy, int32_t in_dtype,
+                        int64_t n, int64_t n2, int64_t d, int64_t d2, const double* Ts,
+                        int64_t ldts, const double* ts_diag, int32_t weights_mode, double* M,
+                        int64_t ldm, void* workspace, size_t ws_bytes, otf_stream_t stream);
+
 /* COOT cost (perturbot/perturbot/match/utils.py:125-184 init_matrix_np and its uses in
  * cot_labels.py:155-160, 173, 192):
  *   M (p x q, ldm) = t1[:, None] + t2[None, :] - 2 A T B^T,
@@ -252,12 +264,58 @@ int otf_sinkhorn_finish(const void* a, const void* b, const void* C, int64_t n, 
                         int64_t ldp, int32_t P_dtype, otf_sinkhorn_info* info, double* errlog,
                         void* workspace, size_t ws_bytes, otf_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * RCCL communicator.  The reference has no collectives; these
+ * carry the path's two exchanges: the all-gather of per-epoch embedding shards
+ * (MRI_PET_OT_OT_per_epoch_attn.py:940-960 run data-parallel) and the per-iteration
+ * all-reduce of the row-sharded Sinkhorn's column sums.  One process per GPU, one
+ * rank each; RCCL is resolved at run time from the copy already loaded in the
+ * process (PyTorch's "nccl" backend), so both share one RCCL instance.
+ *   rank 0: otf_comm_unique_id(id); share the 128 id bytes (e.g. torch broadcast);
+ *   every rank: otf_comm_init(&comm, id, nranks, rank) with its device current.
+ * Collectives are enqueued on `stream` (stream-ordered, no host sync).
+ * ------------------------------------------------------------------------- */
+typedef struct otf_comm otf_comm;
+enum { OTF_RED_SUM = 0, OTF_RED_MAX = 1 };
+#define OTF_COMM_ID_BYTES 128
+
+int otf_comm_unique_id(void* id_out);
+int otf_comm_init(otf_comm** comm_out, const void* id, int32_t nranks, int32_t rank);
+int otf_comm_destroy(otf_comm* comm);
+/* In-place all-reduce of count elements (dtype OTF_F32/F64/F16, op OTF_RED_*).     */
+int otf_comm_all_reduce(void* buf, int64_t count, int32_t dtype, int32_t op, otf_comm* comm,
+                        otf_stream_t stream);
+/* recv = concat over ranks of send (count_per_rank elements each), rank order.     */
+int otf_comm_all_gather(const void* send, void* recv, int64_t count_per_rank, int32_t dtype,
+                        otf_comm* comm, otf_stream_t stream);
+
+/* The whole row-sharded solve in one call: otf_sinkhorn_pass for every pass, each
+ * followed by the RCCL all-reduce(sum) of its column-sum buffer on the same stream,
+ * then otf_sinkhorn_finish — no host round trip per iteration (finished passes are
+ * device-side no-ops).  Same arguments as the pass / finish pair; opts.n_total = rows
+ * of the whole problem.  comm = NULL runs the single-rank solve through the same path. */
+int otf_sinkhorn_row_sharded(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                             int64_t ldc, int32_t dtype, const void* cost_scale,
+                             const otf_sinkhorn_opts* opts, otf_comm* comm, void* u_out,
+                             void* v_out, void* P_out, int64_t ldp, int32_t P_dtype,
+                             otf_sinkhorn_info* info, double* errlog, void* workspace,
+                             size_t ws_bytes, otf_stream_t stream);
+
 /* Plan post-processing (MRI_PET_OT_nojax.py:702-715): T (d x d2, ldt, dtype
  * float32/64) -> Tn float32 (ldtn): NaN -> nan_fill, row sums (0 -> 1e-8),
  * Tn = T / rowsum.  rownorm = 0 only converts + fills.                          */
 int otf_plan_postprocess(const void* T, int64_t d, int64_t d2, int64_t ldt, int32_t dtype,
                          float nan_fill, int32_t rownorm, float* Tn, int64_t ldtn,
                          otf_stream_t stream);
+
+/* Fused post-process + apply (MRI_PET_OT_nojax.py:702-718) in ONE pass over the plan:
+ * out (B x d, ldo) = Z (B x d2, ldz, float32: pet_fused) @ Tn^T with Tn the
+ * post-processed plan (NaN -> nan_fill, rows / rowsum, 0 -> 1e-8); Tn (d x d2,
+ * ldtn, nullable) is also written for the backward G @ Tn.                        */
+int otf_plan_postprocess_apply(const void* T, int64_t d, int64_t d2, int64_t ldt, int32_t dtype,
+                               float nan_fill, int32_t rownorm, const float* Z, int64_t ldz,
+                               int64_t B, float* out, int64_t ldo, float* Tn, int64_t ldtn,
+                               otf_stream_t stream);
 
 /* out (M x N, ldo) = alpha * op(A) op(B) (+ beta * out), float32, where
  * op(A)_{ik} = A[i*sa0 + k*sa1] and op(B)_{kj} = B[k*sb0 + j*sb1]: the plan

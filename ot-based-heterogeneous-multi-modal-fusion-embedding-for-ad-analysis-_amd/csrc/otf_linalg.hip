@@ -13,6 +13,15 @@
 namespace otf {
 namespace {
 
+// bf16 storage (BASELINE config 4: bf16 encoder outputs): the upper 16 bits of an fp32,
+// so the widening is exact and the reference's float32 arithmetic on the bf16-rounded
+// embeddings is reproduced bit for bit
+struct bf16 {
+    uint16_t bits;
+    __device__ __forceinline__ operator float() const { return __uint_as_float((uint32_t)bits << 16); }
+    __device__ __forceinline__ operator double() const { return (double)(float)*this; }
+};
+
 // Generic tiled GEMM  out[i][j] = alpha * sum_k A(i,k) B(k,j) + beta * out[i][j]
 //                                 + rowadd[i] + coladd[j]
 // with A(i,k) = A[i*sa0 + k*sa1], B(k,j) = B[k*sb0 + j*sb1].  64 x 64 tile, BK 16,
@@ -103,13 +112,14 @@ __global__ void ts_sums_kernel(const double* Ts, int64_t ldts, const double* dia
 }
 
 // t[k] = sum_i float(x_ik * x_ik) * w[i]   ((X**2).T @ w with X**2 in float32)
-__global__ void weighted_sq_colsum_kernel(const float* X, int64_t ldx, int n, int d,
+template <typename TI>
+__global__ void weighted_sq_colsum_kernel(const TI* X, int64_t ldx, int n, int d,
                                           const double* w, double* t) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= d) return;
     double s = 0.0;
     for (int i = 0; i < n; ++i) {
-        const float x = X[(int64_t)i * ldx + k];
+        const float x = (float)X[(int64_t)i * ldx + k];
         s += (double)(x * x) * w[i];
     }
     t[k] = s;
@@ -130,12 +140,13 @@ __global__ void weighted_sq_strided_kernel(const float* A, int64_t so, int64_t s
 }
 
 // Z[i][l] = diag[i] * Y[i][l]   (Ts diagonal, e.g. np.eye(B)/B)
-__global__ void diag_scale_kernel(const float* Y, int64_t ldy, int n, int d2, const double* diag,
+template <typename TI>
+__global__ void diag_scale_kernel(const TI* Y, int64_t ldy, int n, int d2, const double* diag,
                                   double* Z) {
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < (int64_t)n * d2;
          t += (int64_t)gridDim.x * blockDim.x) {
         const int i = (int)(t / d2), l = (int)(t % d2);
-        Z[t] = diag[i] * (double)Y[(int64_t)i * ldy + l];
+        Z[t] = diag[i] * (double)(float)Y[(int64_t)i * ldy + l];
     }
 }
 
@@ -160,6 +171,57 @@ __global__ __launch_bounds__(256) void postprocess_kernel(const T* Tm, int d, in
         if (s == 0.f) s = 1e-8f;
         for (int j = threadIdx.x; j < d2; j += blockDim.x) dst[j] = dst[j] / s;
         __syncthreads();
+    }
+}
+
+// Fused post-process + apply (MRI_PET_OT_nojax.py:702-718): one workgroup per plan
+// row i, ONE pass over the row: v = fill_nan(float(T[i][j])), rowsum s and the B
+// dot products z_b . v together; out[b][i] = (z_b . v) / s (= pet_fused @ Tn^T),
+// then Tn[i][j] = v / s (kept for the backward G @ Tn) from the L2-resident row.
+constexpr int kPaB = 16;   // batch rows per register block
+template <typename T>
+__global__ __launch_bounds__(256) void postprocess_apply_kernel(
+    const T* Tm, int d, int d2, int64_t ldt, float nan_fill, int rownorm, const float* Z,
+    int64_t ldz, int B, float* out, int64_t ldo, float* Tn, int64_t ldtn) {
+    __shared__ float red[17 * kPaB];
+    __shared__ float red1[17];
+    for (int row = blockIdx.x; row < d; row += gridDim.x) {
+        const T* src = Tm + (int64_t)row * ldt;
+        float s = 0.f;
+        for (int b0 = 0; b0 < B; b0 += kPaB) {
+            float acc[kPaB];
+            float sp = 0.f;
+#pragma unroll
+            for (int b = 0; b < kPaB; ++b) acc[b] = 0.f;
+            for (int j = threadIdx.x; j < d2; j += blockDim.x) {
+                float v = (float)src[j];
+                if (isnan(v)) v = nan_fill;
+                sp += v;
+#pragma unroll
+                for (int b = 0; b < kPaB; ++b)
+                    if (b0 + b < B) acc[b] += Z[(int64_t)(b0 + b) * ldz + j] * v;
+            }
+            block_sum_multi<float, kPaB>(acc, red);
+            s = block_sum<float>(sp, red1);
+            const float sd = (rownorm && s == 0.f) ? 1e-8f : s;
+            if (threadIdx.x < kPaB && b0 + (int)threadIdx.x < B) {
+                float mine = acc[0];
+#pragma unroll
+                for (int b = 1; b < kPaB; ++b)
+                    if ((int)threadIdx.x == b) mine = acc[b];
+                out[(int64_t)(b0 + threadIdx.x) * ldo + row] = rownorm ? mine / sd : mine;
+            }
+            __syncthreads();
+        }
+        if (Tn) {
+            const float sd = (rownorm && s == 0.f) ? 1e-8f : s;
+            float* dst = Tn + (int64_t)row * ldtn;
+            for (int j = threadIdx.x; j < d2; j += blockDim.x) {
+                float v = (float)src[j];
+                if (isnan(v)) v = nan_fill;
+                dst[j] = rownorm ? v / sd : v;
+            }
+        }
     }
 }
 
@@ -194,11 +256,15 @@ size_t otf_feature_cost_workspace_size(int64_t n, int64_t n2, int64_t d, int64_t
            align_up(8 * (size_t)(n * d2), 256);
 }
 
-int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
-                     int64_t n2, int64_t d, int64_t d2, const double* Ts, int64_t ldts,
-                     const double* ts_diag, int32_t weights_mode, double* M, int64_t ldm,
-                     void* workspace, size_t ws_bytes, otf_stream_t stream) {
-    using otf::align_up;
+}  // extern "C"
+
+namespace otf {
+namespace {
+template <typename TI>
+int feature_cost_t(const TI* X, int64_t ldx, const TI* Y, int64_t ldy, int64_t n, int64_t n2,
+                   int64_t d, int64_t d2, const double* Ts, int64_t ldts, const double* ts_diag,
+                   int32_t weights_mode, double* M, int64_t ldm, void* workspace, size_t ws_bytes,
+                   hipStream_t s) {
     if (!X || !Y || !M || !workspace || n <= 0 || n2 <= 0 || d <= 0 || d2 <= 0) return OTF_EINVAL;
     if (!Ts && !ts_diag) return OTF_EINVAL;
     if ((ts_diag || weights_mode == 1) && n != n2) return OTF_EINVAL;
@@ -206,7 +272,6 @@ int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, i
     if (ldx < d || ldy < d2 || ldm < d2 || (Ts && ldts < n2)) return OTF_EINVAL;
     if (ws_bytes < otf_feature_cost_workspace_size(n, n2, d, d2)) return OTF_EINVAL;
     if (n > 65535 * 64 || d > 65535 * 64 || d2 > 65535 * 64) return OTF_EUNSUPPORTED;
-    hipStream_t s = (hipStream_t)stream;
     char* p = (char*)workspace;
     double* w1 = (double*)p; p += align_up(8 * (size_t)n, 256);
     double* w2 = (double*)p; p += align_up(8 * (size_t)n2, 256);
@@ -215,27 +280,62 @@ int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, i
     double* Z = (double*)p;
 
     const int nmax = (int)(n > n2 ? n : n2);
-    otf::ts_sums_kernel<<<(nmax + 255) / 256, 256, 0, s>>>(Ts, ldts, ts_diag, (int)n, (int)n2,
-                                                          weights_mode, w1, w2);
+    ts_sums_kernel<<<(nmax + 255) / 256, 256, 0, s>>>(Ts, ldts, ts_diag, (int)n, (int)n2,
+                                                      weights_mode, w1, w2);
     OTF_HIP(hipGetLastError());
-    otf::weighted_sq_colsum_kernel<<<(int)((d + 255) / 256), 256, 0, s>>>(X, ldx, (int)n, (int)d, w1, t1);
-    otf::weighted_sq_colsum_kernel<<<(int)((d2 + 255) / 256), 256, 0, s>>>(Y, ldy, (int)n2, (int)d2, w2, t2);
+    weighted_sq_colsum_kernel<TI><<<(int)((d + 255) / 256), 256, 0, s>>>(X, ldx, (int)n, (int)d, w1, t1);
+    weighted_sq_colsum_kernel<TI><<<(int)((d2 + 255) / 256), 256, 0, s>>>(Y, ldy, (int)n2, (int)d2, w2, t2);
     OTF_HIP(hipGetLastError());
     // Z = Ts @ Y  (n x d2)
     if (ts_diag) {
-        otf::diag_scale_kernel<<<256, 256, 0, s>>>(Y, ldy, (int)n, (int)d2, ts_diag, Z);
+        diag_scale_kernel<TI><<<256, 256, 0, s>>>(Y, ldy, (int)n, (int)d2, ts_diag, Z);
     } else {
-        dim3 grid((unsigned)((d2 + otf::GT - 1) / otf::GT), (unsigned)((n + otf::GT - 1) / otf::GT));
-        otf::gemm_kernel<double, float, double, double><<<grid, 256, 0, s>>>(
+        dim3 grid((unsigned)((d2 + GT - 1) / GT), (unsigned)((n + GT - 1) / GT));
+        gemm_kernel<double, TI, double, double><<<grid, 256, 0, s>>>(
             Ts, ldts, 1, Y, ldy, 1, Z, d2, (int)n, (int)d2, (int)n2, 1.0, 0.0, nullptr, nullptr);
     }
     OTF_HIP(hipGetLastError());
     // M = -2 X^T Z + t1[:, None] + t2[None, :]   (d x d2, sum over the n samples)
-    dim3 grid((unsigned)((d2 + otf::GT - 1) / otf::GT), (unsigned)((d + otf::GT - 1) / otf::GT));
-    otf::gemm_kernel<float, double, double, double><<<grid, 256, 0, s>>>(
+    dim3 grid((unsigned)((d2 + GT - 1) / GT), (unsigned)((d + GT - 1) / GT));
+    gemm_kernel<TI, double, double, double><<<grid, 256, 0, s>>>(
         X, 1, ldx, Z, d2, 1, M, ldm, (int)d, (int)d2, (int)n, -2.0, 0.0, t1, t2);
     OTF_HIP(hipGetLastError());
     return OTF_OK;
+}
+}  // namespace
+}  // namespace otf
+
+extern "C" {
+
+int otf_feature_cost(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n,
+                     int64_t n2, int64_t d, int64_t d2, const double* Ts, int64_t ldts,
+                     const double* ts_diag, int32_t weights_mode, double* M, int64_t ldm,
+                     void* workspace, size_t ws_bytes, otf_stream_t stream) {
+    return otf::feature_cost_t<float>(X, ldx, Y, ldy, n, n2, d, d2, Ts, ldts, ts_diag, weights_mode,
+                                      M, ldm, workspace, ws_bytes, (hipStream_t)stream);
+}
+
+int otf_feature_cost_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy, int32_t in_dtype,
+                        int64_t n, int64_t n2, int64_t d, int64_t d2, const double* Ts,
+                        int64_t ldts, const double* ts_diag, int32_t weights_mode, double* M,
+                        int64_t ldm, void* workspace, size_t ws_bytes, otf_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    switch (in_dtype) {
+        case OTF_F32:
+            return otf::feature_cost_t<float>((const float*)X, ldx, (const float*)Y, ldy, n, n2, d, d2,
+                                              Ts, ldts, ts_diag, weights_mode, M, ldm, workspace,
+                                              ws_bytes, s);
+        case OTF_BF16:
+            return otf::feature_cost_t<otf::bf16>((const otf::bf16*)X, ldx, (const otf::bf16*)Y, ldy, n,
+                                                  n2, d, d2, Ts, ldts, ts_diag, weights_mode, M, ldm,
+                                                  workspace, ws_bytes, s);
+        case OTF_F16:
+            return otf::feature_cost_t<_Float16>((const _Float16*)X, ldx, (const _Float16*)Y, ldy, n,
+                                                 n2, d, d2, Ts, ldts, ts_diag, weights_mode, M, ldm,
+                                                 workspace, ws_bytes, s);
+        default:
+            return OTF_EINVAL;
+    }
 }
 
 size_t otf_coupled_cost_workspace_size(int64_t p, int64_t q, int64_t r) {
@@ -290,6 +390,27 @@ int otf_plan_postprocess(const void* T, int64_t d, int64_t d2, int64_t ldt, int3
     else if (dtype == OTF_F32)
         otf::postprocess_kernel<float><<<grid, 256, 0, s>>>((const float*)T, (int)d, (int)d2, ldt,
                                                             nan_fill, rownorm, Tn, ldtn);
+    else
+        return OTF_EINVAL;
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+int otf_plan_postprocess_apply(const void* T, int64_t d, int64_t d2, int64_t ldt, int32_t dtype,
+                               float nan_fill, int32_t rownorm, const float* Z, int64_t ldz,
+                               int64_t B, float* out, int64_t ldo, float* Tn, int64_t ldtn,
+                               otf_stream_t stream) {
+    if (!T || !Z || !out || d <= 0 || d2 <= 0 || B <= 0 || ldt < d2 || ldz < d2 || ldo < d ||
+        (Tn && ldtn < d2))
+        return OTF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const int grid = d < 4096 ? (int)d : 4096;
+    if (dtype == OTF_F64)
+        otf::postprocess_apply_kernel<double><<<grid, 256, 0, s>>>(
+            (const double*)T, (int)d, (int)d2, ldt, nan_fill, rownorm, Z, ldz, (int)B, out, ldo, Tn, ldtn);
+    else if (dtype == OTF_F32)
+        otf::postprocess_apply_kernel<float><<<grid, 256, 0, s>>>(
+            (const float*)T, (int)d, (int)d2, ldt, nan_fill, rownorm, Z, ldz, (int)B, out, ldo, Tn, ldtn);
     else
         return OTF_EINVAL;
     OTF_HIP(hipGetLastError());

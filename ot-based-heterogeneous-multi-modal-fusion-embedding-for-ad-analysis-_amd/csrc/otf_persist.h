@@ -11,6 +11,8 @@
 // the solve with OTF_SK_TIMEOUT instead of hanging.  The deadline is re-armed after
 // every completed barrier, so only a stall times out, never a long healthy solve.
 #pragma once
+#include <stdlib.h>
+
 #include "otf_device.h"
 
 namespace otf {
@@ -49,8 +51,14 @@ __device__ unsigned long long g_stamps[256 * 16 * 8];
     } while (0)
 #endif
 
-// 5 s of no progress at the 100 MHz s_memrealtime clock
+// No progress for this long at a device-wide wait ends the solve with OTF_SK_TIMEOUT:
+// 5 s at the 100 MHz s_memrealtime clock, or OTF_STALL_MS from the environment (tests)
 constexpr unsigned long long kStallTicks = 500000000ull;
+inline unsigned long long stall_ticks() {
+    const char* e = getenv("OTF_STALL_MS");
+    const long long ms = e ? atoll(e) : 0;
+    return ms > 0 ? (unsigned long long)ms * 100000ull : kStallTicks;
+}
 
 // XCD this wave runs on (0..7).  Only speed depends on it (replica choice, grouping).
 __device__ __forceinline__ int xcc_id() {

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include "otf_persist.h"
+#include "otf_comm.h"
 
 namespace otf {
 namespace {
@@ -1543,7 +1544,7 @@ hipError_t run_resident(const PassCfg& cfg, int grid, const CT* C, int64_t ldc, 
     p.P = P_out;
     p.ldp = ldp;
     p.p_f64 = P_dtype == OTF_F64;
-    p.timeout_ticks = kStallTicks;
+    p.timeout_ticks = stall_ticks();
     hipError_t e = hipMemsetAsync(w.res, 0, w.res_bytes, s);
     if (e != hipSuccess) return e;
     if (P_out && P_dtype == OTF_F64) return launch_resident<T, CT, double>(cfg, grid, p, s);
@@ -1607,7 +1608,7 @@ hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const T* cost_scale
     p.v_out = v_out;
     p.P = P_out;
     p.ldp = ldp;
-    p.timeout_ticks = kStallTicks;
+    p.timeout_ticks = stall_ticks();
     hipError_t e = hipMemsetAsync(w.res, 0, w.res_bytes, s);
     if (e != hipSuccess) return e;
     const int grid = (int)(w.t_nrb * w.t_ncb);
@@ -1741,6 +1742,15 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     rc = sk_init<T>(su, a, b, n, m, info, s);
     if (rc != OTF_OK) return rc;
 
+    // deterministic mode: only the sweep engine reduces the column sums in a fixed order
+    if (o.deterministic) {
+        if (LOG || avg_pass_ms || !(o.engine == OTF_ENGINE_AUTO || o.engine == OTF_ENGINE_SWEEP) ||
+            o.max_iter < 1 || !sweep_supported<T, CT>(n, m, ldc) || !(o.n_total <= 0 || o.n_total == n))
+            return OTF_EUNSUPPORTED;
+        return check_hip(run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
+                                          (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
+                                          v_out, P_out, ldp, P_dtype, info, errlog, s));
+    }
     // resident engine: the whole solve in one persistent launch when every row block
     // gets its own CU (POT flavour, no per-pass profiling requested)
     const bool whole = o.n_total <= 0 || o.n_total == n;
@@ -1979,6 +1989,29 @@ int otf_sinkhorn_pass(const void* a, const void* b, const void* C, int64_t n, in
                                                 n, m, ldc, (const double*)cost_scale, o, pass, info,
                                                 errlog, workspace, ws_bytes, colsum, colsum_len, s);
     return OTF_EINVAL;
+}
+
+int otf_sinkhorn_row_sharded(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                             int64_t ldc, int32_t dtype, const void* cost_scale,
+                             const otf_sinkhorn_opts* opts, otf_comm* comm, void* u_out,
+                             void* v_out, void* P_out, int64_t ldp, int32_t P_dtype,
+                             otf_sinkhorn_info* info, double* errlog, void* workspace,
+                             size_t ws_bytes, otf_stream_t stream) {
+    if (!opts) return OTF_EINVAL;
+    if (opts->flavor != OTF_FLAVOR_POT) return OTF_EUNSUPPORTED;
+    for (int32_t pass = 0; pass <= opts->max_iter; ++pass) {
+        void* cs = nullptr;
+        int64_t len = 0;
+        int rc = otf_sinkhorn_pass(a, b, C, n, m, ldc, dtype, cost_scale, opts, pass, info, errlog,
+                                   workspace, ws_bytes, &cs, &len, stream);
+        if (rc != OTF_OK) return rc;
+        if (comm) {
+            rc = otf::comm_all_reduce(cs, len, dtype, OTF_RED_SUM, comm, (hipStream_t)stream);
+            if (rc != OTF_OK) return rc;
+        }
+    }
+    return otf_sinkhorn_finish(a, b, C, n, m, ldc, dtype, cost_scale, opts, u_out, v_out, P_out,
+                               ldp, P_dtype, info, errlog, workspace, ws_bytes, stream);
 }
 
 int otf_sinkhorn_finish(const void* a, const void* b, const void* C, int64_t n, int64_t m,

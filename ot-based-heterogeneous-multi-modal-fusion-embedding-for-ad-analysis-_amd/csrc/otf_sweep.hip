@@ -64,6 +64,7 @@ template <typename T> struct SkSweepArgs {
     int64_t ldp;
     unsigned long long stall_ticks;
     int nt_loads;       // 1: cost larger than the Infinity Cache, stream it non-temporal
+    int det;            // 1: fixed-order column sums (one group = the whole grid, no atomics)
 };
 
 using Raw = __attribute__((ext_vector_type(4))) unsigned int;  // 16 B of cost
@@ -371,10 +372,17 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         s_pop[4] = base;
     }
     __syncthreads();
-    const int nx = s_pop[0], nact = s_pop[1], gslot = s_pop[3], gbase = s_pop[4];
+    const int nx = s_pop[0], nact = s_pop[1];
     const unsigned act_mask = (unsigned)s_pop[2];
+    // reduction group: the workgroups of this XCD (slot = registration order), or in the
+    // deterministic mode the whole grid by blockIdx (placement- and timing-independent
+    // order: every column sum is added in slab-row order by one workgroup, no atomics)
+    const int gsz = p.det ? nwg : nx;
+    const int gslot = p.det ? (int)blockIdx.x : s_pop[3];
+    const int gfirst = p.det ? 0 : s_pop[4];
+    int* const gctr = p.gcnt + (p.det ? 0 : xcd * 64);
     // this workgroup's column slice of the group reduction: [sl0, sl1) of m_pad
-    const int slw = ((p.m_pad + nx * VT - 1) / (nx * VT)) * VT;
+    const int slw = ((p.m_pad + gsz * VT - 1) / (gsz * VT)) * VT;
     const int sl0 = gslot * slw < p.m_pad ? gslot * slw : p.m_pad;
     const int sl1 = sl0 + slw < p.m_pad ? sl0 + slw : p.m_pad;
 
@@ -384,7 +392,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     // column slice over the group's rows in a fixed order and adds it to the slot with
     // memory-side atomics: 8 x m atomics per iteration instead of grid x m.
     int gep = 0;
-    const __amdgpu_buffer_rsrc_t srow = sums_rsrc(p.slab + (size_t)(gbase + gslot) * p.m_pad);
+    const __amdgpu_buffer_rsrc_t srow = sums_rsrc(p.slab + (size_t)(gfirst + gslot) * p.m_pad);
     auto flush = [&](int k) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -404,8 +412,8 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         __syncthreads();
         if (tid == 0) {
             int ok = 1;
-            __hip_atomic_fetch_add(p.gcnt + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while (load_agent(p.gcnt + xcd * 64) < gep * nx) {
+            __hip_atomic_fetch_add(gctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (load_agent(gctr) < gep * gsz) {
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = 0; break; }
             }
@@ -417,9 +425,9 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         // slice reduce: thread (q, j) sums rows q, q + Q, ... of vector j of the slice
         const int nv = (sl1 - sl0) / VT;
         int Q = 1;
-        while (Q * 2 <= nx && kSwNT / (Q * 2) >= nv) Q *= 2;
+        while (Q * 2 <= gsz && kSwNT / (Q * 2) >= nv) Q *= 2;
         const int W = kSwNT / Q, q = tid / W, j = tid % W;
-        const __amdgpu_buffer_rsrc_t sr = sums_rsrc(p.slab + (size_t)gbase * p.m_pad);
+        const __amdgpu_buffer_rsrc_t sr = sums_rsrc(p.slab + (size_t)gfirst * p.m_pad);
         for (int jb = 0; jb < nv; jb += W) {
             const int jv = jb + j;
             V acc;
@@ -427,7 +435,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             for (int k2 = 0; k2 < VT; ++k2) acc[k2] = 0;
             if (jv < nv) {
 #pragma unroll 4
-                for (int r = q; r < nx; r += Q) {
+                for (int r = q; r < gsz; r += Q) {
                     const V t = load_sum_vec<T>(sr, (uint32_t)(((size_t)r * p.m_pad + sl0 + jv * VT) * sizeof(T)));
 #pragma unroll
                     for (int k2 = 0; k2 < VT; ++k2) acc[k2] += t[k2];
@@ -448,7 +456,11 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         }
         T* dst = p.ring + (size_t)(k & 3) * p.slot_stride;
         const int send = sl1 < p.m ? sl1 : p.m;
-        for (int c = sl0 + tid; c < send; c += kSwNT) atomicAdd(dst + c, vbuf[c - sl0]);
+        if (p.det) {
+            for (int c = sl0 + tid; c < send; c += kSwNT) store_wt(dst + c, vbuf[c - sl0]);
+        } else {
+            for (int c = sl0 + tid; c < send; c += kSwNT) atomicAdd(dst + c, vbuf[c - sl0]);
+        }
         // slot k + 1 (= S[k - 3]) is free: this workgroup's share of it, write-through
         T* zs = p.ring + (size_t)((k + 1) & 3) * p.slot_stride;
         const int64_t per = (p.slot_stride + nwg - 1) / nwg;
@@ -760,8 +772,9 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     p.v_out = v_out;
     p.P = P_out;
     p.ldp = ldp;
-    p.stall_ticks = kStallTicks;
+    p.stall_ticks = stall_ticks();
     p.nt_loads = (double)n * ldc * sizeof(CT) > 192.0 * (1 << 20) ? 1 : 0;
+    p.det = o.deterministic ? 1 : 0;
     hipError_t e = hipMemsetAsync(region, 0, sweep_ctrl_bytes(m_pad, sizeof(T)), s);
     if (e != hipSuccess) return e;
     int R = 1;

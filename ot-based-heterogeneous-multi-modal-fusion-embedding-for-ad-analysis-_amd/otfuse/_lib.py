@@ -22,9 +22,11 @@ LIB_PATH = os.path.join(_HERE, "lib", "libotfuse.so")
 HEADER_PATH = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "otfuse.h"))
 
 OTF_OK, OTF_EINVAL, OTF_EUNSUPPORTED, OTF_EHIP = 0, 1, 2, -1
-OTF_F32, OTF_F64, OTF_F16 = 0, 1, 2
+OTF_F32, OTF_F64, OTF_F16, OTF_BF16 = 0, 1, 2, 3
 OTF_SQEUCLIDEAN, OTF_EUCLIDEAN = 0, 1
 OTF_FLAVOR_POT, OTF_FLAVOR_OTT = 0, 1
+OTF_RED_SUM, OTF_RED_MAX = 0, 1
+COMM_ID_BYTES = 128
 SK_RUNNING, SK_CONVERGED, SK_MAX_ITER, SK_NUMERICAL_BREAK, SK_TIMEOUT = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "running", 1: "converged", 2: "max_iter", 3: "numerical_break",
                 4: "timeout"}
@@ -39,7 +41,8 @@ class SinkhornOpts(ctypes.Structure):
                 ("max_iter", ctypes.c_int32), ("check_every", ctypes.c_int32),
                 ("flavor", ctypes.c_int32), ("err_squared", ctypes.c_int32),
                 ("sync_every", ctypes.c_int32), ("engine", ctypes.c_int32),
-                ("cost_f16", ctypes.c_int32), ("n_total", ctypes.c_int32)]
+                ("cost_f16", ctypes.c_int32), ("n_total", ctypes.c_int32),
+                ("deterministic", ctypes.c_int32)]
 
 
 class GwOpts(ctypes.Structure):
@@ -80,6 +83,8 @@ _SIGS = {
     "otf_feature_cost_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i64]),
     "otf_feature_cost": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64,
                                         _vp, _i32, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
+    "otf_feature_cost_ex": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i32, _i64, _i64, _i64, _i64, _vp,
+                                           _i64, _vp, _i32, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
     "otf_coupled_cost_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64]),
     "otf_coupled_cost": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
                                         _vp, _i64, _vp, _vp, _vp, _i64, _vp, ctypes.c_size_t,
@@ -98,8 +103,18 @@ _SIGS = {
     "otf_sinkhorn_finish": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
                                            ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _i64, _i32,
                                            _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "otf_comm_unique_id": (ctypes.c_int, [_vp]),
+    "otf_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), _vp, _i32, _i32]),
+    "otf_comm_destroy": (ctypes.c_int, [_vp]),
+    "otf_comm_all_reduce": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
+    "otf_comm_all_gather": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "otf_sinkhorn_row_sharded": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
+                                                ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _vp,
+                                                _i64, _i32, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "otf_plan_postprocess": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i32, ctypes.c_float, _i32,
                                             _vp, _i64, _vp]),
+    "otf_plan_postprocess_apply": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i32, ctypes.c_float, _i32,
+                                                  _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "otf_gemm_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
                                     ctypes.c_float, ctypes.c_float, _vp]),
     "otf_cost_pairwise_f64_workspace_size": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64]),

@@ -136,13 +136,28 @@ class DevicePasses:
     def stopped(self) -> bool:
         return bool(self.info[0].item())
 
-    def finish(self, want_plan=True, plan_dtype=None) -> ops.SinkhornResult:
+    def _outputs(self, want_plan, plan_dtype):
         dev = self.C.device
         u = torch.empty(self.n, dtype=self.dt, device=dev)
         v = torch.empty(self.m, dtype=self.dt, device=dev)
-        P = None
-        if want_plan:
-            P = ops._alloc_rowmajor(self.n, self.m, plan_dtype or self.dt, dev, 4)
+        P = ops._alloc_rowmajor(self.n, self.m, plan_dtype or self.dt, dev, 4) if want_plan else None
+        return u, v, P
+
+    def solve_with_comm(self, comm, want_plan=True, plan_dtype=None) -> ops.SinkhornResult:
+        """Every pass + its RCCL all-reduce + the finish in ONE C call
+        (otf_sinkhorn_row_sharded): no Python / host round trip per iteration."""
+        u, v, P = self._outputs(want_plan, plan_dtype)
+        L.check(L.lib().otf_sinkhorn_row_sharded(
+            *self._common(), ctypes.byref(self.opts), comm.handle if comm is not None else None,
+            u.data_ptr(), v.data_ptr(), L.ptr(P), P.stride(0) if P is not None else 0,
+            ops._DT[P.dtype] if P is not None else 0, self.info.data_ptr(), self.errlog.data_ptr(),
+            self.ws.data_ptr(), self.ws.numel(), L.stream_handle(self.C.device)),
+            "otf_sinkhorn_row_sharded")
+        return ops.SinkhornResult(u=u, v=v, plan=P, info_dev=self.info, errlog_dev=self.errlog)
+
+    def finish(self, want_plan=True, plan_dtype=None) -> ops.SinkhornResult:
+        dev = self.C.device
+        u, v, P = self._outputs(want_plan, plan_dtype)
         L.check(L.lib().otf_sinkhorn_finish(
             *self._common(), ctypes.byref(self.opts), u.data_ptr(), v.data_ptr(), L.ptr(P),
             P.stride(0) if P is not None else 0, ops._DT[P.dtype] if P is not None else 0,
@@ -155,13 +170,17 @@ def sinkhorn_row_sharded(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.
                          max_iter: int = 1000, stop_thr: float = 1e-9,
                          cost_scale: torch.Tensor | None = None, n_total: int | None = None,
                          check_every: int = 10, err_squared: bool = False, sync_every: int = 0,
-                         want_plan: bool = True, plan_dtype=None, group=None, backend=None):
+                         want_plan: bool = True, plan_dtype=None, group=None, backend=None,
+                         comm=None):
     """POT ``sinkhorn_knopp`` on a problem whose cost rows are split over the ranks.
 
     Rank r passes its rows ``C_local`` (n_r x m), ``a_local = a[R_r]`` and the full
     ``b``; the result holds this rank's rows of u and of the plan, and the full v.
-    One all-reduce(SUM) of m + 1 values per iteration.  With
-    ``sync_every`` > 0 the host polls the (rank-identical) stop flag to end early.
+    One all-reduce(SUM) of m + 1 values per iteration.  With an RCCL
+    ``comm`` (otfuse.comm.Communicator) the whole loop is one C call and the
+    all-reduces are RCCL kernels on the same stream; otherwise the passes are
+    driven from Python over torch.distributed (any backend; gloo in the CPU tests).
+    With ``sync_every`` > 0 the host polls the (rank-identical) stop flag to end early.
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if n_total is None:
@@ -172,6 +191,8 @@ def sinkhorn_row_sharded(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.
             n_total = int(t.item())
     be = (backend or DevicePasses)(a_local, b, C_local, reg, max_iter, stop_thr, cost_scale,
                                    n_total, check_every, err_squared)
+    if comm is not None and isinstance(be, DevicePasses) and sync_every == 0:
+        return be.solve_with_comm(comm, want_plan, plan_dtype)
     for p in range(max_iter + 1):
         cs = be.run_pass(p)
         if world > 1:
@@ -183,26 +204,33 @@ def sinkhorn_row_sharded(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.
 
 def coupled_solve_sharded(X_local: torch.Tensor, Y_local: torch.Tensor, reg: float,
                           max_iter: int = 200, stop_thr: float = 0.0, cost_dtype=torch.float16,
-                          want_plan: bool = True, sync_every: int = 0, group=None):
+                          want_plan: bool = True, sync_every: int = 0, group=None, comm=None):
     """The per-epoch global OT of one large problem over the data-parallel ranks:
     all-gather the PET embedding shards (RCCL), cost rows of this rank's MRI shard
     against every PET embedding (fp16 storage by default, BASELINE config 5), one
     all-reduce(MAX) for scale_cost="max_cost", then the row-sharded Sinkhorn with
     uniform marginals.  Returns (SinkhornResult of this rank's rows, n_total)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    Y_all = all_gather_rows(Y_local, group) if world > 1 else Y_local
+    if comm is not None and world > 1:   # equal shards: one RCCL all-gather on the stream
+        Y_all = comm.all_gather(Y_local)
+    else:
+        Y_all = all_gather_rows(Y_local, group) if world > 1 else Y_local
     C, cmax, unit = ops.pairwise_cost_ex(X_local, Y_all, zero_diag=False, out_dtype=cost_dtype)
     # the max in true cost units, agreed over ranks; each rank's stored unit may differ
     gmax = cmax * unit
-    n = torch.tensor([X_local.shape[0]], dtype=torch.int64, device=X_local.device)
-    if world > 1:
-        dist.all_reduce(gmax, op=dist.ReduceOp.MAX, group=group)
-        dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
-    n_total = int(n.item())
+    if comm is not None:
+        comm.all_reduce(gmax, op="max")
+        n_total = X_local.shape[0] * comm.nranks
+    else:
+        n = torch.tensor([X_local.shape[0]], dtype=torch.int64, device=X_local.device)
+        if world > 1:
+            dist.all_reduce(gmax, op=dist.ReduceOp.MAX, group=group)
+            dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
+        n_total = int(n.item())
     m = Y_all.shape[0]
     a = torch.full((X_local.shape[0],), 1.0 / n_total, dtype=torch.float32, device=X_local.device)
     b = torch.full((m,), 1.0 / m, dtype=torch.float32, device=X_local.device)
     res = sinkhorn_row_sharded(a, b, C, reg, max_iter=max_iter, stop_thr=stop_thr,
                                cost_scale=gmax / unit, n_total=n_total, sync_every=sync_every,
-                               want_plan=want_plan, group=group)
+                               want_plan=want_plan, group=group, comm=comm)
     return res, n_total

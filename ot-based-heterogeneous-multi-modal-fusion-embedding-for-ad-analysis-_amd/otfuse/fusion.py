@@ -4,9 +4,13 @@ The reference (MRI_PET_OT_nojax.py:679-725) copies ``mri_fused`` / ``pet_fused``
 the host, runs POT in float64, copies the plan back and post-processes it in
 torch.  Here the whole block stays on the device and in HIP kernels:
 
-    feature cost (float64, Ts = I/B)  ->  POT-flavour Sinkhorn (float64, eps 1e-2,
-    2000 iterations, stopThr 1e-9)  ->  NaN -> 1e-8 + row normalisation (float32)
-    ->  ot_mri_from_pet = pet_fused @ T^T (HIP GEMM, autograd)  ->  cosine loss.
+    feature cost (float64, Ts = I/B; float32 / bf16 / fp16 embeddings read as
+    stored)  ->  POT-flavour Sinkhorn (float64, eps 1e-2, 2000 iterations, stopThr
+    1e-9, one persistent launch, no host sync)  ->  ONE fused kernel: NaN -> 1e-8 + row
+    normalisation (float32) and ot_mri_from_pet = pet_fused @ T^T (autograd: G @ T)
+    ->  cosine loss, zeroed with its gradients when non-finite (the reference's
+    NaN -> 0 at :724-725 replaces the loss by a constant) or when the solve reported a
+    stalled device barrier (decided on the device: no host sync).
 
 ``group_features_by_label`` mirrors MRI_PET_OT_nojax.py:884-903 for the per-epoch path.
 """
@@ -32,7 +36,7 @@ def cosine_loss(x, y):
 
 
 def batch_feature_plan(mri_fused: torch.Tensor, pet_fused: torch.Tensor, eps: float = 1e-2,
-                       numItermax: int = 2000, stopThr: float = 1e-9, sync_every: int = 50):
+                       numItermax: int = 2000, stopThr: float = 1e-9, sync_every: int = 0):
     """PET->MRI feature coupling of one batch, Ts = eye(B)/B (MRI_PET_OT_nojax.py:683-699).
     Returns the raw float64 plan (d, d) and the SinkhornResult."""
     B = mri_fused.shape[0]
@@ -43,6 +47,51 @@ def batch_feature_plan(mri_fused: torch.Tensor, pet_fused: torch.Tensor, eps: fl
     return res.plan, res
 
 
+class _OTAlignLoss(torch.autograd.Function):
+    """ot_mri_from_pet = pet_fused @ Tn^T and cosine_loss(mri_fused, ot_mri_from_pet) as
+    one autograd node (MRI_PET_OT_nojax.py:702-725).  ``raw=True``: T is the raw
+    Sinkhorn plan and the post-processing is fused into the apply
+    (otf_plan_postprocess_apply, one pass); else T is the plan to apply as given.
+    A non-finite loss -- or ``ok`` false (a stalled solve, decided on the device) --
+    becomes a constant 0 that sends no gradient to mri_fused / pet_fused, like the
+    reference's swap for torch.tensor(0.0) at :724-725.  The loss gradients are formed
+    in forward (B x d, cheap) so the zeroing is a select, never 0 * NaN."""
+
+    @staticmethod
+    def forward(ctx, mri, pet, T, ok, raw):
+        ctx.set_materialize_grads(False)   # an unused ot_mri_from_pet sends None, not zeros
+        if raw:
+            ot, Tn = ops.plan_postprocess_apply(T, pet)
+        else:
+            Tn = T.float().contiguous()
+            ot = ops.gemm_f32(pet.float(), Tn, transpose_b=True)
+        with torch.enable_grad():
+            xd = mri.detach().float().requires_grad_(True)
+            yd = ot.detach().requires_grad_(True)
+            loss = cosine_loss(xd, yd)
+            gx, gy = torch.autograd.grad(loss, (xd, yd))
+        keep = torch.isfinite(loss.detach()) & ok
+        zero = torch.zeros((), dtype=loss.dtype, device=loss.device)
+        ctx.save_for_backward(torch.where(keep, gx, zero), torch.where(keep, gy, zero), Tn, keep)
+        ctx.dtypes = (mri.dtype, pet.dtype)
+        ctx.mark_non_differentiable(Tn)
+        return torch.where(keep, loss.detach(), zero), ot, Tn
+
+    @staticmethod
+    def backward(ctx, g_loss, g_ot, _g_tn):
+        gx, gy, Tn, keep = ctx.saved_tensors
+        if g_loss is None:
+            g_loss = torch.zeros((), dtype=gx.dtype, device=gx.device)
+        g_mri = g_loss * gx
+        gyt = g_loss * gy
+        if g_ot is not None:
+            gpet = ops.gemm_f32((gyt + g_ot).contiguous(), Tn)
+        else:   # only the loss used ot: exact zeros when it was dropped (Tn may hold NaN)
+            gpet = torch.where(keep, ops.gemm_f32(gyt.contiguous(), Tn),
+                               torch.zeros((), dtype=gyt.dtype, device=gyt.device))
+        return g_mri.to(ctx.dtypes[0]), gpet.to(ctx.dtypes[1]), None, None, None
+
+
 def ot_alignment_loss(mri_fused: torch.Tensor, pet_fused: torch.Tensor,
                       T_feature_pet2mri: torch.Tensor | None = None, eps: float = 1e-2,
                       numItermax: int = 2000, stopThr: float = 1e-9):
@@ -50,16 +99,20 @@ def ot_alignment_loss(mri_fused: torch.Tensor, pet_fused: torch.Tensor,
 
     Returns ``(ot_loss, ot_mri_from_pet, T)``; T is the post-processed float32 plan.
     A provided ``T_feature_pet2mri`` is applied as is (the reference skips the
-    post-processing for a given plan).  A NaN loss becomes 0 without a host sync.
+    post-processing for a given plan).  A NaN loss becomes 0 (and contributes no
+    gradient) without a host sync; so does the loss of a solve whose device barrier
+    stalled (status timeout), instead of training on an invalid plan.
     """
+    ok = torch.ones((), dtype=torch.bool, device=mri_fused.device)
     if T_feature_pet2mri is None:
-        plan, _ = batch_feature_plan(mri_fused, pet_fused, eps, numItermax, stopThr)
-        T = ops.plan_postprocess(plan, nan_fill=1e-8, rownorm=True)
+        plan, res = batch_feature_plan(mri_fused, pet_fused, eps, numItermax, stopThr)
+        info = res.info_dev
+        from . import _lib as L
+        ok = (info[3] != L.SK_TIMEOUT) & (info[7] == 0)
+        ot_loss, ot_mri_from_pet, T = _OTAlignLoss.apply(mri_fused, pet_fused, plan, ok, True)
     else:
-        T = T_feature_pet2mri.float()
-    ot_mri_from_pet = ops.apply_plan(pet_fused, T)
-    ot_loss = cosine_loss(mri_fused, ot_mri_from_pet)
-    ot_loss = torch.nan_to_num(ot_loss, nan=0.0)
+        ot_loss, ot_mri_from_pet, T = _OTAlignLoss.apply(mri_fused, pet_fused, T_feature_pet2mri,
+                                                         ok, False)
     return ot_loss, ot_mri_from_pet, T
 
 

@@ -16,6 +16,7 @@ from . import _lib as L
 
 _VEC = {torch.float32: 4, torch.float64: 2, torch.float16: 8}   # elements per 16 B
 _DT = {torch.float32: L.OTF_F32, torch.float64: L.OTF_F64, torch.float16: L.OTF_F16}
+_EMB_DT = {torch.float32: L.OTF_F32, torch.bfloat16: L.OTF_BF16, torch.float16: L.OTF_F16}
 
 
 def _dev(t: torch.Tensor, name: str):
@@ -144,14 +145,18 @@ def feature_cost(X: torch.Tensor, Y: torch.Tensor, Ts: torch.Tensor | None = Non
 
     ``weights="pot"``: w1 = Ts.sum(1), w2 = Ts.sum(0) (get_feature_coupling_pot);
     ``weights="fot"``: w1 = Ts.sum(0), w2 = Ts.sum(1) (perturbot fot.py:109-118).
-    Give ``Ts`` (n, n2) or its diagonal ``ts_diag`` (n,).
+    Give ``Ts`` (n, n2) or its diagonal ``ts_diag`` (n,).  X, Y may be float32,
+    bfloat16 or float16 (BASELINE config 4: bf16 encoder outputs): the kernels read them
+    as stored and widen each element exactly to float32, the reference's arithmetic on
+    the rounded values; other dtypes are cast to float32.
     """
     _dev(X, "X")
     _dev(Y, "Y")
     if (Ts is None) == (ts_diag is None):
         raise ValueError("pass exactly one of Ts / ts_diag")
-    X = _rowmajor(X.float())
-    Y = _rowmajor(Y.float())
+    edt = X.dtype if (X.dtype == Y.dtype and X.dtype in _EMB_DT) else torch.float32
+    X = _rowmajor(X.to(edt))
+    Y = _rowmajor(Y.to(edt))
     n, d = X.shape
     n2, d2 = Y.shape
     if Ts is not None:
@@ -167,10 +172,10 @@ def feature_cost(X: torch.Tensor, Y: torch.Tensor, Ts: torch.Tensor | None = Non
     lib = L.lib()
     wsb = lib.otf_feature_cost_workspace_size(n, n2, d, d2)
     ws = torch.empty(wsb, dtype=torch.uint8, device=X.device)
-    L.check(lib.otf_feature_cost(
-        X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, n2, d, d2, L.ptr(Ts),
+    L.check(lib.otf_feature_cost_ex(
+        X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), _EMB_DT[edt], n, n2, d, d2, L.ptr(Ts),
         Ts.stride(0) if Ts is not None else 0, L.ptr(ts_diag), mode, M.data_ptr(), M.stride(0),
-        ws.data_ptr(), wsb, L.stream_handle(X.device)), "otf_feature_cost")
+        ws.data_ptr(), wsb, L.stream_handle(X.device)), "otf_feature_cost_ex")
     return M
 
 
@@ -243,13 +248,16 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
              stop_thr: float = 1e-9, flavor: str = "pot", cost_scale: torch.Tensor | None = None,
              check_every: int = 10, err_squared: bool = False, sync_every: int = 0,
              want_plan: bool = True, plan_dtype=None, workspace: torch.Tensor | None = None,
-             plan_out: torch.Tensor | None = None, engine: str = "auto") -> SinkhornResult:
+             plan_out: torch.Tensor | None = None, engine: str = "auto",
+             deterministic: bool = False) -> SinkhornResult:
     """Entropic OT on the device.  ``flavor="pot"`` is POT's sinkhorn_knopp (u, v scalings,
     revert-and-break), ``flavor="ott"`` OTT's lse-mode solver (potentials f, g).
 
     ``cost_scale`` (device scalar) divides the cost first (scale_cost="max_cost").
     Compute dtype = ``C.dtype`` (float32 or float64); a float16 ``C`` (fp16 cost
-    storage, BASELINE config 5) is computed in float32.
+    storage, BASELINE config 5) is computed in float32.  ``deterministic=True``
+    reduces the column sums in a fixed order without float atomics (sweep engine, POT
+    flavour): bitwise-identical results run to run.
     """
     _dev(C, "C")
     if C.dtype not in _VEC:
@@ -281,7 +289,8 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
                           check_every=int(check_every),
                           flavor=L.OTF_FLAVOR_OTT if flavor == "ott" else L.OTF_FLAVOR_POT,
                           err_squared=int(err_squared), sync_every=int(sync_every),
-                          engine=L.ENGINES[engine], cost_f16=int(cost_f16))
+                          engine=L.ENGINES[engine], cost_f16=int(cost_f16),
+                          deterministic=int(bool(deterministic)))
     L.check(L.lib().otf_sinkhorn(
         a.data_ptr(), b.data_ptr(), C.data_ptr(), n, m, C.stride(0), _DT[dt], L.ptr(cost_scale),
         ctypes.byref(opts), u.data_ptr(), v.data_ptr(), L.ptr(P), P.stride(0) if P is not None else 0,
@@ -349,6 +358,46 @@ def gemm_f32(A: torch.Tensor, B: torch.Tensor, transpose_b: bool = False) -> tor
                                  out.data_ptr(), out.stride(0), M, N, K, 1.0, 0.0,
                                  L.stream_handle(A.device)), "otf_gemm_f32")
     return out
+
+
+def plan_postprocess_apply(T: torch.Tensor, Z: torch.Tensor, nan_fill: float = 1e-8,
+                           rownorm: bool = True):
+    """Fused MRI_PET_OT_nojax.py:702-718 in one pass over the plan: returns
+    ``(Z @ Tn^T, Tn)`` with Tn the post-processed float32 plan (NaN -> nan_fill, rows
+    normalised, zero rows -> 1e-8) -- otf_plan_postprocess_apply."""
+    _dev(T, "T")
+    _dev(Z, "Z")
+    T = _rowmajor(T if T.dtype in (torch.float32, torch.float64) else T.double())
+    Z = Z.float().contiguous()
+    d, d2 = T.shape
+    B = Z.shape[0]
+    if Z.dim() != 2 or Z.shape[1] != d2:
+        raise ValueError(f"Z {tuple(Z.shape)} must be (B, {d2})")
+    out = torch.empty((B, d), dtype=torch.float32, device=T.device)
+    Tn = torch.empty((d, d2), dtype=torch.float32, device=T.device)
+    L.check(L.lib().otf_plan_postprocess_apply(
+        T.data_ptr(), d, d2, T.stride(0), _DT[T.dtype], float(nan_fill), int(rownorm), Z.data_ptr(),
+        Z.stride(0), B, out.data_ptr(), out.stride(0), Tn.data_ptr(), Tn.stride(0),
+        L.stream_handle(T.device)), "otf_plan_postprocess_apply")
+    return out, Tn
+
+
+class PostprocessApply(torch.autograd.Function):
+    """``Z @ Tn^T`` with Tn = post-processed raw plan T (constant): one fused kernel
+    forward, ``G @ Tn`` backward (MRI_PET_OT_nojax.py:702-718)."""
+
+    @staticmethod
+    def forward(ctx, Z, T):
+        out, Tn = plan_postprocess_apply(T, Z)
+        ctx.save_for_backward(Tn)
+        ctx.zdtype = Z.dtype
+        ctx.mark_non_differentiable(Tn)
+        return out, Tn
+
+    @staticmethod
+    def backward(ctx, grad, _gtn):
+        (Tn,) = ctx.saved_tensors
+        return gemm_f32(grad.contiguous(), Tn).to(ctx.zdtype), None
 
 
 class PlanApply(torch.autograd.Function):

@@ -37,9 +37,11 @@ def test_version_and_workspace_queries_are_host_only():
 def test_abi_structs_and_enums_match_header():
     from otfuse import _lib as L
     src = open(L.HEADER_PATH).read()
-    assert ctypes.sizeof(L.SinkhornOpts) == 48
+    assert ctypes.sizeof(L.SinkhornOpts) == 56   # 2 doubles + 9 int32, 8-aligned
     assert L.INFO_INT32S * 4 == 32
-    for name, val in [("OTF_F32", 0), ("OTF_F64", 1), ("OTF_F16", 2), ("OTF_FLAVOR_POT", 0),
+    for name, val in [("OTF_F32", 0), ("OTF_F64", 1), ("OTF_F16", 2), ("OTF_BF16", 3),
+                      ("OTF_ENGINE_SWEEP", 4), ("OTF_RED_SUM", 0), ("OTF_RED_MAX", 1),
+                      ("OTF_FLAVOR_POT", 0),
                       ("OTF_FLAVOR_OTT", 1),
                       ("OTF_SK_CONVERGED", 1), ("OTF_SK_MAX_ITER", 2),
                       ("OTF_SK_NUMERICAL_BREAK", 3)]:

@@ -1,0 +1,239 @@
+"""BASELINE configs 3 and 4 at their real sizes against the oracle, plus the boundary
+pieces added for them (needs an MI355X).
+
+* Config 3 -- the per-epoch chain of MRI_PET_OT_OT_per_epoch_attn.py:940-960: 2 labels x
+  64 samples of d = 2048 backbone features (depth >= 50: 512 x 4), per-label entropic GW
+  (get_coupling_egw_ott_fixed), then get_coupling_fot on the 2048 x 2048 float64
+  feature cost at eps = 5e-3; and the POT form of the same chain (get_feature_coupling_pot
+  with the block-diagonal GW plans, MRI_PET_OT_nojax.py:1110-1111).  OTT is absent, so
+  the OTT-flavour steps are checked against the oracle's restatements (parity unpinned);
+  the POT step is pinned like F2/F4 (float64, 1e-9).
+* Config 4 -- MRI_T1_T2_OT.py:708-745 with bf16 encoder outputs: the bf16 embeddings go
+  through ot_alignment_loss natively (otf_feature_cost_ex reads bf16); the reference
+  is the oracle on the bf16-rounded values upcast to float32 (what the reference's
+  float32 NumPy arrays would hold).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def nrel(x, ref):
+    x = np.asarray(x, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    return np.abs(x - ref).max() / np.abs(ref).max()
+
+
+def _emb(n, d, seed):
+    from otfuse.synthetic import paired_embeddings
+    return paired_embeddings(n, d, seed=seed)
+
+
+@pytest.fixture(scope="module")
+def config3(dev):
+    """2 labels x 64 paired samples, d = 2048, and the device EGW plans."""
+    from otfuse import perturbot
+    pet, mri = {}, {}
+    for k in range(2):
+        X, Y, _ = _emb(64, 2048, 900 + k)
+        mri[k], pet[k] = X, Y
+    Ts, log = perturbot.get_coupling_egw_ott_fixed((pet, mri), eps=5e-3)
+    return pet, mri, Ts, log
+
+
+def test_config3_egw_per_label_vs_oracle(config3, orc):
+    pet, mri, Ts, log = config3
+    for k in pet:
+        C1, _ = orc.pairwise_cost(pet[k], pet[k], scale_max=True)
+        C2, _ = orc.pairwise_cost(mri[k], mri[k], scale_max=True)
+        Pr, ref = orc.gw_entropic(C1, C2, 5e-3)
+        assert log[k]["n_iters_outer"] == ref["n_iters"]
+        assert nrel(Ts[k], Pr) < 1e-4
+
+
+def test_config3_get_coupling_fot_2048_vs_oracle(config3, orc):
+    """get_coupling_fot on the 2048^2 float64 feature cost (fot.py:108-134): normalised
+    block-diagonal Ts, column-sum w1, OTT max-cost Sinkhorn at eps = 5e-3."""
+    from otfuse import perturbot
+    pet, mri, Ts, _ = config3
+    Tv, log = perturbot.get_coupling_fot((pet, mri), Ts, eps=5e-3)
+    assert Tv.shape == (2048, 2048) and np.isfinite(Tv).all()
+    X = np.concatenate([pet[k] for k in pet])
+    Y = np.concatenate([mri[k] for k in pet])
+    Tfull = perturbot.mdict_to_matrix(Ts, np.repeat([0, 1], 64), np.repeat([0, 1], 64))
+    Tfull = Tfull / Tfull.sum()
+    M = orc.feature_cost(X, Y, Tfull, weights="fot")
+    orc.set_threads(16)
+    u = np.full(2048, 1.0 / 2048)
+    Pr, _, _, info = orc.sinkhorn_log(u, u, M, 5e-3, max_iter=2000, threshold=1e-3,
+                                      cscale=1.0 / M.max())
+    assert nrel(Tv, Pr) < 1e-8
+    np.testing.assert_allclose(Tv.sum(1), 1.0 / 2048, rtol=1e-6)
+
+
+def test_config3_pot_form_2048_vs_oracle(config3, orc):
+    """POT form of the per-epoch chain: get_feature_coupling_pot with the block-diagonal
+    GW plans (MRI_PET_OT_nojax.py:91-145), 2048^2 float64, eps = 5e-3, 2000 iterations,
+    stopThr 1e-9 -- against the oracle at 1e-9 with the same iteration count."""
+    from otfuse import pot
+    pet, mri, Ts, _ = config3
+    Tf, _ = pot.get_feature_coupling_pot((pet, mri), Ts, eps=5e-3)
+    X = np.concatenate([pet[k] for k in sorted(pet)])
+    Y = np.concatenate([mri[k] for k in sorted(pet)])
+    Tbd = orc.block_diag_ts(Ts, pet, mri)
+    M = orc.feature_cost(X, Y, Tbd)
+    orc.set_threads(16)
+    u = np.full(2048, 1.0 / 2048)
+    Pr, *_ = orc.sinkhorn_knopp(u, u, M, 5e-3, 2000, 1e-9)
+    assert Tf.shape == (2048, 2048)
+    assert nrel(Tf, Pr) < 1e-9
+
+
+@pytest.mark.parametrize("d", [512, 2048])
+def test_config4_bf16_embeddings_through_ot_alignment_loss(orc, dev, d):
+    from otfuse import ops
+    from otfuse.fusion import cosine_loss, ot_alignment_loss
+    X, Y, _ = _emb(8, d, 40 + d)
+    mri = torch.as_tensor(X, device=dev).to(torch.bfloat16).requires_grad_(True)
+    pet = torch.as_tensor(Y, device=dev).to(torch.bfloat16).requires_grad_(True)
+    loss, ot_mri, T = ot_alignment_loss(mri, pet, eps=1e-2)
+    # native bf16 read == the same kernels on the upcast values, bit for bit
+    ts = torch.full((8,), 1.0 / 8, dtype=torch.float64, device=dev)
+    assert torch.equal(ops.feature_cost(mri.detach(), pet.detach(), ts_diag=ts),
+                       ops.feature_cost(mri.detach().float(), pet.detach().float(), ts_diag=ts))
+    # oracle: the reference's chain on the bf16-rounded float32 arrays
+    Xr = mri.detach().float().cpu().numpy()
+    Yr = pet.detach().float().cpu().numpy()
+    M = orc.feature_cost(Xr, Yr, np.eye(8) / 8)
+    u = np.full(d, 1.0 / d)
+    P, *_ = orc.sinkhorn_knopp(u, u, M, 1e-2, 2000, 1e-9)
+    Tn = np.nan_to_num(P.astype(np.float32), nan=1e-8)
+    rs = Tn.sum(1, keepdims=True)
+    Tn = Tn / np.where(rs == 0, 1e-8, rs)
+    np.testing.assert_allclose(T.cpu().numpy(), Tn, rtol=1e-4, atol=1e-9)
+    Zr = Yr @ Tn.T
+    np.testing.assert_allclose(ot_mri.detach().cpu().numpy(), Zr, rtol=1e-4, atol=1e-6)
+    lr = float(cosine_loss(torch.from_numpy(Xr), torch.from_numpy(Zr)))
+    assert abs(float(loss) - lr) < 1e-4
+    loss.backward()
+    assert mri.grad.dtype == torch.bfloat16 and pet.grad.dtype == torch.bfloat16
+    assert torch.isfinite(mri.grad.float()).all() and torch.isfinite(pet.grad.float()).all()
+
+
+# ------------------------------------------------------------------ boundary pieces
+def test_fused_postprocess_apply_vs_torch(dev):
+    from otfuse import ops
+    g = torch.Generator(device=dev).manual_seed(5)
+    T = torch.rand(300, 200, dtype=torch.float64, device=dev, generator=g)
+    T[3, 7] = float("nan")
+    T[10] = 0
+    Z = torch.randn(20, 200, device=dev, generator=g)          # B = 20 > one 16-row block
+    out, Tn = ops.plan_postprocess_apply(T, Z)
+    Tr = T.float()
+    Tr = torch.where(torch.isnan(Tr), torch.full_like(Tr, 1e-8), Tr)
+    rs = Tr.sum(1, keepdim=True)
+    Tr = Tr / torch.where(rs == 0, torch.full_like(rs, 1e-8), rs)
+    assert torch.allclose(Tn, Tr, rtol=1e-6, atol=0)
+    assert torch.allclose(out, Z @ Tr.t(), rtol=1e-4, atol=1e-5)
+    # autograd: d/dZ of sum(out * G) = G @ Tn
+    Zg = Z.clone().requires_grad_(True)
+    o, _ = ops.PostprocessApply.apply(Zg, T)
+    G = torch.randn_like(o)
+    (o * G).sum().backward()
+    assert torch.allclose(Zg.grad, G @ Tr, rtol=1e-4, atol=1e-5)
+
+
+def test_nan_loss_contributes_no_gradient(dev):
+    """MRI_PET_OT_nojax.py:724-725: a NaN OT loss is replaced by a constant 0."""
+    from otfuse.fusion import ot_alignment_loss
+    X, Y, _ = _emb(8, 64, 3)
+    mri = torch.as_tensor(X, device=dev).requires_grad_(True)
+    pet = torch.as_tensor(Y, device=dev).requires_grad_(True)
+    T = torch.full((64, 64), float("nan"), device=dev)        # a given (bad) plan
+    loss, _, _ = ot_alignment_loss(mri, pet, T_feature_pet2mri=T)
+    assert float(loss) == 0.0
+    loss.backward()
+    assert torch.equal(mri.grad, torch.zeros_like(mri)) and torch.equal(pet.grad, torch.zeros_like(pet))
+
+
+@pytest.mark.parametrize("dt,n,m", [(torch.float32, 2000, 3000), (torch.float64, 700, 450),
+                                    (torch.float32, 37, 5)])
+def test_deterministic_mode_is_bitwise_reproducible(orc, dev, dt, n, m):
+    from otfuse import ops
+    rng = np.random.default_rng(n)
+    C = rng.random((n, m))
+    a = np.full(n, 1.0 / n)
+    b = np.full(m, 1.0 / m)
+    Ct, at, bt = (torch.as_tensor(x, device=dev, dtype=dt) for x in (C, a, b))
+    plans = []
+    for _ in range(3):
+        res = ops.sinkhorn(at, bt, Ct, 0.05, max_iter=80, stop_thr=0.0, deterministic=True)
+        assert res.info()["engine_name"] == "sweep"
+        plans.append(res.plan.clone())
+    assert torch.equal(plans[0], plans[1]) and torch.equal(plans[0], plans[2])
+    Pr, *_ = orc.sinkhorn_knopp(a, b, C, 0.05, 80, 0.0)
+    assert nrel(plans[0].cpu().numpy(), Pr) < (1e-4 if dt == torch.float32 else 1e-10)
+    with pytest.raises(Exception):
+        ops.sinkhorn(at, bt, Ct, 0.05, max_iter=80, deterministic=True, engine="tiled")
+
+
+def test_eot_and_leot_dropins_vs_oracle(orc, dev):
+    """get_coupling_eot_ott / get_coupling_leot_ott (perturbot ott_egwl.py:299-454):
+    PointCloud(x, y, scale_cost="max_cost") + OTT Sinkhorn, against the oracle's lse
+    restatement on the same max-scaled cost (parity unpinned: OTT absent)."""
+    from otfuse import ops, perturbot
+    X, Y, lab = _emb(96, 48, 61)
+    xd = {0: X[lab == 0][:40], 1: X[lab == 1][:40]}
+    yd = {0: Y[lab == 0][:40], 1: Y[lab == 1][:40]}
+
+    def ref(Xs, Xt):
+        C, cmax = ops.pairwise_cost(torch.as_tensor(Xs, device=dev), torch.as_tensor(Xt, device=dev))
+        Cs = ops.scale_inplace(C.double(), cmax).cpu().numpy()
+        n, m = Cs.shape
+        P, f, g, info = orc.sinkhorn_log(np.full(n, 1.0 / n), np.full(m, 1.0 / m), Cs, 5e-3)
+        return P, info
+
+    T, log = perturbot.get_coupling_eot_ott((xd, yd), eps=5e-3)
+    Xs = np.concatenate([xd[k] for k in xd])
+    Xt = np.concatenate([yd[k] for k in xd])
+    Pr, info = ref(Xs, Xt)
+    assert T.shape == (len(Xs), len(Xt)) and log["n_iters_outer"] == info["n_iters"]
+    assert nrel(T, Pr) < 1e-9
+    Td, logs = perturbot.get_coupling_leot_ott((xd, yd), eps=5e-3)
+    for k in xd:
+        Pr, info = ref(xd[k], yd[k])
+        assert logs[k]["n_iters_outer"] == info["n_iters"]
+        assert nrel(Td[k], Pr) < 1e-9
+
+
+def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch):
+    """Two persistent solves (tiled engine, a full grid each) launched together on two
+    streams cannot both be co-resident: each must either complete with the right plan
+    or report the stall cleanly (OtfError from info(), status timeout) -- never hang
+    and never return a silently wrong plan.  A short stall limit keeps it quick."""
+    from otfuse import _lib as L, ops
+    monkeypatch.setenv("OTF_STALL_MS", "300")
+    N = 4096
+    g = torch.Generator(device=dev).manual_seed(9)
+    C = torch.rand(N, N, device=dev, generator=g)
+    a = torch.full((N,), 1.0 / N, device=dev)
+    ref = ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine="stream").plan
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    outs = []
+    for s in (s1, s2):
+        with torch.cuda.stream(s):
+            outs.append(ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine="tiled"))
+    torch.cuda.synchronize()
+    for res in outs:
+        try:
+            info = res.info()
+        except L.OtfError:
+            continue                      # reported cleanly
+        assert info["status_name"] == "max_iter"
+        assert (res.plan - ref).abs().max() / ref.abs().max() < 1e-5
+    # the device is healthy afterwards
+    res = ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine="tiled")
+    assert res.info()["status_name"] == "max_iter"

@@ -21,8 +21,18 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 PROF = os.path.join(REPO, "profiles")
-HOT = ("sk_resident_kernel", "sk_tiled_kernel", "sk_pass_kernel", "cost_split16_kernel", "split16_prep2_kernel",
-       "sk_init_kernel", "sk_plan_kernel")
+HOT = ("sk_resident_kernel", "sk_tiled_kernel", "sk_pass_kernel", "sk_sweep_kernel", "cost_split16_kernel",
+       "split16_prep2_kernel", "cost_f16_kernel", "sk_init_kernel", "sk_plan_kernel")
+LIB = os.path.join(REPO, "ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd",
+                   "otfuse", "lib", "libotfuse.so")
+
+
+def lib_md5():
+    import hashlib
+    try:
+        return hashlib.md5(open(LIB, "rb").read()).hexdigest()
+    except OSError:
+        return None
 
 
 def short(name):
@@ -83,6 +93,7 @@ def main():
                           + v.get("WRITE_SIZE_bytes_corrected", 0.0)}
     if traffic:
         json.dump({"n": cfg.get("N", 4096), "iters": cfg.get("iters", 100), "round": tag,
+                   "lib_md5": lib_md5(),
                    "source": f"profiles/{tag}_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                              "with --kernel-trace --stats only, separate passes; FETCH x2 gfx950 "
                              "correction)",
