@@ -105,6 +105,12 @@ __device__ __forceinline__ double bcast_lane(double x, int r) {
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
+// 1: one raw buffer, the next block loaded as soon as the current one is widened;
+// 2: two raw buffers (ping-pong), two blocks in flight across the sweep boundary
+#ifndef OTF_SWEEP_PIPE
+#define OTF_SWEEP_PIPE 1
+#endif
+
 template <typename T, typename CT, typename TP, int G, int R, int NREP>
 __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     constexpr int VC = RawN<CT>::N;            // cost elements per 16-B chunk
@@ -170,6 +176,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         }
     const int nrb = (p.n + R - 1) / R;
     const int my_nb = nrb > (int)blockIdx.x ? (nrb - 1 - (int)blockIdx.x) / nwg + 1 : 0;
+    [[maybe_unused]] const bool even_nb = (my_nb & 1) == 0;
     const int64_t ld_bytes = p.ldc * (int64_t)sizeof(CT);
     for (int i = tid; i < my_nb * R; i += kSwNT) {
         const int row = ((int)blockIdx.x + (i / R) * nwg) * R + i % R;
@@ -263,7 +270,10 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 
     const T u0 = (T)1 / (T)p.n;
     const int xcd = xcc_id();
-    Raw bufA[R][G], bufB[R][G];
+    Raw bufA[R][G];
+#if OTF_SWEEP_PIPE != 1
+    Raw bufB[R][G];
+#endif
     T colacc[G][VC];
 
     // One sweep over this workgroup's row blocks.  it = -1: the prologue (u = u0, no
@@ -274,18 +284,30 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int k = 0; k < VC; ++k) colacc[g][k] = 0;
-        auto process = [&](int bi, Raw (&buf)[R][G]) {
+        auto process = [&](int bi, Raw (&buf)[R][G], int next) {
             const int r0 = ((int)blockIdx.x + bi * nwg) * R;
             const int nrow = p.n - r0 < R ? p.n - r0 : R;
             sanitize(buf);
             T e[R][G][VC];
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    T c[VC];
+                    widen<T, CT>(buf[r][g], c);
+#pragma unroll
+                    for (int k = 0; k < VC; ++k) e[r][g][k] = fast_exp(c[k] * ks);
+                }
+            // single-buffer pipeline: the raw block is dead once widened, so the next
+            // block's loads go out now and fly during this block's reductions
+            if (OTF_SWEEP_PIPE == 1 && next >= 0) load_block(next, buf);
             T rp[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) rp[r] = 0;
+            if (it >= 0) {
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                T vv[VC];
-                if (it >= 0) {
+                for (int g = 0; g < G; ++g) {
+                    T vv[VC];
                     // a chunk past m re-reads column 0's cost: weight it 0
                     const bool live = cnt[g] > 0;
 #pragma unroll
@@ -294,16 +316,10 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 #pragma unroll
                         for (int k2 = 0; k2 < VT; ++k2) vv[h * VT + k2] = live ? t[k2] : (T)0;
                     }
-                }
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    T c[VC];
-                    widen<T, CT>(buf[r][g], c);
+                    for (int r = 0; r < R; ++r)
 #pragma unroll
-                    for (int k = 0; k < VC; ++k) {
-                        e[r][g][k] = fast_exp(c[k] * ks);
-                        if (it >= 0) rp[r] += e[r][g][k] * vv[k];
-                    }
+                        for (int k = 0; k < VC; ++k) rp[r] += e[r][g][k] * vv[k];
                 }
             }
             T u[R];
@@ -339,13 +355,26 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                     colacc[g][k] = acc;
                 }
         };
+#if OTF_SWEEP_PIPE == 1
+        // one buffer: block bi + 1 (past the last block: the NEXT sweep's block 0, C does
+        // not change) is loaded as soon as block bi is widened
+        for (int bi = 0; bi < my_nb; ++bi) process(bi, bufA, bi + 1 < my_nb ? bi + 1 : 0);
+#else
+        // bufA holds the even blocks, bufB the odd ones; while block k is reduced, block
+        // k + 1 is in flight.  The loads that run past the last block fetch the NEXT
+        // sweep's blocks 0 and 1 (C does not change), so two blocks stay in flight across
+        // the flush, the barriers and the sums read between sweeps.
+        if (!even_nb && my_nb > 1) load_block(1, bufB);
         for (int bi = 0; bi < my_nb; bi += 2) {
-            if (bi + 1 < my_nb) load_block(bi + 1, bufB);
-            process(bi, bufA);
-            // the next sweep starts at block 0 again: keep the stream going
+            process(bi, bufA, -1);
             load_block(bi + 2 < my_nb ? bi + 2 : 0, bufA);
-            if (bi + 1 < my_nb) process(bi + 1, bufB);
+            if (bi + 1 < my_nb) {
+                process(bi + 1, bufB, -1);
+                if (bi + 3 < my_nb) load_block(bi + 3, bufB);
+                else if (even_nb) load_block(1, bufB);
+            }
         }
+#endif
     };
 
     // ---- registration: XCD population, this workgroup's slot in its XCD group and the
@@ -476,6 +505,9 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 
     // ---- prologue: S[0] = K^T u0
     if (my_nb > 0) load_block(0, bufA);
+#if OTF_SWEEP_PIPE != 1
+    if (even_nb && my_nb > 1) load_block(1, bufB);
+#endif
     sweep(-1);
     flush(0);
     int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
@@ -656,7 +688,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 constexpr int pow2_floor(int x) { return x >= 16 ? 16 : x >= 8 ? 8 : x >= 4 ? 4 : x >= 2 ? 2 : 1; }
 template <typename T, typename CT> constexpr int sweep_rows(int G) {
     return pow2_floor((OTF_SWEEP_RBUDGET / (G * RawN<CT>::N) - (int)sizeof(T)) /
-                      ((int)sizeof(T) + 2 * (int)sizeof(CT)));
+                      ((int)sizeof(T) + (OTF_SWEEP_PIPE == 1 ? 1 : 2) * (int)sizeof(CT)));
 }
 constexpr int kSwMaxG = 8;
 

@@ -7,11 +7,12 @@
 //   2->3 partials staged + atomics issued + slot zeroing   3->4 atomics performed
 //   4->5 device-wide barrier
 // Build: hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -DOTF_STAMPS -I include \
-//        -I <pkg>/csrc tools/stamps_sweep.hip -o tools/stamps_sweep
+//        -I <pkg>/csrc tools/stamps_sweep.hip -o tools/stamps_sweep -ldl
 // Run:   tools/stamps_sweep [N] [f16|f32]
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_common.hip"
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sinkhorn.hip"
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sweep.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_comm.hip"
 
 #include <cstdio>
 #include <cstring>
