@@ -65,6 +65,7 @@ template <typename T> struct SkSweepArgs {
     unsigned long long stall_ticks;
     int nt_loads;       // 1: cost larger than the Infinity Cache, stream it non-temporal
     int det;            // 1: fixed-order column sums (one group = the whole grid, no atomics)
+    int nres;           // row blocks per workgroup kept in LDS (< the fewest blocks any has)
 };
 
 using Raw = __attribute__((ext_vector_type(4))) unsigned int;  // 16 B of cost
@@ -94,6 +95,28 @@ __device__ __forceinline__ void widen(const Raw& r, T (&out)[RawN<CT>::N]) {
     }
 }
 
+// 16 B of cost -> pairs of (cost x ks) in the compute type.  fp16 x f32 in one
+// v_fma_mix_f32 per element (the fp16 -> f32 conversion is exact, so this rounds once,
+// exactly like convert-then-multiply), f32 pairs by one v_pk_mul_f32.
+template <typename T> using Pair = __attribute__((ext_vector_type(2))) T;
+template <typename T, typename CT>
+__device__ __forceinline__ void scaled_pairs(const Raw& r, T ks, Pair<T> (&out)[RawN<CT>::N / 2]) {
+    if constexpr (sizeof(CT) == 2 && sizeof(T) == 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float lo, hi;
+            asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(r[q]), "v"(ks));
+            asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(hi) : "v"(r[q]), "v"(ks));
+            out[q] = Pair<T>{lo, hi};
+        }
+    } else {
+        T c[RawN<CT>::N];
+        widen<T, CT>(r, c);
+#pragma unroll
+        for (int j = 0; j < RawN<CT>::N / 2; ++j) out[j] = Pair<T>{c[2 * j], c[2 * j + 1]} * ks;
+    }
+}
+
 // value of lane r (uniform result)
 __device__ __forceinline__ float bcast_lane(float x, int r) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), r));
@@ -105,11 +128,6 @@ __device__ __forceinline__ double bcast_lane(double x, int r) {
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
-// 1: one raw buffer, the next block loaded as soon as the current one is widened;
-// 2: two raw buffers (ping-pong), two blocks in flight across the sweep boundary
-#ifndef OTF_SWEEP_PIPE
-#define OTF_SWEEP_PIPE 1
-#endif
 
 template <typename T, typename CT, typename TP, int G, int R, int NREP>
 __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
@@ -125,6 +143,9 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     T* uhist = vbuf + p.m_pad;                                       // [2][kSwRowMax]
     T* ialds = uhist + 2 * kSwRowMax;                                // 1 / a of own rows
     T* gred = ialds + kSwRowMax;                                     // [kSwNT * VT] group reduce
+    // the workgroup's last nres row blocks (sanitized raw cost, thread-private 16-B slots):
+    // read from LDS instead of the memory system on every sweep after the prologue
+    Raw* resb = reinterpret_cast<Raw*>(gred + kSwNT * VT);
     __shared__ T red[2][NW][R];
     __shared__ T ered[17];
     __shared__ int s_flag;
@@ -176,7 +197,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         }
     const int nrb = (p.n + R - 1) / R;
     const int my_nb = nrb > (int)blockIdx.x ? (nrb - 1 - (int)blockIdx.x) / nwg + 1 : 0;
-    [[maybe_unused]] const bool even_nb = (my_nb & 1) == 0;
+    const int res0 = my_nb - p.nres;  // first LDS-resident block (nres < every my_nb)
     const int64_t ld_bytes = p.ldc * (int64_t)sizeof(CT);
     for (int i = tid; i < my_nb * R; i += kSwNT) {
         const int row = ((int)blockIdx.x + (i / R) * nwg) * R + i % R;
@@ -270,11 +291,15 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 
     const T u0 = (T)1 / (T)p.n;
     const int xcd = xcc_id();
-    Raw bufA[R][G];
-#if OTF_SWEEP_PIPE != 1
-    Raw bufB[R][G];
+#ifdef OTF_STAMPS
+    if (tid == 0 && blockIdx.x < 256) g_stamps[(blockIdx.x * 16 + 15) * 8 + 7] = (unsigned long long)xcd;
 #endif
-    T colacc[G][VC];
+    Raw bufA[R][G];
+    // column partials as pairs of adjacent columns: the e * u products go out as packed
+    // FMAs (v_pk_fma_f32), as do the e * v row-sum products
+    using T2 = Pair<T>;
+    constexpr int VP2 = VC / 2;
+    T2 colacc[G][VP2];
 
     // One sweep over this workgroup's row blocks.  it = -1: the prologue (u = u0, no
     // row sums).  bufA holds block 0's cost on entry (already in flight).
@@ -283,44 +308,64 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int k = 0; k < VC; ++k) colacc[g][k] = 0;
+            for (int k = 0; k < VP2; ++k) colacc[g][k] = T2{0, 0};
         auto process = [&](int bi, Raw (&buf)[R][G], int next) {
             const int r0 = ((int)blockIdx.x + bi * nwg) * R;
             const int nrow = p.n - r0 < R ? p.n - r0 : R;
             sanitize(buf);
-            T e[R][G][VC];
+            if (it < 0 && bi >= res0) {  // prologue: keep this block in LDS
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int g = 0; g < G; ++g) resb[(((bi - res0) * R + r) * G + g) * kSwNT + tid] = buf[r][g];
+            }
+            T2 e[R][G][VP2];
 #pragma unroll
             for (int g = 0; g < G; ++g)
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    T c[VC];
-                    widen<T, CT>(buf[r][g], c);
+                    T2 c[VP2];
+                    scaled_pairs<T, CT>(buf[r][g], ks, c);
 #pragma unroll
-                    for (int k = 0; k < VC; ++k) e[r][g][k] = fast_exp(c[k] * ks);
+                    for (int k = 0; k < VP2; ++k) e[r][g][k] = T2{fast_exp(c[k].x), fast_exp(c[k].y)};
                 }
             // single-buffer pipeline: the raw block is dead once widened, so the next
             // block's loads go out now and fly during this block's reductions
-            if (OTF_SWEEP_PIPE == 1 && next >= 0) load_block(next, buf);
+            // LDS-resident blocks come from LDS once the prologue sweep has put them there
+            if (it >= 0 && next >= res0) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int g = 0; g < G; ++g) buf[r][g] = resb[(((next - res0) * R + r) * G + g) * kSwNT + tid];
+            } else {
+                load_block(next, buf);
+            }
             T rp[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) rp[r] = 0;
             if (it >= 0) {
+                T2 rp2[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) rp2[r] = T2{0, 0};
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    T vv[VC];
+                    T2 vv[VP2];
                     // a chunk past m re-reads column 0's cost: weight it 0
                     const bool live = cnt[g] > 0;
 #pragma unroll
                     for (int h = 0; h < VC / VT; ++h) {
                         const V t = *reinterpret_cast<const V*>(vbuf + colc[g] + h * VT);
 #pragma unroll
-                        for (int k2 = 0; k2 < VT; ++k2) vv[h * VT + k2] = live ? t[k2] : (T)0;
+                        for (int k2 = 0; k2 < VT; k2 += 2)
+                            vv[(h * VT + k2) / 2] = live ? T2{t[k2], t[k2 + 1]} : T2{0, 0};
                     }
 #pragma unroll
                     for (int r = 0; r < R; ++r)
 #pragma unroll
-                        for (int k = 0; k < VC; ++k) rp[r] += e[r][g][k] * vv[k];
+                        for (int k = 0; k < VP2; ++k) rp2[r] = e[r][g][k] * vv[k] + rp2[r];
                 }
+#pragma unroll
+                for (int r = 0; r < R; ++r) rp[r] = rp2[r].x + rp2[r].y;
             }
             T u[R];
             if (it >= 0) {
@@ -348,33 +393,16 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 #pragma unroll
             for (int g = 0; g < G; ++g)
 #pragma unroll
-                for (int k = 0; k < VC; ++k) {
-                    T acc = colacc[g][k];
+                for (int k = 0; k < VP2; ++k) {
+                    T2 acc = colacc[g][k];
 #pragma unroll
-                    for (int r = 0; r < R; ++r) acc += e[r][g][k] * u[r];
+                    for (int r = 0; r < R; ++r) acc = e[r][g][k] * T2{u[r], u[r]} + acc;
                     colacc[g][k] = acc;
                 }
         };
-#if OTF_SWEEP_PIPE == 1
         // one buffer: block bi + 1 (past the last block: the NEXT sweep's block 0, C does
         // not change) is loaded as soon as block bi is widened
         for (int bi = 0; bi < my_nb; ++bi) process(bi, bufA, bi + 1 < my_nb ? bi + 1 : 0);
-#else
-        // bufA holds the even blocks, bufB the odd ones; while block k is reduced, block
-        // k + 1 is in flight.  The loads that run past the last block fetch the NEXT
-        // sweep's blocks 0 and 1 (C does not change), so two blocks stay in flight across
-        // the flush, the barriers and the sums read between sweeps.
-        if (!even_nb && my_nb > 1) load_block(1, bufB);
-        for (int bi = 0; bi < my_nb; bi += 2) {
-            process(bi, bufA, -1);
-            load_block(bi + 2 < my_nb ? bi + 2 : 0, bufA);
-            if (bi + 1 < my_nb) {
-                process(bi + 1, bufB, -1);
-                if (bi + 3 < my_nb) load_block(bi + 3, bufB);
-                else if (even_nb) load_block(1, bufB);
-            }
-        }
-#endif
     };
 
     // ---- registration: XCD population, this workgroup's slot in its XCD group and the
@@ -431,7 +459,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                 for (int h = 0; h < VC / VT; ++h) {
                     V wv;
 #pragma unroll
-                    for (int k2 = 0; k2 < VT; ++k2) wv[k2] = colacc[g][h * VT + k2];
+                    for (int k2 = 0; k2 < VT; ++k2) wv[k2] = colacc[g][(h * VT + k2) / 2][k2 & 1];
                     store_sum_vec<T>(srow, (uint32_t)((c0 + h * VT) * sizeof(T)), wv);
                 }
             }
@@ -505,9 +533,6 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 
     // ---- prologue: S[0] = K^T u0
     if (my_nb > 0) load_block(0, bufA);
-#if OTF_SWEEP_PIPE != 1
-    if (even_nb && my_nb > 1) load_block(1, bufB);
-#endif
     sweep(-1);
     flush(0);
     int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
@@ -615,7 +640,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             for (int k = 0; k < VC; ++k) vo[k] = v0;
         }
 #pragma unroll
-        for (int k = 0; k < VC; ++k) colacc[g][k] = vo[k];  // v(last_good) from here on
+        for (int k = 0; k < VC; ++k) colacc[g][k / 2][k & 1] = vo[k];  // v(last_good) from here on
         if (blockIdx.x == 0) {
 #pragma unroll
             for (int k = 0; k < VC; ++k)
@@ -647,7 +672,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                     widen<T, CT>(bufA[r][g], c);
                     TP o[VC];
 #pragma unroll
-                    for (int k = 0; k < VC; ++k) o[k] = (TP)(ur * fast_exp(c[k] * ks) * colacc[g][k]);
+                    for (int k = 0; k < VC; ++k) o[k] = (TP)(ur * fast_exp(c[k] * ks) * colacc[g][k / 2][k & 1]);
                     if (cnt[g] == VC) {
 #pragma unroll
                         for (int h = 0; h < VC / VP; ++h) {
@@ -678,8 +703,8 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 }
 
 // Columns per thread (G chunks of 16 B) and rows per block R.  Per thread and column:
-// the column partial (sizeof(T) / 4 VGPRs), then per row of a block the e value and two
-// raw cost buffers (the block being reduced and the next one in flight); R is the
+// the column partial (sizeof(T) / 4 VGPRs), then per row of a block the e value and the
+// raw cost (one buffer: refilled with the next block once widened); R is the
 // largest power of two that keeps these under ~150 of the 256 VGPRs a 512-thread
 // workgroup gets at one workgroup per CU (the rest: addresses, masks, reductions).
 #ifndef OTF_SWEEP_RBUDGET
@@ -688,7 +713,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 constexpr int pow2_floor(int x) { return x >= 16 ? 16 : x >= 8 ? 8 : x >= 4 ? 4 : x >= 2 ? 2 : 1; }
 template <typename T, typename CT> constexpr int sweep_rows(int G) {
     return pow2_floor((OTF_SWEEP_RBUDGET / (G * RawN<CT>::N) - (int)sizeof(T)) /
-                      ((int)sizeof(T) + (OTF_SWEEP_PIPE == 1 ? 1 : 2) * (int)sizeof(CT)));
+                      ((int)sizeof(T) + (int)sizeof(CT)));
 }
 constexpr int kSwMaxG = 8;
 
@@ -703,13 +728,31 @@ template <typename CT> int sweep_g(int64_t m) {
 #endif
 constexpr int kSwMaxGrid = 256;  // slab rows in the workspace (one per workgroup)
 
+// LDS: vbuf | u history | 1 / a | group-reduce staging (T), then the resident blocks
+template <typename T> size_t sweep_lds_base(int64_t m_pad) {
+    return ((size_t)m_pad + 3 * kSwRowMax + (size_t)kSwNT * Vec<T>::N) * sizeof(T);
+}
+size_t sweep_block_lds(int R, int G) { return (size_t)R * G * kSwNT * 16; }
+constexpr size_t kSwLdsMax = 160 * 1024 - 4096;  // the CU's LDS less the static arrays
+#ifndef OTF_SWEEP_MAXRES
+#define OTF_SWEEP_MAXRES 4
+#endif
+
 template <typename T, typename CT, typename TP, int G>
 hipError_t launch_sweep_g(int grid, SkSweepArgs<T>& p, hipStream_t s) {
     constexpr int R = sweep_rows<T, CT>(G);
+    // as many whole row blocks in LDS as fit, fewer than the smallest per-workgroup count
+    const int nrb = (p.n + R - 1) / R;
+    const int min_nb = nrb / grid;
+    const size_t base = sweep_lds_base<T>(p.m_pad);
+    int nres = base < kSwLdsMax ? (int)((kSwLdsMax - base) / sweep_block_lds(R, G)) : 0;
+    if (nres > OTF_SWEEP_MAXRES) nres = OTF_SWEEP_MAXRES;
+    if (nres > min_nb - 1) nres = min_nb - 1 > 0 ? min_nb - 1 : 0;
+    if (const char* e = getenv("OTF_SWEEP_NRES")) nres = atoi(e) < nres ? atoi(e) : nres;
+    p.nres = nres;
     void* args[] = {&p};
     const void* k = (const void*)sk_sweep_kernel<T, CT, TP, G, R, OTF_SWEEP_NREP>;
-    const size_t lds = ((size_t)p.m_pad + 3 * kSwRowMax + (size_t)kSwNT * Vec<T>::N) * sizeof(T);
-    const int nrb = (p.n + R - 1) / R;
+    const size_t lds = sweep_lds_base<T>(p.m_pad) + (size_t)p.nres * sweep_block_lds(R, G);
     if ((int64_t)((nrb + grid - 1) / grid) * R > kSwRowMax) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

@@ -90,6 +90,30 @@ int main(int argc, char** argv) {
         arrive_spread += (double)(amax - amin);
         sweep_spread += (double)(smax - smin);
     }
+    // per-XCD mean sweep duration, sweep-start spread, duration min / max over workgroups
+    double xd[8] = {0}, xn[8] = {0}, start_spread = 0, dmin_s = 0, dmax_s = 0;
+    for (int it = 2; it < 15; ++it) {
+        unsigned long long s0 = ~0ull, s1 = 0, dmn = ~0ull, dmx = 0;
+        for (int w = 0; w < nwg; ++w) {
+            const unsigned long long* x = &st[(w * 16 + it) * 8];
+            const int xc = (int)(st[(w * 16 + 15) * 8 + 7] & 7);
+            const unsigned long long d = x[2] - x[1];
+            xd[xc] += (double)d;
+            xn[xc] += 1;
+            s0 = x[1] < s0 ? x[1] : s0;
+            s1 = x[1] > s1 ? x[1] : s1;
+            dmn = d < dmn ? d : dmn;
+            dmx = d > dmx ? d : dmx;
+        }
+        start_spread += (double)(s1 - s0);
+        dmin_s += (double)dmn;
+        dmax_s += (double)dmx;
+    }
+    printf("sweep-start spread           %8.2f us\n", start_spread / 13 / 100.0);
+    printf("sweep duration min / max     %8.2f / %.2f us\n", dmin_s / 13 / 100.0, dmax_s / 13 / 100.0);
+    printf("sweep duration per XCD (us):");
+    for (int x = 0; x < 8; ++x) printf(" %.2f(%d)", xn[x] ? xd[x] / xn[x] / 100.0 : 0.0, (int)(xn[x] / 13));
+    printf("\n");
     const char* names[6] = {"sums+v+decide", "sweep (stream rows)", "flush: stage+atomics issue",
                             "atomics performed", "grid barrier", "loop back"};
     for (int ph = 0; ph < 6; ++ph) printf("%-28s %8.2f us\n", names[ph], span[ph] / cnt / 100.0);
