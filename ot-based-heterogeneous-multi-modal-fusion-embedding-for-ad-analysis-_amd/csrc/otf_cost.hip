@@ -204,7 +204,7 @@ __global__ void scale_inplace_kernel(T* C, int64_t n, int64_t m, int64_t ldc, co
 // accumulator) instead of eight v_mfma_f32_32x32x2_f32: ~5x the MFMA rate.
 // ============================================================================
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
-constexpr int SBK = 64;        // K per LDS stage
+constexpr int SBK = 64;        // K per LDS stage (the fp16 images are padded to it)
 constexpr int SLD = SBK + 8;   // padded LDS row (144 B): conflict-free ds_read_b128
 constexpr int SCPR = SBK / 8;  // 16-B chunks per row per stage
 constexpr int SCPT = BM * SCPR / 256;  // chunks per thread per image
@@ -230,7 +230,12 @@ template <typename TI> struct PrepSide {
 
 template <typename TI, bool SPLIT>
 __global__ __launch_bounds__(256) void split16_prep2_kernel(PrepSide<TI> A, PrepSide<TI> B, int d,
-                                                           int ldh) {
+                                                           int ldh, int vec) {
+    // lane handles 8 consecutive elements per 512-wide pass: 16-B (fp16) / 2 x 16-B
+    // (fp32) loads when the rows allow it, 16-B image stores; h == nullptr: norms only
+    // (the fp16 input is its own image)
+    using TV = __attribute__((ext_vector_type(8))) TI;
+    using H8 = __attribute__((ext_vector_type(8))) _Float16;
     const int lane = threadIdx.x & 63;
     const int total = A.n + B.n;
     float nmax[2] = {0.f, 0.f};
@@ -239,11 +244,25 @@ __global__ __launch_bounds__(256) void split16_prep2_kernel(PrepSide<TI> A, Prep
         const PrepSide<TI>& P = sb ? B : A;
         const int r = sb ? row - A.n : row;
         const TI* x = P.X + (int64_t)r * P.ldx;
+        auto load8 = [&](int k0, float (&v)[8]) {
+            if (vec && k0 + 8 <= d) {
+                const TV t = *reinterpret_cast<const TV*>(x + k0);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = (float)t[e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = k0 + e < d ? (float)x[k0 + e] : 0.f;
+            }
+        };
         float mx = 0.f, s2 = 0.f;
-        for (int k = lane; k < d; k += 64) {
-            const float v = (float)x[k];
-            mx = fmaxf(mx, fabsf(v));
-            s2 = fmaf(v, v, s2);
+        for (int k0 = 8 * lane; k0 < d; k0 += 512) {
+            float v[8];
+            load8(k0, v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                mx = fmaxf(mx, fabsf(v[e]));
+                s2 = fmaf(v[e], v[e], s2);
+            }
         }
         s2 = wave_sum(s2);
         int e = 0;
@@ -252,13 +271,22 @@ __global__ __launch_bounds__(256) void split16_prep2_kernel(PrepSide<TI> A, Prep
             e = mx > 0.f ? ilogbf(mx) : 0;
         }
         const float sc = SPLIT ? ldexpf(1.0f, 14 - e) : 1.0f;
-        _Float16* h = P.hi + (int64_t)r * ldh;
-        _Float16* l = SPLIT ? P.lo + (int64_t)r * ldh : nullptr;
-        for (int k = lane; k < ldh; k += 64) {
-            const float v = k < d ? (float)x[k] * sc : 0.f;
-            const _Float16 vh = (_Float16)v;
-            h[k] = vh;
-            if (SPLIT) l[k] = (_Float16)(v - (float)vh);
+        if (P.hi) {
+            _Float16* hrow = P.hi + (int64_t)r * ldh;
+            _Float16* lrow = SPLIT ? P.lo + (int64_t)r * ldh : nullptr;
+            for (int k0 = 8 * lane; k0 < ldh; k0 += 512) {
+                float v[8];
+                load8(k0, v);
+                H8 hv, lv;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const float w = v[q] * sc;
+                    hv[q] = (_Float16)w;
+                    lv[q] = (_Float16)(w - (float)hv[q]);
+                }
+                *reinterpret_cast<H8*>(hrow + k0) = hv;
+                if (SPLIT) *reinterpret_cast<H8*>(lrow + k0) = lv;
+            }
         }
         if (lane == 0) {
             P.inv_scale[r] = SPLIT ? ldexpf(1.0f, e - 14) : 1.0f;
@@ -266,9 +294,21 @@ __global__ __launch_bounds__(256) void split16_prep2_kernel(PrepSide<TI> A, Prep
             nmax[sb ? 1 : 0] = fmaxf(nmax[sb ? 1 : 0], s2);
         }
     }
+    // one max per workgroup, and only when it raises the running max: per-wave
+    // atomics on one address serialised to ~10 ns each (16384 rows: 190 us)
+    __shared__ float pmx[2][4];
     if (lane == 0) {
-        if (A.max_norm && nmax[0] > 0.f) atomicMax(A.max_norm, __float_as_uint(nmax[0]));
-        if (B.max_norm && nmax[1] > 0.f) atomicMax(B.max_norm, __float_as_uint(nmax[1]));
+        pmx[0][threadIdx.x >> 6] = nmax[0];
+        pmx[1][threadIdx.x >> 6] = nmax[1];
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        unsigned int* dst = threadIdx.x == 0 ? A.max_norm : B.max_norm;
+        const float* v = pmx[threadIdx.x];
+        const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        if (dst && mx > 0.f &&
+            __float_as_uint(mx) > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMax(dst, __float_as_uint(mx));
     }
 }
 
@@ -295,7 +335,7 @@ template <int NS, typename TC>
 __global__ __launch_bounds__(256) void cost_split16_kernel(
     const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
     const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
-    const float* __restrict__ ys, const float* __restrict__ yy, int ldh, int n, int m, int kpad,
+    const float* __restrict__ ys, const float* __restrict__ yy, int64_t ldxh, int64_t ldyh, int n, int m, int kpad,
     int metric, int zero_diag, TC* __restrict__ C, int64_t ldc, unsigned int* cmax, int tiles_n,
     const float* __restrict__ store_scale) {
     constexpr int NI = NS == 3 ? 2 : 1;  // fp16 images per operand
@@ -331,11 +371,11 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
             const int row = chunk / SCPR, kc = (chunk % SCPR) * 8;
             const int gi = i0 + row < n ? i0 + row : n - 1;
             const int gj = j0 + row < m ? j0 + row : m - 1;
-            st[c][0] = *reinterpret_cast<const u4*>(Xh + (int64_t)gi * ldh + k0 + kc);
-            st[c][NI] = *reinterpret_cast<const u4*>(Yh + (int64_t)gj * ldh + k0 + kc);
+            st[c][0] = *reinterpret_cast<const u4*>(Xh + (int64_t)gi * ldxh + k0 + kc);
+            st[c][NI] = *reinterpret_cast<const u4*>(Yh + (int64_t)gj * ldyh + k0 + kc);
             if (NI == 2) {
-                st[c][1] = *reinterpret_cast<const u4*>(Xl + (int64_t)gi * ldh + k0 + kc);
-                st[c][NI + 1] = *reinterpret_cast<const u4*>(Yl + (int64_t)gj * ldh + k0 + kc);
+                st[c][1] = *reinterpret_cast<const u4*>(Xl + (int64_t)gi * ldxh + k0 + kc);
+                st[c][NI + 1] = *reinterpret_cast<const u4*>(Yl + (int64_t)gj * ldyh + k0 + kc);
             }
         }
     };
@@ -497,24 +537,39 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     unsigned int* mn = f16out ? (unsigned int*)small : nullptr;
     if (f16out) OTF_HIP(hipMemsetAsync(small, 0, 2 * sizeof(float), s));
     const bool same = (X == Y && n == m && ldx == ldy);
+    // fp16 rows that are whole K stages, 16-B aligned, are their own MFMA image
+    const bool alias = !split && d % otf::SBK == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
+                       (uintptr_t)X % 16 == 0 && (uintptr_t)Y % 16 == 0;
+    int64_t ldxh = ldh, ldyh = ldh;
     {
         const int rows = (int)n + (same ? 0 : (int)m);
-        const int nblk = (rows + 3) / 4 < 4096 ? (rows + 3) / 4 : 4096;
+        const int nblk = (rows + 3) / 4 < 1024 ? (rows + 3) / 4 : 1024;
+        const size_t isz = split ? 4 : 2;
+        const int vec = (ldx * isz % 16 == 0 && ldy * isz % 16 == 0 && (uintptr_t)X % 16 == 0 &&
+                         (uintptr_t)Y % 16 == 0) ? 1 : 0;
         if (split) {
             const otf::PrepSide<float> A{(const float*)X, ldx, (int)n, Xh, Xl, xs, xx, mn};
             const otf::PrepSide<float> B{(const float*)Y, ldy, same ? 0 : (int)m, Yh, Yl, ys, yy,
                                          mn ? mn + 1 : nullptr};
-            otf::split16_prep2_kernel<float, true><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh);
+            otf::split16_prep2_kernel<float, true><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh, vec);
         } else {
-            const otf::PrepSide<_Float16> A{(const _Float16*)X, ldx, (int)n, Xh, nullptr, xs, xx, mn};
-            const otf::PrepSide<_Float16> B{(const _Float16*)Y, ldy, same ? 0 : (int)m, Yh, nullptr,
-                                            ys, yy, mn ? mn + 1 : nullptr};
-            otf::split16_prep2_kernel<_Float16, false><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh);
+            if (alias) {
+                Xh = (_Float16*)X;
+                Yh = (_Float16*)Y;
+                ldxh = ldx;
+                ldyh = ldy;
+            }
+            const otf::PrepSide<_Float16> A{(const _Float16*)X, ldx, (int)n, alias ? nullptr : Xh,
+                                            nullptr, xs, xx, mn};
+            const otf::PrepSide<_Float16> B{(const _Float16*)Y, ldy, same ? 0 : (int)m,
+                                            alias ? nullptr : Yh, nullptr, ys, yy,
+                                            mn ? mn + 1 : nullptr};
+            otf::split16_prep2_kernel<_Float16, false><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh, vec);
         }
     }
     OTF_HIP(hipGetLastError());
     if (same) {
-        Yh = Xh; Yl = Xl; ys = xs; yy = xx;
+        Yh = Xh; Yl = Xl; ys = xs; yy = xx; ldyh = ldxh;
         if (f16out) OTF_HIP(hipMemcpyAsync(mn + 1, mn, sizeof(float), hipMemcpyDeviceToDevice, s));
     }
     const float* store_scale = nullptr;
@@ -532,8 +587,8 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     if (nwg > INT32_MAX) return OTF_EUNSUPPORTED;
 #define OTF_COST_LAUNCH(NS, TC)                                                                   \
     otf::cost_split16_kernel<NS, TC><<<(int)nwg, 256, 0, s>>>(                                  \
-        Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldh, (int)n, (int)m, ldh, metric, zero_diag, (TC*)C, ldc, \
-        (unsigned int*)cmax, tiles_n, store_scale)
+        Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric, zero_diag,      \
+        (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale)
     if (split && !f16out) OTF_COST_LAUNCH(3, float);
     else if (split) OTF_COST_LAUNCH(3, _Float16);
     else if (!f16out) OTF_COST_LAUNCH(1, float);
