@@ -418,6 +418,43 @@ int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* 
                  otf_gw_info* info, double* costlog, int32_t costlog_len, void* workspace,
                  size_t ws_bytes, otf_stream_t stream);
 
+/* ---- exact EMD, general marginals: pot.emd(a, b, M, numItermax)
+ * (perturbot/perturbot/match/cot_labels.py:178,195 in get_coupling_cotl :228-276;
+ * the linear step of CG-GW on weighted groups, MRI_PET_OT_nojax.py:80-82).
+ * Primal network simplex on the device, one workgroup per problem.  a and b are
+ * non-negative with equal sums (the caller rescales b, as POT does).            */
+enum {
+    OTF_EMD_OPTIMAL = 0,
+    OTF_EMD_MAX_ITER = 1,   /* numItermax pivots reached (POT: "numItermax reached")    */
+    OTF_EMD_INFEASIBLE = 2, /* artificial flow left (unequal masses)                   */
+    OTF_EMD_UNBOUNDED = 3
+};
+
+/* One problem; all pointers are device pointers (float64). */
+typedef struct {
+    const double* a;  /* (n) source masses                                          */
+    const double* b;  /* (m) target masses                                          */
+    const double* M;  /* (n x m) costs, row stride ldm                              */
+    int64_t ldm;
+    double* T;        /* (n x m) optimal plan out, row stride ldt                    */
+    int64_t ldt;
+    int32_t n;
+    int32_t m;        /* n + m + 1 <= otf_emd_max_nodes()                            */
+} otf_emd_problem;
+
+/* Written on the device, one per problem. */
+typedef struct {
+    double cost;                /* sum T * M                                          */
+    int32_t status;             /* OTF_EMD_*                                           */
+    int32_t n_pivots;
+    double max_artificial_flow; /* 0 at a feasible optimum                              */
+} otf_emd_info;
+
+int otf_emd_max_nodes(void);
+/* probs: HOST array of nprob descriptors; info: device array of nprob. */
+int otf_emd_solve(int32_t nprob, const otf_emd_problem* probs, int64_t max_pivots,
+                  otf_emd_info* info, otf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

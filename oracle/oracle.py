@@ -383,6 +383,66 @@ def cotl_sinkhorn_np(X_dict, Y_dict, eps, niter=100):
     return Ts, Tv, cost, {"cost": costs}
 
 
+def emd_lp(a, b, M):
+    """pot.emd (POT 0.9.x network simplex; POT is absent here) restated as the
+    transportation LP min <M, T> s.t. T 1 = a, T^T 1 = b * sum(a) / sum(b), T >= 0,
+    solved by scipy's HiGHS.  Generic costs have a unique optimum, so plans compare
+    entry-wise.  Returns (T, cost)."""
+    from scipy.optimize import linprog
+    from scipy.sparse import coo_matrix
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    b = b * a.sum() / b.sum()
+    M = np.asarray(M, np.float64)
+    n, m = M.shape
+    rows = np.concatenate([np.repeat(np.arange(n), m), n + np.tile(np.arange(m), n)])
+    cols = np.concatenate([np.arange(n * m), np.arange(n * m)])
+    A = coo_matrix((np.ones(2 * n * m), (rows, cols)), shape=(n + m, n * m)).tocsr()
+    r = linprog(M.ravel(), A_eq=A, b_eq=np.concatenate([a, b]), bounds=(0, None), method="highs",
+                options={"primal_feasibility_tolerance": 1e-10, "dual_feasibility_tolerance": 1e-10})
+    if r.status != 0:
+        raise RuntimeError(f"linprog: {r.message}")
+    return r.x.reshape(n, m), float(r.fun)
+
+
+def cotl_emd_np(X_dict, Y_dict, niter=100):
+    """cot_labels.py:14-225 with algo = algo2 = 'emd' (pot.emd -> emd_lp): same BCD
+    loop and quirks as cotl_sinkhorn_np."""
+    labels = list(X_dict.keys())
+
+    def hist(D):
+        Xc = np.concatenate([np.asarray(D[k]) for k in labels], axis=0)
+        if (Xc >= 0).all():
+            return np.asarray(Xc.sum(axis=0) / Xc.sum(), dtype=np.float64)
+        return np.ones(Xc.shape[1]) / Xc.shape[1]
+
+    v1, v2 = hist(X_dict), hist(Y_dict)
+    X = {k: np.asarray(X_dict[k], np.float32) for k in labels}
+    Y = {k: np.asarray(Y_dict[k], np.float32) for k in labels}
+    w1 = {k: np.ones(len(X[k])) / len(X[k]) for k in labels}
+    w2 = {k: np.ones(len(Y[k])) / len(Y[k]) for k in labels}
+    d, d2 = X[labels[0]].shape[1], Y[labels[0]].shape[1]
+    Ts = {k: np.ones((len(X[k]), len(Y[k]))) / (len(X[k]) * len(Y[k])) for k in labels}
+    Tv = np.ones((d, d2)) / (d * d2)
+    cost, costs = np.inf, []
+    for _ in range(niter):
+        Tvold, costold = Tv, cost
+        for k in labels:
+            Ts[k] = emd_lp(w1[k], w2[k], coupled_cost_np(X[k], Y[k], Tv, v1, v2))[0]
+        M = 0
+        for k in labels:
+            M = M + coupled_cost_np(X[k].T, Y[k].T, Ts[k], w1[k], w2[k])
+        Tv = emd_lp(v1, v2, M)[0]
+        if not np.abs(Tv.sum() - 1.0) < 1e-8:
+            Tv = Tv / Tv.sum()
+        delta = np.linalg.norm(Tv - Tvold)
+        cost = np.sum(M * Tv)
+        costs.append(cost)
+        if delta < 1e-16 or np.abs(costold - cost) < 1e-7:
+            break
+    return Ts, Tv, cost, {"cost": costs}
+
+
 def pairwise_cost_np(X, Y, metric="sqeuclidean", zero_diag=False):
     """POT ``euclidean_distances`` (via ``ot.dist``) in float64."""
     X, Y = _d(X), _d(Y)

@@ -63,6 +63,15 @@ class GwProblem(ctypes.Structure):
                 ("n", ctypes.c_int64), ("m", ctypes.c_int64)]
 
 
+class EmdProblem(ctypes.Structure):
+    _fields_ = [("a", ctypes.c_void_p), ("b", ctypes.c_void_p),
+                ("M", ctypes.c_void_p), ("ldm", ctypes.c_int64),
+                ("T", ctypes.c_void_p), ("ldt", ctypes.c_int64),
+                ("n", ctypes.c_int32), ("m", ctypes.c_int32)]
+
+
+EMD_STATUS = {0: "optimal", 1: "max_iter", 2: "infeasible", 3: "unbounded"}
+
 INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "engine", "stalled")
 INFO_INT32S = len(INFO_FIELDS)  # otf_sinkhorn_info is 8 x int32
 
@@ -124,6 +133,8 @@ _SIGS = {
                                              ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                              ctypes.c_void_p]),
+    "otf_emd_max_nodes": (ctypes.c_int, []),
+    "otf_emd_solve": (ctypes.c_int, [_i32, ctypes.POINTER(EmdProblem), _i64, _vp, _vp]),
     "otf_gw_workspace_size": (ctypes.c_size_t, [ctypes.c_int32, ctypes.POINTER(GwProblem)]),
     "otf_gw_solve": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(GwProblem),
                                     ctypes.POINTER(GwOpts), ctypes.c_void_p, ctypes.c_void_p,

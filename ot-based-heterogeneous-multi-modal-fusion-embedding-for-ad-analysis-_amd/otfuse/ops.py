@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -416,3 +417,57 @@ class PlanApply(torch.autograd.Function):
 
 def apply_plan(Z: torch.Tensor, T: torch.Tensor) -> torch.Tensor:
     return PlanApply.apply(Z, T.detach())
+
+
+# ---------------------------------------------------------------- exact EMD
+@dataclass
+class EmdResult:
+    """Plans (device float64) of a batched ``otf_emd_solve``; ``infos()`` syncs."""
+    plans: list
+    info_raw: torch.Tensor
+    _keep: list = field(default_factory=list, repr=False)
+
+    def infos(self):
+        raw = self.info_raw.cpu().numpy().tobytes()
+        out = []
+        for b in range(len(self.plans)):
+            rec = raw[24 * b:24 * (b + 1)]
+            cost = float(np.frombuffer(rec[0:8], np.float64)[0])
+            status, piv = (int(x) for x in np.frombuffer(rec[8:16], np.int32))
+            art = float(np.frombuffer(rec[16:24], np.float64)[0])
+            out.append({"cost": cost, "status": status, "status_name": L.EMD_STATUS.get(status, str(status)),
+                        "n_pivots": piv, "max_artificial_flow": art})
+        return out
+
+
+def emd_max_nodes() -> int:
+    return int(L.lib().otf_emd_max_nodes())
+
+
+def emd_batched(problems, max_pivots: int = 100000) -> EmdResult:
+    """Exact EMD for each ``(a, b, M)`` (device float64; b already scaled to a's mass):
+    one workgroup per problem, one launch per 64 problems (``otf_emd_solve``)."""
+    if len(problems) == 0:
+        raise ValueError("no problems")
+    keep, plans = [], []
+    probs = (L.EmdProblem * len(problems))()
+    dev = None
+    for k, (a, b, M) in enumerate(problems):
+        M = _dev(M, "M").to(torch.float64).contiguous()
+        dev = M.device
+        n, m = M.shape
+        a = a.to(dev, torch.float64).contiguous()
+        b = b.to(dev, torch.float64).contiguous()
+        if a.numel() != n or b.numel() != m:
+            raise ValueError(f"a ({a.numel()}) / b ({b.numel()}) do not match M {tuple(M.shape)}")
+        if n + m + 1 > emd_max_nodes():
+            raise NotImplementedError(f"EMD {n}x{m}: n + m + 1 must be <= {emd_max_nodes()}")
+        T = torch.empty((n, m), dtype=torch.float64, device=dev)
+        plans.append(T)
+        keep += [a, b, M]
+        probs[k] = L.EmdProblem(a.data_ptr(), b.data_ptr(), M.data_ptr(), M.stride(0), T.data_ptr(),
+                                T.stride(0), n, m)
+    info = torch.zeros(24 * len(problems), dtype=torch.uint8, device=dev)
+    L.check(L.lib().otf_emd_solve(len(problems), probs, int(max_pivots), info.data_ptr(),
+                                  L.stream_handle(dev)), "otf_emd_solve")
+    return EmdResult(plans, info, keep)

@@ -24,6 +24,7 @@ log-domain restatement).
 from __future__ import annotations
 
 import time
+import warnings
 from typing import Dict, Tuple, Union
 from numbers import Number
 
@@ -381,7 +382,8 @@ def _feature_hist(D, labels):
 
 
 def cotl_sinkhorn(X_dict, Y_dict, eps: float = 5e-3, eps2: float | None = None,
-                  niter: int = 100, v1=None, v2=None, w1=None, w2=None, log: bool = False):
+                  niter: int = 100, v1=None, v2=None, w1=None, w2=None, log: bool = False,
+                  algo: str = "sinkhorn", numItermax: int = 10_000_000):
     """``cotl_numpy(X_dict, Y_dict, algo="sinkhorn", algo2="sinkhorn", reg=eps,
     reg2=eps2)`` (perturbot/perturbot/match/cot_labels.py:14-225) on the device.
 
@@ -395,8 +397,14 @@ def cotl_sinkhorn(X_dict, Y_dict, eps: float = 5e-3, eps2: float | None = None,
     ``delta`` counts only Tv (``Tsold = Ts`` aliases the dict that is updated in place,
     :167-172, so the Ts terms are 0); Tv is renormalised when its mass is off by 1e-8;
     stop when delta < 1e-16 or |cost change| < 1e-7.
+    ``algo="emd"``: every linear problem is ``pot.emd(w1[k], w2[k], M_k,
+    numItermax=1e7)`` / ``pot.emd(v1, v2, M, 1e7)`` instead (cot_labels.py:178,195) —
+    the device network simplex (``otf_emd_solve``), the per-label sample plans of one
+    step in one launch.
     Returns ``(Ts dict of numpy, Tv, cost[, {"cost": [...]}])``.
     """
+    if algo not in ("sinkhorn", "emd"):
+        raise NotImplementedError(f"algo={algo!r}")
     assert sorted(X_dict.keys()) == sorted(Y_dict.keys()), "Labels don't match in y1 & y2."
     dev = _device()
     labels = list(X_dict.keys())
@@ -421,16 +429,25 @@ def cotl_sinkhorn(X_dict, Y_dict, eps: float = 5e-3, eps2: float | None = None,
     costs = []
     for _ in range(niter):
         Tvold, costold = Tv, cost
-        for k in labels:  # sample OT per label
-            Mk = ops.coupled_cost(Xs[k], Ys[k], Tv, v1t, v2t)
-            res, _ = solve_ott(Mk, eps, "max_cost", max_iterations=OTT_MAX_ITER)
-            Ts[k] = res.plan
+        if algo == "emd":  # sample OT per label: every label's EMD in one launch
+            Ms = [ops.coupled_cost(Xs[k], Ys[k], Tv, v1t, v2t) for k in labels]
+            for k, T in zip(labels, _emd_many([(w1t[k], w2t[k], Mk) for k, Mk in zip(labels, Ms)],
+                                              numItermax)):
+                Ts[k] = T
+        else:
+            for k in labels:  # sample OT per label
+                Mk = ops.coupled_cost(Xs[k], Ys[k], Tv, v1t, v2t)
+                res, _ = solve_ott(Mk, eps, "max_cost", max_iterations=OTT_MAX_ITER)
+                Ts[k] = res.plan
         M = None  # global feature OT
         for k in labels:
             Mv = ops.coupled_cost(Xs[k].T, Ys[k].T, Ts[k], w1t[k], w2t[k])
             M = Mv if M is None else M + Mv
-        res, _ = solve_ott(M, eps, "max_cost", max_iterations=OTT_MAX_ITER)
-        Tv = res.plan
+        if algo == "emd":
+            Tv = _emd_many([(v1t, v2t, M)], numItermax)[0]
+        else:
+            res, _ = solve_ott(M, eps, "max_cost", max_iterations=OTT_MAX_ITER)
+            Tv = res.plan
         tot = float(Tv.sum())
         if not abs(tot - 1.0) < 1e-8:
             Tv = Tv / tot
@@ -459,9 +476,34 @@ def get_coupling_cotl_sinkhorn(data, eps: float = 5e-3, eps2: float | None = Non
     return Ts, log
 
 
+def _emd_many(problems, numItermax):
+    """pot.emd on each (a, b, M) (device float64), b rescaled to a's mass as POT does;
+    warns like POT when a solve stops at numItermax."""
+    prep = []
+    for a, b, M in problems:
+        sa, sb = float(a.sum()), float(b.sum())
+        np.testing.assert_almost_equal(sa, sb, err_msg="a and b vector must have the same sum",
+                                       decimal=6)
+        prep.append((a, b * (sa / sb), M))
+    res = ops.emd_batched(prep, max_pivots=int(numItermax))
+    for inf in res.infos():
+        if inf["status"] == 1:
+            warnings.warn("numItermax reached before optimality. Try to increase numItermax.",
+                          UserWarning)
+        elif inf["status"] != 0:
+            warnings.warn(f"EMD: {inf['status_name']}", UserWarning)
+    return res.plans
+
+
 def get_coupling_cotl(data):
-    """perturbot cot_labels.py:228-276 (COOT-L with exact EMD on non-uniform marginals).
-    Not provided: it needs a general-marginal network simplex; use
-    ``get_coupling_cotl_sinkhorn``."""
-    raise NotImplementedError("COOT-L with exact EMD (general marginals) is not implemented; "
-                              "get_coupling_cotl_sinkhorn is the device COOT-L")
+    """perturbot cot_labels.py:228-276: COOT-L with exact EMD on general marginals
+    (``cotl_numpy(X_dict, Y_dict, log=True, niter=2000)``, algo = algo2 = "emd").
+    Returns ``(Ts dict, log)`` (``(-1, -1)`` on a FloatingPointError, as the reference)."""
+    X_dict, Y_dict = data
+    start = time.time()
+    try:
+        Ts, Tv, cost, log = cotl_sinkhorn(X_dict, Y_dict, niter=2000, log=True, algo="emd")
+    except FloatingPointError:
+        return -1, -1
+    log["time"] = time.time() - start
+    return Ts, log

@@ -5,6 +5,7 @@ Same names, argument meaning and return conventions as the reference call sites:
 * ``sinkhorn``  -> ``ot.sinkhorn(a, b, M, reg, numItermax, stopThr)`` used at
   MRI_PET_OT_nojax.py:143 (POT 0.9.6 ``sinkhorn_knopp``);
 * ``dist`` / ``unif`` -> ``ot.dist`` / ``ot.unif`` (MRI_PET_OT_nojax.py:70-79);
+* ``emd`` -> ``ot.emd`` (network simplex, general marginals; cot_labels.py:178,195);
 * ``get_feature_coupling_pot`` -> MRI_PET_OT_nojax.py:91-145 (copy in MRI_T1_T2_OT.py:92-146).
 
 NumPy inputs give NumPy outputs (float64 plans, like POT on the reference's
@@ -109,6 +110,62 @@ def sinkhorn(a, b, M, reg: float, method: str = "sinkhorn", numItermax: int = 10
     v = res.v if is_torch else res.v.cpu().numpy()
     return P, {"err": info["err"], "niter": info["niter"], "u": u, "v": v,
                "status": info["status_name"]}
+
+
+def emd(a, b, M, numItermax: int = 100000, log: bool = False, center_dual: bool = True,
+        numThreads=1, check_marginals: bool = True):
+    """``ot.emd`` (POT 0.9.x ``ot.lp.emd``, network simplex) on the device.
+
+    As POT: empty ``a`` / ``b`` mean uniform; the masses must agree to 6 decimals
+    (``check_marginals``) and ``b`` is rescaled to ``a``'s total; a solve that stops
+    at ``numItermax`` pivots warns "numItermax reached before optimality".  The plan
+    is float64 (NumPy in, NumPy out).  ``log`` returns ``cost``, ``warning`` and
+    ``result_code`` (the duals are not returned).  Called by ``get_coupling_cotl``
+    (cot_labels.py:178,195) via ``emd_batch``.
+    """
+    return emd_batch([(a, b, M)], numItermax=numItermax, log=log,
+                     check_marginals=check_marginals)[0]
+
+
+def emd_batch(problems, numItermax: int = 100000, log: bool = False, check_marginals: bool = True):
+    """Several independent ``ot.emd`` problems in one device launch."""
+    is_torch = isinstance(problems[0][2], torch.Tensor) and problems[0][2].is_cuda
+    dev = problems[0][2].device if is_torch else _device()
+    prep = []
+    for a, b, M in problems:
+        Md = _as_dev(M, torch.float64, dev)
+        n, m = Md.shape
+        a = unif(n) if a is None or len(a) == 0 else a
+        b = unif(m) if b is None or len(b) == 0 else b
+        ad = _as_dev(a, torch.float64, dev).reshape(-1)
+        bd = _as_dev(b, torch.float64, dev).reshape(-1)
+        sa, sb = float(ad.sum()), float(bd.sum())
+        if check_marginals:
+            np.testing.assert_almost_equal(sa, sb, err_msg="a and b vector must have the same sum",
+                                           decimal=6)
+        bd = bd * (sa / sb)
+        prep.append((ad, bd, Md))
+    res = ops.emd_batched(prep, max_pivots=int(numItermax))
+    infos = res.infos()
+    out = []
+    for T, inf in zip(res.plans, infos):
+        warn = None
+        if inf["status"] == 1:
+            warn = "numItermax reached before optimality. Try to increase numItermax."
+        elif inf["status"] == 2:
+            warn = "Problem infeasible. Check that a and b are in the simplex"
+        elif inf["status"] == 3:
+            warn = "Problem unbounded"
+        if warn is not None:
+            warnings.warn(warn, UserWarning)
+        G = T if is_torch else T.cpu().numpy()
+        if log:
+            out.append((G, {"cost": inf["cost"], "warning": warn,
+                            "result_code": {0: 1, 1: 3, 2: 0, 3: 2}[inf["status"]],
+                            "n_pivots": inf["n_pivots"]}))
+        else:
+            out.append(G)
+    return out
 
 
 def _concat_sorted(X_dict, Y_dict):

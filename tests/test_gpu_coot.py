@@ -1,7 +1,8 @@
 """COOT-L on the device (perturbot cot_labels.py) vs the oracle restatement.
 
 OTT is absent, so parity is with the oracle's log-domain Sinkhorn restatement
-(UNPINNED against the reference's own outputs).  Bars: coupled costs to 1e-12 relative
+(UNPINNED against the reference's own outputs); the EMD variant is pinned on
+scipy's HiGHS LP (POT's network simplex is absent too).  Bars: coupled costs to 1e-12 relative
 (float64 from float32 squares); the BCD loop must take the same number of iterations
 and reach couplings within 1e-6 normwise."""
 import numpy as np
@@ -50,5 +51,18 @@ def test_cotl_sinkhorn_dropin_vs_oracle(orc, dev):
     np.testing.assert_allclose(log["cost"], log_r["cost"], rtol=1e-6)
     for k in Xd:
         assert nrel(Ts[k], Tr[k]) < 1e-6
-    with pytest.raises(NotImplementedError):
-        perturbot.get_coupling_cotl((Xd, Yd))
+
+
+def test_cotl_emd_dropin_vs_oracle(orc, dev):
+    """get_coupling_cotl: exact EMD (device network simplex) on general feature
+    marginals, vs the BCD loop over HiGHS LP solves: same iterations, same plans."""
+    from otfuse import perturbot
+    rng = np.random.default_rng(1)
+    Xd = {0: rng.random((20, 12)).astype(np.float32), 1: rng.random((25, 12)).astype(np.float32)}
+    Yd = {0: rng.random((22, 9)).astype(np.float32), 1: rng.random((18, 9)).astype(np.float32)}
+    Ts, log = perturbot.get_coupling_cotl((Xd, Yd))
+    Tr, Tvr, cost_r, log_r = orc.cotl_emd_np(Xd, Yd, niter=2000)
+    assert len(log["cost"]) == len(log_r["cost"]) and "time" in log
+    np.testing.assert_allclose(log["cost"], log_r["cost"], rtol=1e-9)
+    for k in Xd:
+        assert np.abs(Ts[k] - Tr[k]).max() < 1e-9
