@@ -257,16 +257,18 @@ def gw_pgd(C1, C2, eps, a=None, b=None, max_iter=1000, tol=1e-9, sk_max=1000, sk
 
 
 # --------------------------------------------------------------------------- NumPy
-def gw_cg_np(C1, C2, max_iter=10000, tol_rel=1e-9, tol_abs=1e-9):
-    """POT 0.9.6 ``gromov_wasserstein(C1, C2, unif, unif, 'square_loss')`` in NumPy, with
-    scipy's ``linear_sum_assignment`` as the exact EMD (uniform marginals, n x n) — an
-    independent LAP implementation for cross-checking ``oro_lap`` / the device solver."""
+def gw_cg_np(C1, C2, max_iter=10000, tol_rel=1e-9, tol_abs=1e-9, p=None, q=None):
+    """POT 0.9.6 ``gromov_wasserstein(C1, C2, p, q, 'square_loss')`` in NumPy.  The exact
+    EMD of the linear step: scipy's ``linear_sum_assignment`` for uniform marginals on
+    n x n (an independent LAP for cross-checking ``oro_lap`` / the device solver),
+    otherwise the HiGHS transportation LP (``emd_lp``)."""
     from scipy.optimize import linear_sum_assignment
 
     C1, C2 = _d(C1), _d(C2)
-    n = C1.shape[0]
-    p = np.full(n, 1.0 / n)
-    q = np.full(n, 1.0 / n)
+    n, m = C1.shape[0], C2.shape[0]
+    general = p is not None or q is not None or n != m
+    p = np.full(n, 1.0 / n) if p is None else np.asarray(p, np.float64)
+    q = np.full(m, 1.0 / m) if q is None else np.asarray(q, np.float64)
     constC = ((C1 ** 2) @ p)[:, None] + ((C2 ** 2) @ q)[None, :]
     hC1, hC2 = C1, 2.0 * C2
 
@@ -282,9 +284,12 @@ def gw_cg_np(C1, C2, max_iter=10000, tol_rel=1e-9, tol_abs=1e-9):
         old = cost
         df = 2.0 * tens(G)
         Mi = df + df.min()
-        rows, cols = linear_sum_assignment(Mi)
-        Gc = np.zeros_like(G)
-        Gc[rows, cols] = 1.0 / n
+        if general:
+            Gc = emd_lp(p, q, Mi)[0]
+        else:
+            rows, cols = linear_sum_assignment(Mi)
+            Gc = np.zeros_like(G)
+            Gc[rows, cols] = 1.0 / n
         dG = Gc - G
         dot = hC1 @ dG @ hC2.T
         a = -np.sum(dot * dG)

@@ -42,6 +42,7 @@
 #include <float.h>
 
 #include "otf_device.h"
+#include "otf_emd.h"
 
 namespace otf {
 namespace {
@@ -718,7 +719,114 @@ __global__ __launch_bounds__(Cfg::NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o,
     bool converged = false, inner_conv = false;
     double cost = 0;
 
-    if (o.solver == OTF_GW_CG) {
+    // CG on weighted or unequal groups: the linear step is the network simplex
+    // (emd_block, dynamic LDS) instead of the assignment solver
+    const bool gen_cg = !Cfg::SMALL && o.solver == OTF_GW_CG && (n != m || P.p || P.q);
+    if (gen_cg) {
+        if constexpr (!Cfg::SMALL) {
+            extern __shared__ __attribute__((aligned(16))) unsigned char gw_dyn[];
+            // G0 = p q^T, constC terms from p, q (POT init_matrix)
+            for (int i = t; i < n; i += Cfg::NT) sh.mg.r[i] = marg(P.p, i, n);
+            for (int j = t; j < m; j += Cfg::NT) sh.mg.c[j] = marg(P.q, j, m);
+            __syncthreads();
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
+                const int i = (int)(e / m), j = (int)(e % m);
+                G[i * ldt + j] = sh.mg.r[i] * sh.mg.c[j];
+            }
+            blk_sq_matvec<Cfg>(sh.x, C1, ldc1, n, sh.mg.r);
+            blk_sq_matvec<Cfg>(sh.y, C2, ldc2, m, sh.mg.c);
+            __syncthreads();
+            blk_gemm<Cfg, false>(D, 1, n, C1, 1, ldc1, G, ldt, 1, n, m, n, nullptr, 1.0);
+            __syncthreads();
+            blk_gemm<Cfg, false>(R, m, 1, D, 1, n, C2, ldc2, 1, n, m, m, nullptr, 1.0);
+            __syncthreads();
+            double acc = 0;
+            for (int64_t e = t; e < nm; e += Cfg::NT) {
+                const int i = (int)(e / m), j = (int)(e % m);
+                acc += (sh.x[i] + sh.y[j] - 2.0 * R[e]) * G[i * ldt + j];
+            }
+            cost = blk_sum(acc, sh.red);
+            if (clog && t == 0 && costlog_len > 0) clog[0] = cost;
+            while (true) {
+                ++it;
+                const double old = cost;
+                // Mi = df + min(df), df = 2 (constC - 2 R)
+                double mn = INFINITY;
+                for (int64_t e = t; e < nm; e += Cfg::NT) {
+                    const int i = (int)(e / m), j = (int)(e % m);
+                    const double df = 2.0 * (sh.x[i] + sh.y[j] - 2.0 * R[e]);
+                    Lm[i * ldl + j] = df;
+                    mn = fmin(mn, df);
+                }
+                mn = blk_minmax<Cfg>(mn, sh.red, false);
+                bool finite = true;
+                for (int64_t e = t; e < nm; e += Cfg::NT) {
+                    const int64_t le = (e / m) * ldl + e % m;
+                    const double v = Lm[le] + mn;
+                    Lm[le] = v;
+                    if (!finite_val(v)) finite = false;
+                }
+                sh.flag = 0;
+                __syncthreads();
+                if (!finite) sh.flag = 1;
+                __syncthreads();
+                if (sh.flag) { status = OTF_GW_NUMERICAL; break; }
+                // Gc = emd(p, q, Mi) (POT cg: numItermaxEmd = 1e5) into D, row-major n x m
+                otf_emd_problem ep;
+                ep.a = sh.mg.r;
+                ep.b = sh.mg.c;
+                ep.M = Lm;
+                ep.ldm = ldl;
+                ep.T = D;
+                ep.ldt = m;
+                ep.n = n;
+                ep.m = m;
+                __syncthreads();
+                const otf_emd_info ei = emd_block<Cfg::NT>(ep, 100000, gw_dyn);
+                __syncthreads();
+                if (ei.status == OTF_EMD_INFEASIBLE || ei.status == OTF_EMD_UNBOUNDED) {
+                    status = OTF_GW_NUMERICAL;
+                    break;
+                }
+                // S = C1 Gc C2 through (C1 Gc)^T in Lm (m x n)
+                blk_gemm<Cfg, false>(Lm, 1, n, C1, 1, ldc1, D, m, 1, n, m, n, nullptr, 1.0);
+                __syncthreads();
+                blk_gemm<Cfg, false>(S, m, 1, Lm, 1, n, C2, ldc2, 1, n, m, m, nullptr, 1.0);
+                __syncthreads();
+                double ta = 0, tb = 0;
+                for (int64_t e = t; e < nm; e += Cfg::NT) {
+                    const int i = (int)(e / m), j = (int)(e % m);
+                    const double dot = 2.0 * (S[e] - R[e]);
+                    const double gv = G[i * ldt + j];
+                    const double gcv = D[e];
+                    ta += dot * (gcv - gv);
+                    tb += dot * gv;
+                }
+                const double a = -blk_sum(ta, sh.red);
+                const double b = -2.0 * blk_sum(tb, sh.red);
+                double alpha;
+                if (a > 0) alpha = fmin(1.0, fmax(0.0, -b / (2.0 * a)));
+                else alpha = (a + b < 0) ? 1.0 : 0.0;
+                cost = cost + a * (alpha * alpha) + b * alpha;
+                for (int64_t e = t; e < nm; e += Cfg::NT) {
+                    const int i = (int)(e / m), j = (int)(e % m);
+                    const double gv = G[i * ldt + j];
+                    G[i * ldt + j] = gv + alpha * (D[e] - gv);
+                }
+                __syncthreads();
+                if (clog && t == 0 && it < costlog_len) clog[it] = cost;
+                blk_gemm<Cfg, false>(D, 1, n, C1, 1, ldc1, G, ldt, 1, n, m, n, nullptr, 1.0);
+                __syncthreads();
+                blk_gemm<Cfg, false>(R, m, 1, D, 1, n, C2, ldc2, 1, n, m, m, nullptr, 1.0);
+                __syncthreads();
+                const double absd = fabs(cost - old);
+                const double reld = cost != 0.0 ? absd / fabs(cost) : NAN;
+                if (reld < o.tol_rel || absd < o.tol_abs) { converged = true; status = OTF_GW_CONVERGED; break; }
+                if (it >= o.max_iter) break;
+                if (blk_timed_out(deadline, sh)) { status = OTF_GW_TIMEOUT; break; }
+            }
+        }
+    } else if (o.solver == OTF_GW_CG) {
         // G0 = p q^T (uniform), constC terms from p, q
         const double g0 = 1.0 / ((double)n * (double)m);
         for (int64_t e = t; e < nm; e += Cfg::NT) G[(e / m) * ldt + (e % m)] = g0;
@@ -1145,10 +1253,7 @@ int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* 
         if (P.ldc1 < P.n || P.ldc2 < P.m || P.ldt < P.m) return OTF_EINVAL;
         if (P.n > GW_MAXN || P.m > GW_MAXN) return OTF_EUNSUPPORTED;
         if ((P.labels_a == nullptr) != (P.labels_b == nullptr)) return OTF_EINVAL;
-        if (o.solver == OTF_GW_CG) {
-            // exact EMD as an assignment: uniform marginals on equal sizes
-            if (P.n != P.m || P.p || P.q || P.labels_a) return OTF_EUNSUPPORTED;
-        }
+        if (o.solver == OTF_GW_CG && P.labels_a) return OTF_EUNSUPPORTED;
         if (o.solver == OTF_GW_PGD && P.labels_a) return OTF_EUNSUPPORTED;
     }
     hipStream_t s = (hipStream_t)stream;
@@ -1164,12 +1269,24 @@ int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* 
             wsp += align256(4 * 8 * (size_t)(probs[first + b].n * probs[first + b].m));
         }
         bool small = true;
-        for (int b = 0; b < L.nprob; ++b)
-            if (L.prob[b].n > GW_SMALLN || L.prob[b].m > GW_SMALLN) small = false;
-        if (small)
+        size_t dyn = 0;  // CG on weighted / unequal groups: the network simplex's LDS
+        for (int b = 0; b < L.nprob; ++b) {
+            const otf_gw_problem& P = L.prob[b];
+            if (P.n > GW_SMALLN || P.m > GW_SMALLN) small = false;
+            if (o.solver == OTF_GW_CG && (P.n != P.m || P.p || P.q)) {
+                small = false;
+                const size_t e = emd_lds_bytes((int)(P.n + P.m + 1));
+                dyn = e > dyn ? e : dyn;
+            }
+        }
+        if (small) {
             gw_kernel<GwSmall><<<L.nprob, GwSmall::NT, 0, s>>>(L, o, info, costlog, costlog_len, ticks);
-        else
-            gw_kernel<GwBig><<<L.nprob, GwBig::NT, 0, s>>>(L, o, info, costlog, costlog_len, ticks);
+        } else {
+            if (dyn)
+                OTF_HIP(hipFuncSetAttribute((const void*)gw_kernel<GwBig>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+            gw_kernel<GwBig><<<L.nprob, GwBig::NT, dyn, s>>>(L, o, info, costlog, costlog_len, ticks);
+        }
         OTF_HIP(hipGetLastError());
     }
     return OTF_OK;

@@ -129,8 +129,6 @@ def solve_batched(C1s, C2s, solver: int, ps=None, qs=None, labels=None, *, max_i
             raise ValueError("C1 must be (n, n) and C2 (m, m)")
         if n > GW_MAXN or m > GW_MAXN:
             raise NotImplementedError(f"GW problem {n}x{m}: at most {GW_MAXN} points per side")
-        if solver == GW_CG and n != m:
-            raise NotImplementedError("exact CG-GW needs n == m (uniform marginals: assignment EMD)")
         T = torch.empty((n, m), dtype=torch.float64, device=dev)
         plans.append(T)
         p = None if ps is None or ps[b] is None else ps[b].to(dev, torch.float64).contiguous()
@@ -168,26 +166,30 @@ def gromov_wasserstein(C1, C2, p=None, q=None, loss_fun: str = "square_loss", sy
                        tol_rel: float = 1e-9, tol_abs: float = 1e-9, **kwargs):
     """``ot.gromov.gromov_wasserstein`` (POT 0.9.6) on device tensors.
 
-    Supported: square loss, symmetric C1 / C2, uniform p / q on n == m points, the
-    default line search and G0 = p q^T — the configuration of every reference call
-    site.  Extra keywords (``epsilon=`` at MRI_PET_OT_nojax.py:81) are ignored, as
-    POT's **kwargs do.  Returns G (and log with 'loss', 'gw_dist').
+    Supported: square loss, symmetric C1 / C2, any marginals p / q (uniform on equal
+    sizes: the linear step is the assignment solver; otherwise the device network
+    simplex, ``emd_block``), the default line search and G0 = p q^T.  Extra keywords
+    (``epsilon=`` at MRI_PET_OT_nojax.py:81) are ignored, as POT's **kwargs do.
+    Returns G (and log with 'loss', 'gw_dist').
     """
     if loss_fun != "square_loss":
         raise NotImplementedError(f"loss_fun={loss_fun!r}: only 'square_loss'")
     if armijo or G0 is not None:
         raise NotImplementedError("armijo / G0 are not supported")
     n, m = C1.shape[0], C2.shape[0]
+    pq = []
     for w, k in ((p, n), (q, m)):
-        if w is not None and not torch.allclose(torch.as_tensor(w, dtype=torch.float64).cpu(),
-                                                torch.full((k,), 1.0 / k, dtype=torch.float64)):
-            raise NotImplementedError("only uniform marginals (ot.unif) are supported")
+        if w is None or torch.allclose(torch.as_tensor(w, dtype=torch.float64).cpu(),
+                                       torch.full((k,), 1.0 / k, dtype=torch.float64), rtol=0, atol=0):
+            pq.append(None)
+        else:
+            pq.append(torch.as_tensor(w, dtype=torch.float64, device=C1.device))
     if symmetric is None:
         symmetric = _symmetric(C1) and _symmetric(C2)
     if not symmetric:
         raise NotImplementedError("asymmetric C1 / C2 are not supported")
-    res = solve_batched([C1], [C2], GW_CG, max_iter=int(max_iter), tol_rel=tol_rel,
-                        tol_abs=tol_abs, log_len=min(int(max_iter) + 1, 4096))
+    res = solve_batched([C1], [C2], GW_CG, ps=[pq[0]], qs=[pq[1]], max_iter=int(max_iter),
+                        tol_rel=tol_rel, tol_abs=tol_abs, log_len=min(int(max_iter) + 1, 4096))
     G = res.plans[0]
     if log:
         info = res.infos()[0]

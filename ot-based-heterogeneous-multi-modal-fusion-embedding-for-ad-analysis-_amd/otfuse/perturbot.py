@@ -316,7 +316,8 @@ def _gw_labels(X_dict, Y_dict, solver, eps=None, max_iter=None):
 
 def gw_cg(X_dict, Y_dict):
     """Per-label POT CG-GW on cdist / max costs (perturbot match/gw.py:7-28).  The exact
-    EMD is the device assignment solver: equal-size label groups (uniform marginals)."""
+    linear step is the device assignment solver on equal-size label groups and the
+    device network simplex on unequal ones."""
     from . import gw
     return _gw_labels(X_dict, Y_dict, gw.GW_CG)
 

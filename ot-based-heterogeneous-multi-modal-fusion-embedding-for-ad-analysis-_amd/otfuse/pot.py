@@ -254,7 +254,8 @@ def get_coupling_gromov_pot(
     ``C1 = ot.dist(x, x, 'euclidean') / max``, ``C2`` likewise, then POT's exact CG
     ``gromov_wasserstein(C1, C2, unif, unif, 'square_loss', epsilon=eps)`` — the
     ``epsilon`` keyword is swallowed by POT's **kwargs, so ``eps`` has no effect
-    there either.  All labels are solved concurrently in one device launch.  Plans
+    there either.  Unequal group sizes take the network-simplex linear step.  All
+    labels are solved concurrently in one device launch.  Plans
     come back as NumPy arrays in the features' dtype (POT returns ``type_as=C1``).
     Returns ``(Ts, log)`` with ``log[label]["time"]``.
     """
@@ -269,10 +270,6 @@ def get_coupling_gromov_pot(
         start[l] = time.time()
         x = _as_dev(X_dict[l], torch.float32, dev)
         y = _as_dev(Y_dict[l], torch.float32, dev)
-        if x.shape[0] != y.shape[0]:
-            raise NotImplementedError(
-                f"label {l}: {x.shape[0]} vs {y.shape[0]} samples — the exact EMD is provided "
-                "for the paired (equal-size) groups the reference builds")
         C1, _ = gw.pairwise_cost_f64(x, None, metric="euclidean", zero_diag=True, scale_max=True)
         C2, _ = gw.pairwise_cost_f64(y, None, metric="euclidean", zero_diag=True, scale_max=True)
         C1s.append(C1)

@@ -90,6 +90,52 @@ def test_gw_cg_random_metric_spaces_many_seeds(orc, dev):
         assert info["cost"] == pytest.approx(ref["gw_dist"], rel=1e-9, abs=1e-13)
 
 
+def test_gw_cg_unequal_and_weighted_vs_oracle(orc, dev):
+    """CG-GW on unequal groups and non-uniform marginals (POT's call with general p, q):
+    the linear step is the device network simplex; the oracle runs the same CG with the
+    HiGHS LP as EMD.  Generic costs -> unique vertices -> same path."""
+    from otfuse import gw
+    rng = np.random.default_rng(77)
+    C1s, C2s, ps, qs = [], [], [], []
+    for k in range(6):
+        n, m = int(rng.integers(3, 60)), int(rng.integers(3, 60))
+        A = rng.standard_normal((n, 3))
+        B = rng.standard_normal((m, 4))
+        C1s.append(orc.pairwise_cost(A, A, metric="euclidean", zero_diag=True, scale_max=True)[0])
+        C2s.append(orc.pairwise_cost(B, B, metric="euclidean", zero_diag=True, scale_max=True)[0])
+        if k % 2:
+            p = rng.random(n) + 0.1
+            q = rng.random(m) + 0.1
+            ps.append(p / p.sum())
+            qs.append(q / q.sum())
+        else:
+            ps.append(None)
+            qs.append(None)
+    res = gw.solve_batched([torch.as_tensor(c, device=dev) for c in C1s],
+                           [torch.as_tensor(c, device=dev) for c in C2s], gw.GW_CG,
+                           ps=[None if p is None else torch.as_tensor(p, device=dev) for p in ps],
+                           qs=[None if q is None else torch.as_tensor(q, device=dev) for q in qs],
+                           max_iter=10000, log_len=64)
+    for C1, C2, p, q, T, info in zip(C1s, C2s, ps, qs, res.plans, res.infos()):
+        G, ref = orc.gw_cg_np(C1, C2, p=p, q=q)
+        assert info["status"] == "converged", info
+        assert info["n_iter"] == ref["n_iter"]
+        assert np.abs(T.cpu().numpy() - G).max() < 1e-9
+        assert info["cost"] == pytest.approx(ref["gw_dist"], rel=1e-8, abs=1e-12)
+    # the POT-form wrapper with weights and the unequal-group drop-in
+    from otfuse import pot
+    G1, log1 = gw.gromov_wasserstein(torch.as_tensor(C1s[1], device=dev), torch.as_tensor(C2s[1], device=dev),
+                                     p=ps[1], q=qs[1], log=True)
+    Gr, ref = orc.gw_cg_np(C1s[1], C2s[1], p=ps[1], q=qs[1])
+    assert np.abs(G1.cpu().numpy() - Gr).max() < 1e-9
+    Xd = {0: rng.standard_normal((12, 6)).astype(np.float32), 1: rng.standard_normal((20, 6)).astype(np.float32)}
+    Yd = {0: rng.standard_normal((15, 6)).astype(np.float32), 1: rng.standard_normal((9, 6)).astype(np.float32)}
+    Ts, _ = pot.get_coupling_gromov_pot((Xd, Yd))
+    for k in Xd:
+        assert Ts[k].shape == (len(Xd[k]), len(Yd[k]))
+        np.testing.assert_allclose(Ts[k].sum(1), np.full(len(Xd[k]), 1.0 / len(Xd[k])), atol=1e-12)
+
+
 def test_gw_cg_isometry(orc, dev):
     from otfuse import gw
     rng = np.random.default_rng(5)
