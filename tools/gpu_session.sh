@@ -20,6 +20,16 @@ if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --profile-only --steps 10 --warmup 2 > gpurun_out/rocprof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; stop_if_fatal $rc rocprof
 fi
+if [ "${PROFILE:-1}" = "1" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run --output-format csv -- python3 bench.py --profile-only --profile-config5 --steps 3 > gpurun_out/rocprof_c5.log 2>&1
+  rc=$?; echo "rocprof c5 rc=$rc"; stop_if_fatal $rc rocprof_c5
+fi
+if [ "${PMC:-0}" = "1" ]; then
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --stats -d gpurun_out/pmc_${ctr}_c5 -o run --output-format csv -- python3 bench.py --profile-only --profile-config5 --steps 2 > gpurun_out/pmc_${ctr}_c5.log 2>&1
+    rc=$?; echo "pmc $ctr c5 rc=$rc"; stop_if_fatal $rc pmc_c5
+  done
+fi
 if [ "${PMC:-0}" = "1" ]; then
   for eng in auto stream; do
     for ctr in FETCH_SIZE WRITE_SIZE; do

@@ -69,11 +69,19 @@ def main():
                 os.path.join(PROF, f"{tag}_kernel_stats.csv"))
     dur, cnt = medians(os.path.join(OUT, "prof", "run_kernel_trace.csv"))
     summary = {"kernels": {k: {"median_us": dur[k] / 1e3, "launches": cnt[k]} for k in dur}}
+    # config-5 passes (pmc_*_c5, bench.py --profile-config5: N = 8192 fp16, sweep engine)
+    # go to their own section: same kernel names, different shapes
+    summary["config5_kernels"] = {}
+    c5trace = os.path.join(OUT, "prof_c5", "run_kernel_trace.csv")
+    if os.path.exists(c5trace):
+        d5, n5 = medians(c5trace)
+        summary["config5_kernels"] = {k: {"median_us": d5[k] / 1e3, "launches": n5[k]} for k in d5}
     for ctr, factor in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
         for p in glob.glob(os.path.join(OUT, f"pmc_{ctr}*", "run_counter_collection.csv")):
             med, _ = medians(p, "Counter_Value")
+            sect = "config5_kernels" if os.path.basename(os.path.dirname(p)).endswith("_c5") else "kernels"
             for k, v in med.items():
-                summary["kernels"].setdefault(k, {})[ctr + "_bytes_corrected"] = v * 1024 * factor
+                summary[sect].setdefault(k, {})[ctr + "_bytes_corrected"] = v * 1024 * factor
     bench = os.path.join(OUT, "bench.log")
     cfg = {}
     if os.path.exists(bench):
