@@ -237,3 +237,26 @@ def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch)
     # the device is healthy afterwards
     res = ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine="tiled")
     assert res.info()["status_name"] == "max_iter"
+
+
+@pytest.mark.parametrize("engine,n,m,dt,iters", [("tiled", 4096, 4096, torch.float32, 20000),
+                                                 ("resident", 512, 512, torch.float64, 30000),
+                                                 ("sweep", 1024, 8192, torch.float32, 20000)])
+def test_long_persistent_solve_outlives_the_stall_limit(dev, monkeypatch, engine, n, m, dt, iters):
+    """The stall deadline is re-armed at every completed barrier: a solve that runs far
+    longer than OTF_STALL_MS but keeps making progress finishes normally."""
+    import time
+    from otfuse import ops
+    monkeypatch.setenv("OTF_STALL_MS", "40")
+    g = torch.Generator(device=dev).manual_seed(4)
+    C = torch.rand(n, m, device=dev, generator=g).to(dt)
+    a = torch.full((n,), 1.0 / n, device=dev, dtype=dt)
+    b = torch.full((m,), 1.0 / m, device=dev, dtype=dt)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = ops.sinkhorn(a, b, C, 0.5, max_iter=iters, stop_thr=0.0, engine=engine, want_plan=False)
+    info = res.info()
+    elapsed = time.perf_counter() - t0
+    assert info["engine_name"] == engine
+    assert info["status_name"] == "max_iter" and not info["stalled"]
+    assert elapsed > 0.04 * 2       # the solve really outlived the stall limit
