@@ -364,7 +364,7 @@ enum {
     OTF_GW_CONVERGED = 1,
     OTF_GW_MAX_ITER = 2,
     OTF_GW_NUMERICAL = 3,  /* non-finite cost / failed assignment                   */
-    OTF_GW_TIMEOUT = 4     /* device-side wall-clock bound (20 s) reached            */
+    OTF_GW_TIMEOUT = 4     /* no outer iteration completed within 20 s (a stall)    */
 };
 
 typedef struct {

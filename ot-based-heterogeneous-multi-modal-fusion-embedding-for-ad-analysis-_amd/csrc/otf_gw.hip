@@ -708,7 +708,10 @@ __global__ __launch_bounds__(Cfg::NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o,
         G = P.T;
         ldt = P.ldt;
     }
-    const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
+    // the wall-clock bound is per outer iteration (re-armed after each completed one):
+    // a long but progressing solve runs to its iteration cap; a stuck inner loop ends
+    // in OTF_GW_TIMEOUT
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
     const int t = threadIdx.x;
 #ifdef OTF_GW_STAMPS
     unsigned long long gw_acc[4] = {0, 0, 0, 0};
@@ -824,6 +827,7 @@ __global__ __launch_bounds__(Cfg::NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o,
                 if (reld < o.tol_rel || absd < o.tol_abs) { converged = true; status = OTF_GW_CONVERGED; break; }
                 if (it >= o.max_iter) break;
                 if (blk_timed_out(deadline, sh)) { status = OTF_GW_TIMEOUT; break; }
+                deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
             }
         }
     } else if (o.solver == OTF_GW_CG) {
@@ -927,6 +931,7 @@ GW_TEND(0); }
             if (reld < o.tol_rel || absd < o.tol_abs) { converged = true; status = OTF_GW_CONVERGED; break; }
             if (it >= o.max_iter) break;
             if (blk_timed_out(deadline, sh)) { status = OTF_GW_TIMEOUT; break; }
+            deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
         }
     } else if (o.solver == OTF_GW_PGD) {
         // POT entropic GW, solver='PGD'.  T0 = p q^T; constC from (p, q), fixed.
@@ -999,6 +1004,7 @@ GW_TEND(0); }
             }
             ++it;
             if (blk_timed_out(deadline, sh)) { status = OTF_GW_TIMEOUT; break; }
+            deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
         }
         converged = err <= o.tol_abs;
         if (status != OTF_GW_TIMEOUT)
@@ -1093,6 +1099,7 @@ GW_TEND(0); }
             const bool keep = it < o.min_iter || it <= 2 || (isfinite(cprev) && !close);
             if (!keep) { converged = close; status = close ? OTF_GW_CONVERGED : OTF_GW_NUMERICAL; break; }
             if (blk_timed_out(deadline, sh)) { status = OTF_GW_TIMEOUT; break; }
+            deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
         }
     }
     if constexpr (Cfg::SMALL) {
