@@ -328,7 +328,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                     scaled_pairs<T, CT>(buf[r][g], ks, c);
 #pragma unroll
                     for (int k = 0; k < VP2; ++k) {
-#if defined(OTF_SWEEP_ABLATE) && OTF_SWEEP_ABLATE == 1
+#if defined(OTF_SWEEP_ABLATE) && (OTF_SWEEP_ABLATE & 1)
                         e[r][g][k] = c[k];  // diagnostic: no exponentials
 #else
                         e[r][g][k] = T2{fast_exp(c[k].x), fast_exp(c[k].y)};
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             // single-buffer pipeline: the raw block is dead once widened, so the next
             // block's loads go out now and fly during this block's reductions
             // LDS-resident blocks come from LDS once the prologue sweep has put them there
-#if defined(OTF_SWEEP_ABLATE) && OTF_SWEEP_ABLATE == 2
+#if defined(OTF_SWEEP_ABLATE) && (OTF_SWEEP_ABLATE & 2)
             if (it >= 0) {  // diagnostic: after the prologue, no cost loads (stale block)
             } else
 #endif
@@ -384,8 +384,8 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                 wave_sum_multi<T, R>(rp, lane);
                 const int par = bi & 1;
                 if (lane < R) red[par][w][butterfly_row<R>(lane)] = rp[0];
-#if !(defined(OTF_SWEEP_ABLATE) && OTF_SWEEP_ABLATE == 3)
-                __syncthreads();  // (ABLATE 3, diagnostic: no per-block barrier, racy sums)
+#if !(defined(OTF_SWEEP_ABLATE) && (OTF_SWEEP_ABLATE & 4))
+                __syncthreads();  // (ABLATE & 4, diagnostic: no per-block barrier, racy sums)
 #endif
                 const int rr = lane < R ? lane : 0;
                 T s = red[par][0][rr];
