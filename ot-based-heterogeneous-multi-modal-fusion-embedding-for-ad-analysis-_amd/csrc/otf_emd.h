@@ -14,30 +14,45 @@
 // Graph: supply nodes 0..n-1 (a_i), demand nodes n..n+m-1 (-b_j), a root R = n+m with
 // one big-M artificial arc per node (k -> R when a_k > 0, R -> k otherwise), which
 // form the initial strongly feasible spanning tree.  Real arcs i -> n+j, cost M_ij,
-// unbounded.  Per pivot:
+// unbounded.  The tree lives in LDS as parent pointers plus a PRE-ORDER ARRAY
+// (ord / pos) and subtree sizes, so every subtree is one contiguous range of ord and
+// x is an ancestor of y iff pos[x] <= pos[y] < pos[x] + sz[x].  Per pivot:
 //   * pricing: block search over all arcs (blocks of max(sqrt(A), 256) arcs from a
-//     rotating cursor); the workgroup's 256 threads scan a block and reduce to the
-//     most negative reduced cost c_e + pi_s - pi_t (ties -> first in block order);
-//   * one thread does the tree work in LDS: the join of the cycle by depth, the ratio
-//     test with Cunningham's last-blocking-arc rule (keeps the tree strongly
+//     rotating cursor); the workgroup's threads scan a block and reduce to the most
+//     negative reduced cost c_e + pi_s - pi_t (ties -> first in block order);
+//   * one thread: the join of the cycle (walk up from s until an ancestor of t), the
+//     ratio test with Cunningham's last-blocking-arc rule (keeps the tree strongly
 //     feasible, so degenerate pivots cannot cycle), the flow update along the cycle,
-//     the path reversal that re-hangs the cut subtree under the entering arc, and
-//     the depth / potential shift of that subtree (first-child / sibling lists).
+//     and the path u_in .. u_out that the cut subtree S is re-rooted along;
+//   * all threads: S's new pre-order is the concatenation of 2k + 1 ranges of the old
+//     one (each path node's own part before / after the branch towards u_in), built
+//     in parallel; one thread fixes the sizes on the path and on the two ancestor
+//     chains and reverses the parents; all threads then move S behind v_in (one
+//     parallel block shift of ord), update pos and shift the potentials of S by the
+//     entering arc's reduced cost — O(cycle + path) serial work, O(N / threads)
+//     parallel work, instead of a serial walk over the moved subtree.
 // Tree arcs have reduced cost 0, so pricing needs no arc state; the flow of a tree
 // arc lives with its child node, so the plan is written once at the end.
 // One workgroup per problem: a batch (the per-label plans of one COOT-L step) is one
-// launch.  Per node 27 B of LDS: n + m + 1 <= kEmdMaxNodes.
+// launch.  Per node 31 B of LDS: n + m + 1 <= kEmdMaxNodes.
 #pragma once
 #include "otf_device.h"
 
 namespace otf {
 
-constexpr int kEmdMaxNodes = 5600;
-constexpr size_t kEmdScratch = 256 * (8 + 4) + 64;  // reductions of up to 256 threads
+#ifdef OTF_EMD_STAMPS
+// diagnostic build only (tools/stamps_emd.hip): ticks in pricing / tree work, blocks
+// priced, subtree nodes moved, cycle nodes walked (workgroup 0)
+__device__ unsigned long long g_emd_stats[8];
+#endif
+
+constexpr int kEmdMaxNodes = 4800;
+constexpr size_t kEmdScratch = 256 * (8 + 4) + 128;  // reductions of up to 256 threads
+constexpr size_t kEmdNodeBytes = 2 * 8 + 7 * 2 + 1;  // pi, tflow | par sz pos ord tmp shift path | sgn
 
 // LDS of emd_block for n + m + 1 = N nodes
 inline __host__ __device__ size_t emd_lds_bytes(int N) {
-    return ((size_t)N * (2 * 8 + 5 * 2 + 1) + 15) / 16 * 16 + kEmdScratch;
+    return ((size_t)N * kEmdNodeBytes + 15) / 16 * 16 + kEmdScratch;
 }
 
 inline __device__ void argmin_pair(double& v, int& i, double v2, int i2) {
@@ -59,15 +74,18 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
     double* pi = reinterpret_cast<double*>(esm);   // node potentials
     double* tflow = pi + N;                         // flow of the tree arc (u, parent u)
     short* par = reinterpret_cast<short*>(tflow + N);
-    short* fch = par + N;                           // first child
-    short* nsb = fch + N;                           // next / previous sibling
-    short* psb = nsb + N;
-    short* dep = psb + N;                           // depth (root 0)
-    signed char* sgn = reinterpret_cast<signed char*>(dep + N);  // 1: supply > 0
-    unsigned char* scr = esm + ((size_t)N * (2 * 8 + 5 * 2 + 1) + 15) / 16 * 16;
+    short* sz = par + N;                            // subtree sizes
+    short* pos = sz + N;                            // position in the pre-order
+    short* ord = pos + N;                           // the pre-order (ord[pos[x]] = x)
+    short* tmp = ord + N;                           // new pre-order of the moved subtree
+    short* shf = tmp + N;                           // the block of ord that shifts
+    short* path = shf + N;                          // u_in .. u_out
+    signed char* sgn = reinterpret_cast<signed char*>(path + N);  // 1: supply > 0
+    unsigned char* scr = esm + ((size_t)N * kEmdNodeBytes + 15) / 16 * 16;
     double* rv = reinterpret_cast<double*>(scr);
     int* ri = reinterpret_cast<int*>(rv + NT);
-    int* flag = ri + NT;
+    int* flag = ri + NT;      // [0] stop code, [1..7] pivot scalars
+    double* dsc = reinterpret_cast<double*>(scr + NT * 12 + 64);  // [0] sigma
 
     // zero the plan; largest |cost| for the big-M of the artificial arcs
     double mc = 0.0;
@@ -94,19 +112,18 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
         par[k] = (short)R;
         tflow[k] = fabs(sup);
         pi[k] = sup > 0.0 ? -ART : ART;
-        dep[k] = 1;
-        fch[k] = -1;
-        psb[k] = (short)(k - 1);
-        nsb[k] = (short)(k + 1 < N - 1 ? k + 1 : -1);
+        sz[k] = 1;
+        pos[k] = (short)(k + 1);
+        ord[k + 1] = (short)k;
     }
     if (tid == 0) {
         sgn[R] = 0;
         par[R] = -1;
         tflow[R] = 0.0;
         pi[R] = 0.0;
-        dep[R] = 0;
-        fch[R] = (short)(N > 1 ? 0 : -1);
-        psb[R] = nsb[R] = -1;
+        sz[R] = (short)N;
+        pos[R] = 0;
+        ord[0] = (short)R;
         flag[0] = 0;
     }
     __syncthreads();
@@ -125,11 +142,19 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
     };
     // the tree arc between u and its parent runs u -> parent ("up")?
     auto up = [&](int u) -> bool { return par[u] == R ? sgn[u] != 0 : u < n; };
+    auto anc = [&](int x, int y) -> bool { return pos[x] <= pos[y] && pos[y] < pos[x] + sz[x]; };
 
     int next = 0;
     int64_t pivots = 0;
     int status = OTF_EMD_OPTIMAL;
+#ifdef OTF_EMD_STAMPS
+    unsigned long long st_t0 = __builtin_amdgcn_s_memrealtime(), st_price = 0, st_tree = 0, st_blocks = 0,
+                       st_sub = 0;
+#endif
     for (;;) {
+#ifdef OTF_EMD_STAMPS
+        st_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         // ---- pricing: block search from the cursor
         int in_arc = -1;
         double in_rc = 0.0;
@@ -166,6 +191,9 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
             next += len;
             if (next >= A_tot) next -= A_tot;
             scanned += len;
+#ifdef OTF_EMD_STAMPS
+            ++st_blocks;
+#endif
             if (bv < -tol) {
                 in_arc = start + bi;
                 if (in_arc >= A_tot) in_arc -= A_tot;
@@ -173,13 +201,20 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
                 break;
             }
         }
+#ifdef OTF_EMD_STAMPS
+        {
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            st_price += t1 - st_t0;
+            st_t0 = t1;
+        }
+#endif
         if (in_arc < 0) break;  // no arc prices out: optimal
         if (++pivots > max_pivots) {
             status = OTF_EMD_MAX_ITER;
             break;
         }
 
-        // ---- tree work (one thread; everything it touches is in LDS)
+        // ---- tree work.  Phase A (one thread): cycle, ratio test, flows, the path.
         if (tid == 0) {
             int s, t;
             if (in_arc < A_real) {
@@ -190,21 +225,13 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
                 s = sgn[k] ? k : R;
                 t = sgn[k] ? R : k;
             }
-            int u = s, v = t;
-            while (u != v) {
-                if (dep[u] > dep[v]) u = par[u];
-                else if (dep[v] > dep[u]) v = par[v];
-                else {
-                    u = par[u];
-                    v = par[v];
-                }
-            }
-            const int join = u;
-            // ratio test: flow runs join -> ... -> s -> t -> ... -> join; the blocking
-            // arcs are those run against their direction; keep the LAST one met in that
-            // order from the join (strongly feasible trees)
+            int join = s;
+            while (!anc(join, t)) join = par[join];
+            // flow runs join -> ... -> s -> t -> ... -> join; the blocking arcs are
+            // those run against their direction; keep the LAST one met in that order
+            // from the join (strongly feasible trees)
             double delta = INFINITY;
-            int u_out = -1, side = 0;
+            int u_out = -1, side = 0, u;
             for (u = s; u != join; u = par[u])
                 if (up(u) && tflow[u] < delta) {
                     delta = tflow[u];
@@ -224,47 +251,20 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
                     for (u = s; u != join; u = par[u]) tflow[u] += up(u) ? -delta : delta;
                     for (u = t; u != join; u = par[u]) tflow[u] += up(u) ? delta : -delta;
                 }
-                // re-hang the subtree of u_out from u_in (the entering arc's end inside
-                // it) under v_in, reversing the path u_in .. u_out
                 const int u_in = side == 1 ? s : t, v_in = side == 1 ? t : s;
-                const double sigma = side == 1 ? -in_rc : in_rc;
-                int prev = v_in;
-                double carry = delta;
-                u = u_in;
-                for (;;) {
-                    const int nx = par[u];
-                    const double f = tflow[u];
-                    // cut u from nx's children
-                    if (psb[u] >= 0) nsb[psb[u]] = nsb[u];
-                    else fch[nx] = nsb[u];
-                    if (nsb[u] >= 0) psb[nsb[u]] = psb[u];
-                    // link u as prev's first child
-                    nsb[u] = fch[prev];
-                    psb[u] = -1;
-                    if (fch[prev] >= 0) psb[fch[prev]] = (short)u;
-                    fch[prev] = (short)u;
-                    par[u] = (short)prev;
-                    tflow[u] = carry;
-                    carry = f;
-                    if (u == u_out) break;
-                    prev = u;
-                    u = nx;
+                int k = 0;
+                path[0] = (short)u_in;
+                for (u = u_in; u != u_out;) {
+                    u = par[u];
+                    path[++k] = (short)u;
                 }
-                // depth and potentials of the moved subtree (pre-order walk)
-                int x = u_in;
-                dep[x] = (short)(dep[v_in] + 1);
-                pi[x] += sigma;
-                for (;;) {
-                    if (fch[x] >= 0) {
-                        x = fch[x];
-                    } else {
-                        while (x != u_in && nsb[x] < 0) x = par[x];
-                        if (x == u_in) break;
-                        x = nsb[x];
-                    }
-                    dep[x] = (short)(dep[par[x]] + 1);
-                    pi[x] += sigma;
-                }
+                flag[1] = k;
+                flag[2] = u_in;
+                flag[3] = v_in;
+                flag[4] = u_out;
+                flag[5] = join;
+                dsc[0] = side == 1 ? -in_rc : in_rc;  // potential shift of the moved subtree
+                dsc[1] = delta;
             }
         }
         __syncthreads();
@@ -272,8 +272,94 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
             status = flag[0];
             break;
         }
+        {
+            const int k = flag[1], u_in = flag[2], v_in = flag[3], u_out = flag[4], join = flag[5];
+            const int L = sz[u_out], a0 = pos[u_out], q = pos[v_in];
+            // Phase B (all threads): the re-rooted subtree's pre-order from the old one:
+            // u_in's whole old subtree, then for each path node its part before and after
+            // the branch towards u_in
+            {
+                int off = 0;
+                int st = pos[u_in], len = sz[u_in];
+                for (int e = tid; e < len; e += NT) tmp[off + e] = ord[st + e];
+                off += len;
+                for (int i = 1; i <= k; ++i) {
+                    const int pc = path[i], pm = path[i - 1];
+                    st = pos[pc];
+                    len = pos[pm] - pos[pc];
+                    for (int e = tid; e < len; e += NT) tmp[off + e] = ord[st + e];
+                    off += len;
+                    st = pos[pm] + sz[pm];
+                    len = pos[pc] + sz[pc] - st;
+                    for (int e = tid; e < len; e += NT) tmp[off + e] = ord[st + e];
+                    off += len;
+                }
+            }
+            // the block of ord between the old and the new place of the subtree
+            const bool right = q < a0;  // the subtree moves towards the root's end
+            const int b0 = right ? q + 1 : a0 + L;
+            const int nb = right ? a0 - q - 1 : q - a0 - L + 1;
+            __syncthreads();
+            // Phase C: one thread fixes sizes and parents (old sizes read before written,
+            // path nodes in descending order); the others save the shifting block
+            if (tid == 0) {
+                const int w = par[u_out];
+                for (int x = w; x != join; x = par[x]) sz[x] = (short)(sz[x] - L);
+                for (int x = v_in; x != join; x = par[x]) sz[x] = (short)(sz[x] + L);
+                int acc = 0;
+                for (int i = k; i >= 1; --i) {
+                    acc += sz[path[i]] - sz[path[i - 1]];
+                    sz[path[i]] = (short)acc;
+                }
+                sz[u_in] = (short)L;
+                double carry = dsc[1];
+                int prev = v_in;
+                for (int i = 0; i <= k; ++i) {
+                    const int x = path[i];
+                    const double f = tflow[x];
+                    par[x] = (short)prev;
+                    tflow[x] = carry;
+                    carry = f;
+                    prev = x;
+                }
+            }
+            for (int e = tid; e < nb; e += NT) shf[e] = ord[b0 + e];
+            __syncthreads();
+            // Phase D (all threads): the block shifts by L, the subtree lands behind v_in;
+            // positions and the subtree's potentials follow
+            const int nb0 = right ? q + 1 + L : a0;
+            const int ns0 = right ? q + 1 : a0 + nb;
+            const double sigma = dsc[0];
+            for (int e = tid; e < nb; e += NT) {
+                const int x = shf[e];
+                ord[nb0 + e] = (short)x;
+                pos[x] = (short)(nb0 + e);
+            }
+            for (int e = tid; e < L; e += NT) {
+                const int x = tmp[e];
+                ord[ns0 + e] = (short)x;
+                pos[x] = (short)(ns0 + e);
+                pi[x] += sigma;
+            }
+#ifdef OTF_EMD_STAMPS
+            if (tid == 0) st_sub += (unsigned long long)L;
+#endif
+        }
+        __syncthreads();
+#ifdef OTF_EMD_STAMPS
+        st_tree += __builtin_amdgcn_s_memrealtime() - st_t0;
+#endif
     }
 
+#ifdef OTF_EMD_STAMPS
+    if (tid == 0 && blockIdx.x == 0) {
+        g_emd_stats[0] = st_price;
+        g_emd_stats[1] = st_tree;
+        g_emd_stats[2] = st_blocks;
+        g_emd_stats[3] = st_sub;
+        g_emd_stats[4] = (unsigned long long)pivots;
+    }
+#endif
     // ---- the plan: real tree arcs carry the flow, every other arc is 0
     double cost = 0.0, art = 0.0;
     for (int u = tid; u < N - 1; u += NT) {
