@@ -38,4 +38,10 @@ if [ "${PMC:-0}" = "1" ]; then
     done
   done
 fi
+if [ "${PMC:-0}" = "1" ]; then
+  # MFMA utilisation of the cost kernel (SQ_VALU_MFMA_BUSY_CYCLES over all SIMDs; clock
+  # from GRBM_GUI_ACTIVE / 8 XCDs), one pass of its own
+  timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --stats -d gpurun_out/pmc_MFMA_auto -o run --output-format csv -- python3 bench.py --profile-only --steps 3 --warmup 1 > gpurun_out/pmc_MFMA_auto.log 2>&1
+  rc=$?; echo "pmc MFMA rc=$rc"; stop_if_fatal $rc pmc_mfma
+fi
 exit 0

@@ -82,6 +82,20 @@ def main():
             sect = "config5_kernels" if os.path.basename(os.path.dirname(p)).endswith("_c5") else "kernels"
             for k, v in med.items():
                 summary[sect].setdefault(k, {})[ctr + "_bytes_corrected"] = v * 1024 * factor
+    # MFMA utilisation pass: busy fraction = MFMA busy cycles / (1024 SIMDs x kernel
+    # cycles), kernel cycles from GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs)
+    mf = os.path.join(OUT, "pmc_MFMA_auto", "run_counter_collection.csv")
+    if os.path.exists(mf):
+        per = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(mf)):
+            per[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, d in per.items():
+            busy = sorted(d.get("SQ_VALU_MFMA_BUSY_CYCLES", [0]))[len(d.get("SQ_VALU_MFMA_BUSY_CYCLES", [0])) // 2]
+            gui = sorted(d.get("GRBM_GUI_ACTIVE", [0]))[len(d.get("GRBM_GUI_ACTIVE", [0])) // 2]
+            if busy > 0 and gui > 0:
+                summary["kernels"].setdefault(k, {})["mfma_busy_frac"] = busy / 1024.0 / (gui / 8.0)
+                summary["kernels"][k]["SQ_VALU_MFMA_BUSY_CYCLES"] = busy
+                summary["kernels"][k]["GRBM_GUI_ACTIVE"] = gui
     bench = os.path.join(OUT, "bench.log")
     cfg = {}
     if os.path.exists(bench):
