@@ -84,13 +84,20 @@ enum {
  *   HBM / the Infinity Cache once per iteration (costs too large for the register
  *   files, e.g. N = 8192 fp16 or N = 16384 fp32); one workgroup per CU owns row
  *   blocks, the column sums go through a 4-slot ring of per-iteration buffers and an
- *   XCD-hierarchical barrier.  POT flavour, m <= 16384 (float) / 8192 (double).      */
+ *   XCD-hierarchical barrier.  POT flavour, m <= 16384 (float) / 8192 (double).
+ * OTF_ENGINE_GATHER: small problems (ceil(n / 128) float / ceil(n / 64) double row
+ *   tiles <= 16, m <= 512: the per-batch feature plans of the training loop): tiles of
+ *   K in registers as in TILED, but the column partials are exchanged as epoch-tagged
+ *   granules that every workgroup gathers and sums in a fixed order -- no atomics, no
+ *   barrier, one memory hop per iteration, bitwise reproducible.  AUTO picks it first
+ *   for such shapes (and for opts.deterministic).  POT flavour.                       */
 typedef enum {
     OTF_ENGINE_AUTO = 0,
     OTF_ENGINE_STREAM = 1,
     OTF_ENGINE_RESIDENT = 2,
     OTF_ENGINE_TILED = 3,
-    OTF_ENGINE_SWEEP = 4
+    OTF_ENGINE_SWEEP = 4,
+    OTF_ENGINE_GATHER = 5
 } otf_engine;
 
 typedef struct {
@@ -107,8 +114,8 @@ typedef struct {
     int32_t n_total;    /* row-sharded solve: rows of the whole problem (u0 = 1/n_total);
                            0 = n                                                      */
     int32_t deterministic; /* 1: bitwise-reproducible column sums (fixed-order reduction,
-                           no float atomics; sweep engine, POT flavour), e.g. for
-                           parity runs; other engines return OTF_EUNSUPPORTED        */
+                           no float atomics; gather or sweep engine, POT flavour),
+                           e.g. for parity runs; other engines: OTF_EUNSUPPORTED     */
 } otf_sinkhorn_opts;
 
 /* Written on the device by otf_sinkhorn (read it after the stream completes). */

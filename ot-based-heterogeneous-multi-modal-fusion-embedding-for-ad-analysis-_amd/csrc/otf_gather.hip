@@ -1,0 +1,528 @@
+// otf_gather.hip — Sinkhorn for small problems with no device-wide barrier
+// (OTF_ENGINE_GATHER), POT flavour.
+//
+// Replaces ot.sinkhorn (POT 0.9.6 sinkhorn_knopp, MRI_PET_OT_nojax.py:143 /
+// perturbot/perturbot/match/utils.py:6-115) for the per-batch feature plans of the
+// training loop (BASELINE config 2: d x d = 512 x 512, float64, up to 2000 iterations
+// per training step) and every other problem of <= 16 row tiles x <= 512 columns.
+//
+// Like the tiled engine, workgroup w keeps a 2-D tile of K = exp(-C/reg) in registers
+// for the whole solve (8 waves x 8 rows for double / 16 rows for float, every lane 8
+// columns); the tile spans ALL columns, so the row sums K v are finished inside the
+// wave.  The column sums K^T u are the only device-wide exchange.  Instead of float
+// atomics into a shared buffer followed by a grid barrier and a re-read (three memory
+// round trips, 4.4 of 6.7 us per iteration at config 2), every workgroup PUBLISHES its
+// column partials as epoch-tagged granules (R2 form, cdna_hip_programming.md Guideline
+// 16: {value word, tag} 8-byte granules, a float per granule or a double as two, one
+// 16-B write-through store per two granules) and every workgroup GATHERS all the
+// partials itself, polling until every tag carries the epoch it waits for.  The data
+// is its own flag: no fence, no counter, no barrier.  One memory hop per iteration.
+//
+// Every workgroup adds the partials in the same fixed order (workgroup 0, 1, ...), so
+// every workgroup holds bit-identical column sums and takes POT's decisions
+// (convergence, numerical break) at the same iteration with no further exchange, and
+// the result is bitwise reproducible run to run (deterministic by construction).
+//
+// Tags: partials of S[k] = K^T u(k-1) carry epoch k + 1 (slot k & 1) and the OR of the
+// producer's numerical-break flags of iteration k - 1 (non-finite u or v) in bit 0:
+// tag = ((k + 1) << 1) | bad.  A slot is rewritten two epochs later, which no producer
+// can reach before every consumer has finished reading it (producing S[k + 2] needs
+// S[k + 1], which each workgroup publishes only after its gather of S[k]).  Every poll
+// is bounded by s_memrealtime (re-armed after each completed gather): a stall ends in
+// OTF_SK_TIMEOUT.
+#include "otf_persist.h"
+
+namespace otf {
+namespace {
+
+template <typename T> struct GatherCfg {
+    static constexpr int NW = 8;                        // waves per workgroup
+    static constexpr int RW = sizeof(T) == 4 ? 16 : 8;  // rows per wave
+    static constexpr int VEC = Vec<T>::N;
+    static constexpr int G = sizeof(T) == 4 ? 2 : 4;    // VEC-vectors per lane: 8 columns
+    static constexpr int TR = RW * NW;                  // rows per workgroup: 128 / 64
+    static constexpr int C = kWave * G * VEC;           // 512 columns
+    static constexpr int CPC = 8 / (int)sizeof(T);      // columns per 16-B chunk (2 granules)
+    static constexpr int NCH = C / CPC;                 // chunks per producer row
+};
+constexpr int kGatherMaxWG = 16;
+constexpr uint32_t kGatherRow = 8192;  // bytes per producer row of one slot (512 chunks)
+
+template <typename T> struct SkGatherArgs {
+    const void* C;
+    int64_t ldc;
+    int n, m;
+    const T* a;        // padded marginals (zero past n / m)
+    const T* b;
+    const T* cost_scale;
+    double reg;
+    int max_iter, check_every, err_squared;
+    double stop_thr;
+    void* gran;        // [2 slots][grid][kGatherRow] granules, zeroed per solve
+    otf_sinkhorn_info* info;
+    double* errlog;
+    T* u_out;
+    T* v_out;
+    void* P;
+    int64_t ldp;
+    unsigned long long timeout_ticks;
+};
+
+using I4 = __attribute__((ext_vector_type(4))) int;
+
+template <typename T> __device__ __forceinline__ void chunk_values(const I4 x, T (&v)[GatherCfg<T>::CPC]) {
+    if constexpr (sizeof(T) == 8) {
+        v[0] = __builtin_bit_cast(double, ((unsigned long long)(unsigned)x[2] << 32) | (unsigned)x[0]);
+    } else {
+        // element copies first: __builtin_bit_cast of a vector ELEMENT reads the vector's
+        // first word (ROCm 7.2 clang; found by the float parity test)
+        const int w0 = x[0], w2 = x[2];
+        v[0] = __builtin_bit_cast(float, w0);
+        v[1] = __builtin_bit_cast(float, w2);
+    }
+}
+template <typename T> __device__ __forceinline__ I4 make_chunk(const T (&v)[GatherCfg<T>::CPC], int tag) {
+    I4 x;
+    if constexpr (sizeof(T) == 8) {
+        const unsigned long long bits = __builtin_bit_cast(unsigned long long, v[0]);
+        x[0] = (int)(unsigned)bits;
+        x[2] = (int)(unsigned)(bits >> 32);
+    } else {
+        x[0] = __builtin_bit_cast(int, v[0]);
+        x[2] = __builtin_bit_cast(int, v[1]);
+    }
+    x[1] = tag;
+    x[3] = tag;
+    return x;
+}
+
+// NQ: producers polled per pass, the grid rounded up to 4 / 8 / 16 (surplus slots
+// re-read the last producer, so every load is unconditional and in flight together).
+template <typename T, typename CT, typename TP, int NQ>
+__global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
+    using Cf = GatherCfg<T>;
+    constexpr int G = Cf::G, VEC = Cf::VEC, R = Cf::RW, NW = Cf::NW, TR = Cf::TR;
+    constexpr int CPC = Cf::CPC, NCH = Cf::NCH;
+    using V = typename Vec<T>::type;
+    using VP = __attribute__((ext_vector_type(VEC))) TP;
+    __shared__ __attribute__((aligned(16))) T colbuf[NW][Cf::C];
+    __shared__ __attribute__((aligned(16))) T vcur[Cf::C];      // v = b / (gathered K^T u)
+    __shared__ __attribute__((aligned(16))) T vhist[2][Cf::C];  // v by iteration parity
+    __shared__ T urow[NW][R];
+    __shared__ T uhist[2][TR];
+    __shared__ T red[17 + 17];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nwg = gridDim.x;
+    const bool lead = (blockIdx.x == 0 && tid == 0);
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+    const int row0 = blockIdx.x * TR + w * R;
+
+    const double unit = exp_unit<T>();
+    double cinv = 1.0;
+    if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
+    const T ks = (T)(-unit / p.reg * cinv);
+
+    int colc[G];
+    bool cok[G][VEC];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int c0 = (lane + kWave * g) * VEC;
+        colc[g] = c0 < p.m ? c0 : 0;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) cok[g][k] = c0 + k < p.m;
+    }
+    // ---- K for this wave's rows x this lane's 8 columns, once
+    T kv[R][G][VEC];
+    {
+        const CT* crow = (const CT*)p.C + (int64_t)row0 * p.ldc;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const CT* src = (row0 + r < p.n) ? crow : (const CT*)p.C;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const V c = load_cost<T>(src + colc[g]);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
+            }
+            crow += p.ldc;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool rok = row0 + r < p.n;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k)
+                    kv[r][g][k] = (rok && cok[g][k]) ? fast_exp(kv[r][g][k] * ks) : (T)0;
+        }
+    }
+    const T ia_mine = (T)1 / p.a[row0 + (lane & (R - 1)) < p.n ? row0 + (lane & (R - 1)) : p.n - 1];
+    // this thread's gathered columns (chunk tid): their target marginal
+    T bch[CPC];
+#pragma unroll
+    for (int c = 0; c < CPC; ++c) {
+        const int col = tid * CPC + c;
+        bch[c] = (tid < NCH && col < p.m) ? p.b[col] : (T)0;
+    }
+    const T u0 = (T)1 / (T)p.n, v0 = (T)1 / (T)p.m;
+    for (int q = tid; q < Cf::C; q += blockDim.x) vhist[0][q] = vhist[1][q] = v0;
+    if (tid < TR) uhist[0][tid] = uhist[1][tid] = u0;
+
+    const __amdgpu_buffer_rsrc_t rs = sums_rsrc(p.gran);
+    const uint32_t my_row = (uint32_t)blockIdx.x * kGatherRow + (uint32_t)tid * 16;
+
+    // publish this workgroup's partials of S[k] = K_tile^T wr (epoch k + 1, slot k & 1)
+    auto publish = [&](const T (&wr)[R], int k, int bad_local) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            V acc;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+                T sacc = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) sacc += kv[r][g][q] * wr[r];
+                acc[q] = sacc;
+            }
+            *reinterpret_cast<V*>(&colbuf[w][(lane + kWave * g) * VEC]) = acc;
+        }
+        const int bad = __syncthreads_or(bad_local) ? 1 : 0;
+        if (tid < NCH) {
+            T val[CPC];
+#pragma unroll
+            for (int c = 0; c < CPC; ++c) {
+                T sacc = colbuf[0][tid * CPC + c];
+#pragma unroll
+                for (int ww = 1; ww < NW; ++ww) sacc += colbuf[ww][tid * CPC + c];
+                val[c] = sacc;
+            }
+            const uint32_t off = (uint32_t)(k & 1) * (uint32_t)nwg * kGatherRow + my_row;
+            __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(val, ((k + 1) << 1) | bad), rs, off, 0,
+                                                   16 /* sc1 */);
+        }
+    };
+    // gather S[k]: every producer's chunk `tid`, summed in producer order, and, for those
+    // columns, v = b / S[k] into vcur (once per column, not once per wave) and, when
+    // eslot >= 0, this thread's terms of the marginal error of the iterate whose v is
+    // vhist[eslot].  Returns bit 0 = a producer flagged a break in iteration k - 1,
+    // bit 1 = stall, bit 2 = a zero sum or non-finite v (POT's break test on v).
+    auto gather = [&](int k, int eslot, T& e_loc) -> int {
+        int fl = 0;
+        e_loc = 0;
+        if (tid < NCH) {
+            const unsigned ep = (unsigned)(k + 1);
+            const uint32_t base = (uint32_t)(k & 1) * (uint32_t)nwg * kGatherRow + (uint32_t)tid * 16;
+            I4 x[NQ];
+            for (;;) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const uint32_t src = (uint32_t)(q < nwg ? q : nwg - 1) * kGatherRow;
+                    x[q] = __builtin_bit_cast(
+                        I4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + src, 0, 16 /* sc1 */));
+                }
+                bool ok = true;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+                    ok &= ((unsigned)x[q][1] >> 1) == ep && ((unsigned)x[q][3] >> 1) == ep;
+                if (ok) break;
+                if (__builtin_amdgcn_s_memrealtime() > deadline) {
+                    fl |= 2;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            T sv[CPC];
+#pragma unroll
+            for (int c = 0; c < CPC; ++c) sv[c] = 0;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                if (q < nwg) {
+                    T v[CPC];
+                    chunk_values<T>(x[q], v);
+#pragma unroll
+                    for (int c = 0; c < CPC; ++c) sv[c] += v[c];
+                    fl |= x[q][1] & 1;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < CPC; ++c) {
+                const int col = tid * CPC + c;
+                const bool ok = col < p.m;
+                const T val = bch[c] / sv[c];
+                fl |= (ok && ((sv[c] == (T)0) || !finite_val(val))) ? 4 : 0;
+                vcur[col] = ok ? val : (T)0;
+                if (eslot >= 0) {
+                    const T rr = vhist[eslot][col] * sv[c] - bch[c];
+                    e_loc += ok ? rr * rr : (T)0;
+                }
+            }
+        }
+        // one barrier in the common case; which flags were raised only when one was
+        int f = 0;
+        if (__syncthreads_or(fl))
+            f = (__syncthreads_or(fl & 1) ? 1 : 0) | (__syncthreads_or(fl & 2) ? 2 : 0) |
+                (__syncthreads_or(fl & 4) ? 4 : 0);
+        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+        return f;
+    };
+    auto marg_error = [&](T e_loc) -> double {
+        const T e = block_sum<T>(e_loc, red);
+        return p.err_squared ? (double)e : sqrt((double)e);
+    };
+
+    // ---- prologue: S[0] = K^T u0
+    {
+        T wr[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) wr[r] = (row0 + r < p.n) ? u0 : (T)0;
+        publish(wr, 0, 0);
+    }
+    int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
+    bool done = false;
+    const int rowl = butterfly_row<R>(lane);
+
+    for (int it = 0; it < p.max_iter; ++it) {
+        OTF_STAMP(it, 0);
+        const bool check = it >= 1 && ((it - 1) % p.check_every) == 0;
+        T e_loc;
+        const int fl = gather(it, check ? (it - 1) & 1 : -1, e_loc);
+        OTF_STAMP(it, 1);
+        if (fl & 2) {
+            status = OTF_SK_TIMEOUT;
+            done = true;
+            break;
+        }
+        // a numerical break in iteration it-1 (any workgroup) -> revert to it-2
+        if (fl & 1) {
+            last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
+            done = true;
+            break;
+        }
+        // marginal error of iterate it-1 (identical in every workgroup)
+        if (check) {
+            const double err = marg_error(e_loc);
+            if (lead) p.errlog[(it - 1) / p.check_every] = err;
+            n_err = (it - 1) / p.check_every + 1;
+            if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) {
+                last_good = it - 1; niter = it - 1; status = OTF_SK_CONVERGED;
+                done = true;
+                break;
+            }
+        }
+        const int badv = (fl & 4) ? 1 : 0;   // flagged with this iteration's partials
+        T vn[G][VEC];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const V t = *reinterpret_cast<const V*>(&vcur[(lane + kWave * g) * VEC]);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) vn[g][k] = t[k];
+        }
+        OTF_STAMP(it, 2);
+        // row sums over all columns: wave totals are the row sums
+        T rp[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            T acc = 0;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) acc += kv[r][g][k] * vn[g][k];
+            rp[r] = acc;
+        }
+        wave_sum_multi<T, R>(rp, lane);
+        const int slot = it & 1;
+        if (lane < R) urow[w][rowl] = rp[0];
+        __builtin_amdgcn_wave_barrier();
+        const T tot = urow[w][lane & (R - 1)];
+        __builtin_amdgcn_wave_barrier();
+        if (lane < R) {
+            T un = (T)1 / (tot * ia_mine);
+            if (row0 + lane >= p.n) un = 0;
+            urow[w][lane] = un;
+            uhist[slot][w * R + lane] = un;
+        }
+        __builtin_amdgcn_wave_barrier();  // wave-private LDS hand-off (in-order LDS queue)
+        T un[R];
+        int badu = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            un[r] = urow[w][r];
+            badu |= (row0 + r < p.n && !finite_val(un[r])) ? 1 : 0;
+        }
+        if (w == 0) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                V vv;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) vv[q] = vn[g][q];
+                *reinterpret_cast<V*>(&vhist[slot][(lane + kWave * g) * VEC]) = vv;
+            }
+        }
+        OTF_STAMP(it, 3);
+        publish(un, it + 1, badv | badu);
+        OTF_STAMP(it, 4);
+        OTF_STAMP(it, 5);
+    }
+    if (!done && p.max_iter > 0) {
+        // the last iteration's break flags and K^T u(max_iter - 1)
+        const int it = p.max_iter - 1;
+        const bool check = (it % p.check_every) == 0;
+        T e_loc;
+        const int fl = gather(p.max_iter, check ? it & 1 : -1, e_loc);
+        if (fl & 2) {
+            status = OTF_SK_TIMEOUT;
+        } else if (fl & 1) {
+            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
+        } else {
+            last_good = it; niter = it;
+            if (check) {
+                const double err = marg_error(e_loc);
+                if (lead) p.errlog[it / p.check_every] = err;
+                n_err = it / p.check_every + 1;
+                if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) status = OTF_SK_CONVERGED;
+            }
+        }
+    }
+
+    // ---- outputs: (u, v) of last_good from the histories, plan from registers
+    __syncthreads();
+    const int hs = last_good & 1;
+    T uo[R], vo[G][VEC];
+#pragma unroll
+    for (int r = 0; r < R; ++r) uo[r] = last_good < 0 ? u0 : uhist[hs][w * R + r];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+            vo[g][k] = last_good < 0 ? v0 : vhist[hs][(lane + kWave * g) * VEC + k];
+    if (lane < R && row0 + lane < p.n) {
+        T mine = uo[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) if (lane == r) mine = uo[r];
+        p.u_out[row0 + lane] = mine;
+    }
+    if (blockIdx.x == 0 && w == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k)
+                if (cok[g][k]) p.v_out[colc[g] + k] = vo[g][k];
+    }
+    if (p.P) {
+        TP* P = (TP*)p.P;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (row0 + r >= p.n) break;
+            TP* prow = P + (int64_t)(row0 + r) * p.ldp;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int c0 = (lane + kWave * g) * VEC;
+                if (c0 >= p.m) continue;
+                VP o;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) o[k] = (TP)(uo[r] * kv[r][g][k] * vo[g][k]);
+                if (c0 + VEC <= p.m) {
+                    *reinterpret_cast<VP*>(prow + c0) = o;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k)
+                        if (c0 + k < p.m) prow[c0 + k] = o[k];
+                }
+            }
+        }
+    }
+    if (status == OTF_SK_TIMEOUT && tid == 0) store_wt(&p.info->stalled, 1);
+    if (lead) {
+        p.info->last_good = last_good;
+        p.info->niter = niter;
+        p.info->status = status;
+        p.info->break_iter = brk;
+        p.info->n_err = n_err;
+        p.info->engine = OTF_ENGINE_GATHER;
+        p.info->stop = 1;
+    }
+}
+
+template <typename T, typename CT, typename TP, int NQ>
+hipError_t launch_gather_q(int grid, SkGatherArgs<T>& p, hipStream_t s) {
+    void* args[] = {&p};
+    const void* k = (const void*)sk_gather_kernel<T, CT, TP, NQ>;
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1 || grid > per_cu * device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
+    return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
+}
+
+template <typename T, typename CT, typename TP>
+hipError_t launch_gather(int grid, SkGatherArgs<T>& p, hipStream_t s) {
+    if (grid <= 4) return launch_gather_q<T, CT, TP, 4>(grid, p, s);
+    if (grid <= 8) return launch_gather_q<T, CT, TP, 8>(grid, p, s);
+    return launch_gather_q<T, CT, TP, 16>(grid, p, s);
+}
+
+template <typename T> int64_t gather_grid(int64_t n) {
+    return (n + GatherCfg<T>::TR - 1) / GatherCfg<T>::TR;
+}
+
+}  // namespace
+
+template <typename T> bool gather_supported(int64_t n, int64_t m) {
+    return n >= 1 && m >= 1 && m <= GatherCfg<T>::C && gather_grid<T>(n) <= kGatherMaxWG;
+}
+
+template <typename T> size_t gather_region_bytes(int64_t n, int64_t m) {
+    return gather_supported<T>(n, m) ? 2 * (size_t)gather_grid<T>(n) * kGatherRow : 0;
+}
+
+template <typename T, typename CT>
+hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, const T* b_pad,
+                      const T* cost_scale, const otf_sinkhorn_opts& o, void* region, T* u_out,
+                      T* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
+                      double* errlog, hipStream_t s) {
+    if (!gather_supported<T>(n, m) || !region) return hipErrorInvalidValue;
+    SkGatherArgs<T> p{};
+    p.C = C;
+    p.ldc = ldc;
+    p.n = n;
+    p.m = m;
+    p.a = a_pad;
+    p.b = b_pad;
+    p.cost_scale = cost_scale;
+    p.reg = o.reg;
+    p.max_iter = o.max_iter;
+    p.check_every = o.check_every;
+    p.err_squared = o.err_squared;
+    p.stop_thr = o.stop_thr;
+    p.gran = region;
+    p.info = info;
+    p.errlog = errlog;
+    p.u_out = u_out;
+    p.v_out = v_out;
+    p.P = P_out;
+    p.ldp = ldp;
+    p.timeout_ticks = stall_ticks();
+    hipError_t e = hipMemsetAsync(region, 0, gather_region_bytes<T>(n, m), s);
+    if (e != hipSuccess) return e;
+    const int grid = (int)gather_grid<T>(n);
+    if (P_out && P_dtype == OTF_F64) return launch_gather<T, CT, double>(grid, p, s);
+    return launch_gather<T, CT, float>(grid, p, s);
+}
+
+template bool gather_supported<float>(int64_t, int64_t);
+template bool gather_supported<double>(int64_t, int64_t);
+template size_t gather_region_bytes<float>(int64_t, int64_t);
+template size_t gather_region_bytes<double>(int64_t, int64_t);
+template hipError_t run_gather<float, float>(const float*, int64_t, int, int, const float*, const float*,
+                                             const float*, const otf_sinkhorn_opts&, void*, float*,
+                                             float*, void*, int64_t, int, otf_sinkhorn_info*, double*,
+                                             hipStream_t);
+template hipError_t run_gather<float, _Float16>(const _Float16*, int64_t, int, int, const float*,
+                                                const float*, const float*, const otf_sinkhorn_opts&,
+                                                void*, float*, float*, void*, int64_t, int,
+                                                otf_sinkhorn_info*, double*, hipStream_t);
+template hipError_t run_gather<double, double>(const double*, int64_t, int, int, const double*,
+                                               const double*, const double*, const otf_sinkhorn_opts&,
+                                               void*, double*, double*, void*, int64_t, int,
+                                               otf_sinkhorn_info*, double*, hipStream_t);
+
+}  // namespace otf

@@ -1425,6 +1425,8 @@ struct Workspace {
     size_t res_bytes;
     void* sweep;      // sweep engine region (otf_sweep.hip)
     size_t sweep_bytes;
+    void* gather;     // gather engine granules (otf_gather.hip); 0 bytes if not taken
+    size_t gather_bytes;
     int nrep;
     size_t bytes;
     int64_t m_pad;
@@ -1480,6 +1482,8 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.res = take(w.res_bytes);
     w.sweep_bytes = esz == 8 ? sweep_region_bytes<double>(w.m_pad) : sweep_region_bytes<float>(w.m_pad);
     w.sweep = take(w.sweep_bytes);
+    w.gather_bytes = esz == 8 ? gather_region_bytes<double>(n, m) : gather_region_bytes<float>(n, m);
+    w.gather = take(w.gather_bytes);
     w.bytes = off;
     return w;
 }
@@ -1727,6 +1731,16 @@ int sk_finish(SkArgs<T>& p, const SkSetup<T>& su, const CT* C, int64_t ldc, int6
     return OTF_OK;
 }
 
+// OTF_GATHER=0 keeps AUTO off the gather engine (A/B measurements); GATHER still forces it
+inline bool gather_enabled() {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("OTF_GATHER");
+        env = e ? atoi(e) : 1;
+    }
+    return env != 0;
+}
+
 template <typename T, typename CT, bool LOG>
 int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_t ldc,
                  const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out, void* P_out,
@@ -1742,10 +1756,24 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     rc = sk_init<T>(su, a, b, n, m, info, s);
     if (rc != OTF_OK) return rc;
 
-    // deterministic mode: only the sweep engine reduces the column sums in a fixed order
+    const bool whole = o.n_total <= 0 || o.n_total == n;
+    // gather engine: small problems, one granule hop per iteration, no barrier (and
+    // deterministic by construction)
+    const bool gfits = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && gather_supported<T>(n, m) &&
+                       su.w.gather_bytes > 0;
+    if (o.engine == OTF_ENGINE_GATHER && !gfits) return OTF_EUNSUPPORTED;
+    if (gfits && (o.engine == OTF_ENGINE_GATHER || (o.engine == OTF_ENGINE_AUTO && gather_enabled()))) {
+        const hipError_t e = run_gather<T, CT>(C, ldc, (int)n, (int)m, (const T*)su.w.a_pad,
+                                               (const T*)su.w.b_pad, cost_scale, o, su.w.gather, u_out,
+                                               v_out, P_out, ldp, P_dtype, info, errlog, s);
+        if (e == hipSuccess) return OTF_OK;
+        (void)hipGetLastError();
+        if (o.engine == OTF_ENGINE_GATHER) return check_hip(e);
+    }
+    // deterministic mode otherwise: the sweep engine reduces the column sums in a fixed order
     if (o.deterministic) {
         if (LOG || avg_pass_ms || !(o.engine == OTF_ENGINE_AUTO || o.engine == OTF_ENGINE_SWEEP) ||
-            o.max_iter < 1 || !sweep_supported<T, CT>(n, m, ldc) || !(o.n_total <= 0 || o.n_total == n))
+            o.max_iter < 1 || !sweep_supported<T, CT>(n, m, ldc) || !whole)
             return OTF_EUNSUPPORTED;
         return check_hip(run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
                                           (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
@@ -1753,7 +1781,6 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     }
     // resident engine: the whole solve in one persistent launch when every row block
     // gets its own CU (POT flavour, no per-pass profiling requested)
-    const bool whole = o.n_total <= 0 || o.n_total == n;
     const bool fits = su.nrb <= device_cu_count() && su.cfg.G <= 4 && whole;
     // tiled engine: every (128 x 512 float / 64 x 512 double) tile on its own CU
     const bool tfits = whole && su.w.t_nrb * su.w.t_ncb <= device_cu_count() &&

@@ -1,49 +1,52 @@
 // Diagnostic: where does a resident-engine iteration spend its time?
 // Builds the library sources with -DOTF_STAMPS, runs the bench workload shape
-// (N = 4096 fp32, 100 iterations) and prints per-phase wall-clock spans averaged
+// (N = 4096 fp32, 100 iterations; "N resident double": config 2, float64, 1999 iterations) and prints per-phase wall-clock spans averaged
 // over workgroups and iterations 2..15 (s_memrealtime, 100 MHz => 10 ns ticks):
 //   0->1 sums read + v + decisions   1->2 row dots + block reduction
 //   2->3 u + column partials + atomics issued   3->4 atomics performed (vmcnt 0)
 //   4->5 device-wide barrier            5->0' next iteration start
 // Build: hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -DOTF_STAMPS -I include \
-//        -I <pkg>/csrc tools/stamps_resident.hip -o tools/stamps_resident
+//        -I <pkg>/csrc tools/stamps_resident.hip -o tools/stamps_resident -ldl
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_common.hip"
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sinkhorn.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sweep.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_gather.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_comm.hip"
 
 #include <cmath>
 #include <cstdio>
 #include <vector>
 
-int main(int argc, char** argv) {
-    const int N = argc > 1 ? atoi(argv[1]) : 4096;
-    const bool tiled = argc > 2 && argv[2][0] == 't';  // second argument "tiled": OTF_ENGINE_TILED
-    const int iters = 100;
-    float *C, *a, *u, *v, *P;
+template <typename T>
+int run(const int N, const char eng, const int iters, const double reg) {
+    const bool tiled = eng == 't';
+    const int dt = sizeof(T) == 8 ? OTF_F64 : OTF_F32;
+    T *C, *a, *u, *v, *P;
     otf_sinkhorn_info* info;
-    (void)hipMalloc(&C, (size_t)N * N * 4);
-    (void)hipMalloc(&a, N * 4);
-    (void)hipMalloc(&u, N * 4);
-    (void)hipMalloc(&v, N * 4);
-    (void)hipMalloc(&P, (size_t)N * N * 4);
+    (void)hipMalloc(&C, (size_t)N * N * sizeof(T));
+    (void)hipMalloc(&a, N * sizeof(T));
+    (void)hipMalloc(&u, N * sizeof(T));
+    (void)hipMalloc(&v, N * sizeof(T));
+    (void)hipMalloc(&P, (size_t)N * N * sizeof(T));
     (void)hipMalloc(&info, sizeof(otf_sinkhorn_info));
-    std::vector<float> h((size_t)N * N);
+    std::vector<T> h((size_t)N * N);
     unsigned s = 1;
-    for (auto& x : h) { s = s * 1664525u + 1013904223u; x = (s >> 8) * (1.0f / 16777216.0f); }
-    (void)hipMemcpy(C, h.data(), h.size() * 4, hipMemcpyHostToDevice);
-    std::vector<float> ha(N, 1.0f / N);
-    (void)hipMemcpy(a, ha.data(), N * 4, hipMemcpyHostToDevice);
-    const size_t wsb = otf_sinkhorn_workspace_size(N, N, OTF_F32, iters);
+    for (auto& x : h) { s = s * 1664525u + 1013904223u; x = (T)((s >> 8) * (1.0 / 16777216.0)); }
+    (void)hipMemcpy(C, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+    std::vector<T> ha(N, (T)1 / N);
+    (void)hipMemcpy(a, ha.data(), N * sizeof(T), hipMemcpyHostToDevice);
+    const size_t wsb = otf_sinkhorn_workspace_size(N, N, dt, iters);
     void* ws;
     (void)hipMalloc(&ws, wsb);
     otf_sinkhorn_opts o{};
-    o.reg = 0.1; o.stop_thr = 0; o.max_iter = iters; o.check_every = 10;
-    o.flavor = OTF_FLAVOR_POT; o.engine = tiled ? OTF_ENGINE_TILED : OTF_ENGINE_RESIDENT;
+    o.reg = reg; o.stop_thr = 0; o.max_iter = iters; o.check_every = 10;
+    o.flavor = OTF_FLAVOR_POT; o.engine = eng == 't' ? OTF_ENGINE_TILED : eng == 'g' ? OTF_ENGINE_GATHER : OTF_ENGINE_RESIDENT;
     for (int rep = 0; rep < 3; ++rep) {
         hipEvent_t e0, e1;
         (void)hipEventCreate(&e0);
         (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0, 0);
-        int rc = otf_sinkhorn(a, a, C, N, N, N, OTF_F32, nullptr, &o, u, v, P, N, OTF_F32, info,
+        int rc = otf_sinkhorn(a, a, C, N, N, N, dt, nullptr, &o, u, v, P, N, dt, info,
                               nullptr, ws, wsb, 0);
         (void)hipEventRecord(e1, 0);
         (void)hipEventSynchronize(e1);
@@ -56,16 +59,16 @@ int main(int argc, char** argv) {
     }
     // correctness: the resident result against the streaming engine on the same input
     {
-        std::vector<float> ur(N), vr(N), us(N), vs(N);
-        (void)hipMemcpy(ur.data(), u, N * 4, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(vr.data(), v, N * 4, hipMemcpyDeviceToHost);
+        std::vector<T> ur(N), vr(N), us(N), vs(N);
+        (void)hipMemcpy(ur.data(), u, N * sizeof(T), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(vr.data(), v, N * sizeof(T), hipMemcpyDeviceToHost);
         otf_sinkhorn_opts os = o;
         os.engine = OTF_ENGINE_STREAM;
-        int rc = otf_sinkhorn(a, a, C, N, N, N, OTF_F32, nullptr, &os, u, v, nullptr, N, OTF_F32,
+        int rc = otf_sinkhorn(a, a, C, N, N, N, dt, nullptr, &os, u, v, nullptr, N, dt,
                               info, nullptr, ws, wsb, 0);
         (void)hipDeviceSynchronize();
-        (void)hipMemcpy(us.data(), u, N * 4, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(vs.data(), v, N * 4, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(us.data(), u, N * sizeof(T), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(vs.data(), v, N * sizeof(T), hipMemcpyDeviceToHost);
         // u, v are defined up to a scale (u*c, v/c): compare the products u_i v_j
         double umax = 0, vmax = 0, du = 0, dv = 0;
         const double cu = (double)ur[0] / us[0];
@@ -80,8 +83,10 @@ int main(int argc, char** argv) {
     }
     std::vector<unsigned long long> st(256 * 16 * 8);
     (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(otf::g_stamps), st.size() * 8);
-    int nwg = (N + 15) / 16 < 256 ? (N + 15) / 16 : 256;
-    if (tiled) nwg = ((N + 127) / 128) * ((N + 511) / 512) < 256 ? ((N + 127) / 128) * ((N + 511) / 512) : 256;
+    // resident grid: the rows per workgroup the library picked are in the stamps
+    int nwg = 0;
+    for (int w = 0; w < 256; ++w)
+        if (st[(w * 16 + 2) * 8] != 0) nwg = w + 1;
     double span[6] = {0};
     int cnt = 0;
     double arrive_spread = 0;
@@ -102,8 +107,18 @@ int main(int argc, char** argv) {
                              "atomics performed", "grid barrier", "loop back"};
     const char* tnames[6] = {"sums+v+decide", "row partials+group wait", "gather+u",
                              "col partials+atomics done", "grid barrier", "loop back"};
-    const char* const* names = tiled ? tnames : rnames;
+    const char* gnames[6] = {"gather (poll) + sums", "v + decide", "row sums + u",
+                             "col partials + publish", "-", "loop back"};
+    const char* const* names = tiled ? tnames : eng == 'g' ? gnames : rnames;
     for (int ph = 0; ph < 6; ++ph) printf("%-26s %8.2f us\n", names[ph], span[ph] / cnt / 100.0);
     printf("barrier arrival spread     %8.2f us\n", arrive_spread / 13 / 100.0);
     return 0;
+}
+
+int main(int argc, char** argv) {
+    const int N = argc > 1 ? atoi(argv[1]) : 4096;
+    const char eng = argc > 2 ? argv[2][0] : 'r';  // "tiled" / "gather" / "resident"
+    const bool f64 = argc > 3 && argv[3][0] == 'd';     // third argument "double": config-2 form
+    if (f64) return run<double>(N, eng, 1999, 1e-2);
+    return run<float>(N, eng, 100, 0.1);
 }
