@@ -153,8 +153,8 @@ __global__ __launch_bounds__(256) void cost_pairwise_kernel(
         float sx = nx[qq], sy = ny[qq];
 #pragma unroll
         for (int o = 1; o < 8; o <<= 1) {
-            sx += __shfl_xor(sx, o, 64);
-            sy += __shfl_xor(sy, o, 64);
+            sx += wave_xor_n<float>(sx, o);
+            sy += wave_xor_n<float>(sy, o);
         }
         if ((tid & 7) == 0) {
             sxx[lrow + 32 * qq] = sx;

@@ -50,15 +50,69 @@ template <typename T> __device__ __forceinline__ bool finite_val(T x) {
     return !(isnan(x) || isinf(x));
 }
 
+// x of lane (lane ^ O) for O = 1, 2, 4, 8, 16, 32, entirely in the VALU: DPP quad_perm
+// (1, 2), DPP row_shl / row_shr + a lane select (4, 8: within a 16-lane row), and the
+// gfx950 v_permlane16_swap / v_permlane32_swap (16, 32).  No LDS crossbar round trip
+// (ds_bpermute, what __shfl_xor lowers to): a dependent chain of exchanges -- the
+// butterfly reductions below -- costs a few cycles per step instead of ~100.
+// tools/ubench_xor.hip checks every offset on the device.
+template <int O> __device__ __forceinline__ unsigned wave_xor_u32(unsigned x) {
+    if constexpr (O == 1) {
+        return __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    } else if constexpr (O == 2) {
+        return __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    } else if constexpr (O == 4 || O == 8) {
+        const unsigned from_up = __builtin_amdgcn_update_dpp(0u, x, 0x100 + O, 0xF, 0xF, false);  // row_shl
+        const unsigned from_dn = __builtin_amdgcn_update_dpp(0u, x, 0x110 + O, 0xF, 0xF, false);  // row_shr
+        return (__lane_id() & O) ? from_dn : from_up;
+    } else if constexpr (O == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (__lane_id() & 16) ? r[0] : r[1];
+    } else {
+        static_assert(O == 32, "lane offset");
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (__lane_id() & 32) ? r[0] : r[1];
+    }
+}
+template <typename T, int O> __device__ __forceinline__ T wave_xor(T x) {
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, wave_xor_u32<O>(__builtin_bit_cast(unsigned, x)));
+    } else {
+        static_assert(sizeof(T) == 8, "4- or 8-byte values");
+        const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+        const unsigned lo = wave_xor_u32<O>((unsigned)b), hi = wave_xor_u32<O>((unsigned)(b >> 32));
+        return __builtin_bit_cast(T, ((unsigned long long)hi << 32) | lo);
+    }
+}
+// runtime offset (a power of two <= 32) -> the compile-time exchange
+template <typename T> __device__ __forceinline__ T wave_xor_n(T x, int o) {
+    switch (o) {
+        case 1: return wave_xor<T, 1>(x);
+        case 2: return wave_xor<T, 2>(x);
+        case 4: return wave_xor<T, 4>(x);
+        case 8: return wave_xor<T, 8>(x);
+        case 16: return wave_xor<T, 16>(x);
+        default: return wave_xor<T, 32>(x);
+    }
+}
+
 template <typename T> __device__ __forceinline__ T wave_sum(T x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, kWave);
+    x += wave_xor<T, 32>(x);
+    x += wave_xor<T, 16>(x);
+    x += wave_xor<T, 8>(x);
+    x += wave_xor<T, 4>(x);
+    x += wave_xor<T, 2>(x);
+    x += wave_xor<T, 1>(x);
     return x;
 }
 
 template <typename T> __device__ __forceinline__ T wave_max(T x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o, kWave));
+    x = fmax(x, wave_xor<T, 32>(x));
+    x = fmax(x, wave_xor<T, 16>(x));
+    x = fmax(x, wave_xor<T, 8>(x));
+    x = fmax(x, wave_xor<T, 4>(x));
+    x = fmax(x, wave_xor<T, 2>(x));
+    x = fmax(x, wave_xor<T, 1>(x));
     return x;
 }
 
@@ -84,11 +138,11 @@ template <typename T, int R> __device__ __forceinline__ void wave_sum_multi(T (&
         for (int i = 0; i < h; ++i) {
             const T send = upper ? x[i] : x[i + h];
             const T keep = upper ? x[i + h] : x[i];
-            x[i] = keep + __shfl_xor(send, o, kWave);
+            x[i] = keep + wave_xor_n<T>(send, o);
         }
     }
 #pragma unroll
-    for (int o = (R > 1 ? R : 1); o < kWave; o <<= 1) x[0] += __shfl_xor(x[0], o, kWave);
+    for (int o = (R > 1 ? R : 1); o < kWave; o <<= 1) x[0] += wave_xor_n<T>(x[0], o);
 }
 
 // Block-wide sum of R values per thread.  `red` is LDS of >= (nwaves + 1) * R
@@ -131,7 +185,7 @@ __device__ __forceinline__ void block_sum_rows(T (&x)[R], T* tbuf, T* wbuf) {
 #pragma unroll
     for (int k = 0; k < R; ++k) s += tbuf[(q + Q * k) * R + r];
 #pragma unroll
-    for (int o = R; o < kWave; o <<= 1) s += __shfl_xor(s, o, kWave);
+    for (int o = R; o < kWave; o <<= 1) s += wave_xor_n<T>(s, o);
     if (lane < R) wbuf[wid * R + lane] = s;
     __syncthreads();
     if (t < R) {

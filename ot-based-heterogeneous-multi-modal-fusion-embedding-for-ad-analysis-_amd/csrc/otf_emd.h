@@ -173,8 +173,8 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
             }
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) {
-                const double v2 = __shfl_xor(bv, o, 64);
-                const int i2 = __shfl_xor(bi, o, 64);
+                const double v2 = wave_xor_n<double>(bv, o);
+                const int i2 = wave_xor_n<int>(bi, o);
                 argmin_pair(bv, bi, v2, i2);
             }
             if (lane == 0) {

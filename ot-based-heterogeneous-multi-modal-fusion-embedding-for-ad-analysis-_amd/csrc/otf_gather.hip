@@ -111,6 +111,11 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
     __shared__ T urow[NW][R];
     __shared__ T uhist[2][TR];
     __shared__ T red[17 + 17];
+    // workgroup-wide flags without a reduction: a raised flag is the EPOCH written by any
+    // lane that raises it before the barrier, compared with the epoch after it (epochs
+    // only grow, so no word is ever reset).  [0] publish: break in this workgroup's
+    // rows; [1..3] gather: break flagged by a producer, stall, break in v.
+    __shared__ int s_ep[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nwg = gridDim.x;
     const bool lead = (blockIdx.x == 0 && tid == 0);
@@ -165,6 +170,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
         bch[c] = (tid < NCH && col < p.m) ? p.b[col] : (T)0;
     }
     const T u0 = (T)1 / (T)p.n, v0 = (T)1 / (T)p.m;
+    if (tid < 4) s_ep[tid] = -1;
     for (int q = tid; q < Cf::C; q += blockDim.x) vhist[0][q] = vhist[1][q] = v0;
     if (tid < TR) uhist[0][tid] = uhist[1][tid] = u0;
 
@@ -179,13 +185,19 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
 #pragma unroll
             for (int q = 0; q < VEC; ++q) {
                 T sacc = 0;
+#if defined(OTF_GATHER_ABLATE) && (OTF_GATHER_ABLATE & 4)
+                sacc = kv[0][g][q] * wr[0];  // diagnostic: no column-partial FMAs
+#else
 #pragma unroll
                 for (int r = 0; r < R; ++r) sacc += kv[r][g][q] * wr[r];
+#endif
                 acc[q] = sacc;
             }
             *reinterpret_cast<V*>(&colbuf[w][(lane + kWave * g) * VEC]) = acc;
         }
-        const int bad = __syncthreads_or(bad_local) ? 1 : 0;
+        if (bad_local) s_ep[0] = k;
+        __syncthreads();
+        const int bad = s_ep[0] == k ? 1 : 0;
         if (tid < NCH) {
             T val[CPC];
 #pragma unroll
@@ -223,6 +235,9 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
 #pragma unroll
                 for (int q = 0; q < NQ; ++q)
                     ok &= ((unsigned)x[q][1] >> 1) == ep && ((unsigned)x[q][3] >> 1) == ep;
+#if defined(OTF_GATHER_ABLATE) && (OTF_GATHER_ABLATE & 1)
+                ok = true;  // diagnostic: one load pass, no wait for the producers
+#endif
                 if (ok) break;
                 if (__builtin_amdgcn_s_memrealtime() > deadline) {
                     fl |= 2;
@@ -256,11 +271,11 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
                 }
             }
         }
-        // one barrier in the common case; which flags were raised only when one was
-        int f = 0;
-        if (__syncthreads_or(fl))
-            f = (__syncthreads_or(fl & 1) ? 1 : 0) | (__syncthreads_or(fl & 2) ? 2 : 0) |
-                (__syncthreads_or(fl & 4) ? 4 : 0);
+        if (fl & 1) s_ep[1] = k;
+        if (fl & 2) s_ep[2] = k;
+        if (fl & 4) s_ep[3] = k;
+        __syncthreads();
+        const int f = (s_ep[1] == k ? 1 : 0) | (s_ep[2] == k ? 2 : 0) | (s_ep[3] == k ? 4 : 0);
         deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
         return f;
     };
@@ -326,6 +341,9 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
             for (int g = 0; g < G; ++g)
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) acc += kv[r][g][k] * vn[g][k];
+#if defined(OTF_GATHER_ABLATE) && (OTF_GATHER_ABLATE & 2)
+            acc = kv[r][0][0] * vn[0][0];  // diagnostic: no row-sum FMAs
+#endif
             rp[r] = acc;
         }
         wave_sum_multi<T, R>(rp, lane);

@@ -168,7 +168,7 @@ __device__ double blk_minmax(double v, double* red, bool want_max) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const double t = __shfl_xor(v, o, kWave);
+        const double t = wave_xor_n<double>(v, o);
         v = want_max ? fmax(v, t) : fmin(v, t);
     }
     if (lane == 0) red[w] = v;

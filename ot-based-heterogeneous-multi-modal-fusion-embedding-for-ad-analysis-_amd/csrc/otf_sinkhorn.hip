@@ -1250,7 +1250,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
                 tot += __hip_atomic_load(xg + (size_t)mb * TR + w * R + rr, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-            for (int o = R; o < kWave; o <<= 1) tot += __shfl_xor(tot, o, kWave);
+            for (int o = R; o < kWave; o <<= 1) tot += wave_xor_n<T>(tot, o);
         }
         if (lane < R) {
             const int rr = lane;
