@@ -90,14 +90,20 @@ enum {
  *   K in registers as in TILED, but the column partials are exchanged as epoch-tagged
  *   granules that every workgroup gathers and sums in a fixed order -- no atomics, no
  *   barrier, one memory hop per iteration, bitwise reproducible.  AUTO picks it first
- *   for such shapes (and for opts.deterministic).  POT flavour.                       */
+ *   for such shapes (and for opts.deterministic).  POT flavour.
+ * OTF_ENGINE_MESH: float32, 4..64 row tiles x 1..8 column tiles of 128 x 512 (the
+ *   N = 4096 metric config): tiles of K in registers as in TILED, but both reductions
+ *   are epoch-tagged granule hops -- row partials within the row block, column partials
+ *   through one reducer workgroup per column slice -- no atomics, no barrier, three
+ *   memory hops per iteration, bitwise reproducible.  AUTO picks it before TILED.     */
 typedef enum {
     OTF_ENGINE_AUTO = 0,
     OTF_ENGINE_STREAM = 1,
     OTF_ENGINE_RESIDENT = 2,
     OTF_ENGINE_TILED = 3,
     OTF_ENGINE_SWEEP = 4,
-    OTF_ENGINE_GATHER = 5
+    OTF_ENGINE_GATHER = 5,
+    OTF_ENGINE_MESH = 6
 } otf_engine;
 
 typedef struct {

@@ -128,21 +128,36 @@ template <int R> __device__ __forceinline__ int butterfly_row(int lane) {
         if (lane & (1 << s)) r += h;
     return r;
 }
-template <typename T, int R> __device__ __forceinline__ void wave_sum_multi(T (&x)[R], int lane) {
-    int s = 0;
-#pragma unroll
-    for (int h = R / 2; h >= 1; h >>= 1, ++s) {
-        const int o = 1 << s;
+// One halving step per template level: H pairs, lane bit 1 << S picks which half a lane
+// keeps.  Compile-time H and S keep every index static: the earlier loop form
+// (for h = R/2 ...; h >>= 1, ++s) was not unrolled by ROCm 7.2 clang, so x[i] became a
+// dynamic register index -- a 15-way compare/select chain per access, ~900 VALU
+// instructions for R = 16 instead of ~100 (measured in the mesh engine's ISA).
+template <typename T, int R, int H, int S>
+__device__ __forceinline__ void wave_sum_step(T (&x)[R], int lane) {
+    if constexpr (H >= 1) {
+        constexpr int o = 1 << S;
         const bool upper = (lane & o) != 0;
 #pragma unroll
-        for (int i = 0; i < h; ++i) {
-            const T send = upper ? x[i] : x[i + h];
-            const T keep = upper ? x[i + h] : x[i];
-            x[i] = keep + wave_xor_n<T>(send, o);
+        for (int i = 0; i < H; ++i) {
+            const T send = upper ? x[i] : x[i + H];
+            const T keep = upper ? x[i + H] : x[i];
+            x[i] = keep + wave_xor<T, o>(send);
         }
+        wave_sum_step<T, R, H / 2, S + 1>(x, lane);
     }
-#pragma unroll
-    for (int o = (R > 1 ? R : 1); o < kWave; o <<= 1) x[0] += wave_xor_n<T>(x[0], o);
+}
+// x += x of lane ^ O, ^ 2O, ... ^ 32 (compile-time offsets)
+template <typename T, int O> __device__ __forceinline__ void wave_sum_from(T& x) {
+    if constexpr (O < kWave) {
+        x += wave_xor<T, O>(x);
+        wave_sum_from<T, O * 2>(x);
+    }
+}
+template <typename T, int R> __device__ __forceinline__ void wave_sum_multi(T (&x)[R], int lane) {
+    static_assert(R >= 1 && R <= 64 && (R & (R - 1)) == 0, "R: a power of two <= 64");
+    wave_sum_step<T, R, R / 2, 0>(x, lane);
+    wave_sum_from<T, (R > 1 ? R : 1)>(x[0]);
 }
 
 // Block-wide sum of R values per thread.  `red` is LDS of >= (nwaves + 1) * R
@@ -184,8 +199,7 @@ __device__ __forceinline__ void block_sum_rows(T (&x)[R], T* tbuf, T* wbuf) {
     T s = 0;
 #pragma unroll
     for (int k = 0; k < R; ++k) s += tbuf[(q + Q * k) * R + r];
-#pragma unroll
-    for (int o = R; o < kWave; o <<= 1) s += wave_xor_n<T>(s, o);
+    wave_sum_from<T, R>(s);
     if (lane < R) wbuf[wid * R + lane] = s;
     __syncthreads();
     if (t < R) {

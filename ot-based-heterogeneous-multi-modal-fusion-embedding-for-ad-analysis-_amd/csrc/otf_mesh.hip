@@ -1,0 +1,748 @@
+// otf_mesh.hip — Sinkhorn on a mesh of register-resident K tiles with no device-wide
+// barrier and no atomics (OTF_ENGINE_MESH), POT flavour, float32 compute.
+//
+// Replaces ot.sinkhorn (POT 0.9.6 sinkhorn_knopp, MRI_PET_OT_nojax.py:143 /
+// perturbot/perturbot/match/utils.py:6-115) for the coupled problems whose K fits the
+// register files of the chip: the headline N = 4096 metric config (BASELINE.json
+// configs[1]) and every shape of 4..64 row tiles x 1..8 column tiles.
+//
+// Workgroup (rb, cb) keeps the 128-row x 512-column tile (rb, cb) of K = exp(-C/reg)
+// in registers for the whole solve (8 waves x 16 rows, every lane 8 columns), as the
+// tiled engine does.  Per iteration Sinkhorn needs two reductions: the row sums K v
+// over the ncb column tiles of a row block, and the column sums K^T u over the nrb row
+// blocks of a column tile.  The tiled engine does the first through a write-through
+// exchange + arrival counter and the second through float atomics + a grid barrier +
+// a re-read: five memory-side hand-offs, 8.9 us per iteration at N = 4096.  Here all
+// traffic is epoch-tagged granules (R2 form, cdna_hip_programming.md Guideline 16:
+// 8-byte {value, tag} granules, two per 16-B write-through store, consumers poll the
+// data itself until every tag carries the epoch they wait for -- no fence, no counter,
+// no barrier), in three hops per iteration:
+//
+//   row hop  every WAVE publishes its 16 row partials (8 chunks) and gathers the same
+//            rows' partials of the ncb members of its row block (one chunk per lane),
+//            sums them in a fixed butterfly order -> u for its rows;
+//   hop A    every workgroup publishes its 512 column partials K_tile^T u (256 chunks);
+//   reduce   workgroup rb of column tile cb is the REDUCER of chunks [rb*CPR, ..+CPR):
+//            one wave gathers them from the nrb producers and sums them in a fixed
+//            order, then publishes the column sums S (hop B) -- plus its share of the
+//            marginal error of the previous iterate (POT's err, utils.py:83-90);
+//   hop B    every workgroup gathers the 512 sums of its column tile from the
+//            reducers -> v = b / S.
+//
+// Every sum has one fixed order, so all members of a group hold bit-identical values
+// and the result is bitwise reproducible run to run.  POT's decisions travel in the tag
+// bits and the extra error chunks, so every workgroup takes them at the same point:
+//   * a zero / non-finite v of iteration it (known to a column tile after hop B) rides
+//     in the row-hop tags of it -> everyone knows it after the row hop of it;
+//   * a non-finite u of iteration it (known to a row block after the row hop) rides in
+//     the hop-A tags -> reducers -> hop-B tags -> everyone knows it at hop B of it + 1;
+//   * the marginal error of iterate it - 1 = sum of the reducers' terms (hop B of it),
+//     summed per column tile, then over column tiles in the row hop of it.
+// which reproduces POT's order (break of iterate k before its error check, error of
+// k before the break test of k + 1) with the same (last_good, niter, break_iter).
+//
+// Double buffering by epoch parity is enough for every hop: a member publishes epoch
+// e + 2 only after its own gather of e + 1, which needed every member's publish of
+// e + 1, which each made after finishing its gather of e.  Every poll is bounded by
+// s_memrealtime (re-armed after each completed gather): a stall ends in OTF_SK_TIMEOUT.
+#include "otf_persist.h"
+
+namespace otf {
+namespace {
+
+constexpr int kMeshNW = 8;      // waves per workgroup
+constexpr int kMeshRW = 16;     // rows per wave
+constexpr int kMeshTR = 128;    // rows per tile
+constexpr int kMeshTC = 512;    // columns per tile
+constexpr int kMeshNCH = 256;   // 16-B chunks (two {value, tag} granules) per 512 columns
+constexpr int kMeshMaxNcb = 8;  // row hop: ncb producers x 8 chunks <= one chunk per lane
+constexpr int kMeshMinNrb = 4;  // reducer chunks per workgroup (CPR) <= 64
+constexpr int kMeshMaxNrb = 64; // hop-B error chunks: one per lane of one wave
+constexpr uint32_t kRowStride = 1280;  // per producer: 64 row chunks + the error chunk
+constexpr uint32_t kColStride = 4096;  // per producer: 256 column chunks
+
+struct SkMeshArgs {
+    const void* C;
+    int64_t ldc;
+    int n, m;
+    const float* a;  // padded marginals (zero past n / m)
+    const float* b;
+    const float* cost_scale;
+    double reg;
+    int max_iter, check_every, err_squared;
+    double stop_thr;
+    void* gran;  // granule region, zeroed per solve
+    uint32_t off_row, off_cola, off_colb, bstride;
+    int nrb, ncb, cpr, xcd_rows;
+    otf_sinkhorn_info* info;
+    double* errlog;
+    float* u_out;
+    float* v_out;
+    void* P;
+    int64_t ldp;
+    unsigned long long timeout_ticks;
+};
+
+using I4 = __attribute__((ext_vector_type(4))) int;
+
+__device__ __forceinline__ I4 chunk2(float v0, float v1, int tag) {
+    I4 x;
+    x[0] = __builtin_bit_cast(int, v0);
+    x[1] = tag;
+    x[2] = __builtin_bit_cast(int, v1);
+    x[3] = tag;
+    return x;
+}
+__device__ __forceinline__ bool chunk_at(const I4 x, unsigned e) {
+    return ((unsigned)x[1] >> 2) == e && ((unsigned)x[3] >> 2) == e;
+}
+// element copies first (ROCm 7.2: a bit_cast of a vector ELEMENT reads element 0)
+__device__ __forceinline__ float chunk_v0(const I4 x) { const int w = x[0]; return __builtin_bit_cast(float, w); }
+__device__ __forceinline__ float chunk_v1(const I4 x) { const int w = x[2]; return __builtin_bit_cast(float, w); }
+
+__device__ __forceinline__ I4 gload(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(I4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16 /* sc1 */));
+}
+__device__ __forceinline__ void gstore(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x) {
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
+}
+
+// KQ: reducer loads per lane, ceil(nrb * CPR / 64): 4 when nrb is a power of two
+// (nrb * CPR = 256), up to 8 otherwise
+template <typename CT, typename TP, int KQ>
+__global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
+    using T = float;
+    constexpr int G = 2, VEC = 4, R = kMeshRW, NW = kMeshNW, TR = kMeshTR, TC = kMeshTC;
+    using V = Vec<float>::type;
+    using VP = __attribute__((ext_vector_type(VEC))) TP;
+    __shared__ __attribute__((aligned(16))) T colbuf[NW][TC];
+    __shared__ __attribute__((aligned(16))) T vcur[TC];      // v = b / S of this tile's columns
+    __shared__ __attribute__((aligned(16))) T vhist[2][TC];  // v by iteration parity
+    __shared__ T urow[NW][R];
+    __shared__ T uhist[2][TR];
+    __shared__ T s_E;  // this column tile's error partial (hop B)
+    // workgroup-wide flags without a reduction: a raised flag holds the KEY (epoch or
+    // iteration) of the step that raised it, compared after the barrier (keys only grow)
+    // [0] non-finite u in this workgroup (iteration key), [1] hop-B stall, [2] hop-B
+    // producer flag (non-finite u of the previous iteration), [3] zero / non-finite v
+    // (epoch keys), [4] row-hop stall (iteration key)
+    __shared__ int s_ep[5];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const bool lead = (blockIdx.x == 0 && tid == 0);
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+    const int nrb = p.nrb, ncb = p.ncb, CPR = p.cpr;
+
+    // tile of this workgroup: xcd_rows (nrb % 8 == 0) deals the members of a row block
+    // to one XCD under round-robin placement; otherwise consecutive workgroups are the
+    // column tiles of a row block (ncb = 8: a column tile's members share an XCD).
+    // Speed only: no hop assumes any placement.
+    int rb, cb;
+    {
+        const int bi = blockIdx.x;
+        if (p.xcd_rows && (nrb & 7) == 0) {
+            const int x = bi & 7, q = bi >> 3;
+            cb = q % ncb;
+            rb = (q / ncb) * 8 + x;
+        } else {
+            rb = bi / ncb;
+            cb = bi % ncb;
+        }
+    }
+    const int row0 = rb * TR + w * R;
+    const int col0 = cb * TC;
+    const int ncols = p.m - col0 < TC ? p.m - col0 : TC;
+    const int nch = (ncols + 1) >> 1;          // chunks of this column tile
+    const int nred = (nch + CPR - 1) / CPR;    // reducers of this column tile
+
+    const double unit = exp_unit<T>();
+    double cinv = 1.0;
+    if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
+    const T ks = (T)(-unit / p.reg * cinv);
+
+    // ---- K for this wave's 16 rows x this lane's 8 columns, once (0 outside C)
+    T kv[R][G][VEC];
+    {
+        int colc[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int c0 = col0 + (lane + kWave * g) * VEC;
+            colc[g] = c0 < p.m ? c0 : 0;
+        }
+        const CT* crow = (const CT*)p.C + (int64_t)row0 * p.ldc;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const CT* src = (row0 + r < p.n) ? crow : (const CT*)p.C;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const V c = load_cost<T>(src + colc[g]);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
+            }
+            crow += p.ldc;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool rok = row0 + r < p.n;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const bool ok = rok && col0 + (lane + kWave * g) * VEC + k < p.m;
+                    kv[r][g][k] = ok ? fast_exp(kv[r][g][k] * ks) : (T)0;
+                }
+        }
+    }
+    // 1 / a of the rows whose u this lane finishes: row (lane & 15) when the tile spans
+    // whole rows, rows 2c, 2c + 1 (c = lane & 7) after a row hop
+    auto inv_a = [&](int r) -> T { return (T)1 / p.a[r < p.n ? r : p.n - 1]; };
+    const T ia_whole = inv_a(row0 + (lane & (R - 1)));
+    const T ia_c0 = inv_a(row0 + 2 * (lane & 7)), ia_c1 = inv_a(row0 + 2 * (lane & 7) + 1);
+    // hop-B consumer: chunk t = tid - 256 of this tile -> columns col0 + 2t, + 1
+    T bch0 = 0, bch1 = 0;
+    if (tid >= 256) {
+        const int t = tid - 256;
+        if (2 * t < ncols) bch0 = p.b[col0 + 2 * t];
+        if (2 * t + 1 < ncols) bch1 = p.b[col0 + 2 * t + 1];
+    }
+    // reducer (wave 0): chunk cc = lane % CPR of this workgroup's range, producers
+    // q = lane / CPR + LPC * k
+    const int LPC = kWave / CPR;
+    const int r_cc = lane & (CPR - 1), r_qlo = lane / CPR;
+    const int r_ch = rb * CPR + r_cc;
+    const bool r_ok = r_ch < nch;
+    T rb0 = 0, rb1 = 0;  // target marginal of the reducer's two columns
+    if (w == 0 && r_ok) {
+        if (2 * r_ch < ncols) rb0 = p.b[col0 + 2 * r_ch];
+        if (2 * r_ch + 1 < ncols) rb1 = p.b[col0 + 2 * r_ch + 1];
+    }
+    const bool rc0 = r_ok && 2 * r_ch < ncols, rc1 = r_ok && 2 * r_ch + 1 < ncols;
+    T sp0 = 1, sp1 = 1;  // the reducer's previous sums S[k - 1]
+
+    const T u0 = (T)1 / (T)p.n, v0 = (T)1 / (T)p.m;
+    if (tid < 5) s_ep[tid] = -1;
+    for (int q = tid; q < TC; q += blockDim.x) {
+        vhist[0][q] = vhist[1][q] = v0;
+        vcur[q] = 0;  // columns past m stay 0 (their K entries are 0 too)
+    }
+    if (tid < TR) uhist[0][tid] = uhist[1][tid] = u0;
+
+    const __amdgpu_buffer_rsrc_t rs = sums_rsrc(p.gran);
+    auto rowx = [&](int e, int q) -> uint32_t {
+        return p.off_row + ((uint32_t)((e & 1) * nrb + rb) * (uint32_t)ncb + (uint32_t)q) * kRowStride;
+    };
+    auto cola = [&](int e, int q) -> uint32_t {
+        return p.off_cola + ((uint32_t)((e & 1) * ncb + cb) * (uint32_t)nrb + (uint32_t)q) * kColStride;
+    };
+    auto colb = [&](int e, int j) -> uint32_t {
+        return p.off_colb + ((uint32_t)((e & 1) * ncb + cb) * (uint32_t)nrb + (uint32_t)j) * p.bstride;
+    };
+
+    // hop A: this workgroup's column partials K_tile^T wr (the per-wave partials are in
+    // colbuf, after the barrier), epoch e; flag = non-finite u in this workgroup
+    auto publish_cols = [&](int e, int flag) {
+        if (tid < nch) {
+            T s0 = colbuf[0][2 * tid], s1 = colbuf[0][2 * tid + 1];
+#pragma unroll
+            for (int ww = 1; ww < NW; ++ww) {
+                s0 += colbuf[ww][2 * tid];
+                s1 += colbuf[ww][2 * tid + 1];
+            }
+            gstore(rs, cola(e, rb) + (uint32_t)tid * 16, chunk2(s0, s1, (e << 2) | flag));
+        }
+    };
+    auto col_partials = [&](const T (&wr)[R]) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            V acc;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+                T sacc = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) sacc += kv[r][g][q] * wr[r];
+                acc[q] = sacc;
+            }
+            *reinterpret_cast<V*>(&colbuf[w][(lane + kWave * g) * VEC]) = acc;
+        }
+    };
+    // reducer (wave 0): S[e - 1] for this workgroup's chunk range from the nrb
+    // producers of epoch e, fixed order; hop B carries the OR of their flags and the
+    // error terms of iterate e - 2 (S[e - 1] against S[e - 2]).  Returns false on a stall.
+    auto reduce = [&](int e) -> bool {
+        I4 x[KQ];
+        bool act[KQ];
+        unsigned pend = 0;
+#pragma unroll
+        for (int k = 0; k < KQ; ++k) {
+            const int q = r_qlo + LPC * k;
+            act[k] = r_ok && q < nrb;
+            x[k] = I4{0, 0, 0, 0};
+            if (act[k]) pend |= 1u << k;
+        }
+        bool ok = true;
+        for (;;) {
+#pragma unroll
+            for (int k = 0; k < KQ; ++k)
+                if (pend & (1u << k)) x[k] = gload(rs, cola(e, r_qlo + LPC * k) + (uint32_t)r_ch * 16);
+#pragma unroll
+            for (int k = 0; k < KQ; ++k)
+                if ((pend & (1u << k)) && chunk_at(x[k], (unsigned)e)) pend &= ~(1u << k);
+            if (!__any(pend != 0)) break;
+            if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        T s0 = 0, s1 = 0;
+        int fl = 0;
+#pragma unroll
+        for (int k = 0; k < KQ; ++k)
+            if (act[k]) {
+                s0 += chunk_v0(x[k]);
+                s1 += chunk_v1(x[k]);
+                fl |= x[k][1] & 1;
+            }
+        for (int o = CPR; o < kWave; o <<= 1) {
+            s0 += wave_xor_n<T>(s0, o);
+            s1 += wave_xor_n<T>(s1, o);
+        }
+        const int bad = __any(fl) ? 1 : 0;
+        // POT's marginal error of the iterate whose v = b / S[e - 2]
+        T term = 0;
+        if (rc0) { const T rr = (rb0 / sp0) * s0 - rb0; term += rr * rr; }
+        if (rc1) { const T rr = (rb1 / sp1) * s1 - rb1; term += rr * rr; }
+        for (int o = 1; o < CPR; o <<= 1) term += wave_xor_n<T>(term, o);
+        sp0 = s0;
+        sp1 = s1;
+        const int tag = (e << 2) | bad;
+        if (lane < CPR && r_ok) gstore(rs, colb(e, rb) + (uint32_t)r_cc * 16, chunk2(s0, s1, tag));
+        if (lane == 0 && rb < nred) gstore(rs, colb(e, rb) + (uint32_t)CPR * 16, chunk2(term, 0.f, tag));
+        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+        return ok;
+    };
+    // hop B: the sums S[e - 1] of this tile's columns -> v into vcur; the column tile's
+    // error partial into s_E.  Returns bit 0 = producer flag, 1 = stall, 2 = bad v.
+    auto gather_b = [&](int e) -> int {
+        int fl = 0;
+        T ep = 0;
+        if (tid >= 256) {
+            const int t = tid - 256;
+            if (t < nch) {
+                const uint32_t off = colb(e, t / CPR) + (uint32_t)(t & (CPR - 1)) * 16;
+                I4 x;
+                for (;;) {
+                    x = gload(rs, off);
+                    if (chunk_at(x, (unsigned)e)) break;
+                    if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                fl |= x[1] & 1;
+                const T s0 = chunk_v0(x), s1 = chunk_v1(x);
+                const bool ok0 = 2 * t < ncols, ok1 = 2 * t + 1 < ncols;
+                const T v0n = bch0 / s0, v1n = bch1 / s1;
+                if ((ok0 && (s0 == (T)0 || !finite_val(v0n))) || (ok1 && (s1 == (T)0 || !finite_val(v1n))))
+                    fl |= 4;
+                vcur[2 * t] = ok0 ? v0n : (T)0;
+                vcur[2 * t + 1] = ok1 ? v1n : (T)0;
+            }
+        } else if (w == 3) {
+            if (lane < nred) {
+                const uint32_t off = colb(e, lane) + (uint32_t)CPR * 16;
+                I4 x;
+                for (;;) {
+                    x = gload(rs, off);
+                    if (chunk_at(x, (unsigned)e)) break;
+                    if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                ep = chunk_v0(x);
+            }
+            ep = wave_sum<T>(ep);
+            if (lane == 0) s_E = ep;
+        }
+        if (fl & 1) s_ep[2] = e;
+        if (fl & 2) s_ep[1] = e;
+        if (fl & 4) s_ep[3] = e;
+        __syncthreads();
+        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+        return (s_ep[2] == e ? 1 : 0) | (s_ep[1] == e ? 2 : 0) | (s_ep[3] == e ? 4 : 0);
+    };
+    // the total error from the ncb column tiles' partials (row-hop error chunks of epoch
+    // er): wave-level, lanes < ncb poll.  Returns false on a stall.
+    auto err_total = [&](int er, T& tot) -> bool {
+        T ev = 0;
+        bool ok = true;
+        if (lane < ncb) {
+            const uint32_t off = rowx(er, lane) + 64 * 16;
+            I4 x;
+            for (;;) {
+                x = gload(rs, off);
+                if (chunk_at(x, (unsigned)er)) break;
+                if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            ev = chunk_v0(x);
+        }
+        ev += wave_xor<T, 1>(ev);
+        ev += wave_xor<T, 2>(ev);
+        ev += wave_xor<T, 4>(ev);
+        tot = __builtin_bit_cast(T, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ev)));
+        return __all(ok);
+    };
+    auto to_err = [&](T e) -> double { return p.err_squared ? (double)e : sqrt((double)e); };
+    auto stop_ok = [&](double err) -> bool {
+        return p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr);
+    };
+
+    // ---- prologue: S[0] = K^T u0 (epoch 1)
+    {
+        T wr[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) wr[r] = (row0 + r < p.n) ? u0 : (T)0;
+        col_partials(wr);
+        __syncthreads();
+        publish_cols(1, 0);
+    }
+    int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
+    bool done = false;
+    if (w == 0 && !reduce(1)) s_ep[1] = 1;  // seen after the hop-B barrier of epoch 1
+    const int rowl = butterfly_row<R>(lane);
+
+    for (int it = 0; it < p.max_iter; ++it) {
+        OTF_STAMP(it, 0);
+        const int e = it + 1;  // hop-B epoch of S[it]; row-hop epoch of iteration it
+        const int fl = gather_b(e);
+        OTF_STAMP(it, 1);
+        if (fl & 2) { status = OTF_SK_TIMEOUT; done = true; break; }
+        // a non-finite u in iteration it - 1 (any row block) -> revert to it - 2
+        if (fl & 1) {
+            last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
+            done = true;
+            break;
+        }
+        const int vbad_cb = (fl & 4) ? 1 : 0;
+        T vn[G][VEC];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const V t = *reinterpret_cast<const V*>(&vcur[(lane + kWave * g) * VEC]);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) vn[g][k] = t[k];
+        }
+        // row partials over this tile's columns, wave totals
+        T rp[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            T acc = 0;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) acc += kv[r][g][k] * vn[g][k];
+            rp[r] = acc;
+        }
+        wave_sum_multi<T, R>(rp, lane);
+        if (lane < R) urow[w][rowl] = rp[0];
+        __builtin_amdgcn_wave_barrier();
+        const bool check = it >= 1 && ((it - 1) % p.check_every) == 0;
+        T errv = 0;
+        int vbad = vbad_cb, stall = 0;
+        if (ncb == 1) {
+            // the tile spans whole rows: totals, v flags and the error are already global
+            const T tot = urow[w][lane & (R - 1)];
+            __builtin_amdgcn_wave_barrier();
+            errv = s_E;
+            OTF_STAMP(it, 2);
+            OTF_STAMP(it, 3);
+            if (lane < R) {
+                T un = (T)1 / (tot * ia_whole);
+                if (row0 + lane >= p.n) un = 0;
+                urow[w][lane] = un;
+            }
+        } else {
+            // row hop: publish this wave's 16 row partials (8 chunks) and the column tile's
+            // error partial, gather the ncb members' chunks of the same rows
+            if (lane < 8) {
+                const T t0 = urow[w][2 * lane], t1 = urow[w][2 * lane + 1];
+                gstore(rs, rowx(e, cb) + (uint32_t)(w * 8 + lane) * 16, chunk2(t0, t1, (e << 2) | vbad_cb));
+            }
+            if (w == 0 && lane == 8) gstore(rs, rowx(e, cb) + 64 * 16, chunk2(s_E, 0.f, e << 2));
+            __builtin_amdgcn_wave_barrier();
+            OTF_STAMP(it, 2);
+            const int q = lane >> 3, c = lane & 7;
+            const bool act = q < ncb;
+            I4 x = I4{0, 0, 0, 0};
+            if (act) {
+                const uint32_t off = rowx(e, q) + (uint32_t)(w * 8 + c) * 16;
+                for (;;) {
+                    x = gload(rs, off);
+                    if (chunk_at(x, (unsigned)e)) break;
+                    if (__builtin_amdgcn_s_memrealtime() > deadline) { stall = 1; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            T t0 = act ? chunk_v0(x) : (T)0, t1 = act ? chunk_v1(x) : (T)0;
+            vbad = __any(act && (x[1] & 1)) ? 1 : 0;
+            t0 += wave_xor<T, 8>(t0);
+            t1 += wave_xor<T, 8>(t1);
+            t0 += wave_xor<T, 16>(t0);
+            t1 += wave_xor<T, 16>(t1);
+            t0 += wave_xor<T, 32>(t0);
+            t1 += wave_xor<T, 32>(t1);
+            if (check && !err_total(e, errv)) stall = 1;
+            stall = __any(stall) ? 1 : 0;
+            OTF_STAMP(it, 3);
+            if (lane < 8) {
+                T un0 = (T)1 / (t0 * ia_c0), un1 = (T)1 / (t1 * ia_c1);
+                if (row0 + 2 * lane >= p.n) un0 = 0;
+                if (row0 + 2 * lane + 1 >= p.n) un1 = 0;
+                urow[w][2 * lane] = un0;
+                urow[w][2 * lane + 1] = un1;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // wave-private LDS hand-off (in-order LDS queue)
+        T un[R];
+        int badu = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            un[r] = urow[w][r];
+            badu |= (row0 + r < p.n && !finite_val(un[r])) ? 1 : 0;
+        }
+        // POT's decisions for iterate it - 1 (error) and iterate it (v); identical in
+        // every wave of every workgroup unless a wave stalled (then all time out)
+        double err = 0.0;
+        int dec = 0;
+        if (check) {
+            err = to_err(errv);
+            if (stop_ok(err)) dec = 1;
+        }
+        if (dec == 0 && vbad) dec = 2;
+        col_partials(un);
+        // histories of iterate it (slot it & 1; only read when last_good >= it, i.e. when
+        // this iteration is not the one a decision below reverts)
+        const int slot = it & 1;
+        vhist[slot][tid] = vcur[tid];
+        if (lane < R) uhist[slot][w * R + lane] = urow[w][lane];
+        if (badu) s_ep[0] = it;
+        if (stall) s_ep[4] = it;
+        __syncthreads();
+        OTF_STAMP(it, 4);
+        if (s_ep[4] == it) { status = OTF_SK_TIMEOUT; done = true; break; }
+        if (check) {
+            if (lead) p.errlog[(it - 1) / p.check_every] = err;
+            n_err = (it - 1) / p.check_every + 1;
+        }
+        if (dec == 1) {
+            last_good = it - 1; niter = it - 1; status = OTF_SK_CONVERGED;
+            done = true;
+            break;
+        }
+        if (dec == 2) {
+            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
+            done = true;
+            break;
+        }
+        publish_cols(e + 1, s_ep[0] == it ? 1 : 0);
+        if (w == 0 && !reduce(e + 1)) s_ep[1] = e + 1;  // seen after the next hop-B barrier
+        OTF_STAMP(it, 5);
+    }
+    if (!done && p.max_iter > 0) {
+        // the last iteration's u flags and S[max_iter]; its error needs one more
+        // exchange of the column tiles' partials
+        const int it = p.max_iter - 1;
+        const int e = p.max_iter + 1;
+        const int fl = gather_b(e);
+        if (fl & 2) {
+            status = OTF_SK_TIMEOUT;
+        } else if (fl & 1) {
+            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
+        } else {
+            last_good = it; niter = it;
+            if ((it % p.check_every) == 0) {
+                T errv = s_E;
+                int stall = 0;
+                if (ncb > 1) {
+                    if (w == 0 && lane == 8) gstore(rs, rowx(e, cb) + 64 * 16, chunk2(s_E, 0.f, e << 2));
+                    if (!err_total(e, errv)) stall = 1;
+                    if (stall) s_ep[4] = e;
+                    __syncthreads();
+                    stall = s_ep[4] == e;
+                }
+                if (stall) {
+                    status = OTF_SK_TIMEOUT;
+                } else {
+                    const double err = to_err(errv);
+                    if (lead) p.errlog[it / p.check_every] = err;
+                    n_err = it / p.check_every + 1;
+                    if (stop_ok(err)) status = OTF_SK_CONVERGED;
+                }
+            }
+        }
+    }
+
+    // ---- outputs: (u, v) of last_good from the histories, plan from registers
+    __syncthreads();
+    const int hs = last_good & 1;
+    T uo[R], vo[G][VEC];
+#pragma unroll
+    for (int r = 0; r < R; ++r) uo[r] = last_good < 0 ? u0 : uhist[hs][w * R + r];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+            vo[g][k] = last_good < 0 ? v0 : vhist[hs][(lane + kWave * g) * VEC + k];
+    if (cb == 0 && lane < R && row0 + lane < p.n) {
+        T mine = uo[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) if (lane == r) mine = uo[r];
+        p.u_out[row0 + lane] = mine;
+    }
+    if (rb == 0 && w == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const int c = col0 + (lane + kWave * g) * VEC + k;
+                if (c < p.m) p.v_out[c] = vo[g][k];
+            }
+    }
+    if (p.P) {
+        TP* P = (TP*)p.P;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (row0 + r >= p.n) break;
+            TP* prow = P + (int64_t)(row0 + r) * p.ldp;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int c0 = col0 + (lane + kWave * g) * VEC;
+                if (c0 >= p.m) continue;
+                VP o;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) o[k] = (TP)(uo[r] * kv[r][g][k] * vo[g][k]);
+                if (c0 + VEC <= p.m) {
+                    *reinterpret_cast<VP*>(prow + c0) = o;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k)
+                        if (c0 + k < p.m) prow[c0 + k] = o[k];
+                }
+            }
+        }
+    }
+    if (status == OTF_SK_TIMEOUT && tid == 0) store_wt(&p.info->stalled, 1);
+    if (lead) {
+        p.info->last_good = last_good;
+        p.info->niter = niter;
+        p.info->status = status;
+        p.info->break_iter = brk;
+        p.info->n_err = n_err;
+        p.info->engine = OTF_ENGINE_MESH;
+        p.info->stop = 1;
+    }
+}
+
+template <typename CT, typename TP>
+hipError_t launch_mesh_t(int grid, SkMeshArgs& p, hipStream_t s) {
+    void* args[] = {&p};
+    const bool pow2 = (p.nrb & (p.nrb - 1)) == 0;
+    const void* k = pow2 ? (const void*)sk_mesh_kernel<CT, TP, 4> : (const void*)sk_mesh_kernel<CT, TP, 8>;
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1 || grid > per_cu * device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
+    return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
+}
+
+struct MeshShape {
+    int nrb, ncb, cpr;
+    uint32_t bstride;
+    size_t row_bytes, cola_bytes, colb_bytes;
+};
+
+MeshShape mesh_shape(int64_t n, int64_t m) {
+    MeshShape s{};
+    s.nrb = (int)((n + kMeshTR - 1) / kMeshTR);
+    s.ncb = (int)((m + kMeshTC - 1) / kMeshTC);
+    int per = (kMeshNCH + s.nrb - 1) / (s.nrb > 0 ? s.nrb : 1);
+    int cpr = 1;
+    while (cpr < per) cpr <<= 1;
+    s.cpr = cpr;
+    s.bstride = (uint32_t)((cpr + 1) * 16 + 255) / 256 * 256;
+    s.row_bytes = 2 * (size_t)s.nrb * s.ncb * kRowStride;
+    s.cola_bytes = 2 * (size_t)s.nrb * s.ncb * kColStride;
+    s.colb_bytes = 2 * (size_t)s.nrb * s.ncb * s.bstride;
+    return s;
+}
+
+// OTF_MESH_XCD_ROWS=1: a row block's members on one XCD instead of a column tile's
+inline int mesh_xcd_rows() {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("OTF_MESH_XCD_ROWS");
+        env = e ? atoi(e) : 0;
+    }
+    return env;
+}
+
+}  // namespace
+
+bool mesh_supported(int64_t n, int64_t m) {
+    if (n < 1 || m < 1) return false;
+    const MeshShape s = mesh_shape(n, m);
+    return s.nrb >= kMeshMinNrb && s.nrb <= kMeshMaxNrb && s.ncb <= kMeshMaxNcb && s.cpr <= 64 &&
+           (int64_t)s.nrb * s.ncb <= 1024;
+}
+
+size_t mesh_region_bytes(int64_t n, int64_t m) {
+    if (!mesh_supported(n, m)) return 0;
+    const MeshShape s = mesh_shape(n, m);
+    return s.row_bytes + s.cola_bytes + s.colb_bytes;
+}
+
+template <typename CT>
+hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
+                    const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
+                    float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
+                    double* errlog, hipStream_t s) {
+    if (!mesh_supported(n, m) || !region) return hipErrorInvalidValue;
+    const MeshShape sh = mesh_shape(n, m);
+    if (sh.nrb * sh.ncb > device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
+    SkMeshArgs p{};
+    p.C = C;
+    p.ldc = ldc;
+    p.n = n;
+    p.m = m;
+    p.a = a_pad;
+    p.b = b_pad;
+    p.cost_scale = cost_scale;
+    p.reg = o.reg;
+    p.max_iter = o.max_iter;
+    p.check_every = o.check_every;
+    p.err_squared = o.err_squared;
+    p.stop_thr = o.stop_thr;
+    p.gran = region;
+    p.off_row = 0;
+    p.off_cola = (uint32_t)sh.row_bytes;
+    p.off_colb = (uint32_t)(sh.row_bytes + sh.cola_bytes);
+    p.bstride = sh.bstride;
+    p.nrb = sh.nrb;
+    p.ncb = sh.ncb;
+    p.cpr = sh.cpr;
+    p.xcd_rows = mesh_xcd_rows();
+    p.info = info;
+    p.errlog = errlog;
+    p.u_out = u_out;
+    p.v_out = v_out;
+    p.P = P_out;
+    p.ldp = ldp;
+    p.timeout_ticks = stall_ticks();
+    hipError_t e = hipMemsetAsync(region, 0, mesh_region_bytes(n, m), s);
+    if (e != hipSuccess) return e;
+    const int grid = sh.nrb * sh.ncb;
+    if (P_out && P_dtype == OTF_F64) return launch_mesh_t<CT, double>(grid, p, s);
+    return launch_mesh_t<CT, float>(grid, p, s);
+}
+
+template hipError_t run_mesh<float>(const float*, int64_t, int, int, const float*, const float*,
+                                    const float*, const otf_sinkhorn_opts&, void*, float*, float*,
+                                    void*, int64_t, int, otf_sinkhorn_info*, double*, hipStream_t);
+template hipError_t run_mesh<_Float16>(const _Float16*, int64_t, int, int, const float*, const float*,
+                                       const float*, const otf_sinkhorn_opts&, void*, float*, float*,
+                                       void*, int64_t, int, otf_sinkhorn_info*, double*, hipStream_t);
+
+}  // namespace otf

@@ -207,4 +207,16 @@ hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, co
                       T* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                       double* errlog, hipStream_t s);
 
+// Mesh engine (otf_mesh.hip): float32 problems of 4..64 row tiles x 1..8 column tiles
+// of K in registers, row and column reductions as epoch-tagged granule hops (no atomics,
+// no barrier).  `region` is zeroed by the launcher; mesh_region_bytes is 0 for shapes
+// it does not take.
+bool mesh_supported(int64_t n, int64_t m);
+size_t mesh_region_bytes(int64_t n, int64_t m);
+template <typename CT>
+hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
+                    const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
+                    float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
+                    double* errlog, hipStream_t s);
+
 }  // namespace otf

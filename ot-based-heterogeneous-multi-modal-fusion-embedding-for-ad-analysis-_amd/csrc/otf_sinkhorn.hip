@@ -1249,8 +1249,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
             for (int mb = lane / R; mb < p.ncb; mb += kWave / R)
                 tot += __hip_atomic_load(xg + (size_t)mb * TR + w * R + rr, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int o = R; o < kWave; o <<= 1) tot += wave_xor_n<T>(tot, o);
+            wave_sum_from<T, R>(tot);
         }
         if (lane < R) {
             const int rr = lane;
@@ -1427,6 +1426,8 @@ struct Workspace {
     size_t sweep_bytes;
     void* gather;     // gather engine granules (otf_gather.hip); 0 bytes if not taken
     size_t gather_bytes;
+    void* mesh;       // mesh engine granules (otf_mesh.hip); 0 bytes if not taken
+    size_t mesh_bytes;
     int nrep;
     size_t bytes;
     int64_t m_pad;
@@ -1484,6 +1485,8 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.sweep = take(w.sweep_bytes);
     w.gather_bytes = esz == 8 ? gather_region_bytes<double>(n, m) : gather_region_bytes<float>(n, m);
     w.gather = take(w.gather_bytes);
+    w.mesh_bytes = esz == 4 ? mesh_region_bytes(n, m) : 0;
+    w.mesh = take(w.mesh_bytes);
     w.bytes = off;
     return w;
 }
@@ -1741,6 +1744,16 @@ inline bool gather_enabled() {
     return env != 0;
 }
 
+// OTF_MESH=0 keeps AUTO off the mesh engine (A/B measurements); MESH still forces it
+inline bool mesh_enabled() {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("OTF_MESH");
+        env = e ? atoi(e) : 1;
+    }
+    return env != 0;
+}
+
 template <typename T, typename CT, bool LOG>
 int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_t ldc,
                  const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out, void* P_out,
@@ -1769,6 +1782,23 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         if (e == hipSuccess) return OTF_OK;
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_GATHER) return check_hip(e);
+    }
+    // mesh engine: float32 tiles of K in registers, three granule hops per iteration, no
+    // atomics or barrier (deterministic by construction)
+    bool mfits = false;
+    if constexpr (sizeof(T) == 4)
+        mfits = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && mesh_supported(n, m) &&
+                su.w.mesh_bytes > 0;
+    if (o.engine == OTF_ENGINE_MESH && !mfits) return OTF_EUNSUPPORTED;
+    if constexpr (sizeof(T) == 4) {
+        if (mfits && (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled()))) {
+            const hipError_t e = run_mesh<CT>(C, ldc, (int)n, (int)m, (const float*)su.w.a_pad,
+                                              (const float*)su.w.b_pad, cost_scale, o, su.w.mesh,
+                                              u_out, v_out, P_out, ldp, P_dtype, info, errlog, s);
+            if (e == hipSuccess) return OTF_OK;
+            (void)hipGetLastError();
+            if (o.engine == OTF_ENGINE_MESH) return check_hip(e);
+        }
     }
     // deterministic mode otherwise: the sweep engine reduces the column sums in a fixed order
     if (o.deterministic) {

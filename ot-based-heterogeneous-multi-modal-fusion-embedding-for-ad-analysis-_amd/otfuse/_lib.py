@@ -30,9 +30,11 @@ COMM_ID_BYTES = 128
 SK_RUNNING, SK_CONVERGED, SK_MAX_ITER, SK_NUMERICAL_BREAK, SK_TIMEOUT = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "running", 1: "converged", 2: "max_iter", 3: "numerical_break",
                 4: "timeout"}
-ENGINE_AUTO, ENGINE_STREAM, ENGINE_RESIDENT, ENGINE_TILED, ENGINE_SWEEP, ENGINE_GATHER = 0, 1, 2, 3, 4, 5
+ENGINE_AUTO, ENGINE_STREAM, ENGINE_RESIDENT, ENGINE_TILED, ENGINE_SWEEP, ENGINE_GATHER, ENGINE_MESH = (
+    0, 1, 2, 3, 4, 5, 6)
 ENGINES = {"auto": ENGINE_AUTO, "stream": ENGINE_STREAM, "resident": ENGINE_RESIDENT,
-           "tiled": ENGINE_TILED, "sweep": ENGINE_SWEEP, "gather": ENGINE_GATHER}
+           "tiled": ENGINE_TILED, "sweep": ENGINE_SWEEP, "gather": ENGINE_GATHER,
+           "mesh": ENGINE_MESH}
 ENGINE_NAMES = {v: k for k, v in ENGINES.items()}
 
 

@@ -162,7 +162,7 @@ def test_feature_cost_dense_ts_vs_oracle(ops, orc, dev):
     assert nrel(M2, orc.feature_cost(X, Y2, Tsq, weights="fot")) < 1e-13
 
 
-@pytest.mark.parametrize("engine", ["stream", "resident", "tiled", "sweep", "gather"])
+@pytest.mark.parametrize("engine", ["stream", "resident", "tiled", "sweep", "gather", "mesh"])
 @pytest.mark.parametrize("n,m,dt", [(300, 200, torch.float32), (64, 4099, torch.float32),
                                     (1024, 512, torch.float64), (2048, 500, torch.float32),
                                     (1000, 8191, torch.float32), (513, 2049, torch.float64),
@@ -181,7 +181,7 @@ def test_sinkhorn_ragged_shapes_vs_oracle(ops, orc, dev, n, m, dt, engine):
         res = ops.sinkhorn(_t(a, dev, dt), _t(b, dev, dt), _t(C, dev, dt), 0.1, max_iter=60,
                            stop_thr=0.0, engine=engine)
     except Exception as e:  # resident / tiled need one row block / tile per CU; tiled is fp32
-        if engine in ("resident", "tiled", "sweep", "gather") and "unsupported" in str(e):
+        if engine in ("resident", "tiled", "sweep", "gather", "mesh") and "unsupported" in str(e):
             pytest.skip(f"problem does not fit the {engine} engine")
         raise
     tol = 1e-4 if dt == torch.float32 else 1e-10
@@ -193,7 +193,7 @@ def test_sinkhorn_ragged_shapes_vs_oracle(ops, orc, dev, n, m, dt, engine):
                                u_r * v_r.mean(), rtol=tol * 10)
 
 
-@pytest.mark.parametrize("engine", ["stream", "resident", "tiled", "sweep", "gather"])
+@pytest.mark.parametrize("engine", ["stream", "resident", "tiled", "sweep", "gather", "mesh"])
 def test_float32_stop_and_break_all_engines(ops, orc, dev, engine):
     """float32 inputs: the convergence stop lands on the oracle's check (every 10) and a
     zero column of K (K^T u = 0 at iteration 0) reverts to (u0, v0) in every engine."""

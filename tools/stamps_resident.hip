@@ -11,6 +11,7 @@
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sinkhorn.hip"
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sweep.hip"
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_gather.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_mesh.hip"
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_comm.hip"
 
 #include <cmath>
@@ -40,7 +41,7 @@ int run(const int N, const char eng, const int iters, const double reg) {
     (void)hipMalloc(&ws, wsb);
     otf_sinkhorn_opts o{};
     o.reg = reg; o.stop_thr = 0; o.max_iter = iters; o.check_every = 10;
-    o.flavor = OTF_FLAVOR_POT; o.engine = eng == 't' ? OTF_ENGINE_TILED : eng == 'g' ? OTF_ENGINE_GATHER : OTF_ENGINE_RESIDENT;
+    o.flavor = OTF_FLAVOR_POT; o.engine = eng == 't' ? OTF_ENGINE_TILED : eng == 'g' ? OTF_ENGINE_GATHER : eng == 'm' ? OTF_ENGINE_MESH : OTF_ENGINE_RESIDENT;
     for (int rep = 0; rep < 3; ++rep) {
         hipEvent_t e0, e1;
         (void)hipEventCreate(&e0);
@@ -112,7 +113,9 @@ int run(const int N, const char eng, const int iters, const double reg) {
                              "col partials+atomics done", "grid barrier", "loop back"};
     const char* gnames[6] = {"gather (poll) + sums", "v + decide", "row sums + u",
                              "col partials + publish", "-", "loop back"};
-    const char* const* names = tiled ? tnames : eng == 'g' ? gnames : rnames;
+    const char* mnames[6] = {"hop B (poll) + v", "row partials + publish", "row hop (poll) + u",
+                             "col partials + barrier", "publish + reduce (wave 0)", "loop back"};
+    const char* const* names = tiled ? tnames : eng == 'g' ? gnames : eng == 'm' ? mnames : rnames;
     for (int ph = 0; ph < 6; ++ph) printf("%-26s %8.2f us\n", names[ph], span[ph] / cnt / 100.0);
     printf("barrier arrival spread     %8.2f us\n", arrive_spread / 13 / 100.0);
     return 0;
@@ -121,7 +124,7 @@ int run(const int N, const char eng, const int iters, const double reg) {
 
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 4096;
-    const char eng = argc > 2 ? argv[2][0] : 'r';  // "tiled" / "gather" / "resident"
+    const char eng = argc > 2 ? argv[2][0] : 'r';  // "tiled" / "gather" / "mesh" / "resident"
     const bool f64 = argc > 3 && argv[3][0] == 'd';     // third argument "double": config-2 form
     if (f64) return run<double>(N, eng, 1999, 1e-2);
     return run<float>(N, eng, 100, 0.1);
