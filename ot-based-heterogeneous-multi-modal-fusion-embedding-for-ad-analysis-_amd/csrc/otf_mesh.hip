@@ -84,6 +84,7 @@ struct SkMeshArgs {
 };
 
 using I4 = __attribute__((ext_vector_type(4))) int;
+using F2 = __attribute__((ext_vector_type(2))) float;
 
 __device__ __forceinline__ I4 chunk2(float v0, float v1, int tag) {
     I4 x;
@@ -127,7 +128,8 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     // producer flag (non-finite u of the previous iteration), [3] zero / non-finite v
     // (epoch keys), [4] row-hop stall (iteration key)
     __shared__ int s_ep[5];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int tid = threadIdx.x, lane = tid & 63;
+    const int w = (int)threadIdx.x >> 6;
     const bool lead = (blockIdx.x == 0 && tid == 0);
     unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
     const int nrb = p.nrb, ncb = p.ncb, CPR = p.cpr;
@@ -159,8 +161,9 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
     const T ks = (T)(-unit / p.reg * cinv);
 
-    // ---- K for this wave's 16 rows x this lane's 8 columns, once (0 outside C)
-    T kv[R][G][VEC];
+    // ---- K for this wave's 16 rows x this lane's 8 columns, once (0 outside C), as
+    // pairs of adjacent columns: the row and column partials run on v_pk_fma_f32
+    F2 kv[R][G][2];
     {
         int colc[G];
 #pragma unroll
@@ -172,24 +175,20 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const CT* src = (row0 + r < p.n) ? crow : (const CT*)p.C;
+            const bool rok = row0 + r < p.n;
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const V c = load_cost<T>(src + colc[g]);
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
-            }
-            crow += p.ldc;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const bool rok = row0 + r < p.n;
-#pragma unroll
-            for (int g = 0; g < G; ++g)
+                T e[VEC];
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
                     const bool ok = rok && col0 + (lane + kWave * g) * VEC + k < p.m;
-                    kv[r][g][k] = ok ? fast_exp(kv[r][g][k] * ks) : (T)0;
+                    e[k] = ok ? fast_exp(c[k] * ks) : (T)0;
                 }
+                kv[r][g][0] = F2{e[0], e[1]};
+                kv[r][g][1] = F2{e[2], e[3]};
+            }
+            crow += p.ldc;
         }
     }
     // 1 / a of the rows whose u this lane finishes: row (lane & 15) when the tile spans
@@ -253,15 +252,13 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     auto col_partials = [&](const T (&wr)[R]) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            V acc;
+            F2 acc0 = kv[0][g][0] * wr[0], acc1 = kv[0][g][1] * wr[0];
 #pragma unroll
-            for (int q = 0; q < VEC; ++q) {
-                T sacc = 0;
-#pragma unroll
-                for (int r = 0; r < R; ++r) sacc += kv[r][g][q] * wr[r];
-                acc[q] = sacc;
+            for (int r = 1; r < R; ++r) {
+                acc0 = __builtin_elementwise_fma(kv[r][g][0], F2{wr[r], wr[r]}, acc0);
+                acc1 = __builtin_elementwise_fma(kv[r][g][1], F2{wr[r], wr[r]}, acc1);
             }
-            *reinterpret_cast<V*>(&colbuf[w][(lane + kWave * g) * VEC]) = acc;
+            *reinterpret_cast<V*>(&colbuf[w][(lane + kWave * g) * VEC]) = V{acc0[0], acc0[1], acc1[0], acc1[1]};
         }
     };
     // reducer (wave 0): S[e - 1] for this workgroup's chunk range from the nrb
@@ -299,16 +296,24 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                 s1 += chunk_v1(x[k]);
                 fl |= x[k][1] & 1;
             }
-        for (int o = CPR; o < kWave; o <<= 1) {
-            s0 += wave_xor_n<T>(s0, o);
-            s1 += wave_xor_n<T>(s1, o);
-        }
+        // lanes with equal chunk: offsets CPR, 2 CPR, ..., 32 (uniform branches, static DPP)
+        if (CPR <= 1) { s0 += wave_xor<T, 1>(s0); s1 += wave_xor<T, 1>(s1); }
+        if (CPR <= 2) { s0 += wave_xor<T, 2>(s0); s1 += wave_xor<T, 2>(s1); }
+        if (CPR <= 4) { s0 += wave_xor<T, 4>(s0); s1 += wave_xor<T, 4>(s1); }
+        if (CPR <= 8) { s0 += wave_xor<T, 8>(s0); s1 += wave_xor<T, 8>(s1); }
+        if (CPR <= 16) { s0 += wave_xor<T, 16>(s0); s1 += wave_xor<T, 16>(s1); }
+        if (CPR <= 32) { s0 += wave_xor<T, 32>(s0); s1 += wave_xor<T, 32>(s1); }
         const int bad = __any(fl) ? 1 : 0;
         // POT's marginal error of the iterate whose v = b / S[e - 2]
         T term = 0;
         if (rc0) { const T rr = (rb0 / sp0) * s0 - rb0; term += rr * rr; }
         if (rc1) { const T rr = (rb1 / sp1) * s1 - rb1; term += rr * rr; }
-        for (int o = 1; o < CPR; o <<= 1) term += wave_xor_n<T>(term, o);
+        if (CPR > 1) term += wave_xor<T, 1>(term);
+        if (CPR > 2) term += wave_xor<T, 2>(term);
+        if (CPR > 4) term += wave_xor<T, 4>(term);
+        if (CPR > 8) term += wave_xor<T, 8>(term);
+        if (CPR > 16) term += wave_xor<T, 16>(term);
+        if (CPR > 32) term += wave_xor<T, 32>(term);
         sp0 = s0;
         sp1 = s1;
         const int tag = (e << 2) | bad;
@@ -406,6 +411,10 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     const int rowl = butterfly_row<R>(lane);
 
     for (int it = 0; it < p.max_iter; ++it) {
+        // re-derive the lane predicates every iteration (one v_cmp each) instead of
+        // keeping ~20 hoisted 64-bit lane masks live across the loop: that set spilled
+        // the SGPR file into VGPR lanes (v_readlane / v_writelane on every use)
+        asm volatile("" : "+v"(tid), "+v"(lane));
         OTF_STAMP(it, 0);
         const int e = it + 1;  // hop-B epoch of S[it]; row-hop epoch of iteration it
         const int fl = gather_b(e);
@@ -418,23 +427,22 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             break;
         }
         const int vbad_cb = (fl & 4) ? 1 : 0;
-        T vn[G][VEC];
+        F2 vn[G][2];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const V t = *reinterpret_cast<const V*>(&vcur[(lane + kWave * g) * VEC]);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) vn[g][k] = t[k];
+            vn[g][0] = F2{t[0], t[1]};
+            vn[g][1] = F2{t[2], t[3]};
         }
         // row partials over this tile's columns, wave totals
         T rp[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            T acc = 0;
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) acc += kv[r][g][k] * vn[g][k];
-            rp[r] = acc;
+            F2 acc = kv[r][0][0] * vn[0][0];
+            acc = __builtin_elementwise_fma(kv[r][0][1], vn[0][1], acc);
+            acc = __builtin_elementwise_fma(kv[r][1][0], vn[1][0], acc);
+            acc = __builtin_elementwise_fma(kv[r][1][1], vn[1][1], acc);
+            rp[r] = acc[0] + acc[1];
         }
         wave_sum_multi<T, R>(rp, lane);
         if (lane < R) urow[w][rowl] = rp[0];
@@ -613,7 +621,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                 if (c0 >= p.m) continue;
                 VP o;
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) o[k] = (TP)(uo[r] * kv[r][g][k] * vo[g][k]);
+                for (int k = 0; k < VEC; ++k) o[k] = (TP)(uo[r] * kv[r][g][k >> 1][k & 1] * vo[g][k]);
                 if (c0 + VEC <= p.m) {
                     *reinterpret_cast<VP*>(prow + c0) = o;
                 } else {
