@@ -120,7 +120,7 @@ typedef struct {
     int32_t n_total;    /* row-sharded solve: rows of the whole problem (u0 = 1/n_total);
                            0 = n                                                      */
     int32_t deterministic; /* 1: bitwise-reproducible column sums (fixed-order reduction,
-                           no float atomics; gather or sweep engine, POT flavour),
+                           no float atomics; gather, mesh or sweep engine, POT flavour),
                            e.g. for parity runs; other engines: OTF_EUNSUPPORTED     */
 } otf_sinkhorn_opts;
 

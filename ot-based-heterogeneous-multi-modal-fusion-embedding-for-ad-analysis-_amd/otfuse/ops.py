@@ -257,8 +257,9 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
     ``cost_scale`` (device scalar) divides the cost first (scale_cost="max_cost").
     Compute dtype = ``C.dtype`` (float32 or float64); a float16 ``C`` (fp16 cost
     storage, BASELINE config 5) is computed in float32.  ``deterministic=True``
-    reduces the column sums in a fixed order without float atomics (sweep engine, POT
-    flavour): bitwise-identical results run to run.
+    reduces the column sums in a fixed order without float atomics (gather / mesh engines
+    by construction, else the sweep engine's fixed-order mode; POT flavour):
+    bitwise-identical results run to run.
     """
     _dev(C, "C")
     if C.dtype not in _VEC:

@@ -159,7 +159,7 @@ def test_nan_loss_contributes_no_gradient(dev):
 
 
 @pytest.mark.parametrize("dt,n,m", [(torch.float32, 2000, 3000), (torch.float64, 700, 450),
-                                    (torch.float32, 37, 5)])
+                                    (torch.float32, 37, 5), (torch.float32, 200, 9000)])
 def test_deterministic_mode_is_bitwise_reproducible(orc, dev, dt, n, m):
     from otfuse import ops
     rng = np.random.default_rng(n)
@@ -168,8 +168,10 @@ def test_deterministic_mode_is_bitwise_reproducible(orc, dev, dt, n, m):
     b = np.full(m, 1.0 / m)
     Ct, at, bt = (torch.as_tensor(x, device=dev, dtype=dt) for x in (C, a, b))
     plans = []
-    # small problems take the gather engine (fixed-order by construction), larger the sweep
-    want = "sweep" if m > 512 else "gather"
+    # engines that are fixed-order by construction: gather (small problems), mesh (float32,
+    # 4..64 row tiles x <= 8 column tiles); the sweep engine's deterministic mode otherwise
+    want = ("gather" if m <= 512 else "mesh" if dt == torch.float32 and n >= 385 and m <= 4096
+            else "sweep")
     for _ in range(3):
         res = ops.sinkhorn(at, bt, Ct, 0.05, max_iter=80, stop_thr=0.0, deterministic=True)
         assert res.info()["engine_name"] == want
