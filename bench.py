@@ -7,11 +7,12 @@ so every iteration runs) -> N x N transport plan written to HBM.
 
   value            = MRI+PET pairs aligned per second, whole job (N x ranks / step time)
   sinkhorn_iters_per_sec = iterations / time of the Sinkhorn call (incl. plan write)
-  roofline         = the dominant kernel, sk_tiled_kernel (one launch runs all 100
+  roofline         = the dominant kernel, sk_mesh_kernel (one launch runs all 100
                      iterations with K = exp(-C/eps) held in registers, so C crosses HBM
-                     once per solve): its bound is LATENCY (per iteration five in-launch
-                     hand-offs), reported as us per iteration against the VALU floor of
-                     the iteration's 2 N^2 FMAs; the contract's algorithmic-byte rate and
+                     once per solve): its bound is LATENCY (per iteration three in-launch
+                     granule hops: row partials within the row block, column partials to
+                     the reducers, sums back), reported as us per iteration against the
+                     VALU floor of the iteration's 2 N^2 FMAs; the algorithmic-byte rate and
                      the PMC HBM traffic (profiles/kernel_traffic.json, only when it was
                      measured on this exact library build) are reported beside it
   cost_roofline    = the split-fp16 MFMA cost kernel vs the dense fp16 MFMA peak (its
@@ -91,8 +92,10 @@ def parse():
                    help="skip the per-training-step OT block leg (config 2)")
     p.add_argument("--multi-legs", action="store_true",
                    help="run the sharded RCCL legs also at world = 1 (they always run at world > 1)")
-    p.add_argument("--engine", default="auto", choices=("auto", "stream", "resident", "tiled", "sweep"),
-                   help="Sinkhorn engine (auto = tiled / resident when the cost fits the register file)")
+    p.add_argument("--engine", default="auto",
+                   choices=("auto", "stream", "resident", "tiled", "sweep", "gather", "mesh"),
+                   help="Sinkhorn engine (auto = mesh / tiled / resident when the cost fits the "
+                        "register files)")
     return p.parse_args()
 
 
@@ -173,7 +176,8 @@ def main():
                        plan_out=P, engine=args.engine)
     engine = res.info()["engine_name"]
     kernel_name = {"resident": "sk_resident_kernel", "tiled": "sk_tiled_kernel",
-                   "sweep": "sk_sweep_kernel"}.get(engine, "sk_pass_kernel")
+                   "sweep": "sk_sweep_kernel", "mesh": "sk_mesh_kernel",
+                   "gather": "sk_gather_kernel"}.get(engine, "sk_pass_kernel")
 
     # PMC traffic: only when profiles/kernel_traffic.json was measured on THIS library
     # build and shape (a stale profile is reported as null, not reused)
@@ -196,7 +200,7 @@ def main():
     # VALU floor of one resident iteration: 2 N^2 FMAs (row sums K v, column sums K^T u)
     floor_us = 2.0 * N * N / (VALU_F32_PEAK_TFMA * 1e12) * 1e6
     algo_gbs = iter_bytes * iters / sk_s / 1e9
-    if engine in ("resident", "tiled"):
+    if engine in ("resident", "tiled", "mesh", "gather"):
         roofline = {"bound": "latency", "kernel": kernel_name, "achieved": us_per_iter,
                     "peak": floor_us, "unit": "us per iteration", "frac": floor_us / us_per_iter,
                     "traffic": traffic,
@@ -207,10 +211,11 @@ def main():
                     "note": ("the whole solve is one launch holding K = exp(-C/eps) in registers: C "
                              "crosses HBM once, so the HBM-equivalent rate (algorithmic_GBs, iters x "
                              "N*N*4 B / launch time) is not an HBM measurement; per iteration the "
-                             "kernel pays ~5 in-launch hand-offs (column-sum read, row-partial "
-                             "exchange, gather, atomics drain, grid barrier: tools/stamps_resident.hip, "
-                             "DESIGN.md 4) against a VALU floor (peak) of 2 N^2 FMAs at 78.6 TFMA/s; "
-                             "the HBM-bound engine is measured in sweep_config5 / hbm_probe")}
+                             "mesh kernel pays three in-launch granule hops (row partials within the "
+                             "row block, column partials to the reducers, sums back; "
+                             "tools/stamps_resident.hip, DESIGN.md 4) against a VALU floor (peak) of "
+                             "2 N^2 FMAs at 78.6 TFMA/s; the HBM-bound engine is measured in "
+                             "sweep_config5 / hbm_probe")}
     else:
         roofline = {"bound": "hbm", "kernel": kernel_name, "achieved": algo_gbs,
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": algo_gbs / HBM_PEAK_GBS,

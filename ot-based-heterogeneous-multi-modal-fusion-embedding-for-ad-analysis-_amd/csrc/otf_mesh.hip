@@ -240,13 +240,10 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     // colbuf, after the barrier), epoch e; flag = non-finite u in this workgroup
     auto publish_cols = [&](int e, int flag) {
         if (tid < nch) {
-            T s0 = colbuf[0][2 * tid], s1 = colbuf[0][2 * tid + 1];
+            F2 s = *reinterpret_cast<const F2*>(&colbuf[0][2 * tid]);
 #pragma unroll
-            for (int ww = 1; ww < NW; ++ww) {
-                s0 += colbuf[ww][2 * tid];
-                s1 += colbuf[ww][2 * tid + 1];
-            }
-            gstore(rs, cola(e, rb) + (uint32_t)tid * 16, chunk2(s0, s1, (e << 2) | flag));
+            for (int ww = 1; ww < NW; ++ww) s += *reinterpret_cast<const F2*>(&colbuf[ww][2 * tid]);
+            gstore(rs, cola(e, rb) + (uint32_t)tid * 16, chunk2(s[0], s[1], (e << 2) | flag));
         }
     };
     auto col_partials = [&](const T (&wr)[R]) {
@@ -409,6 +406,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     bool done = false;
     if (w == 0 && !reduce(1)) s_ep[1] = 1;  // seen after the hop-B barrier of epoch 1
     const int rowl = butterfly_row<R>(lane);
+    int chk = 0;  // (it - 1) % check_every for it >= 1
 
     for (int it = 0; it < p.max_iter; ++it) {
         // re-derive the lane predicates every iteration (one v_cmp each) instead of
@@ -447,7 +445,9 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         wave_sum_multi<T, R>(rp, lane);
         if (lane < R) urow[w][rowl] = rp[0];
         __builtin_amdgcn_wave_barrier();
-        const bool check = it >= 1 && ((it - 1) % p.check_every) == 0;
+        // (it - 1) % check_every == 0, kept as a counter (no integer division per iteration)
+        const bool check = it >= 1 && chk == 0;
+        if (it >= 1) chk = chk + 1 == p.check_every ? 0 : chk + 1;
         T errv = 0;
         int vbad = vbad_cb, stall = 0;
         if (ncb == 1) {
@@ -532,8 +532,8 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         OTF_STAMP(it, 4);
         if (s_ep[4] == it) { status = OTF_SK_TIMEOUT; done = true; break; }
         if (check) {
-            if (lead) p.errlog[(it - 1) / p.check_every] = err;
-            n_err = (it - 1) / p.check_every + 1;
+            if (lead) p.errlog[n_err] = err;
+            ++n_err;
         }
         if (dec == 1) {
             last_good = it - 1; niter = it - 1; status = OTF_SK_CONVERGED;
