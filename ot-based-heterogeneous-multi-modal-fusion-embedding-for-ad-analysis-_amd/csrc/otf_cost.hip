@@ -468,6 +468,167 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
     if (cmax) block_max_publish(cmax, lmax);
 }
 
+// 256 x 256 output tile per 512-thread workgroup for large problems (one tile per CU at
+// N = 4096): twice the arithmetic intensity of the 128 x 128 tile, whose 64 KB of operand
+// fetch per 48 MFMAs per wave outran the per-CU L2 / Infinity Cache rate (MFMA busy
+// 20-28 %).  8 waves = 4 along M x 2 along N, each 64 x 128 = 2 x 4 MFMA 32x32 tiles
+// (128 accumulators).  32-deep K stages, double-buffered in LDS (2 x 64 KB for the
+// split-fp16 images); the next stage's 16-B global loads are in registers while the
+// current stage computes, so one barrier per stage.  LDS rows are 64 B with the 16-B
+// chunk index XORed with (row >> 2) & 3: 16 consecutive rows of one ds_read_b128 phase
+// (and 4 rows x 4 chunks of a ds_write_b128 phase) hit 16 distinct 16-B bank groups.
+constexpr int GBM = 256, GBN = 256, GBK = 32, GCPR = GBK / 8;
+__device__ __forceinline__ int gswz(int row, int kc) { return row * GBK + ((kc ^ ((row >> 2) & 3)) << 3); }
+
+template <int NS, typename TC>
+__global__ __launch_bounds__(512) void cost_big_kernel(
+    const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
+    const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
+    const float* __restrict__ ys, const float* __restrict__ yy, int64_t ldxh, int64_t ldyh, int n, int m, int kpad,
+    int metric, int zero_diag, TC* __restrict__ C, int64_t ldc, unsigned int* cmax, int tiles_n,
+    const float* __restrict__ store_scale) {
+    constexpr int NI = NS == 3 ? 2 : 1;           // fp16 images per operand
+    constexpr int NCH = GBM * GCPR / 512;         // 16-B chunks per thread per image per stage
+    __shared__ __attribute__((aligned(16))) _Float16 As[2][NI][GBM * GBK];
+    __shared__ __attribute__((aligned(16))) _Float16 Bs[2][NI][GBN * GBK];
+    __shared__ float sxs[GBM], sxx[GBM];
+    __shared__ float wmx[8];
+
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    int tm, tn;
+    grouped_tile(wg, nwg, tiles_n, tm, tn);
+    const int i0 = tm * GBM, j0 = tn * GBN;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+    using u4 = __attribute__((ext_vector_type(4))) unsigned int;
+    u4 st[NCH][2 * NI];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int chunk = tid + 512 * c;
+            const int row = chunk / GCPR, kc = (chunk % GCPR) * 8;
+            const int gi = i0 + row < n ? i0 + row : n - 1;
+            const int gj = j0 + row < m ? j0 + row : m - 1;
+            st[c][0] = *reinterpret_cast<const u4*>(Xh + (int64_t)gi * ldxh + k0 + kc);
+            st[c][NI] = *reinterpret_cast<const u4*>(Yh + (int64_t)gj * ldyh + k0 + kc);
+            if (NI == 2) {
+                st[c][1] = *reinterpret_cast<const u4*>(Xl + (int64_t)gi * ldxh + k0 + kc);
+                st[c][NI + 1] = *reinterpret_cast<const u4*>(Yl + (int64_t)gj * ldyh + k0 + kc);
+            }
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int chunk = tid + 512 * c;
+            const int row = chunk / GCPR, kc = chunk % GCPR;
+#pragma unroll
+            for (int h = 0; h < NI; ++h) {
+                *reinterpret_cast<u4*>(&As[buf][h][gswz(row, kc)]) = st[c][h];
+                *reinterpret_cast<u4*>(&Bs[buf][h][gswz(row, kc)]) = st[c][NI + h];
+            }
+        }
+    };
+
+    if (tid < GBM) {
+        const int gi = i0 + tid < n ? i0 + tid : n - 1;
+        sxs[tid] = xs[gi];
+        sxx[tid] = xx[gi];
+    }
+    float cys[4], cyy[4];
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+        const int gj0 = j0 + wn * 128 + nj * 32 + (lane & 31);
+        const int gj = gj0 < m ? gj0 : m - 1;
+        cys[nj] = ys[gj];
+        cyy[nj] = yy[gj];
+    }
+
+    const int nk = kpad / GBK;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) gload((kt + 1) * GBK);
+#pragma unroll
+        for (int ks = 0; ks < GBK / 16; ++ks) {
+            const int kc = ks * 2 + (lane >> 5);
+            f16x8 ah[2], al[2], bh[4], bl[4];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int ar = wm * 64 + t * 32 + (lane & 31);
+                ah[t] = *reinterpret_cast<const f16x8*>(&As[buf][0][gswz(ar, kc)]);
+                if (NI == 2) al[t] = *reinterpret_cast<const f16x8*>(&As[buf][NI - 1][gswz(ar, kc)]);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int br = wn * 128 + t * 32 + (lane & 31);
+                bh[t] = *reinterpret_cast<const f16x8*>(&Bs[buf][0][gswz(br, kc)]);
+                if (NI == 2) bl[t] = *reinterpret_cast<const f16x8*>(&Bs[buf][NI - 1][gswz(br, kc)]);
+            }
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int nj = 0; nj < 4; ++nj) {
+                    if (NS == 3) {
+                        acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mi], bh[nj], acc[mi][nj], 0, 0, 0);
+                        acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bl[nj], acc[mi][nj], 0, 0, 0);
+                    }
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bh[nj], acc[mi][nj], 0, 0, 0);
+                }
+        }
+        if (kt + 1 < nk) lstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    const float os = store_scale ? store_scale[0] : 1.0f;
+    float lmax = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int rl = wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                const int cl = wn * 128 + nj * 32 + (lane & 31);
+                const int gi = i0 + rl, gj = j0 + cl;
+                if (gi < n && gj < m) {
+                    const float dot = acc[mi][nj][e] * sxs[rl] * cys[nj];
+                    float c = sxx[rl] + cyy[nj] - 2.f * dot;
+                    c = c > 0.f ? c : 0.f;
+                    if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
+                    if (zero_diag && gi == gj) c = 0.f;
+                    const TC cs = (TC)(c * os);
+                    C[(int64_t)gi * ldc + gj] = cs;
+                    lmax = fmaxf(lmax, (float)cs);
+                }
+            }
+    if (cmax) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmx[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            float v = wmx[0];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) v = fmaxf(v, wmx[w]);
+            const unsigned int u = __float_as_uint(v);
+            if (u > __hip_atomic_load(cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(cmax, u);
+        }
+    }
+}
+
 }  // namespace
 }  // namespace otf
 
@@ -496,6 +657,16 @@ int otf_cost_pairwise(const float* X, int64_t ldx, const float* Y, int64_t ldy, 
 }
 
 static size_t otf_al(size_t x) { return (x + 255) / 256 * 256; }
+
+// OTF_COST_BIG=0 keeps the 128 x 128 tile for every shape (A/B measurements)
+static bool cost_big_enabled() {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("OTF_COST_BIG");
+        env = e ? atoi(e) : 1;
+    }
+    return env != 0;
+}
 
 size_t otf_cost_ex_workspace_size(int64_t n, int64_t m, int64_t d, int32_t in_dtype) {
     const size_t ldh = (size_t)((d + otf::SBK - 1) / otf::SBK * otf::SBK);
@@ -581,14 +752,32 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
         OTF_HIP(hipMemsetD32Async((hipDeviceptr_t)c_unit, 0x3f800000u /* 1.0f */, 1, s));
     }
     if (cmax) OTF_HIP(hipMemsetAsync(cmax, 0, sizeof(float), s));
-    const int tiles_m = (int)((n + otf::BM - 1) / otf::BM);
-    const int tiles_n = (int)((m + otf::BN - 1) / otf::BN);
+    // Tile choice by rounds of resident workgroups (two 128 x 128 per CU, one 256 x 256):
+    // a round of 256 x 256 tiles took 1.8x a round of 128 x 128 ones at N = 4096
+    // (68 vs 38 us), so big tiles win when they need fewer than 1 / 1.8 of the rounds
+    // (N = 4096: 1 vs 2 rounds; config 5: 4 vs 8), not for a ragged 17 x 16 grid (2 vs 3).
+    const int64_t cus = otf::device_cu_count();
+    const int64_t big_tiles = ((n + otf::GBM - 1) / otf::GBM) * ((m + otf::GBN - 1) / otf::GBN);
+    const int64_t small_tiles = ((n + otf::BM - 1) / otf::BM) * ((m + otf::BN - 1) / otf::BN);
+    const int64_t big_rounds = (big_tiles + cus - 1) / cus;
+    const int64_t small_rounds = (small_tiles + 2 * cus - 1) / (2 * cus);
+    const bool big = 18 * big_rounds < 10 * small_rounds && cost_big_enabled();
+    const int BMx = big ? otf::GBM : otf::BM, BNx = big ? otf::GBN : otf::BN;
+    const int tiles_m = (int)((n + BMx - 1) / BMx);
+    const int tiles_n = (int)((m + BNx - 1) / BNx);
     const int64_t nwg = (int64_t)tiles_m * tiles_n;
     if (nwg > INT32_MAX) return OTF_EUNSUPPORTED;
 #define OTF_COST_LAUNCH(NS, TC)                                                                   \
-    otf::cost_split16_kernel<NS, TC><<<(int)nwg, 256, 0, s>>>(                                  \
-        Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric, zero_diag,      \
-        (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale)
+    do {                                                                                          \
+        if (big)                                                                                  \
+            otf::cost_big_kernel<NS, TC><<<(int)nwg, 512, 0, s>>>(                               \
+                Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
+                zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
+        else                                                                                      \
+            otf::cost_split16_kernel<NS, TC><<<(int)nwg, 256, 0, s>>>(                          \
+                Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
+                zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
+    } while (0)
     if (split && !f16out) OTF_COST_LAUNCH(3, float);
     else if (split) OTF_COST_LAUNCH(3, _Float16);
     else if (!f16out) OTF_COST_LAUNCH(1, float);

@@ -31,7 +31,7 @@ def _t(x, dev, dt=None):
 # ----------------------------------------------------------------------------- cost
 @pytest.mark.parametrize("algo", ["split16", "f32"])
 @pytest.mark.parametrize("n,m,d", [(256, 256, 64), (130, 77, 40), (4096, 4096, 512), (1, 5, 3),
-                                   (300, 129, 1000)])
+                                   (300, 129, 1000), (4100, 3999, 300)])
 def test_pairwise_cost_vs_oracle(ops, orc, dev, n, m, d, algo):
     from otfuse.synthetic import paired_embeddings
     X, _, _ = paired_embeddings(n, d, seed=n)

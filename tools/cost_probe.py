@@ -60,6 +60,7 @@ def main():
     case("metric_f32", 4096, 4096, 512, torch.float32, torch.float32)
     case("config5_f16", 8192, 8192, 1024, torch.float16, torch.float16)
     case("ragged_f32", 1000, 777, 300, torch.float32, torch.float32)
+    case("ragged_big_f32", 4100, 3999, 300, torch.float32, torch.float32)
     case("ragged_f16", 999, 1025, 130, torch.float16, torch.float16)
 
 
