@@ -73,7 +73,8 @@ struct SkMeshArgs {
     double stop_thr;
     void* gran;  // granule region, zeroed per solve
     uint32_t off_row, off_cola, off_colb, bstride;
-    int nrb, ncb, cpr, xcd_rows;
+    int nrb, ncb, cpr, xcd_rows, xcc_local;
+    int* xreg;  // [8 x 64] workgroups per XCC (registration), then the flat barrier word
     otf_sinkhorn_info* info;
     double* errlog;
     float* u_out;
@@ -107,6 +108,15 @@ __device__ __forceinline__ I4 gload(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
 __device__ __forceinline__ void gstore(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x) {
     __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
 }
+// Column-path store: plain (xl = 1) when producer and consumers share one XCC, so the
+// line stays in that XCC's L2 -- see the tile assignment in the kernel -- else
+// write-through (sc1) like every cross-XCC hop
+__device__ __forceinline__ void gstore_col(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x, int xl) {
+    if (xl)
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
+    else
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
+}
 
 // KQ: reducer loads per lane, ceil(nrb * CPR / 64): 4 when nrb is a power of two
 // (nrb * CPR = 256), up to 8 otherwise
@@ -134,12 +144,48 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
     const int nrb = p.nrb, ncb = p.ncb, CPR = p.cpr;
 
-    // tile of this workgroup: xcd_rows (nrb % 8 == 0) deals the members of a row block
-    // to one XCD under round-robin placement; otherwise consecutive workgroups are the
-    // column tiles of a row block (ncb = 8: a column tile's members share an XCD).
-    // Speed only: no hop assumes any placement.
-    int rb, cb;
-    {
+    // Tile of this workgroup.  XCC-local column path (p.xcc_local): every workgroup
+    // registers on its XCC (the hardware id, not an assumed placement), one flat
+    // barrier, and when there are exactly ncb active XCCs holding exactly nrb workgroups
+    // each (N = 4096: 8 x 32, one workgroup per CU), column tile cb = the rank of this
+    // XCC and row block rb = the registration slot.  A column tile's hop A, reduce and
+    // hop B then stay inside one XCC's L2, which is the point of coherence for all its
+    // CUs: plain stores (L1 is write-through, the line stays in L2) read by L1-bypassing
+    // sc1 loads -- the single-L2 protocol; only the cross-XCC hops (row hop, error
+    // chunks) need write-through stores.  Measured 7.2 -> 5.7 us per iteration; with the
+    // column tiles spread over XCCs the same plain stores are never seen (the solve ends
+    // in OTF_SK_TIMEOUT), which is why roles follow the registration, never blockIdx.
+    // Otherwise: blockIdx roles, every hop write-through (xcd_rows: a row block's members
+    // on one XCD under round-robin placement, speed only).
+    int rb = 0, cb = 0, xl = 0;
+    if (p.xcc_local) {
+        __shared__ int s_reg[4];
+        const int xcd = xcc_id();
+        if (tid == 0)
+            s_reg[0] = __hip_atomic_fetch_add(p.xreg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool ok = grid_barrier(p.xreg + 8 * 64, gridDim.x, deadline, p.timeout_ticks, &s_reg[3]);
+        if (tid == 0) {
+            int good = ok ? 1 : 0, rank = 0, nact = 0;
+            for (int x = 0; x < 8; ++x) {
+                const int c = load_agent(p.xreg + x * 64);
+                if (c > 0) {
+                    rank += x < xcd ? 1 : 0;
+                    ++nact;
+                    if (c != nrb) good = 0;
+                }
+            }
+            if (nact != ncb) good = 0;
+            s_reg[1] = good;
+            s_reg[2] = rank;
+        }
+        __syncthreads();
+        if (s_reg[1]) {
+            rb = s_reg[0];
+            cb = s_reg[2];
+            xl = 1;
+        }
+    }
+    if (!xl) {
         const int bi = blockIdx.x;
         if (p.xcd_rows && (nrb & 7) == 0) {
             const int x = bi & 7, q = bi >> 3;
@@ -243,7 +289,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             F2 s = *reinterpret_cast<const F2*>(&colbuf[0][2 * tid]);
 #pragma unroll
             for (int ww = 1; ww < NW; ++ww) s += *reinterpret_cast<const F2*>(&colbuf[ww][2 * tid]);
-            gstore(rs, cola(e, rb) + (uint32_t)tid * 16, chunk2(s[0], s[1], (e << 2) | flag));
+            gstore_col(rs, cola(e, rb) + (uint32_t)tid * 16, chunk2(s[0], s[1], (e << 2) | flag), xl);
         }
     };
     auto col_partials = [&](const T (&wr)[R]) {
@@ -314,8 +360,8 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         sp0 = s0;
         sp1 = s1;
         const int tag = (e << 2) | bad;
-        if (lane < CPR && r_ok) gstore(rs, colb(e, rb) + (uint32_t)r_cc * 16, chunk2(s0, s1, tag));
-        if (lane == 0 && rb < nred) gstore(rs, colb(e, rb) + (uint32_t)CPR * 16, chunk2(term, 0.f, tag));
+        if (lane < CPR && r_ok) gstore_col(rs, colb(e, rb) + (uint32_t)r_cc * 16, chunk2(s0, s1, tag), xl);
+        if (lane == 0 && rb < nred) gstore_col(rs, colb(e, rb) + (uint32_t)CPR * 16, chunk2(term, 0.f, tag), xl);
         deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
         return ok;
     };
@@ -656,6 +702,8 @@ hipError_t launch_mesh_t(int grid, SkMeshArgs& p, hipStream_t s) {
     return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
 }
 
+constexpr size_t kMeshRegBytes = 9 * 256;  // 8 XCC counters + the barrier word, 256 B each
+
 struct MeshShape {
     int nrb, ncb, cpr;
     uint32_t bstride;
@@ -699,7 +747,7 @@ bool mesh_supported(int64_t n, int64_t m) {
 size_t mesh_region_bytes(int64_t n, int64_t m) {
     if (!mesh_supported(n, m)) return 0;
     const MeshShape s = mesh_shape(n, m);
-    return s.row_bytes + s.cola_bytes + s.colb_bytes;
+    return kMeshRegBytes + s.row_bytes + s.cola_bytes + s.colb_bytes;
 }
 
 template <typename CT>
@@ -723,7 +771,8 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
     p.check_every = o.check_every;
     p.err_squared = o.err_squared;
     p.stop_thr = o.stop_thr;
-    p.gran = region;
+    p.xreg = (int*)region;
+    p.gran = (char*)region + kMeshRegBytes;
     p.off_row = 0;
     p.off_cola = (uint32_t)sh.row_bytes;
     p.off_colb = (uint32_t)(sh.row_bytes + sh.cola_bytes);
@@ -732,6 +781,10 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
     p.ncb = sh.ncb;
     p.cpr = sh.cpr;
     p.xcd_rows = mesh_xcd_rows();
+    {
+        const char* e = getenv("OTF_MESH_XCC");  // 0: blockIdx roles, write-through everywhere
+        p.xcc_local = e ? atoi(e) : 1;
+    }
     p.info = info;
     p.errlog = errlog;
     p.u_out = u_out;

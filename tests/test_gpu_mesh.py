@@ -198,3 +198,39 @@ def test_mesh_unsupported_shapes_are_refused(dev):
         with pytest.raises(Exception, match="unsupported"):
             ops.sinkhorn(a, b, C, 0.1, max_iter=10, engine="mesh")
         assert ops.sinkhorn(a, b, C, 0.1, max_iter=10).info()["engine_name"] != "mesh"
+
+
+def test_mesh_xcc_local_and_write_through_paths_agree_bitwise(dev, monkeypatch):
+    """Roles by XCC registration (column path inside one L2, plain stores) and by
+    blockIdx (every hop write-through) reduce in the same fixed order: identical bits."""
+    from otfuse import ops
+    n = m = 4096
+    g = torch.Generator(device=dev).manual_seed(11)
+    C = torch.rand(n, m, device=dev, generator=g)
+    a = torch.full((n,), 1.0 / n, device=dev)
+    r1 = ops.sinkhorn(a, a, C, 0.05, max_iter=120, stop_thr=0.0, engine="mesh")
+    monkeypatch.setenv("OTF_MESH_XCC", "0")
+    r0 = ops.sinkhorn(a, a, C, 0.05, max_iter=120, stop_thr=0.0, engine="mesh")
+    assert r1.info()["engine_name"] == r0.info()["engine_name"] == "mesh"
+    assert torch.equal(r0.plan, r1.plan) and torch.equal(r0.u, r1.u) and torch.equal(r0.v, r1.v)
+
+
+def test_two_mesh_solves_on_two_streams(dev):
+    """Two concurrent 64-workgroup grids: each registers its own XCC population (or falls
+    back to write-through roles) and both finish with the streaming engine's plan."""
+    from otfuse import ops
+    n = m = 1024
+    g = torch.Generator(device=dev).manual_seed(3)
+    C = torch.rand(n, m, device=dev, generator=g)
+    a = torch.full((n,), 1.0 / n, device=dev)
+    ref = ops.sinkhorn(a, a, C, 0.05, max_iter=400, stop_thr=0.0, engine="stream").plan
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    outs = []
+    for s in (s1, s2):
+        with torch.cuda.stream(s):
+            outs.append(ops.sinkhorn(a, a, C, 0.05, max_iter=400, stop_thr=0.0, engine="mesh"))
+    torch.cuda.synchronize()
+    for r in outs:
+        assert r.info()["status_name"] == "max_iter"
+        assert (r.plan - ref).abs().max() / ref.abs().max() < 1e-5
