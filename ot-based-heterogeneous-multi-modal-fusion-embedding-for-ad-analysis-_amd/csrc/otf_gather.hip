@@ -59,6 +59,9 @@ template <typename T> struct SkGatherArgs {
     int max_iter, check_every, err_squared;
     double stop_thr;
     void* gran;        // [2 slots][grid][kGatherRow] granules, zeroed per solve
+    int* team;         // [8 x 64] workgroups per XCC, [8 * 64] the winning team's XCC + 1
+    int nwg;           // workgroups of the solve (the launch has 8 x nwg in team mode)
+    int team_mode;
     otf_sinkhorn_info* info;
     double* errlog;
     T* u_out;
@@ -117,10 +120,58 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
     // rows; [1..3] gather: break flagged by a producer, stall, break in v.
     __shared__ int s_ep[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int nwg = gridDim.x;
-    const bool lead = (blockIdx.x == 0 && tid == 0);
+    const int nwg = p.nwg;
     unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
-    const int row0 = blockIdx.x * TR + w * R;
+    // Team mode: the launch has 8 x nwg workgroups; each registers on its hardware XCC
+    // and the first XCC whose first nwg registrants are all resident claims the solve,
+    // every other workgroup returns at once.  The team's hand-offs then stay inside one
+    // XCC's L2 -- the point of coherence for all its CUs -- so the granules go out as
+    // plain stores (L1 is write-through; the line stays in L2) read by L1-bypassing sc1
+    // loads: no write-through to the Infinity Fabric and back per iteration.  The roles
+    // follow the registration (hardware ids), never an assumed placement; by pigeonhole
+    // some XCC receives nwg of the 8 x nwg workgroups.
+    int wgi = blockIdx.x, xl = 0;
+    if (p.team_mode) {
+        __shared__ int s_team[2];
+        const int xcd = xcc_id();
+        if (tid == 0) {
+            const int slot = __hip_atomic_fetch_add(p.team + xcd * 64, 1, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+            int keep = slot < nwg ? 1 : 0;
+            if (keep) {
+                // wait until this XCC's team is complete or another team has claimed
+                for (;;) {
+                    const int claim = load_agent(p.team + 8 * 64);
+                    if (claim != 0) {
+                        keep = claim == xcd + 1;
+                        break;
+                    }
+                    if (load_agent(p.team + xcd * 64) >= nwg) {
+                        if (slot == 0) {
+                            int expected = 0;
+                            __hip_atomic_compare_exchange_strong(p.team + 8 * 64, &expected, xcd + 1,
+                                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                    if (__builtin_amdgcn_s_memrealtime() > deadline) {
+                        keep = 0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            s_team[0] = keep;
+            s_team[1] = slot;
+        }
+        __syncthreads();
+        if (!s_team[0]) return;
+        wgi = s_team[1];
+        xl = 1;
+        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+    }
+    const bool lead = (wgi == 0 && tid == 0);
+    const int row0 = wgi * TR + w * R;
 
     const double unit = exp_unit<T>();
     double cinv = 1.0;
@@ -175,7 +226,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
     if (tid < TR) uhist[0][tid] = uhist[1][tid] = u0;
 
     const __amdgpu_buffer_rsrc_t rs = sums_rsrc(p.gran);
-    const uint32_t my_row = (uint32_t)blockIdx.x * kGatherRow + (uint32_t)tid * 16;
+    const uint32_t my_row = (uint32_t)wgi * kGatherRow + (uint32_t)tid * 16;
 
     // publish this workgroup's partials of S[k] = K_tile^T wr (epoch k + 1, slot k & 1)
     auto publish = [&](const T (&wr)[R], int k, int bad_local) {
@@ -208,8 +259,11 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
                 val[c] = sacc;
             }
             const uint32_t off = (uint32_t)(k & 1) * (uint32_t)nwg * kGatherRow + my_row;
-            __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(val, ((k + 1) << 1) | bad), rs, off, 0,
-                                                   16 /* sc1 */);
+            if (xl)  // one XCC: plain store, the line stays in its L2
+                __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(val, ((k + 1) << 1) | bad), rs, off, 0, 0);
+            else
+                __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(val, ((k + 1) << 1) | bad), rs, off, 0,
+                                                       16 /* sc1 */);
         }
     };
     // gather S[k]: every producer's chunk `tid`, summed in producer order, and, for those
@@ -418,7 +472,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
         for (int r = 1; r < R; ++r) if (lane == r) mine = uo[r];
         p.u_out[row0 + lane] = mine;
     }
-    if (blockIdx.x == 0 && w == 0) {
+    if (wgi == 0 && w == 0) {
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -473,8 +527,9 @@ hipError_t launch_gather_q(int grid, SkGatherArgs<T>& p, hipStream_t s) {
 
 template <typename T, typename CT, typename TP>
 hipError_t launch_gather(int grid, SkGatherArgs<T>& p, hipStream_t s) {
-    if (grid <= 4) return launch_gather_q<T, CT, TP, 4>(grid, p, s);
-    if (grid <= 8) return launch_gather_q<T, CT, TP, 8>(grid, p, s);
+    // NQ follows the solve's workgroups (p.nwg), not the launch (8 x nwg in team mode)
+    if (p.nwg <= 4) return launch_gather_q<T, CT, TP, 4>(grid, p, s);
+    if (p.nwg <= 8) return launch_gather_q<T, CT, TP, 8>(grid, p, s);
     return launch_gather_q<T, CT, TP, 16>(grid, p, s);
 }
 
@@ -488,8 +543,16 @@ template <typename T> bool gather_supported(int64_t n, int64_t m) {
     return n >= 1 && m >= 1 && m <= GatherCfg<T>::C && gather_grid<T>(n) <= kGatherMaxWG;
 }
 
+constexpr size_t kTeamBytes = 9 * 256;  // 8 XCC registration counters + the claim word
+
 template <typename T> size_t gather_region_bytes(int64_t n, int64_t m) {
-    return gather_supported<T>(n, m) ? 2 * (size_t)gather_grid<T>(n) * kGatherRow : 0;
+    return gather_supported<T>(n, m) ? kTeamBytes + 2 * (size_t)gather_grid<T>(n) * kGatherRow : 0;
+}
+
+// OTF_GATHER_TEAM=0: one workgroup per row tile anywhere on the chip, write-through hops
+inline int gather_team_mode() {
+    const char* e = getenv("OTF_GATHER_TEAM");
+    return e ? atoi(e) : 1;
 }
 
 template <typename T, typename CT>
@@ -511,7 +574,8 @@ hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, co
     p.check_every = o.check_every;
     p.err_squared = o.err_squared;
     p.stop_thr = o.stop_thr;
-    p.gran = region;
+    p.team = (int*)region;
+    p.gran = (char*)region + kTeamBytes;
     p.info = info;
     p.errlog = errlog;
     p.u_out = u_out;
@@ -522,8 +586,11 @@ hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, co
     hipError_t e = hipMemsetAsync(region, 0, gather_region_bytes<T>(n, m), s);
     if (e != hipSuccess) return e;
     const int grid = (int)gather_grid<T>(n);
-    if (P_out && P_dtype == OTF_F64) return launch_gather<T, CT, double>(grid, p, s);
-    return launch_gather<T, CT, float>(grid, p, s);
+    p.nwg = grid;
+    p.team_mode = gather_team_mode();
+    const int launch = p.team_mode ? 8 * grid : grid;
+    if (P_out && P_dtype == OTF_F64) return launch_gather<T, CT, double>(launch, p, s);
+    return launch_gather<T, CT, float>(launch, p, s);
 }
 
 template bool gather_supported<float>(int64_t, int64_t);

@@ -129,3 +129,19 @@ def test_two_gather_solves_on_two_streams(dev):
     for r in outs:
         assert r.info()["status_name"] == "max_iter"
         assert (r.plan - ref).abs().max() / ref.abs().max() < 1e-12
+
+
+def test_gather_team_mode_agrees_bitwise(dev, monkeypatch):
+    """XCC team mode (8 x nwg workgroups launched, the first complete XCC team solves with
+    plain stores inside its L2) and the one-workgroup-per-tile write-through launch add
+    the partials in the same order: identical bits, config-2 shape, float64."""
+    from otfuse import ops
+    n = m = 512
+    g = torch.Generator(device=dev).manual_seed(21)
+    C = torch.rand(n, m, device=dev, generator=g, dtype=torch.float64)
+    a = torch.full((n,), 1.0 / n, device=dev, dtype=torch.float64)
+    r1 = ops.sinkhorn(a, a, C, 0.02, max_iter=500, stop_thr=0.0, engine="gather")
+    monkeypatch.setenv("OTF_GATHER_TEAM", "0")
+    r0 = ops.sinkhorn(a, a, C, 0.02, max_iter=500, stop_thr=0.0, engine="gather")
+    assert r1.info()["engine_name"] == r0.info()["engine_name"] == "gather"
+    assert torch.equal(r0.plan, r1.plan) and torch.equal(r0.u, r1.u) and torch.equal(r0.v, r1.v)

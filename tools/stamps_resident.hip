@@ -99,6 +99,7 @@ int run(const int N, const char eng, const int iters, const double reg) {
         for (int w = 0; w < nwg; ++w) {
             const unsigned long long* x = &st[(w * 16 + it) * 8];
             const unsigned long long* nx = &st[(w * 16 + it + 1) * 8];
+            if (x[0] == 0 || nx[0] == 0) continue;  // a workgroup that left (gather team mode)
             for (int ph = 0; ph < 5; ++ph) span[ph] += (double)(x[ph + 1] - x[ph]);
             span[5] += (double)(nx[0] - x[5]);
             amin = x[4] < amin ? x[4] : amin;
