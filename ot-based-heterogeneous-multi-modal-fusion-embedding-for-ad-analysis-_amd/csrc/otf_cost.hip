@@ -230,7 +230,14 @@ template <typename TI> struct PrepSide {
 
 template <typename TI, bool SPLIT>
 __global__ __launch_bounds__(256) void split16_prep2_kernel(PrepSide<TI> A, PrepSide<TI> B, int d,
-                                                           int ldh, int vec) {
+                                                           int ldh, int vec, unsigned int* zero_word,
+                                                           float* one_word) {
+    // the cost kernel's running max (zeroed) and the fp32-storage unit (1.0), written here
+    // instead of two memset launches ahead of the cost kernel
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (zero_word) *zero_word = 0u;
+        if (one_word) *one_word = 1.0f;
+    }
     // lane handles 8 consecutive elements per 512-wide pass: 16-B (fp16) / 2 x 16-B
     // (fp32) loads when the rows allow it, 16-B image stores; h == nullptr: norms only
     // (the fp16 input is its own image)
@@ -722,7 +729,9 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
             const otf::PrepSide<float> A{(const float*)X, ldx, (int)n, Xh, Xl, xs, xx, mn};
             const otf::PrepSide<float> B{(const float*)Y, ldy, same ? 0 : (int)m, Yh, Yl, ys, yy,
                                          mn ? mn + 1 : nullptr};
-            otf::split16_prep2_kernel<float, true><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh, vec);
+            otf::split16_prep2_kernel<float, true><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh, vec,
+                                                                       (unsigned int*)cmax,
+                                                                       f16out ? nullptr : c_unit);
         } else {
             if (alias) {
                 Xh = (_Float16*)X;
@@ -735,7 +744,9 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
             const otf::PrepSide<_Float16> B{(const _Float16*)Y, ldy, same ? 0 : (int)m,
                                             alias ? nullptr : Yh, nullptr, ys, yy,
                                             mn ? mn + 1 : nullptr};
-            otf::split16_prep2_kernel<_Float16, false><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh, vec);
+            otf::split16_prep2_kernel<_Float16, false><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh, vec,
+                                                                           (unsigned int*)cmax,
+                                                                           f16out ? nullptr : c_unit);
         }
     }
     OTF_HIP(hipGetLastError());
@@ -748,10 +759,8 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
         otf::cost_store_scale_kernel<<<1, 1, 0, s>>>(mn, metric, small + 2, c_unit);
         OTF_HIP(hipGetLastError());
         store_scale = small + 2;
-    } else if (c_unit) {
-        OTF_HIP(hipMemsetD32Async((hipDeviceptr_t)c_unit, 0x3f800000u /* 1.0f */, 1, s));
     }
-    if (cmax) OTF_HIP(hipMemsetAsync(cmax, 0, sizeof(float), s));
+    // cmax = 0 and c_unit = 1 (fp32 storage) were written by the prep kernel
     // Tile choice by rounds of resident workgroups (two 128 x 128 per CU, one 256 x 256):
     // a round of 256 x 256 tiles took 1.8x a round of 128 x 128 ones at N = 4096
     // (68 vs 38 us), so big tiles win when they need fewer than 1 / 1.8 of the rounds

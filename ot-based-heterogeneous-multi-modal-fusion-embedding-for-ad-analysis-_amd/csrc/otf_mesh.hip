@@ -754,7 +754,7 @@ template <typename CT>
 hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                    double* errlog, hipStream_t s) {
+                    double* errlog, bool zeroed, hipStream_t s) {
     if (!mesh_supported(n, m) || !region) return hipErrorInvalidValue;
     const MeshShape sh = mesh_shape(n, m);
     if (sh.nrb * sh.ncb > device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
@@ -792,8 +792,10 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
     p.P = P_out;
     p.ldp = ldp;
     p.timeout_ticks = stall_ticks();
-    hipError_t e = hipMemsetAsync(region, 0, mesh_region_bytes(n, m), s);
-    if (e != hipSuccess) return e;
+    if (!zeroed) {  // else the Sinkhorn init kernel zeroed it
+        const hipError_t e = hipMemsetAsync(region, 0, mesh_region_bytes(n, m), s);
+        if (e != hipSuccess) return e;
+    }
     const int grid = sh.nrb * sh.ncb;
     if (P_out && P_dtype == OTF_F64) return launch_mesh_t<CT, double>(grid, p, s);
     return launch_mesh_t<CT, float>(grid, p, s);
@@ -801,9 +803,11 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
 
 template hipError_t run_mesh<float>(const float*, int64_t, int, int, const float*, const float*,
                                     const float*, const otf_sinkhorn_opts&, void*, float*, float*,
-                                    void*, int64_t, int, otf_sinkhorn_info*, double*, hipStream_t);
+                                    void*, int64_t, int, otf_sinkhorn_info*, double*, bool,
+                                    hipStream_t);
 template hipError_t run_mesh<_Float16>(const _Float16*, int64_t, int, int, const float*, const float*,
                                        const float*, const otf_sinkhorn_opts&, void*, float*, float*,
-                                       void*, int64_t, int, otf_sinkhorn_info*, double*, hipStream_t);
+                                       void*, int64_t, int, otf_sinkhorn_info*, double*, bool,
+                                       hipStream_t);
 
 }  // namespace otf

@@ -360,9 +360,11 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
 template <typename T>
 __global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, T* a_pad, T* b_pad,
                                T* cs, int cs_stride, T* u2, T* v2, int* cmin_key,
-                               otf_sinkhorn_info* info) {
+                               otf_sinkhorn_info* info, uint4* zero, int64_t zero_n) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int stride = gridDim.x * blockDim.x;
+    // a persistent engine's granule region (mesh), zeroed here instead of by a memset launch
+    for (int64_t j = t; j < zero_n; j += stride) zero[j] = make_uint4(0u, 0u, 0u, 0u);
     for (int j = t; j < m_pad; j += stride) {
         b_pad[j] = j < m ? b[j] : (T)0;
         cs[j] = cs[cs_stride + j] = cs[2 * cs_stride + j] = 0;
@@ -1698,10 +1700,12 @@ void sk_set_pass(SkArgs<T>& p, const SkSetup<T>& su, int pass) {
 
 template <typename T>
 int sk_init(const SkSetup<T>& su, const T* a, const T* b, int64_t n, int64_t m,
-            otf_sinkhorn_info* info, hipStream_t s) {
-    sk_init_kernel<T><<<64, 256, 0, s>>>(a, b, (int)n, (int)m, su.m_pad, (T*)su.w.a_pad,
-                                         (T*)su.w.b_pad, (T*)su.w.cs, (int)su.w.cs_stride,
-                                         (T*)su.w.u2, (T*)su.w.v2, su.w.cmin_key, info);
+            otf_sinkhorn_info* info, hipStream_t s, void* zero = nullptr, size_t zero_bytes = 0) {
+    const int grid = zero_bytes > (1u << 20) ? 256 : 64;
+    sk_init_kernel<T><<<grid, 256, 0, s>>>(a, b, (int)n, (int)m, su.m_pad, (T*)su.w.a_pad,
+                                           (T*)su.w.b_pad, (T*)su.w.cs, (int)su.w.cs_stride,
+                                           (T*)su.w.u2, (T*)su.w.v2, su.w.cmin_key, info,
+                                           (uint4*)zero, (int64_t)(zero_bytes / 16));
     OTF_HIP(hipGetLastError());
     return OTF_OK;
 }
@@ -1766,10 +1770,18 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     int rc = sk_prepare<T, CT>(a, b, C, n, m, ldc, o, info, ws, ws_bytes, su);
     if (rc != OTF_OK) return rc;
     double* errlog = errlog_user ? errlog_user : su.w.errlog;
-    rc = sk_init<T>(su, a, b, n, m, info, s);
+    const bool whole = o.n_total <= 0 || o.n_total == n;
+    // the mesh engine's region is zeroed by the init kernel (no memset launch)
+    bool mesh_pick = false;
+    if constexpr (sizeof(T) == 4)
+        mesh_pick = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && su.w.mesh_bytes > 0 &&
+                    mesh_supported(n, m) &&
+                    (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled() &&
+                                                     !(gather_supported<T>(n, m) && su.w.gather_bytes > 0)));
+    rc = sk_init<T>(su, a, b, n, m, info, s, mesh_pick ? su.w.mesh : nullptr,
+                    mesh_pick ? su.w.mesh_bytes : 0);
     if (rc != OTF_OK) return rc;
 
-    const bool whole = o.n_total <= 0 || o.n_total == n;
     // gather engine: small problems, one granule hop per iteration, no barrier (and
     // deterministic by construction)
     const bool gfits = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && gather_supported<T>(n, m) &&
@@ -1794,7 +1806,8 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         if (mfits && (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled()))) {
             const hipError_t e = run_mesh<CT>(C, ldc, (int)n, (int)m, (const float*)su.w.a_pad,
                                               (const float*)su.w.b_pad, cost_scale, o, su.w.mesh,
-                                              u_out, v_out, P_out, ldp, P_dtype, info, errlog, s);
+                                              u_out, v_out, P_out, ldp, P_dtype, info, errlog,
+                                              /*zeroed=*/mesh_pick, s);
             if (e == hipSuccess) return OTF_OK;
             (void)hipGetLastError();
             if (o.engine == OTF_ENGINE_MESH) return check_hip(e);

@@ -278,7 +278,8 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
     u = torch.empty(n, dtype=dt, device=dev)
     v = torch.empty(m, dtype=dt, device=dev)
     info = torch.empty(L.INFO_INT32S, dtype=torch.int32, device=dev)
-    errlog = torch.zeros(max_iter // max(check_every, 1) + 2, dtype=torch.float64, device=dev)
+    # written by the solve for every check it reports (info n_err): no zero fill needed
+    errlog = torch.empty(max_iter // max(check_every, 1) + 2, dtype=torch.float64, device=dev)
     if workspace is None:
         workspace = sinkhorn_workspace(n, m, dt, max_iter, dev)
     P = None
