@@ -76,7 +76,7 @@ def sharded_batch_feature_plan(mri_local: torch.Tensor, pet_local: torch.Tensor,
     a = torch.full((d,), 1.0 / d, dtype=torch.float64, device=M.device)
     b = torch.full((d2,), 1.0 / d2, dtype=torch.float64, device=M.device)
     res = ops.sinkhorn(a, b, M, float(eps), max_iter=numItermax, stop_thr=stopThr, flavor="pot",
-                       sync_every=50, want_plan=True)
+                       sync_every=0, want_plan=True)  # no host poll in the loop
     return res.plan, res
 
 
