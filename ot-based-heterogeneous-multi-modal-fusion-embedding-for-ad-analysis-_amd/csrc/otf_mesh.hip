@@ -140,15 +140,15 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     __shared__ int s_ep[5];
     int tid = threadIdx.x, lane = tid & 63;
     const int w = (int)threadIdx.x >> 6;
-    const bool lead = (blockIdx.x == 0 && tid == 0);
     unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
     const int nrb = p.nrb, ncb = p.ncb, CPR = p.cpr;
 
     // Tile of this workgroup.  XCC-local column path (p.xcc_local): every workgroup
     // registers on its XCC (the hardware id, not an assumed placement), one flat
-    // barrier, and when there are exactly ncb active XCCs holding exactly nrb workgroups
-    // each (N = 4096: 8 x 32, one workgroup per CU), column tile cb = the rank of this
-    // XCC and row block rb = the registration slot.  A column tile's hop A, reduce and
+    // barrier over the launch of 8 x nrb workgroups, and when ncb XCCs hold at least nrb
+    // registrants each (N = 4096: 8 x 32, one workgroup per CU), column tile cb = the
+    // rank of this XCC among them and row block rb = the registration slot (the surplus
+    // leaves).  A column tile's hop A, reduce and
     // hop B then stay inside one XCC's L2, which is the point of coherence for all its
     // CUs: plain stores (L1 is write-through, the line stays in L2) read by L1-bypassing
     // sc1 loads -- the single-L2 protocol; only the cross-XCC hops (row hop, error
@@ -165,21 +165,23 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             s_reg[0] = __hip_atomic_fetch_add(p.xreg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool ok = grid_barrier(p.xreg + 8 * 64, gridDim.x, deadline, p.timeout_ticks, &s_reg[3]);
         if (tid == 0) {
-            int good = ok ? 1 : 0, rank = 0, nact = 0;
+            // the first ncb XCCs (by id) holding >= nrb registrants are the column tiles;
+            // registrants beyond slot nrb - 1 and XCCs past the ncb-th leave
+            int good = ok ? 1 : 0, rank = -1, nq = 0;
             for (int x = 0; x < 8; ++x) {
                 const int c = load_agent(p.xreg + x * 64);
-                if (c > 0) {
-                    rank += x < xcd ? 1 : 0;
-                    ++nact;
-                    if (c != nrb) good = 0;
+                if (c >= nrb && nq < ncb) {
+                    if (x == xcd) rank = nq;
+                    ++nq;
                 }
             }
-            if (nact != ncb) good = 0;
+            if (nq < ncb) good = 0;
             s_reg[1] = good;
             s_reg[2] = rank;
         }
         __syncthreads();
         if (s_reg[1]) {
+            if (s_reg[2] < 0 || s_reg[0] >= nrb) return;  // a surplus workgroup of the launch
             rb = s_reg[0];
             cb = s_reg[2];
             xl = 1;
@@ -187,6 +189,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     }
     if (!xl) {
         const int bi = blockIdx.x;
+        if (bi >= nrb * ncb) return;  // the launch's surplus (XCC mode launches 8 x nrb)
         if (p.xcd_rows && (nrb & 7) == 0) {
             const int x = bi & 7, q = bi >> 3;
             cb = q % ncb;
@@ -196,6 +199,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             cb = bi % ncb;
         }
     }
+    const bool lead = (rb == 0 && cb == 0 && tid == 0);  // writes info and the error log
     const int row0 = rb * TR + w * R;
     const int col0 = cb * TC;
     const int ncols = p.m - col0 < TC ? p.m - col0 : TC;
@@ -796,7 +800,11 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
         const hipError_t e = hipMemsetAsync(region, 0, mesh_region_bytes(n, m), s);
         if (e != hipSuccess) return e;
     }
-    const int grid = sh.nrb * sh.ncb;
+    // XCC mode launches nrb workgroups per XCC (8 x nrb) so that every column tile can
+    // find a whole XCC of them even when ncb < 8; the surplus leaves after registration
+    int grid = sh.nrb * sh.ncb;
+    if (p.xcc_local && 8 * sh.nrb <= device_cu_count()) grid = 8 * sh.nrb;
+    else p.xcc_local = 0;
     if (P_out && P_dtype == OTF_F64) return launch_mesh_t<CT, double>(grid, p, s);
     return launch_mesh_t<CT, float>(grid, p, s);
 }

@@ -200,17 +200,19 @@ def test_mesh_unsupported_shapes_are_refused(dev):
         assert ops.sinkhorn(a, b, C, 0.1, max_iter=10).info()["engine_name"] != "mesh"
 
 
-def test_mesh_xcc_local_and_write_through_paths_agree_bitwise(dev, monkeypatch):
-    """Roles by XCC registration (column path inside one L2, plain stores) and by
-    blockIdx (every hop write-through) reduce in the same fixed order: identical bits."""
+@pytest.mark.parametrize("n,m", [(4096, 4096), (1000, 1500)])
+def test_mesh_xcc_local_and_write_through_paths_agree_bitwise(dev, monkeypatch, n, m):
+    """Roles by XCC registration (column path inside one L2, plain stores; 8 x nrb
+    workgroups launched, surplus leaves) and by blockIdx (every hop write-through) reduce
+    in the same fixed order: identical bits."""
     from otfuse import ops
-    n = m = 4096
     g = torch.Generator(device=dev).manual_seed(11)
     C = torch.rand(n, m, device=dev, generator=g)
     a = torch.full((n,), 1.0 / n, device=dev)
-    r1 = ops.sinkhorn(a, a, C, 0.05, max_iter=120, stop_thr=0.0, engine="mesh")
+    b = torch.full((m,), 1.0 / m, device=dev)
+    r1 = ops.sinkhorn(a, b, C, 0.05, max_iter=120, stop_thr=0.0, engine="mesh")
     monkeypatch.setenv("OTF_MESH_XCC", "0")
-    r0 = ops.sinkhorn(a, a, C, 0.05, max_iter=120, stop_thr=0.0, engine="mesh")
+    r0 = ops.sinkhorn(a, b, C, 0.05, max_iter=120, stop_thr=0.0, engine="mesh")
     assert r1.info()["engine_name"] == r0.info()["engine_name"] == "mesh"
     assert torch.equal(r0.plan, r1.plan) and torch.equal(r0.u, r1.u) and torch.equal(r0.v, r1.v)
 
