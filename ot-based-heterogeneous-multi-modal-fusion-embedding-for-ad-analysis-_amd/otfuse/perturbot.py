@@ -92,10 +92,12 @@ def fot_numpy(X1, X2, Ts, v1=None, v2=None, niter=10, algo="emd", reg=0, algo2="
     M = ops.feature_cost(Xd, Yd, Ts=torch.as_tensor(Ts, device=dev), weights="fot")
     res, _ = solve_ott(M, float(reg2))
     Tv = res.plan
-    cost = float((M * Tv).sum())
     d, d2 = M.shape
     Tv0 = 1.0 / (d * d2)
-    delta = float(torch.linalg.norm(Tv - Tv0))
+    # cost, delta and the finiteness test on the device, one host read
+    stats = torch.stack([(M * Tv).sum(), torch.linalg.norm(Tv - Tv0),
+                         torch.isfinite(Tv).all().to(Tv.dtype)]).cpu().tolist()
+    cost, delta, finite = float(stats[0]), float(stats[1]), stats[2] > 0.5
     costs = [cost]
     if verbose:
         print("Delta: {0}  Loss: {1}".format(delta, cost))
@@ -104,9 +106,9 @@ def fot_numpy(X1, X2, Ts, v1=None, v2=None, niter=10, algo="emd", reg=0, algo2="
         if verbose:
             print("Delta: {0}  Loss: {1}".format(0.0, cost))
             print("converged at iter ", 1)
-    Tv_np = Tv.cpu().numpy()
-    if not np.all(np.isfinite(Tv_np)):
+    if not finite:
         raise FloatingPointError("non-finite feature coupling")
+    Tv_np = ops.to_host(Tv)
     if log:
         return Tv_np, cost, {"cost": costs}
     return Tv_np, cost
@@ -155,7 +157,7 @@ def _eot(Xs, Xt, eps):
     reg_ot_cost = float((res.u * (1.0 / n)).sum() + (res.v * (1.0 / m)).sum())
     log = {"n_iters_outer": info["niter"] + 1, "converged": info["status"] == 1,
            "OT cost": reg_ot_cost, "time": time.time() - t0, "cost_time": cost_time}
-    return res.plan.cpu().numpy(), log
+    return ops.to_host(res.plan), log
 
 
 def get_coupling_eot_ott(data, eps: float = 5e-3):
@@ -459,8 +461,8 @@ def cotl_sinkhorn(X_dict, Y_dict, eps: float = 5e-3, eps2: float | None = None,
             break
     Ts_np = {k: Ts[k].cpu().numpy() for k in labels}
     if log:
-        return Ts_np, Tv.cpu().numpy(), cost, {"cost": costs}
-    return Ts_np, Tv.cpu().numpy(), cost
+        return Ts_np, ops.to_host(Tv), cost, {"cost": costs}
+    return Ts_np, ops.to_host(Tv), cost
 
 
 def get_coupling_cotl_sinkhorn(data, eps: float = 5e-3, eps2: float | None = None):

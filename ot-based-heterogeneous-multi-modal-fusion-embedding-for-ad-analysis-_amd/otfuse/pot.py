@@ -103,7 +103,7 @@ def sinkhorn(a, b, M, reg: float, method: str = "sinkhorn", numItermax: int = 10
     if verbose:
         for k, e in enumerate(info["err"]):
             print("{:5d}|{:8e}|".format(10 * k, e))
-    P = res.plan if is_torch else res.plan.cpu().numpy()
+    P = res.plan if is_torch else ops.to_host(res.plan)
     if not log:
         return P
     u = res.u if is_torch else res.u.cpu().numpy()
@@ -242,7 +242,7 @@ def get_feature_coupling_pot(
     info = res.info()
     if info["status"] == 3:
         warnings.warn("Warning: numerical errors at iteration %d" % info["break_iter"])
-    return res.plan.cpu().numpy(), {}
+    return ops.to_host(res.plan), {}
 
 
 def get_coupling_gromov_pot(
