@@ -85,6 +85,10 @@ struct SkMeshArgs {
 };
 
 using I4 = __attribute__((ext_vector_type(4))) int;
+// s_sleep units between polls of a granule that has not arrived (64 clocks each)
+#ifndef OTF_MESH_SLEEP
+#define OTF_MESH_SLEEP 1
+#endif
 using F2 = __attribute__((ext_vector_type(2))) float;
 
 __device__ __forceinline__ I4 chunk2(float v0, float v1, int tag) {
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                 if ((pend & (1u << k)) && chunk_at(x[k], (unsigned)e)) pend &= ~(1u << k);
             if (!__any(pend != 0)) break;
             if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
         }
         T s0 = 0, s1 = 0;
         int fl = 0;
@@ -383,7 +387,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                     x = gload(rs, off);
                     if (chunk_at(x, (unsigned)e)) break;
                     if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; break; }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
                 }
                 fl |= x[1] & 1;
                 const T s0 = chunk_v0(x), s1 = chunk_v1(x);
@@ -402,7 +406,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                     x = gload(rs, off);
                     if (chunk_at(x, (unsigned)e)) break;
                     if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; break; }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
                 }
                 ep = chunk_v0(x);
             }
@@ -428,7 +432,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                 x = gload(rs, off);
                 if (chunk_at(x, (unsigned)er)) break;
                 if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
             }
             ev = chunk_v0(x);
         }
@@ -531,7 +535,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                     x = gload(rs, off);
                     if (chunk_at(x, (unsigned)e)) break;
                     if (__builtin_amdgcn_s_memrealtime() > deadline) { stall = 1; break; }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
                 }
             }
             T t0 = act ? chunk_v0(x) : (T)0, t1 = act ? chunk_v1(x) : (T)0;
