@@ -184,6 +184,14 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             s_reg[2] = rank;
         }
         __syncthreads();
+        // a registration that timed out (the grid was not co-resident in time) must not
+        // go on with blockIdx roles while the workgroups that did see the barrier complete
+        // take XCC roles: it reports the stall and leaves; the rest then stall on its
+        // missing data and report it too -- never a plan from mixed roles
+        if (!s_reg[3]) {
+            if (tid == 0) store_wt(&p.info->stalled, 1);
+            return;
+        }
         if (s_reg[1]) {
             if (s_reg[2] < 0 || s_reg[0] >= nrb) return;  // a surplus workgroup of the launch
             rb = s_reg[0];

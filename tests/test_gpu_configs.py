@@ -212,7 +212,8 @@ def test_eot_and_leot_dropins_vs_oracle(orc, dev):
         assert nrel(Td[k], Pr) < 1e-9
 
 
-def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch):
+@pytest.mark.parametrize("engine", ["tiled", "mesh"])
+def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch, engine):
     """Two persistent solves (tiled engine, a full grid each) launched together on two
     streams cannot both be co-resident: each must either complete with the right plan
     or report the stall cleanly (OtfError from info(), status timeout) -- never hang
@@ -229,7 +230,7 @@ def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch)
     outs = []
     for s in (s1, s2):
         with torch.cuda.stream(s):
-            outs.append(ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine="tiled"))
+            outs.append(ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine=engine))
     torch.cuda.synchronize()
     for res in outs:
         try:
@@ -239,11 +240,13 @@ def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch)
         assert info["status_name"] == "max_iter"
         assert (res.plan - ref).abs().max() / ref.abs().max() < 1e-5
     # the device is healthy afterwards
-    res = ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine="tiled")
+    res = ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine=engine)
     assert res.info()["status_name"] == "max_iter"
+    assert (res.plan - ref).abs().max() / ref.abs().max() < 1e-5
 
 
 @pytest.mark.parametrize("engine,n,m,dt,iters", [("tiled", 4096, 4096, torch.float32, 20000),
+                                                 ("mesh", 4096, 4096, torch.float32, 20000),
                                                  ("resident", 512, 512, torch.float64, 30000),
                                                  ("gather", 512, 512, torch.float64, 60000),
                                                  ("sweep", 1024, 8192, torch.float32, 20000)])
