@@ -126,3 +126,19 @@ def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "_lib", None)
     with pytest.raises(L.OtfError):
         L.lib()
+
+
+def test_engine_enum_matches_header():
+    """The Python engine table (otfuse._lib.ENGINES) and the header's otf_engine enum agree,
+    including the gather and mesh engines (host-only: parses include/otfuse.h)."""
+    import os
+    import re
+    from otfuse import _lib as L
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "include", "otfuse.h")).read()
+    body = hdr[hdr.index("typedef enum {\n    OTF_ENGINE_AUTO"):]
+    body = body[:body.index("} otf_engine;")]
+    enum = {m.group(1).lower(): int(m.group(2))
+            for m in re.finditer(r"OTF_ENGINE_([A-Z]+)\s*=\s*(\d+)", body)}
+    assert enum == L.ENGINES
+    assert {"gather", "mesh"} <= set(enum)
