@@ -102,8 +102,10 @@ int run(const int N, const char eng, const int iters, const double reg) {
             if (x[0] == 0 || nx[0] == 0) continue;  // a workgroup that left (gather team mode)
             for (int ph = 0; ph < 5; ++ph) span[ph] += (double)(x[ph + 1] - x[ph]);
             span[5] += (double)(nx[0] - x[5]);
-            amin = x[4] < amin ? x[4] : amin;
-            amax = x[4] > amax ? x[4] : amax;
+            if (x[4] != 0) {
+                amin = x[4] < amin ? x[4] : amin;
+                amax = x[4] > amax ? x[4] : amax;
+            }
             ++cnt;
         }
         arrive_spread += (double)(amax - amin);
