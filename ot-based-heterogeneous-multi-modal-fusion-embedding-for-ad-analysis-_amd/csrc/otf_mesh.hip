@@ -1,5 +1,6 @@
-// otf_mesh.hip — Sinkhorn on a mesh of register-resident K tiles with no device-wide
-// barrier and no atomics (OTF_ENGINE_MESH), POT flavour, float32 compute.
+// otf_mesh.hip — Sinkhorn on a mesh of register-resident K tiles with no per-iteration
+// device-wide barrier and no float atomics (OTF_ENGINE_MESH), POT flavour, float32
+// compute.  (One grid barrier per solve: the XCC registration before the first iteration.)
 //
 // Replaces ot.sinkhorn (POT 0.9.6 sinkhorn_knopp, MRI_PET_OT_nojax.py:143 /
 // perturbot/perturbot/match/utils.py:6-115) for the coupled problems whose K fits the
