@@ -270,8 +270,14 @@ def main():
     if rank == 0 and not args.no_batch_ot:
         out["batch_ot_per_step"] = batch_ot_leg(dev, world == 1 and not args.no_cpu_baseline)
     if world > 1 or args.multi_legs:
-        out["sharded_config5"] = sharded_config5_leg(dev, world)
-        out["config3_epoch_chain"] = config3_leg(dev, world)
+        # the sharded legs are extra evidence beside the headline: a failure that every
+        # rank hits alike (same exception on every rank, so the collectives stay in step)
+        # is recorded instead of costing the run its JSON line
+        for key, leg in (("sharded_config5", sharded_config5_leg), ("config3_epoch_chain", config3_leg)):
+            try:
+                out[key] = leg(dev, world)
+            except Exception as e:  # noqa: BLE001
+                out[key] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(X_np, Y_np, N, iters, eps, args.cpu_threads)
         out["vs_cpu"] = value / out["cpu_baseline"]["value"]
