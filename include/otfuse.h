@@ -295,7 +295,7 @@ enum { OTF_RED_SUM = 0, OTF_RED_MAX = 1 };
 int otf_comm_unique_id(void* id_out);
 int otf_comm_init(otf_comm** comm_out, const void* id, int32_t nranks, int32_t rank);
 int otf_comm_destroy(otf_comm* comm);
-/* In-place all-reduce of count elements (dtype OTF_F32/F64/F16, op OTF_RED_*).     */
+/* In-place all-reduce of count elements (dtype OTF_F32/F64/F16/BF16, op OTF_RED_*). */
 int otf_comm_all_reduce(void* buf, int64_t count, int32_t dtype, int32_t op, otf_comm* comm,
                         otf_stream_t stream);
 /* recv = concat over ranks of send (count_per_rank elements each), rank order.     */

@@ -61,12 +61,14 @@ Rccl& rccl() {
     return r;
 }
 
-// otf_dtype -> ncclDataType_t (rccl.h: ncclFloat16 6, ncclFloat32 7, ncclFloat64 8)
+// otf_dtype -> ncclDataType_t (rccl.h: ncclFloat16 6, ncclFloat32 7, ncclFloat64 8,
+// ncclBfloat16 9; bf16: the config-4 encoder outputs, BASELINE.json configs[3])
 int nccl_dtype(int32_t dt) {
     switch (dt) {
         case OTF_F32: return 7;
         case OTF_F64: return 8;
         case OTF_F16: return 6;
+        case OTF_BF16: return 9;
         default: return -1;
     }
 }

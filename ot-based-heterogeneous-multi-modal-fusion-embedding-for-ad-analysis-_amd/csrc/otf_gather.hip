@@ -155,7 +155,11 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
                         }
                     }
                     if (__builtin_amdgcn_s_memrealtime() > deadline) {
+                        // no XCC team ever claimed the solve (a slot already left, or
+                        // another persistent grid holds the CUs): report the stall, or
+                        // the untouched u / v / plan would read as a finished solve
                         keep = 0;
+                        store_wt(&p.info->stalled, 1);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
@@ -525,6 +529,21 @@ hipError_t launch_gather_q(int grid, SkGatherArgs<T>& p, hipStream_t s) {
     return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
 }
 
+// co-resident 512-thread workgroups per CU of the instance launch_gather picks (0 on error)
+template <typename T, typename CT, typename TP>
+int gather_per_cu_t(int nwg) {
+    const void* k = nwg <= 4   ? (const void*)sk_gather_kernel<T, CT, TP, 4>
+                    : nwg <= 8 ? (const void*)sk_gather_kernel<T, CT, TP, 8>
+                               : (const void*)sk_gather_kernel<T, CT, TP, 16>;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0) != hipSuccess) return 0;
+    return per_cu;
+}
+template <typename T, typename CT>
+int gather_per_cu(bool plan_f64, int nwg) {
+    return plan_f64 ? gather_per_cu_t<T, CT, double>(nwg) : gather_per_cu_t<T, CT, float>(nwg);
+}
+
 template <typename T, typename CT, typename TP>
 hipError_t launch_gather(int grid, SkGatherArgs<T>& p, hipStream_t s) {
     // NQ follows the solve's workgroups (p.nwg), not the launch (8 x nwg in team mode)
@@ -588,6 +607,11 @@ hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, co
     const int grid = (int)gather_grid<T>(n);
     p.nwg = grid;
     p.team_mode = gather_team_mode();
+    // team mode needs 8 x grid co-resident workgroups; on a smaller (or partitioned)
+    // device fall back to one workgroup per row tile anywhere on the chip, as the mesh
+    // engine does, instead of refusing the shape
+    if (p.team_mode && 8 * grid > gather_per_cu<T, CT>(P_out && P_dtype == OTF_F64, grid) * device_cu_count())
+        p.team_mode = 0;
     const int launch = p.team_mode ? 8 * grid : grid;
     if (P_out && P_dtype == OTF_F64) return launch_gather<T, CT, double>(launch, p, s);
     return launch_gather<T, CT, float>(launch, p, s);

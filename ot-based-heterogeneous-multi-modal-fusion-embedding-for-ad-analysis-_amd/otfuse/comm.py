@@ -17,6 +17,10 @@ import torch.distributed as dist
 from . import _lib as L
 from . import ops
 
+# element types the RCCL collectives take (bf16: the config-4 encoder outputs)
+_COMM_DT = {torch.float32: L.OTF_F32, torch.float64: L.OTF_F64, torch.float16: L.OTF_F16,
+            torch.bfloat16: L.OTF_BF16}
+
 
 class Communicator:
     """An RCCL communicator of ``nranks`` processes (``group``'s ranks, or one rank)."""
@@ -51,12 +55,12 @@ class Communicator:
         self.handle = None
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-        """In place; float32 / float64 / float16, contiguous."""
+        """In place; float32 / float64 / float16 / bfloat16, contiguous."""
         ops._dev(t, "t")
-        if not t.is_contiguous() or t.dtype not in ops._DT:
-            raise TypeError("all_reduce: contiguous float16/32/64 tensors only")
+        if not t.is_contiguous() or t.dtype not in _COMM_DT:
+            raise TypeError("all_reduce: contiguous float16/bfloat16/32/64 tensors only")
         red = {"sum": L.OTF_RED_SUM, "max": L.OTF_RED_MAX}[op]
-        L.check(L.lib().otf_comm_all_reduce(t.data_ptr(), t.numel(), ops._DT[t.dtype], red, self.handle,
+        L.check(L.lib().otf_comm_all_reduce(t.data_ptr(), t.numel(), _COMM_DT[t.dtype], red, self.handle,
                                             L.stream_handle(t.device)), "otf_comm_all_reduce")
         return t
 
@@ -64,11 +68,27 @@ class Communicator:
         """Concatenation of every rank's equally-shaped ``t`` along dim 0, rank order."""
         ops._dev(t, "t")
         t = t.contiguous()
-        if t.dtype not in ops._DT:
-            raise TypeError("all_gather: float16/32/64 tensors only")
+        if t.dtype not in _COMM_DT:
+            raise TypeError("all_gather: float16/bfloat16/32/64 tensors only")
         out = torch.empty((self.nranks * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
                           device=t.device)
-        L.check(L.lib().otf_comm_all_gather(t.data_ptr(), out.data_ptr(), t.numel(), ops._DT[t.dtype],
+        L.check(L.lib().otf_comm_all_gather(t.data_ptr(), out.data_ptr(), t.numel(), _COMM_DT[t.dtype],
                                             self.handle, L.stream_handle(t.device)),
                 "otf_comm_all_gather")
         return out
+
+    def all_gather_rows(self, t: torch.Tensor) -> tuple[torch.Tensor, list[int]]:
+        """Concatenation of every rank's (n_r, ...) ``t`` along dim 0 in rank order when
+        the n_r differ: the row counts are exchanged first (one tiny all-gather and one
+        host read), the shards padded to the largest for the collective and trimmed
+        after.  Returns (rows, [n_0, ..., n_{R-1}])."""
+        ops._dev(t, "t")
+        n = torch.tensor([float(t.shape[0])], dtype=torch.float64, device=t.device)
+        sizes = [int(x) for x in self.all_gather(n).cpu().tolist()]
+        nmax = max(sizes)
+        if all(s == nmax for s in sizes):
+            return self.all_gather(t), sizes
+        pad = t.new_zeros((nmax,) + tuple(t.shape[1:]))
+        pad[: t.shape[0]] = t
+        out = self.all_gather(pad)
+        return torch.cat([out[r * nmax: r * nmax + sizes[r]] for r in range(self.nranks)]), sizes

@@ -211,8 +211,17 @@ def coupled_solve_sharded(X_local: torch.Tensor, Y_local: torch.Tensor, reg: flo
     all-reduce(MAX) for scale_cost="max_cost", then the row-sharded Sinkhorn with
     uniform marginals.  Returns (SinkhornResult of this rank's rows, n_total)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    if comm is not None and world > 1:   # equal shards: one RCCL all-gather on the stream
-        Y_all = comm.all_gather(Y_local)
+    x_sizes = None
+    if comm is not None and comm.nranks > 1:
+        # shard sizes may differ (a ragged last shard): the row counts of X and Y are
+        # exchanged through the communicator, never assumed equal -- a wrong n_total
+        # would make a = 1/n_total sum to != 1 and a fixed-count all-gather would read
+        # garbage or hang
+        Y_all, _ = comm.all_gather_rows(Y_local)
+        nx = torch.tensor([float(X_local.shape[0])], dtype=torch.float64, device=X_local.device)
+        x_sizes = [int(x) for x in comm.all_gather(nx).cpu().tolist()]
+    elif comm is not None:
+        Y_all = Y_local
     else:
         Y_all = all_gather_rows(Y_local, group) if world > 1 else Y_local
     C, cmax, unit = ops.pairwise_cost_ex(X_local, Y_all, zero_diag=False, out_dtype=cost_dtype)
@@ -220,7 +229,7 @@ def coupled_solve_sharded(X_local: torch.Tensor, Y_local: torch.Tensor, reg: flo
     gmax = cmax * unit
     if comm is not None:
         comm.all_reduce(gmax, op="max")
-        n_total = X_local.shape[0] * comm.nranks
+        n_total = sum(x_sizes) if x_sizes is not None else X_local.shape[0]
     else:
         n = torch.tensor([X_local.shape[0]], dtype=torch.int64, device=X_local.device)
         if world > 1:

@@ -108,7 +108,10 @@ def ot_alignment_loss(mri_fused: torch.Tensor, pet_fused: torch.Tensor,
         plan, res = batch_feature_plan(mri_fused, pet_fused, eps, numItermax, stopThr)
         info = res.info_dev
         from . import _lib as L
-        ok = (info[3] != L.SK_TIMEOUT) & (info[7] == 0)
+        # a finished solve: final status written (not running / timeout), stop set,
+        # no stalled workgroup
+        ok = ((info[3] != L.SK_TIMEOUT) & (info[3] != L.SK_RUNNING) & (info[0] != 0)
+              & (info[7] == 0))
         ot_loss, ot_mri_from_pet, T = _OTAlignLoss.apply(mri_fused, pet_fused, plan, ok, True)
     else:
         ot_loss, ot_mri_from_pet, T = _OTAlignLoss.apply(mri_fused, pet_fused, T_feature_pet2mri,

@@ -246,6 +246,11 @@ class SinkhornResult:
             if d["status"] == L.SK_TIMEOUT or d["stalled"]:
                 raise L.OtfError("persistent Sinkhorn: a device-wide barrier made no progress "
                                  "(grid not co-resident?); results are invalid")
+            if d["status"] == L.SK_RUNNING or not d["stop"]:
+                # every engine writes a final status and stop = 1; a solve that left
+                # them untouched never ran to its end (u, v, plan are uninitialised)
+                raise L.OtfError("Sinkhorn: the solve reported no final status; results are "
+                                 "invalid")
             d["err"] = self.errlog_dev[: max(d["n_err"], 0)].cpu().tolist()
             self._info = d
         return self._info

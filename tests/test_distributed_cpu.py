@@ -137,3 +137,81 @@ def test_row_sharded_sinkhorn_protocol_world2(tmp_path):
     world = 2
     mp.spawn(_sharded_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     assert all((tmp_path / f"sharded{r}").exists() for r in range(world))
+
+
+class GlooComm:
+    """Stand-in for otfuse.comm.Communicator over gloo (CPU): same all_gather /
+    all_reduce contract, so coupled_solve_sharded's communicator path runs here."""
+
+    def __init__(self):
+        self.rank, self.nranks = dist.get_rank(), dist.get_world_size()
+
+    def all_gather(self, t):
+        t = t.contiguous()
+        out = t.new_empty((self.nranks * t.shape[0],) + tuple(t.shape[1:]))
+        dist.all_gather_into_tensor(out, t)
+        return out
+
+    def all_reduce(self, t, op="sum"):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
+        return t
+
+
+def _coupled_worker(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as orc
+    import otfuse.comm as CM
+    import otfuse.distributed as D
+    D.ops._dev = lambda t, name: t          # CPU tensors stand in for device tensors
+    GlooComm.all_gather_rows = CM.Communicator.all_gather_rows
+
+    def cost_ex(X, Y, zero_diag=False, out_dtype=None):
+        C = torch.from_numpy(((X.double().numpy()[:, None, :] - Y.double().numpy()[None]) ** 2).sum(-1))
+        return C, C.max().reshape(1), torch.ones(1, dtype=torch.float64)
+
+    class Passes(NumpyPasses):
+        def __init__(self, a_local, b, C_local, reg, max_iter, stop_thr, cost_scale, n_total,
+                     *args):
+            super().__init__(a_local.double(), b.double(), C_local / cost_scale, reg, max_iter,
+                             stop_thr, None, n_total)
+            self.max_iter = max_iter
+
+        def solve_with_comm(self, comm, want_plan=True, plan_dtype=None):
+            for p in range(self.max_iter + 1):
+                comm.all_reduce(self.run_pass(p))
+            return self.finish()
+
+    D.ops.pairwise_cost_ex = cost_ex
+    D.DevicePasses = Passes
+    rng = np.random.default_rng(11)
+    rows_x, rows_y = [5, 9], [7, 4]       # unequal shards on both sides
+    X = rng.random((sum(rows_x), 3))
+    Y = rng.random((sum(rows_y), 3))
+    sx = slice(sum(rows_x[:rank]), sum(rows_x[:rank + 1]))
+    sy = slice(sum(rows_y[:rank]), sum(rows_y[:rank + 1]))
+    P_local, n_total = D.coupled_solve_sharded(torch.from_numpy(X[sx]), torch.from_numpy(Y[sy]),
+                                               0.3, max_iter=20, comm=GlooComm())
+    assert n_total == sum(rows_x)
+    C = ((X[:, None, :] - Y[None]) ** 2).sum(-1)
+    a = np.full(len(X), 1.0 / len(X))
+    b = np.full(len(Y), 1.0 / len(Y))
+    P_ref, *_ = orc.sinkhorn_knopp(a, b, C / C.max(), 0.3, 20, 0.0)
+    # a, b are float32 in coupled_solve_sharded; a wrong n_total would be an O(1) error
+    np.testing.assert_allclose(P_local, P_ref[sx], rtol=1e-6, atol=1e-12)
+    open(os.path.join(out_dir, f"coupled{rank}"), "w").write("ok")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_coupled_solve_unequal_shards_through_communicator_world2(tmp_path):
+    """with a communicator, unequal shard sizes must give n_total = sum of
+    the rows (a sums to 1) and a ragged all-gather of Y, matching the single solve."""
+    world = 2
+    mp.spawn(_coupled_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert all((tmp_path / f"coupled{r}").exists() for r in range(world))
