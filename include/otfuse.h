@@ -18,6 +18,8 @@
  *                          (POT sinkhorn_knopp; vendored twin perturbot/perturbot/match/utils.py:6-115)
  *                          and OTT linear.solve(Geometry(M, eps, "max_cost"))  perturbot/perturbot/match/fot.py:128-134
  *   otf_plan_postprocess   NaN->1e-8 + row normalisation            MRI_PET_OT_nojax.py:702-715
+ *   otf_cosine_align       cosine_loss + gradients                   MRI_PET_OT_nojax.py:552-560,721-725
+ *   otf_ot_align_backward  backward of the apply + loss scaling      MRI_PET_OT_nojax.py:718-721
  *   otf_gemm_f32           ot_mri_from_pet = pet_fused @ T^T         MRI_PET_OT_nojax.py:718,
  *                                                                    MRI_PET_OT_OT_per_epoch_attn.py:728
  *
@@ -329,6 +331,27 @@ int otf_plan_postprocess_apply(const void* T, int64_t d, int64_t d2, int64_t ldt
                                float nan_fill, int32_t rownorm, const float* Z, int64_t ldz,
                                int64_t B, float* out, int64_t ldo, float* Tn, int64_t ldtn,
                                otf_stream_t stream);
+
+/* The training-time alignment loss of one batch and its gradients, one launch
+ * (cosine_loss MRI_PET_OT_nojax.py:552-560 applied at :721, NaN -> 0 at :724-725):
+ * loss = 1 - mean_b cos(normalize(X_b), normalize(Y_b)) with torch's normalize /
+ * cosine_similarity clamps; gx = dloss/dX, gy = dloss/dY (B x d float32).  X is
+ * x_dtype OTF_F32 / OTF_BF16 / OTF_F16 (the encoder output as stored), Y float32.
+ * keep = (ok == NULL || *ok) && loss finite; when keep is 0 the loss and both
+ * gradients are exact zeros.  keep_out (device uint8, nullable) receives keep.
+ * B <= 1024.                                                                      */
+int otf_cosine_align(const void* X, int64_t ldx, int32_t x_dtype, const float* Y, int64_t ldy,
+                     int64_t B, int64_t d, const uint8_t* ok, float* loss, float* gx, int64_t ldgx,
+                     float* gy, int64_t ldgy, uint8_t* keep_out, otf_stream_t stream);
+
+/* Backward of ot_mri_from_pet = pet @ Tn^T under the alignment loss, one launch:
+ * g_pet = (g_loss * gy + g_ot) @ Tn (B x d2), g_mri = g_loss * gx (B x d).  g_loss
+ * (device float), g_ot (B x d, ldgo) and keep (device uint8) are nullable; without
+ * g_ot and with *keep == 0, g_pet is written as zeros (Tn may hold NaN).          */
+int otf_ot_align_backward(const float* gx, int64_t ldgx, const float* gy, int64_t ldgy,
+                          const float* g_ot, int64_t ldgo, const float* g_loss, const uint8_t* keep,
+                          const float* Tn, int64_t ldt, int64_t B, int64_t d, int64_t d2, float* g_mri,
+                          int64_t ldm, float* g_pet, int64_t ldp, otf_stream_t stream);
 
 /* out (M x N, ldo) = alpha * op(A) op(B) (+ beta * out), float32, where
  * op(A)_{ik} = A[i*sa0 + k*sa1] and op(B)_{kj} = B[k*sb0 + j*sb1]: the plan

@@ -160,6 +160,83 @@ template <typename T, int R> __device__ __forceinline__ void wave_sum_multi(T (&
     wave_sum_from<T, (R > 1 ? R : 1)>(x[0]);
 }
 
+// ---- Row totals with the cheap exchanges first ---------------------------------
+// 32-bit words of a float / double through one lane exchange
+template <typename T, typename F> __device__ __forceinline__ T map_words(T x, F f) {
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, f(__builtin_bit_cast(unsigned, x)));
+    } else {
+        const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+        const unsigned lo = f((unsigned)b), hi = f((unsigned)(b >> 32));
+        return __builtin_bit_cast(T, ((unsigned long long)hi << 32) | lo);
+    }
+}
+// x of another lane by a DPP control: quad_perm 0xB1 (^1), 0x4E (^2), row_half_mirror
+// 0x141 (lane i <-> 7 - i within its 8), row_mirror 0x140 (i <-> 15 - i within its 16)
+template <int CTRL, typename T> __device__ __forceinline__ T dpp_lane(T x) {
+    return map_words(x, [](unsigned w) { return (unsigned)__builtin_amdgcn_update_dpp(0u, w, CTRL, 0xF, 0xF, false); });
+}
+// v_permlane32_swap / v_permlane16_swap of (a, b), then the sum of the two results:
+// lanes of the lower half (row of 16) end with their a plus the partner half's a, lanes
+// of the upper half with their b plus the partner's b -- one keep / send exchange of a
+// halving butterfly in two instructions per 32-bit word and one add
+template <int O, typename T> __device__ __forceinline__ T swap_sum(T a, T b) {
+    static_assert(O == 16 || O == 32, "swap offset");
+    if constexpr (sizeof(T) == 4) {
+        const auto r = O == 32 ? __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b), false, false)
+                               : __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b), false, false);
+        return __builtin_bit_cast(T, (unsigned)r[0]) + __builtin_bit_cast(T, (unsigned)r[1]);
+    } else {
+        const unsigned long long ab = __builtin_bit_cast(unsigned long long, a);
+        const unsigned long long bb = __builtin_bit_cast(unsigned long long, b);
+        const auto lo = O == 32 ? __builtin_amdgcn_permlane32_swap((unsigned)ab, (unsigned)bb, false, false)
+                                : __builtin_amdgcn_permlane16_swap((unsigned)ab, (unsigned)bb, false, false);
+        const auto hi = O == 32 ? __builtin_amdgcn_permlane32_swap((unsigned)(ab >> 32), (unsigned)(bb >> 32), false, false)
+                                : __builtin_amdgcn_permlane16_swap((unsigned)(ab >> 32), (unsigned)(bb >> 32), false, false);
+        const T x = __builtin_bit_cast(T, ((unsigned long long)(unsigned)hi[0] << 32) | (unsigned)lo[0]);
+        const T y = __builtin_bit_cast(T, ((unsigned long long)(unsigned)hi[1] << 32) | (unsigned)lo[1]);
+        return x + y;
+    }
+}
+// Wave totals of R = 8 or 16 per-lane row partials.  A halving butterfly that spends
+// its many-value levels on the cheap exchanges -- lane bits 5 and 4 by the permlane
+// swaps (two instructions per pair), bit 3 (and for R = 16 bit 2) by row_mirror /
+// row_half_mirror with a keep / send select -- and sums the one remaining value over
+// the lanes still to be covered (half mirror, quad ^2, quad ^1).  A mirror's partner
+// also differs in the low bits, which the later steps cover, so every step adds two
+// disjoint lane sets and every lane that ends with a row holds bitwise the same sum.
+// Lane L ends with the total of row L >> (6 - log2 R).  (The generic bits-0-first
+// order needs two DPP moves and a select per bit-2 / bit-3 exchange: ~75 VALU for
+// R = 16 in float against ~35 here.)
+template <typename T, int R>
+__device__ __forceinline__ T wave_row_totals(const T (&x)[R], int lane) {
+    static_assert(R == 8 || R == 16, "8 or 16 rows per wave");
+    T y[R / 2], z[R / 4];
+#pragma unroll
+    for (int i = 0; i < R / 2; ++i) y[i] = swap_sum<32>(x[i], x[i + R / 2]);
+#pragma unroll
+    for (int i = 0; i < R / 4; ++i) z[i] = swap_sum<16>(y[i], y[i + R / 4]);
+    const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0;
+    T t;
+    if constexpr (R == 16) {
+        T w2[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const T send = b3 ? z[i] : z[i + 2], keep = b3 ? z[i + 2] : z[i];
+            w2[i] = keep + dpp_lane<0x140>(send);
+        }
+        const T send = b2 ? w2[0] : w2[1], keep = b2 ? w2[1] : w2[0];
+        t = keep + dpp_lane<0x141>(send);
+    } else {
+        const T send = b3 ? z[0] : z[1], keep = b3 ? z[1] : z[0];
+        t = keep + dpp_lane<0x140>(send);
+        t += dpp_lane<0x141>(t);
+    }
+    t += dpp_lane<0xB1>(t);
+    t += dpp_lane<0x4E>(t);
+    return t;
+}
+
 // Block-wide sum of R values per thread.  `red` is LDS of >= (nwaves + 1) * R
 // elements.  Deterministic (fixed order), result broadcast to every thread.
 template <typename T, int R>

@@ -101,7 +101,10 @@ template <typename T> __device__ __forceinline__ I4 make_chunk(const T (&v)[Gath
 
 // NQ: producers polled per pass, the grid rounded up to 4 / 8 / 16 (surplus slots
 // re-read the last producer, so every load is unconditional and in flight together).
-template <typename T, typename CT, typename TP, int NQ>
+// SNWG: the row tiles compiled in (0 = from the arguments): a compiled-in shape is
+// SNWG whole row tiles x all C columns (BASELINE config 2: 512 x 512 float64 = 8 tiles),
+// so every bound test and derived count folds away.
+template <typename T, typename CT, typename TP, int NQ, int SNWG>
 __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
     using Cf = GatherCfg<T>;
     constexpr int G = Cf::G, VEC = Cf::VEC, R = Cf::RW, NW = Cf::NW, TR = Cf::TR;
@@ -111,7 +114,6 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
     __shared__ __attribute__((aligned(16))) T colbuf[NW][Cf::C];
     __shared__ __attribute__((aligned(16))) T vcur[Cf::C];      // v = b / (gathered K^T u)
     __shared__ __attribute__((aligned(16))) T vhist[2][Cf::C];  // v by iteration parity
-    __shared__ T urow[NW][R];
     __shared__ T uhist[2][TR];
     __shared__ T red[17 + 17];
     // workgroup-wide flags without a reduction: a raised flag is the EPOCH written by any
@@ -120,7 +122,11 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
     // rows; [1..3] gather: break flagged by a producer, stall, break in v.
     __shared__ int s_ep[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int nwg = p.nwg;
+    constexpr bool FULL = SNWG != 0;
+    const int nwg = FULL ? SNWG : p.nwg;
+    const int n_ = FULL ? SNWG * TR : p.n, m_ = FULL ? Cf::C : p.m;
+    auto row_in = [&](int r) -> bool { return FULL || r < n_; };
+    auto col_in = [&](int c) -> bool { return FULL || c < m_; };
     unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
     // Team mode: the launch has 8 x nwg workgroups; each registers on its hardware XCC
     // and the first XCC whose first nwg registrants are all resident claims the solve,
@@ -187,9 +193,9 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const int c0 = (lane + kWave * g) * VEC;
-        colc[g] = c0 < p.m ? c0 : 0;
+        colc[g] = col_in(c0) ? c0 : 0;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) cok[g][k] = c0 + k < p.m;
+        for (int k = 0; k < VEC; ++k) cok[g][k] = col_in(c0 + k);
     }
     // ---- K for this wave's rows x this lane's 8 columns, once
     T kv[R][G][VEC];
@@ -197,7 +203,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
         const CT* crow = (const CT*)p.C + (int64_t)row0 * p.ldc;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const CT* src = (row0 + r < p.n) ? crow : (const CT*)p.C;
+            const CT* src = row_in(row0 + r) ? crow : (const CT*)p.C;
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const V c = load_cost<T>(src + colc[g]);
@@ -208,7 +214,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const bool rok = row0 + r < p.n;
+            const bool rok = row_in(row0 + r);
 #pragma unroll
             for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -216,15 +222,18 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
                     kv[r][g][k] = (rok && cok[g][k]) ? fast_exp(kv[r][g][k] * ks) : (T)0;
         }
     }
-    const T ia_mine = (T)1 / p.a[row0 + (lane & (R - 1)) < p.n ? row0 + (lane & (R - 1)) : p.n - 1];
+    // the row whose total this lane holds after wave_row_totals: lane >> RSH
+    constexpr int RSH = R == 16 ? 2 : 3;
+    const int myrow = lane >> RSH;
+    const T ia_mine = (T)1 / p.a[row_in(row0 + myrow) ? row0 + myrow : n_ - 1];
     // this thread's gathered columns (chunk tid): their target marginal
     T bch[CPC];
 #pragma unroll
     for (int c = 0; c < CPC; ++c) {
         const int col = tid * CPC + c;
-        bch[c] = (tid < NCH && col < p.m) ? p.b[col] : (T)0;
+        bch[c] = (tid < NCH && col_in(col)) ? p.b[col] : (T)0;
     }
-    const T u0 = (T)1 / (T)p.n, v0 = (T)1 / (T)p.m;
+    const T u0 = (T)1 / (T)n_, v0 = (T)1 / (T)m_;
     if (tid < 4) s_ep[tid] = -1;
     for (int q = tid; q < Cf::C; q += blockDim.x) vhist[0][q] = vhist[1][q] = v0;
     if (tid < TR) uhist[0][tid] = uhist[1][tid] = u0;
@@ -319,7 +328,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
 #pragma unroll
             for (int c = 0; c < CPC; ++c) {
                 const int col = tid * CPC + c;
-                const bool ok = col < p.m;
+                const bool ok = col_in(col);
                 const T val = bch[c] / sv[c];
                 fl |= (ok && ((sv[c] == (T)0) || !finite_val(val))) ? 4 : 0;
                 vcur[col] = ok ? val : (T)0;
@@ -346,12 +355,11 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
     {
         T wr[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) wr[r] = (row0 + r < p.n) ? u0 : (T)0;
+        for (int r = 0; r < R; ++r) wr[r] = row_in(row0 + r) ? u0 : (T)0;
         publish(wr, 0, 0);
     }
     int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
     bool done = false;
-    const int rowl = butterfly_row<R>(lane);
 
     for (int it = 0; it < p.max_iter; ++it) {
         OTF_STAMP(it, 0);
@@ -404,25 +412,21 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
 #endif
             rp[r] = acc;
         }
-        wave_sum_multi<T, R>(rp, lane);
+        // wave totals (lane L: row L >> RSH), u of that row in every lane, then to every
+        // lane as wave-uniform values (v_readlane: no LDS round trip); the first lane of
+        // each row group keeps the history
         const int slot = it & 1;
-        if (lane < R) urow[w][rowl] = rp[0];
-        __builtin_amdgcn_wave_barrier();
-        const T tot = urow[w][lane & (R - 1)];
-        __builtin_amdgcn_wave_barrier();
-        if (lane < R) {
-            T un = (T)1 / (tot * ia_mine);
-            if (row0 + lane >= p.n) un = 0;
-            urow[w][lane] = un;
-            uhist[slot][w * R + lane] = un;
-        }
-        __builtin_amdgcn_wave_barrier();  // wave-private LDS hand-off (in-order LDS queue)
         T un[R];
         int badu = 0;
+        {
+            const T tot = wave_row_totals<T, R>(rp, lane);
+            T um = (T)1 / (tot * ia_mine);
+            if (!row_in(row0 + myrow)) um = 0;
+            badu = __any(!finite_val(um)) ? 1 : 0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            un[r] = urow[w][r];
-            badu |= (row0 + r < p.n && !finite_val(un[r])) ? 1 : 0;
+            for (int r = 0; r < R; ++r)
+                un[r] = map_words(um, [&](unsigned wd) { return (unsigned)__builtin_amdgcn_readlane((int)wd, r << RSH); });
+            if ((lane & ((1 << RSH) - 1)) == 0) uhist[slot][w * R + myrow] = um;
         }
         if (w == 0) {
 #pragma unroll
@@ -470,7 +474,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k)
             vo[g][k] = last_good < 0 ? v0 : vhist[hs][(lane + kWave * g) * VEC + k];
-    if (lane < R && row0 + lane < p.n) {
+    if (lane < R && row_in(row0 + lane)) {
         T mine = uo[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) if (lane == r) mine = uo[r];
@@ -487,21 +491,21 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
         TP* P = (TP*)p.P;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if (row0 + r >= p.n) break;
+            if (!row_in(row0 + r)) break;
             TP* prow = P + (int64_t)(row0 + r) * p.ldp;
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const int c0 = (lane + kWave * g) * VEC;
-                if (c0 >= p.m) continue;
+                if (!col_in(c0)) continue;
                 VP o;
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) o[k] = (TP)(uo[r] * kv[r][g][k] * vo[g][k]);
-                if (c0 + VEC <= p.m) {
+                if (FULL || c0 + VEC <= m_) {
                     *reinterpret_cast<VP*>(prow + c0) = o;
                 } else {
 #pragma unroll
                     for (int k = 0; k < VEC; ++k)
-                        if (c0 + k < p.m) prow[c0 + k] = o[k];
+                        if (col_in(c0 + k)) prow[c0 + k] = o[k];
                 }
             }
         }
@@ -521,7 +525,12 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
 template <typename T, typename CT, typename TP, int NQ>
 hipError_t launch_gather_q(int grid, SkGatherArgs<T>& p, hipStream_t s) {
     void* args[] = {&p};
-    const void* k = (const void*)sk_gather_kernel<T, CT, TP, NQ>;
+    // BASELINE config 2 (8 whole row tiles x 512 columns of float64) has its own
+    // compiled-in instance
+    const bool whole = p.n == p.nwg * GatherCfg<T>::TR && p.m == GatherCfg<T>::C;
+    const void* k = (sizeof(T) == 8 && NQ == 8 && p.nwg == 8 && whole)
+                        ? (const void*)sk_gather_kernel<T, CT, TP, NQ, (sizeof(T) == 8 && NQ == 8) ? 8 : 0>
+                        : (const void*)sk_gather_kernel<T, CT, TP, NQ, 0>;
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
     if (e != hipSuccess) return e;
@@ -532,9 +541,9 @@ hipError_t launch_gather_q(int grid, SkGatherArgs<T>& p, hipStream_t s) {
 // co-resident 512-thread workgroups per CU of the instance launch_gather picks (0 on error)
 template <typename T, typename CT, typename TP>
 int gather_per_cu_t(int nwg) {
-    const void* k = nwg <= 4   ? (const void*)sk_gather_kernel<T, CT, TP, 4>
-                    : nwg <= 8 ? (const void*)sk_gather_kernel<T, CT, TP, 8>
-                               : (const void*)sk_gather_kernel<T, CT, TP, 16>;
+    const void* k = nwg <= 4   ? (const void*)sk_gather_kernel<T, CT, TP, 4, 0>
+                    : nwg <= 8 ? (const void*)sk_gather_kernel<T, CT, TP, 8, 0>
+                               : (const void*)sk_gather_kernel<T, CT, TP, 16, 0>;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0) != hipSuccess) return 0;
     return per_cu;

@@ -227,6 +227,175 @@ __global__ __launch_bounds__(256) void postprocess_apply_kernel(
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// ---------------------------------------------------------------------------------
+// The training step's alignment loss and its gradients in ONE workgroup launch
+// (cosine_loss, MRI_PET_OT_nojax.py:552-560, applied at :721 with the NaN -> 0 swap of
+// :724-725): torch's chain  xh = x / max(|x|, 1e-12)  (F.normalize),
+// xt = xh / max(|xh|, 1e-8)  (the norm clamp inside F.cosine_similarity),
+// cos_b = xt_b . yt_b,  L = 1 - mean_b cos_b,  and the backward of that chain:
+//   g_xt = -(1/B) yt,  g_xh = (g_xt - (xt . g_xt) xt) / max(|xh|, 1e-8),
+//   g_x  = (g_xh - (xh . g_xh) xh) / |x|   (|x| > 1e-12; else g_xh / 1e-12)
+// with xt . g_xt = -cos / B and xh . g_xh = (cos / B)(|xh|^2 / max(|xh|,1e-8)^2 - 1).
+// keep = ok && finite(L): otherwise L, g_x, g_y are exact zeros (the reference
+// replaces a NaN loss by a constant 0) and keep_out tells the backward.  Replaces the
+// ~40 small torch launches of the autograd form per training step.
+template <typename TX>
+__global__ __launch_bounds__(1024) void cosine_align_kernel(const TX* X, int64_t ldx, const float* Y,
+                                                            int64_t ldy, int B, int d, const uint8_t* ok,
+                                                            float* loss, float* gx, int64_t ldgx,
+                                                            float* gy, int64_t ldgy, uint8_t* keep_out) {
+    __shared__ float s_cos[1024];
+    __shared__ int s_keep;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int b = w; b < B; b += nw) {
+        const TX* x = X + (int64_t)b * ldx;
+        const float* y = Y + (int64_t)b * ldy;
+        float sxx = 0.f, syy = 0.f;
+        for (int k = lane; k < d; k += kWave) {
+            const float xv = (float)x[k], yv = y[k];
+            sxx += xv * xv;
+            syy += yv * yv;
+        }
+        sxx = wave_sum<float>(sxx);
+        syy = wave_sum<float>(syy);
+        const float dx = fmaxf(sqrtf(sxx), 1e-12f), dy = fmaxf(sqrtf(syy), 1e-12f);
+        float ah = 0.f, bh = 0.f, c = 0.f;
+        for (int k = lane; k < d; k += kWave) {
+            const float xh = (float)x[k] / dx, yh = y[k] / dy;
+            ah += xh * xh;
+            bh += yh * yh;
+            c += xh * yh;
+        }
+        ah = wave_sum<float>(ah);
+        bh = wave_sum<float>(bh);
+        c = wave_sum<float>(c);
+        const float ax = fmaxf(sqrtf(ah), 1e-8f), ay = fmaxf(sqrtf(bh), 1e-8f);
+        if (lane == 0) s_cos[b] = c / (ax * ay);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float sum = 0.f;
+        for (int b = 0; b < B; ++b) sum += s_cos[b];   // fixed order
+        const float L = 1.f - sum / (float)B;
+        const int keep = (ok == nullptr || ok[0] != 0) && finite_val(L);
+        s_keep = keep;
+        loss[0] = keep ? L : 0.f;
+        if (keep_out) keep_out[0] = (uint8_t)keep;
+    }
+    __syncthreads();
+    const bool keep = s_keep != 0;
+    const float invB = 1.f / (float)B;
+    for (int b = w; b < B; b += nw) {
+        const TX* x = X + (int64_t)b * ldx;
+        const float* y = Y + (int64_t)b * ldy;
+        float* ox = gx + (int64_t)b * ldgx;
+        float* oy = gy + (int64_t)b * ldgy;
+        if (!keep) {
+            for (int k = lane; k < d; k += kWave) ox[k] = oy[k] = 0.f;
+            continue;
+        }
+        // the row's norms again (bitwise the values of the first pass: same order)
+        float sxx = 0.f, syy = 0.f;
+        for (int k = lane; k < d; k += kWave) {
+            const float xv = (float)x[k], yv = y[k];
+            sxx += xv * xv;
+            syy += yv * yv;
+        }
+        sxx = wave_sum<float>(sxx);
+        syy = wave_sum<float>(syy);
+        const float nx = sqrtf(sxx), ny = sqrtf(syy);
+        const float dx = fmaxf(nx, 1e-12f), dy = fmaxf(ny, 1e-12f);
+        float ah = 0.f, bh = 0.f;
+        for (int k = lane; k < d; k += kWave) {
+            const float xh = (float)x[k] / dx, yh = y[k] / dy;
+            ah += xh * xh;
+            bh += yh * yh;
+        }
+        ah = wave_sum<float>(ah);
+        bh = wave_sum<float>(bh);
+        const float ax = fmaxf(sqrtf(ah), 1e-8f), ay = fmaxf(sqrtf(bh), 1e-8f);
+        const float cs = s_cos[b];
+        const float tx = -cs * invB;                               // xt . g_xt (= yt . g_yt)
+        const float sx = cs * invB * (ah / (ax * ax) - 1.f);       // xh . g_xh
+        const float sy = cs * invB * (bh / (ay * ay) - 1.f);
+        const bool cx = nx > 1e-12f, cy = ny > 1e-12f;
+        for (int k = lane; k < d; k += kWave) {
+            const float xh = (float)x[k] / dx, yh = y[k] / dy;
+            const float xt = xh / ax, yt = yh / ay;
+            const float gxh = (-invB * yt - tx * xt) / ax;
+            const float gyh = (-invB * xt - tx * yt) / ay;
+            ox[k] = cx ? (gxh - sx * xh) / dx : gxh / dx;
+            oy[k] = cy ? (gyh - sy * yh) / dy : gyh / dy;
+        }
+    }
+}
+
+// Backward of the plan apply ot = pet @ Tn^T together with the loss scaling, ONE launch:
+//   g_pet[b][j] = sum_i G[b][i] Tn[i][j],  G = g_loss * gy + g_ot   (B x d2)
+//   g_mri       = g_loss * gx                                       (B x d)
+// A skinny product (B <= a few tens of rows): workgroup = 64 output columns, its 8
+// waves split the d rows of Tn (coalesced 256-B row segments), G staged transposed
+// in LDS (8 batch rows per pass: two 16-B broadcast reads per Tn element), the 8
+// slices added in a fixed order.  The generic 64 x 64-tile GEMM ran one workgroup
+// per 64 output columns with K in 16-deep steps: 84 us for 8 x 512 x 512.  Without
+// g_ot and keep = 0 the plan may hold NaN: g_pet is written as exact zeros.
+constexpr int kAbB = 8;        // batch rows per pass
+constexpr int kAbS = 8;        // row slices (waves)
+__global__ __launch_bounds__(512) void ot_align_backward_kernel(
+    const float* gx, int64_t ldgx, const float* gy, int64_t ldgy, const float* g_ot, int64_t ldgo,
+    const float* g_loss, const uint8_t* keep, const float* Tn, int64_t ldt, int B, int d, int d2,
+    float* g_mri, int64_t ldm, float* g_pet, int64_t ldp) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* Gt = smem;                        // [d][kAbB]
+    float* red = smem + (size_t)d * kAbB;    // [kAbS][kAbB][64]
+    const int tid = threadIdx.x, jl = tid & 63, ks = tid >> 6;
+    const float gl = g_loss ? g_loss[0] : 0.f;
+    const bool zero = g_ot == nullptr && keep != nullptr && keep[0] == 0;
+    // g_mri: grid-strided elementwise share of every workgroup
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + tid; e < (int64_t)B * d; e += (int64_t)gridDim.x * blockDim.x) {
+        const int b = (int)(e / d), i = (int)(e % d);
+        g_mri[(int64_t)b * ldm + i] = gl * gx[(int64_t)b * ldgx + i];
+    }
+    const int j = blockIdx.x * 64 + jl;
+    const int i0 = (int)((int64_t)d * ks / kAbS), i1 = (int)((int64_t)d * (ks + 1) / kAbS);
+    for (int b0 = 0; b0 < B; b0 += kAbB) {
+        __syncthreads();
+        for (int e = tid; e < d * kAbB; e += blockDim.x) {
+            const int i = e / kAbB, bb = e % kAbB, b = b0 + bb;
+            float g = 0.f;
+            if (b < B) {
+                g = gl * gy[(int64_t)b * ldgy + i];
+                if (g_ot) g += g_ot[(int64_t)b * ldgo + i];
+            }
+            Gt[e] = g;
+        }
+        __syncthreads();
+        float acc[kAbB];
+#pragma unroll
+        for (int bb = 0; bb < kAbB; ++bb) acc[bb] = 0.f;
+        if (j < d2 && !zero) {
+            for (int i = i0; i < i1; ++i) {
+                const float t = Tn[(int64_t)i * ldt + j];
+                const float4 g0 = *reinterpret_cast<const float4*>(&Gt[i * kAbB]);
+                const float4 g1 = *reinterpret_cast<const float4*>(&Gt[i * kAbB + 4]);
+                acc[0] += g0.x * t; acc[1] += g0.y * t; acc[2] += g0.z * t; acc[3] += g0.w * t;
+                acc[4] += g1.x * t; acc[5] += g1.y * t; acc[6] += g1.z * t; acc[7] += g1.w * t;
+            }
+        }
+#pragma unroll
+        for (int bb = 0; bb < kAbB; ++bb) red[(ks * kAbB + bb) * 64 + jl] = acc[bb];
+        __syncthreads();
+        if (ks == 0 && j < d2) {
+            for (int bb = 0; bb < kAbB && b0 + bb < B; ++bb) {
+                float sum = red[bb * 64 + jl];
+#pragma unroll
+                for (int q = 1; q < kAbS; ++q) sum += red[(q * kAbB + bb) * 64 + jl];
+                g_pet[(int64_t)(b0 + bb) * ldp + j] = sum;
+            }
+        }
+    }
+}
+
 }  // namespace
 
 // Host launcher for the tiled GEMM, shared with the other translation units.
@@ -426,6 +595,47 @@ int otf_gemm_f32(const float* A, int64_t sa0, int64_t sa1, const float* B, int64
     dim3 grid((unsigned)((N + otf::GT - 1) / otf::GT), (unsigned)((M + otf::GT - 1) / otf::GT));
     otf::gemm_kernel<float, float, float, float><<<grid, 256, 0, s>>>(
         A, sa0, sa1, B, sb0, sb1, out, ldo, (int)M, (int)N, (int)K, alpha, beta, nullptr, nullptr);
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+int otf_cosine_align(const void* X, int64_t ldx, int32_t x_dtype, const float* Y, int64_t ldy,
+                     int64_t B, int64_t d, const uint8_t* ok, float* loss, float* gx, int64_t ldgx,
+                     float* gy, int64_t ldgy, uint8_t* keep_out, otf_stream_t stream) {
+    if (!X || !Y || !loss || !gx || !gy || B <= 0 || d <= 0 || ldx < d || ldy < d || ldgx < d ||
+        ldgy < d)
+        return OTF_EINVAL;
+    if (B > 1024) return OTF_EUNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    if (x_dtype == OTF_F32)
+        otf::cosine_align_kernel<float><<<1, 1024, 0, s>>>((const float*)X, ldx, Y, ldy, (int)B, (int)d, ok,
+                                                           loss, gx, ldgx, gy, ldgy, keep_out);
+    else if (x_dtype == OTF_BF16)
+        otf::cosine_align_kernel<otf::bf16><<<1, 1024, 0, s>>>((const otf::bf16*)X, ldx, Y, ldy, (int)B,
+                                                               (int)d, ok, loss, gx, ldgx, gy, ldgy, keep_out);
+    else if (x_dtype == OTF_F16)
+        otf::cosine_align_kernel<_Float16><<<1, 1024, 0, s>>>((const _Float16*)X, ldx, Y, ldy, (int)B,
+                                                              (int)d, ok, loss, gx, ldgx, gy, ldgy, keep_out);
+    else
+        return OTF_EINVAL;
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
+}
+
+int otf_ot_align_backward(const float* gx, int64_t ldgx, const float* gy, int64_t ldgy,
+                          const float* g_ot, int64_t ldgo, const float* g_loss, const uint8_t* keep,
+                          const float* Tn, int64_t ldt, int64_t B, int64_t d, int64_t d2, float* g_mri,
+                          int64_t ldm, float* g_pet, int64_t ldp, otf_stream_t stream) {
+    if (!gx || !gy || !Tn || !g_mri || !g_pet || B <= 0 || d <= 0 || d2 <= 0 || ldgx < d ||
+        ldgy < d || ldt < d2 || ldm < d || ldp < d2 || (g_ot && ldgo < d))
+        return OTF_EINVAL;
+    const size_t lds = ((size_t)d * otf::kAbB + (size_t)otf::kAbS * otf::kAbB * 64) * sizeof(float);
+    if (lds > 160 * 1024) return OTF_EUNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    const int grid = (int)((d2 + 63) / 64);
+    otf::ot_align_backward_kernel<<<grid, 512, lds, s>>>(gx, ldgx, gy, ldgy, g_ot, ldgo, g_loss, keep, Tn,
+                                                        ldt, (int)B, (int)d, (int)d2, g_mri, ldm, g_pet,
+                                                        ldp);
     OTF_HIP(hipGetLastError());
     return OTF_OK;
 }

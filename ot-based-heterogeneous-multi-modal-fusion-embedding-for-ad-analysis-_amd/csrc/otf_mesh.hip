@@ -85,7 +85,31 @@ struct SkMeshArgs {
     unsigned long long timeout_ticks;
 };
 
+// Diagnostic build only (-DOTF_MESH_STAMPS, tools/stamps_mesh.hip): per-hop wall-clock
+// stamps keyed by the workgroup's ROLE (rb * ncb + cb), so the tool can pair every
+// consumer with its producers and split a hop into its latency and the producers' skew.
+#ifdef OTF_MESH_STAMPS
+__device__ unsigned long long g_mstamps[256 * 16 * 16];
+__device__ int g_mrole[256 * 4];
+// the stamp buffer's address lives in a VGPR pair (set once): a stamp is then one
+// s_memrealtime + one store, not a GOT load per stamp (two serial scalar round trips)
+#define OTF_MSTAMP(it, slot, who)                                                            \
+    do {                                                                                     \
+        if (threadIdx.x == (who) && (it) >= 0 && (it) < 16 && rb * ncb + cb < 256)           \
+            mst_base[((rb * ncb + cb) * 16 + (it)) * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define OTF_MSTAMP(it, slot, who) \
+    do {                          \
+    } while (0)
+#endif
+
 using I4 = __attribute__((ext_vector_type(4))) int;
+// Waves that share the reducer's gather (1, 2 or 4): each polls KQ / RW producers per lane,
+// the last to finish (an LDS ticket) adds the partials in producer order and publishes
+#ifndef OTF_MESH_RED_WAVES
+#define OTF_MESH_RED_WAVES 1
+#endif
 // s_sleep units between polls of a granule that has not arrived (64 clocks each)
 #ifndef OTF_MESH_SLEEP
 #define OTF_MESH_SLEEP 1
@@ -107,6 +131,8 @@ __device__ __forceinline__ bool chunk_at(const I4 x, unsigned e) {
 __device__ __forceinline__ float chunk_v0(const I4 x) { const int w = x[0]; return __builtin_bit_cast(float, w); }
 __device__ __forceinline__ float chunk_v1(const I4 x) { const int w = x[2]; return __builtin_bit_cast(float, w); }
 
+template <int CTRL> __device__ __forceinline__ float dpp_f(float x) { return dpp_lane<CTRL>(x); }
+
 __device__ __forceinline__ I4 gload(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     return __builtin_bit_cast(I4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16 /* sc1 */));
 }
@@ -123,9 +149,15 @@ __device__ __forceinline__ void gstore_col(__amdgpu_buffer_rsrc_t rs, uint32_t o
         __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
 }
 
+constexpr int pow2_at_least(int x) { return x <= 1 ? 1 : 2 * pow2_at_least((x + 1) / 2); }
+
 // KQ: reducer loads per lane, ceil(nrb * CPR / 64): 4 when nrb is a power of two
-// (nrb * CPR = 256), up to 8 otherwise
-template <typename CT, typename TP, int KQ>
+// (nrb * CPR = 256), up to 8 otherwise.
+// SNRB, SNCB: the shape compiled in (0 = read from the arguments).  A compiled-in shape
+// is a mesh of WHOLE tiles (n = SNRB * 128, m = SNCB * 512): every row / column bound
+// test and every derived count folds away, which also frees the scalar registers whose
+// spills (v_readlane / v_writelane per branch) lengthened every phase of the generic form.
+template <typename CT, typename TP, int KQ, int SNRB, int SNCB>
 __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     using T = float;
     constexpr int G = 2, VEC = 4, R = kMeshRW, NW = kMeshNW, TR = kMeshTR, TC = kMeshTC;
@@ -134,7 +166,6 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     __shared__ __attribute__((aligned(16))) T colbuf[NW][TC];
     __shared__ __attribute__((aligned(16))) T vcur[TC];      // v = b / S of this tile's columns
     __shared__ __attribute__((aligned(16))) T vhist[2][TC];  // v by iteration parity
-    __shared__ T urow[NW][R];
     __shared__ T uhist[2][TR];
     __shared__ T s_E;  // this column tile's error partial (hop B)
     // workgroup-wide flags without a reduction: a raised flag holds the KEY (epoch or
@@ -143,10 +174,21 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     // producer flag (non-finite u of the previous iteration), [3] zero / non-finite v
     // (epoch keys), [4] row-hop stall (iteration key)
     __shared__ int s_ep[5];
+    constexpr int RW = OTF_MESH_RED_WAVES, KQW = KQ / RW;
+    static_assert(KQ % RW == 0, "reducer waves must divide the reducer loads");
+    __shared__ F2 red_s[RW][kWave];   // per-wave partial sums of the reducer's lanes
+    __shared__ int red_f[RW][kWave];  // and their producer flags
+    __shared__ F2 red_sp[kWave];      // previous sums S[k - 1] of the reducer's lanes
+    __shared__ int red_cnt;           // reducer-wave ticket of this epoch
     int tid = threadIdx.x, lane = tid & 63;
     const int w = (int)threadIdx.x >> 6;
     unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
-    const int nrb = p.nrb, ncb = p.ncb, CPR = p.cpr;
+    constexpr bool FULL = SNRB != 0 && SNCB != 0;
+    const int nrb = FULL ? SNRB : p.nrb, ncb = FULL ? SNCB : p.ncb;
+    const int CPR = FULL ? pow2_at_least((kMeshNCH + SNRB - 1) / (SNRB > 0 ? SNRB : 1)) : p.cpr;
+    const int n_ = FULL ? SNRB * TR : p.n, m_ = FULL ? SNCB * TC : p.m;
+    auto row_in = [&](int r) -> bool { return FULL || r < n_; };
+    auto col_in = [&](int c) -> bool { return FULL || c < m_; };
 
     // Tile of this workgroup.  XCC-local column path (p.xcc_local): every workgroup
     // registers on its XCC (the hardware id, not an assumed placement), one flat
@@ -213,9 +255,19 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         }
     }
     const bool lead = (rb == 0 && cb == 0 && tid == 0);  // writes info and the error log
+#ifdef OTF_MESH_STAMPS
+    unsigned long long* mst_base = g_mstamps;
+    asm volatile("" : "+v"(mst_base));
+    if (tid == 0 && rb * ncb + cb < 256) {
+        g_mrole[(rb * ncb + cb) * 4 + 0] = rb;
+        g_mrole[(rb * ncb + cb) * 4 + 1] = cb;
+        g_mrole[(rb * ncb + cb) * 4 + 2] = xcc_id();
+        g_mrole[(rb * ncb + cb) * 4 + 3] = 1 + ncb * 1000 + nrb * 100000;
+    }
+#endif
     const int row0 = rb * TR + w * R;
     const int col0 = cb * TC;
-    const int ncols = p.m - col0 < TC ? p.m - col0 : TC;
+    const int ncols = FULL ? TC : (m_ - col0 < TC ? m_ - col0 : TC);
     const int nch = (ncols + 1) >> 1;          // chunks of this column tile
     const int nred = (nch + CPR - 1) / CPR;    // reducers of this column tile
 
@@ -232,20 +284,20 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int c0 = col0 + (lane + kWave * g) * VEC;
-            colc[g] = c0 < p.m ? c0 : 0;
+            colc[g] = col_in(c0) ? c0 : 0;
         }
         const CT* crow = (const CT*)p.C + (int64_t)row0 * p.ldc;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const CT* src = (row0 + r < p.n) ? crow : (const CT*)p.C;
-            const bool rok = row0 + r < p.n;
+            const CT* src = row_in(row0 + r) ? crow : (const CT*)p.C;
+            const bool rok = row_in(row0 + r);
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const V c = load_cost<T>(src + colc[g]);
                 T e[VEC];
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
-                    const bool ok = rok && col0 + (lane + kWave * g) * VEC + k < p.m;
+                    const bool ok = rok && col_in(col0 + (lane + kWave * g) * VEC + k);
                     e[k] = ok ? fast_exp(c[k] * ks) : (T)0;
                 }
                 kv[r][g][0] = F2{e[0], e[1]};
@@ -256,9 +308,10 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     }
     // 1 / a of the rows whose u this lane finishes: row (lane & 15) when the tile spans
     // whole rows, rows 2c, 2c + 1 (c = lane & 7) after a row hop
-    auto inv_a = [&](int r) -> T { return (T)1 / p.a[r < p.n ? r : p.n - 1]; };
-    const T ia_whole = inv_a(row0 + (lane & (R - 1)));
-    const T ia_c0 = inv_a(row0 + 2 * (lane & 7)), ia_c1 = inv_a(row0 + 2 * (lane & 7) + 1);
+    auto inv_a = [&](int r) -> T { return (T)1 / p.a[row_in(r) ? r : n_ - 1]; };
+    // rows 2c, 2c + 1 (c = lane >> 3) of the wave's 16: the chunk a lane group finishes
+    const int rc = lane >> 3;
+    const T ia_c0 = inv_a(row0 + 2 * rc), ia_c1 = inv_a(row0 + 2 * rc + 1);
     // hop-B consumer: chunk t = tid - 256 of this tile -> columns col0 + 2t, + 1
     T bch0 = 0, bch1 = 0;
     if (tid >= 256) {
@@ -273,15 +326,17 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     const int r_ch = rb * CPR + r_cc;
     const bool r_ok = r_ch < nch;
     T rb0 = 0, rb1 = 0;  // target marginal of the reducer's two columns
-    if (w == 0 && r_ok) {
+    if (w < OTF_MESH_RED_WAVES && r_ok) {
         if (2 * r_ch < ncols) rb0 = p.b[col0 + 2 * r_ch];
         if (2 * r_ch + 1 < ncols) rb1 = p.b[col0 + 2 * r_ch + 1];
     }
     const bool rc0 = r_ok && 2 * r_ch < ncols, rc1 = r_ok && 2 * r_ch + 1 < ncols;
     T sp0 = 1, sp1 = 1;  // the reducer's previous sums S[k - 1]
 
-    const T u0 = (T)1 / (T)p.n, v0 = (T)1 / (T)p.m;
+    const T u0 = (T)1 / (T)n_, v0 = (T)1 / (T)m_;
     if (tid < 5) s_ep[tid] = -1;
+    if (tid < kWave) red_sp[tid] = F2{1.f, 1.f};
+    if (tid == 0) red_cnt = 0;
     for (int q = tid; q < TC; q += blockDim.x) {
         vhist[0][q] = vhist[1][q] = v0;
         vcur[q] = 0;  // columns past m stay 0 (their K entries are 0 too)
@@ -309,28 +364,39 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             gstore_col(rs, cola(e, rb) + (uint32_t)tid * 16, chunk2(s[0], s[1], (e << 2) | flag), xl);
         }
     };
+    // four independent accumulation chains (g, h) advanced together, r ascending in each
     auto col_partials = [&](const T (&wr)[R]) {
+        F2 acc[G][2];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            F2 acc0 = kv[0][g][0] * wr[0], acc1 = kv[0][g][1] * wr[0];
-#pragma unroll
-            for (int r = 1; r < R; ++r) {
-                acc0 = __builtin_elementwise_fma(kv[r][g][0], F2{wr[r], wr[r]}, acc0);
-                acc1 = __builtin_elementwise_fma(kv[r][g][1], F2{wr[r], wr[r]}, acc1);
-            }
-            *reinterpret_cast<V*>(&colbuf[w][(lane + kWave * g) * VEC]) = V{acc0[0], acc0[1], acc1[0], acc1[1]};
+            acc[g][0] = kv[0][g][0] * wr[0];
+            acc[g][1] = kv[0][g][1] * wr[0];
         }
+#pragma unroll
+        for (int r = 1; r < R; ++r)
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                acc[g][0] = __builtin_elementwise_fma(kv[r][g][0], F2{wr[r], wr[r]}, acc[g][0]);
+                acc[g][1] = __builtin_elementwise_fma(kv[r][g][1], F2{wr[r], wr[r]}, acc[g][1]);
+            }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            *reinterpret_cast<V*>(&colbuf[w][(lane + kWave * g) * VEC]) =
+                V{acc[g][0][0], acc[g][0][1], acc[g][1][0], acc[g][1][1]};
     };
     // reducer (wave 0): S[e - 1] for this workgroup's chunk range from the nrb
     // producers of epoch e, fixed order; hop B carries the OR of their flags and the
     // error terms of iterate e - 2 (S[e - 1] against S[e - 2]).  Returns false on a stall.
-    auto reduce = [&](int e) -> bool {
-        I4 x[KQ];
-        bool act[KQ];
+    // need: the marginal error of this epoch is checked (POT tests it every check_every
+    // iterations; the other iterations skip its two divisions and its reduction)
+    auto reduce = [&](int e, bool need) -> bool {
+        I4 x[KQW];
+        bool act[KQW];
         unsigned pend = 0;
+        const int k0 = RW > 1 ? w * KQW : 0;  // this wave's producer slice
 #pragma unroll
-        for (int k = 0; k < KQ; ++k) {
-            const int q = r_qlo + LPC * k;
+        for (int k = 0; k < KQW; ++k) {
+            const int q = r_qlo + LPC * (k0 + k);
             act[k] = r_ok && q < nrb;
             x[k] = I4{0, 0, 0, 0};
             if (act[k]) pend |= 1u << k;
@@ -338,24 +404,49 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         bool ok = true;
         for (;;) {
 #pragma unroll
-            for (int k = 0; k < KQ; ++k)
-                if (pend & (1u << k)) x[k] = gload(rs, cola(e, r_qlo + LPC * k) + (uint32_t)r_ch * 16);
+            for (int k = 0; k < KQW; ++k)
+                if (pend & (1u << k)) x[k] = gload(rs, cola(e, r_qlo + LPC * (k0 + k)) + (uint32_t)r_ch * 16);
 #pragma unroll
-            for (int k = 0; k < KQ; ++k)
+            for (int k = 0; k < KQW; ++k)
                 if ((pend & (1u << k)) && chunk_at(x[k], (unsigned)e)) pend &= ~(1u << k);
             if (!__any(pend != 0)) break;
             if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
             __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
         }
+        OTF_MSTAMP(e - 2, 6, 0);
         T s0 = 0, s1 = 0;
         int fl = 0;
 #pragma unroll
-        for (int k = 0; k < KQ; ++k)
+        for (int k = 0; k < KQW; ++k)
             if (act[k]) {
                 s0 += chunk_v0(x[k]);
                 s1 += chunk_v1(x[k]);
                 fl |= x[k][1] & 1;
             }
+        if (RW > 1) {
+            // partials to LDS, then a ticket: the last reducer wave adds them in producer
+            // order (the single-wave order: 0 + x0 + x1 + ..., bitwise the same sums)
+            red_s[w][lane] = F2{s0, s1};
+            red_f[w][lane] = fl;
+            int t = 0;
+            if (lane == 0) t = __hip_atomic_fetch_add(&red_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            t = __builtin_amdgcn_readfirstlane(t);
+            if (t != RW - 1) {
+                deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+                return ok;
+            }
+            if (lane == 0) red_cnt = 0;  // next use is behind this iteration's barriers
+            s0 = 0;
+            s1 = 0;
+            fl = 0;
+#pragma unroll
+            for (int ww = 0; ww < RW; ++ww) {
+                const F2 q = red_s[ww][lane];
+                s0 += q[0];
+                s1 += q[1];
+                fl |= red_f[ww][lane];
+            }
+        }
         // lanes with equal chunk: offsets CPR, 2 CPR, ..., 32 (uniform branches, static DPP)
         if (CPR <= 1) { s0 += wave_xor<T, 1>(s0); s1 += wave_xor<T, 1>(s1); }
         if (CPR <= 2) { s0 += wave_xor<T, 2>(s0); s1 += wave_xor<T, 2>(s1); }
@@ -365,26 +456,35 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         if (CPR <= 32) { s0 += wave_xor<T, 32>(s0); s1 += wave_xor<T, 32>(s1); }
         const int bad = __any(fl) ? 1 : 0;
         // POT's marginal error of the iterate whose v = b / S[e - 2]
+        const F2 sp = RW > 1 ? red_sp[lane] : F2{sp0, sp1};
         T term = 0;
-        if (rc0) { const T rr = (rb0 / sp0) * s0 - rb0; term += rr * rr; }
-        if (rc1) { const T rr = (rb1 / sp1) * s1 - rb1; term += rr * rr; }
-        if (CPR > 1) term += wave_xor<T, 1>(term);
-        if (CPR > 2) term += wave_xor<T, 2>(term);
-        if (CPR > 4) term += wave_xor<T, 4>(term);
-        if (CPR > 8) term += wave_xor<T, 8>(term);
-        if (CPR > 16) term += wave_xor<T, 16>(term);
-        if (CPR > 32) term += wave_xor<T, 32>(term);
-        sp0 = s0;
-        sp1 = s1;
+        if (need) {
+            if (rc0) { const T rr = (rb0 / sp[0]) * s0 - rb0; term += rr * rr; }
+            if (rc1) { const T rr = (rb1 / sp[1]) * s1 - rb1; term += rr * rr; }
+            if (CPR > 1) term += wave_xor<T, 1>(term);
+            if (CPR > 2) term += wave_xor<T, 2>(term);
+            if (CPR > 4) term += wave_xor<T, 4>(term);
+            if (CPR > 8) term += wave_xor<T, 8>(term);
+            if (CPR > 16) term += wave_xor<T, 16>(term);
+            if (CPR > 32) term += wave_xor<T, 32>(term);
+        }
+        if (RW > 1) {
+            red_sp[lane] = F2{s0, s1};
+        } else {
+            sp0 = s0;
+            sp1 = s1;
+        }
         const int tag = (e << 2) | bad;
         if (lane < CPR && r_ok) gstore_col(rs, colb(e, rb) + (uint32_t)r_cc * 16, chunk2(s0, s1, tag), xl);
-        if (lane == 0 && rb < nred) gstore_col(rs, colb(e, rb) + (uint32_t)CPR * 16, chunk2(term, 0.f, tag), xl);
+        if (need && lane == 0 && rb < nred)
+            gstore_col(rs, colb(e, rb) + (uint32_t)CPR * 16, chunk2(term, 0.f, tag), xl);
+        OTF_MSTAMP(e - 2, 7, 0);
         deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
         return ok;
     };
     // hop B: the sums S[e - 1] of this tile's columns -> v into vcur; the column tile's
     // error partial into s_E.  Returns bit 0 = producer flag, 1 = stall, 2 = bad v.
-    auto gather_b = [&](int e) -> int {
+    auto gather_b = [&](int e, bool need) -> int {
         int fl = 0;
         T ep = 0;
         if (tid >= 256) {
@@ -398,6 +498,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                     if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; break; }
                     __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
                 }
+                OTF_MSTAMP(e - 1, 8, 256);
                 fl |= x[1] & 1;
                 const T s0 = chunk_v0(x), s1 = chunk_v1(x);
                 const bool ok0 = 2 * t < ncols, ok1 = 2 * t + 1 < ncols;
@@ -407,7 +508,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                 vcur[2 * t] = ok0 ? v0n : (T)0;
                 vcur[2 * t + 1] = ok1 ? v1n : (T)0;
             }
-        } else if (w == 3) {
+        } else if (w == 3 && need) {
             if (lane < nred) {
                 const uint32_t off = colb(e, lane) + (uint32_t)CPR * 16;
                 I4 x;
@@ -460,15 +561,14 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     {
         T wr[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) wr[r] = (row0 + r < p.n) ? u0 : (T)0;
+        for (int r = 0; r < R; ++r) wr[r] = row_in(row0 + r) ? u0 : (T)0;
         col_partials(wr);
         __syncthreads();
         publish_cols(1, 0);
     }
     int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
     bool done = false;
-    if (w == 0 && !reduce(1)) s_ep[1] = 1;  // seen after the hop-B barrier of epoch 1
-    const int rowl = butterfly_row<R>(lane);
+    if (w < RW && !reduce(1, false)) s_ep[1] = 1;  // seen after the hop-B barrier of epoch 1
     int chk = 0;  // (it - 1) % check_every for it >= 1
 
     for (int it = 0; it < p.max_iter; ++it) {
@@ -477,9 +577,13 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         // the SGPR file into VGPR lanes (v_readlane / v_writelane on every use)
         asm volatile("" : "+v"(tid), "+v"(lane));
         OTF_STAMP(it, 0);
+        OTF_MSTAMP(it, 0, 0);
         const int e = it + 1;  // hop-B epoch of S[it]; row-hop epoch of iteration it
-        const int fl = gather_b(e);
+        // (it - 1) % check_every == 0, kept as a counter (no integer division per iteration)
+        const bool check = it >= 1 && chk == 0;
+        const int fl = gather_b(e, check);
         OTF_STAMP(it, 1);
+        OTF_MSTAMP(it, 1, 0);
         if (fl & 2) { status = OTF_SK_TIMEOUT; done = true; break; }
         // a non-finite u in iteration it - 1 (any row block) -> revert to it - 2
         if (fl & 1) {
@@ -505,41 +609,39 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             acc = __builtin_elementwise_fma(kv[r][1][1], vn[1][1], acc);
             rp[r] = acc[0] + acc[1];
         }
-        wave_sum_multi<T, R>(rp, lane);
-        if (lane < R) urow[w][rowl] = rp[0];
-        __builtin_amdgcn_wave_barrier();
-        // (it - 1) % check_every == 0, kept as a counter (no integer division per iteration)
-        const bool check = it >= 1 && chk == 0;
+        // wave totals: lane L holds row L >> 2; the lane group c = L >> 3 takes the chunk
+        // (rows 2c, 2c + 1) from its half-mirror partner (the other row of the pair)
+        T t0, t1;
+        {
+            const T mine = wave_row_totals<T, R>(rp, lane), oth = dpp_f<0x141>(mine);
+            const bool odd = (lane & 4) != 0;
+            t0 = odd ? oth : mine;
+            t1 = odd ? mine : oth;
+        }
         if (it >= 1) chk = chk + 1 == p.check_every ? 0 : chk + 1;
         T errv = 0;
         int vbad = vbad_cb, stall = 0;
         if (ncb == 1) {
             // the tile spans whole rows: totals, v flags and the error are already global
-            const T tot = urow[w][lane & (R - 1)];
-            __builtin_amdgcn_wave_barrier();
             errv = s_E;
             OTF_STAMP(it, 2);
             OTF_STAMP(it, 3);
-            if (lane < R) {
-                T un = (T)1 / (tot * ia_whole);
-                if (row0 + lane >= p.n) un = 0;
-                urow[w][lane] = un;
-            }
         } else {
-            // row hop: publish this wave's 16 row partials (8 chunks) and the column tile's
-            // error partial, gather the ncb members' chunks of the same rows
-            if (lane < 8) {
-                const T t0 = urow[w][2 * lane], t1 = urow[w][2 * lane + 1];
-                gstore(rs, rowx(e, cb) + (uint32_t)(w * 8 + lane) * 16, chunk2(t0, t1, (e << 2) | vbad_cb));
-            }
-            if (w == 0 && lane == 8) gstore(rs, rowx(e, cb) + 64 * 16, chunk2(s_E, 0.f, e << 2));
-            __builtin_amdgcn_wave_barrier();
+            // row hop: publish this wave's 16 row partials (8 chunks, lane 8c) and the
+            // column tile's error partial, gather the ncb members' chunks of the same rows
+            if ((lane & 7) == 0)
+                gstore(rs, rowx(e, cb) + (uint32_t)(w * 8 + rc) * 16, chunk2(t0, t1, (e << 2) | vbad_cb));
+            if (check && w == 0 && lane == 1) gstore(rs, rowx(e, cb) + 64 * 16, chunk2(s_E, 0.f, e << 2));
             OTF_STAMP(it, 2);
-            const int q = lane >> 3, c = lane & 7;
+            OTF_MSTAMP(it, 2, 0);
+            OTF_MSTAMP(it, 10, 448);
+            // lane (c = lane >> 3, q = lane & 7): chunk c of member q; the member sum is a
+            // butterfly over the lane's 8 (quad_perm ^1, ^2, half mirror)
+            const int q = lane & 7;
             const bool act = q < ncb;
             I4 x = I4{0, 0, 0, 0};
             if (act) {
-                const uint32_t off = rowx(e, q) + (uint32_t)(w * 8 + c) * 16;
+                const uint32_t off = rowx(e, q) + (uint32_t)(w * 8 + rc) * 16;
                 for (;;) {
                     x = gload(rs, off);
                     if (chunk_at(x, (unsigned)e)) break;
@@ -547,32 +649,37 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
                     __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
                 }
             }
-            T t0 = act ? chunk_v0(x) : (T)0, t1 = act ? chunk_v1(x) : (T)0;
+            OTF_MSTAMP(it, 3, 0);
+            OTF_MSTAMP(it, 9, 448);
+            t0 = act ? chunk_v0(x) : (T)0;
+            t1 = act ? chunk_v1(x) : (T)0;
             vbad = __any(act && (x[1] & 1)) ? 1 : 0;
-            t0 += wave_xor<T, 8>(t0);
-            t1 += wave_xor<T, 8>(t1);
-            t0 += wave_xor<T, 16>(t0);
-            t1 += wave_xor<T, 16>(t1);
-            t0 += wave_xor<T, 32>(t0);
-            t1 += wave_xor<T, 32>(t1);
+            t0 += dpp_f<0xB1>(t0);
+            t1 += dpp_f<0xB1>(t1);
+            t0 += dpp_f<0x4E>(t0);
+            t1 += dpp_f<0x4E>(t1);
+            t0 += dpp_f<0x141>(t0);
+            t1 += dpp_f<0x141>(t1);
             if (check && !err_total(e, errv)) stall = 1;
             stall = __any(stall) ? 1 : 0;
             OTF_STAMP(it, 3);
-            if (lane < 8) {
-                T un0 = (T)1 / (t0 * ia_c0), un1 = (T)1 / (t1 * ia_c1);
-                if (row0 + 2 * lane >= p.n) un0 = 0;
-                if (row0 + 2 * lane + 1 >= p.n) un1 = 0;
-                urow[w][2 * lane] = un0;
-                urow[w][2 * lane + 1] = un1;
-            }
         }
-        __builtin_amdgcn_wave_barrier();  // wave-private LDS hand-off (in-order LDS queue)
+        // u of rows 2c, 2c + 1 in every lane of group c; to every lane as wave-uniform
+        // values (v_readlane, no LDS round trip); the group's first lane keeps the history
         T un[R];
         int badu = 0;
+        {
+            T un0 = (T)1 / (t0 * ia_c0), un1 = (T)1 / (t1 * ia_c1);
+            if (!row_in(row0 + 2 * rc)) un0 = 0;
+            if (!row_in(row0 + 2 * rc + 1)) un1 = 0;
+            badu = __any(!finite_val(un0) || !finite_val(un1)) ? 1 : 0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            un[r] = urow[w][r];
-            badu |= (row0 + r < p.n && !finite_val(un[r])) ? 1 : 0;
+            for (int c = 0; c < 8; ++c) {
+                un[2 * c] = __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, un0), 8 * c));
+                un[2 * c + 1] = __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, un1), 8 * c));
+            }
+            if ((lane & 7) == 0)
+                *reinterpret_cast<F2*>(&uhist[it & 1][w * R + 2 * rc]) = F2{un0, un1};
         }
         // POT's decisions for iterate it - 1 (error) and iterate it (v); identical in
         // every wave of every workgroup unless a wave stalled (then all time out)
@@ -588,11 +695,11 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         // this iteration is not the one a decision below reverts)
         const int slot = it & 1;
         vhist[slot][tid] = vcur[tid];
-        if (lane < R) uhist[slot][w * R + lane] = urow[w][lane];
         if (badu) s_ep[0] = it;
         if (stall) s_ep[4] = it;
         __syncthreads();
         OTF_STAMP(it, 4);
+        OTF_MSTAMP(it, 4, 0);
         if (s_ep[4] == it) { status = OTF_SK_TIMEOUT; done = true; break; }
         if (check) {
             if (lead) p.errlog[n_err] = err;
@@ -609,7 +716,8 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             break;
         }
         publish_cols(e + 1, s_ep[0] == it ? 1 : 0);
-        if (w == 0 && !reduce(e + 1)) s_ep[1] = e + 1;  // seen after the next hop-B barrier
+        OTF_MSTAMP(it, 5, 0);
+        if (w < RW && !reduce(e + 1, chk == 0)) s_ep[1] = e + 1;  // seen after the next hop-B barrier
         OTF_STAMP(it, 5);
     }
     if (!done && p.max_iter > 0) {
@@ -617,7 +725,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         // exchange of the column tiles' partials
         const int it = p.max_iter - 1;
         const int e = p.max_iter + 1;
-        const int fl = gather_b(e);
+        const int fl = gather_b(e, (it % p.check_every) == 0);
         if (fl & 2) {
             status = OTF_SK_TIMEOUT;
         } else if (fl & 1) {
@@ -657,7 +765,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k)
             vo[g][k] = last_good < 0 ? v0 : vhist[hs][(lane + kWave * g) * VEC + k];
-    if (cb == 0 && lane < R && row0 + lane < p.n) {
+    if (cb == 0 && lane < R && row_in(row0 + lane)) {
         T mine = uo[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) if (lane == r) mine = uo[r];
@@ -669,28 +777,28 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
                 const int c = col0 + (lane + kWave * g) * VEC + k;
-                if (c < p.m) p.v_out[c] = vo[g][k];
+                if (col_in(c)) p.v_out[c] = vo[g][k];
             }
     }
     if (p.P) {
         TP* P = (TP*)p.P;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if (row0 + r >= p.n) break;
+            if (!row_in(row0 + r)) break;
             TP* prow = P + (int64_t)(row0 + r) * p.ldp;
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const int c0 = col0 + (lane + kWave * g) * VEC;
-                if (c0 >= p.m) continue;
+                if (!col_in(c0)) continue;
                 VP o;
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) o[k] = (TP)(uo[r] * kv[r][g][k >> 1][k & 1] * vo[g][k]);
-                if (c0 + VEC <= p.m) {
+                if (FULL || c0 + VEC <= m_) {
                     *reinterpret_cast<VP*>(prow + c0) = o;
                 } else {
 #pragma unroll
                     for (int k = 0; k < VEC; ++k)
-                        if (c0 + k < p.m) prow[c0 + k] = o[k];
+                        if (col_in(c0 + k)) prow[c0 + k] = o[k];
                 }
             }
         }
@@ -711,7 +819,11 @@ template <typename CT, typename TP>
 hipError_t launch_mesh_t(int grid, SkMeshArgs& p, hipStream_t s) {
     void* args[] = {&p};
     const bool pow2 = (p.nrb & (p.nrb - 1)) == 0;
-    const void* k = pow2 ? (const void*)sk_mesh_kernel<CT, TP, 4> : (const void*)sk_mesh_kernel<CT, TP, 8>;
+    // the N = 4096 metric shape (32 x 8 whole tiles) has its own compiled-in instance
+    const bool whole = p.n == p.nrb * kMeshTR && p.m == p.ncb * kMeshTC;
+    const void* k = (whole && p.nrb == 32 && p.ncb == 8) ? (const void*)sk_mesh_kernel<CT, TP, 4, 32, 8>
+                    : pow2 ? (const void*)sk_mesh_kernel<CT, TP, 4, 0, 0>
+                           : (const void*)sk_mesh_kernel<CT, TP, 8, 0, 0>;
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
     if (e != hipSuccess) return e;

@@ -49,13 +49,15 @@ def batch_feature_plan(mri_fused: torch.Tensor, pet_fused: torch.Tensor, eps: fl
 
 class _OTAlignLoss(torch.autograd.Function):
     """ot_mri_from_pet = pet_fused @ Tn^T and cosine_loss(mri_fused, ot_mri_from_pet) as
-    one autograd node (MRI_PET_OT_nojax.py:702-725).  ``raw=True``: T is the raw
-    Sinkhorn plan and the post-processing is fused into the apply
-    (otf_plan_postprocess_apply, one pass); else T is the plan to apply as given.
-    A non-finite loss -- or ``ok`` false (a stalled solve, decided on the device) --
-    becomes a constant 0 that sends no gradient to mri_fused / pet_fused, like the
-    reference's swap for torch.tensor(0.0) at :724-725.  The loss gradients are formed
-    in forward (B x d, cheap) so the zeroing is a select, never 0 * NaN."""
+    one autograd node (MRI_PET_OT_nojax.py:702-725), three HIP launches per training
+    step: ``raw=True`` fuses the plan post-processing into the apply
+    (otf_plan_postprocess_apply, one pass; else T is applied as given), the loss and
+    both its gradients come from ONE workgroup (otf_cosine_align), and the backward is
+    ONE launch (otf_ot_align_backward: G @ Tn and the loss scaling).  A non-finite loss
+    -- or ``ok`` false (a stalled solve, decided on the device) -- becomes a constant 0
+    that sends no gradient to mri_fused / pet_fused, like the reference's swap for
+    torch.tensor(0.0) at :724-725; the zeroing is a select in the kernels, never
+    0 * NaN, and needs no host sync."""
 
     @staticmethod
     def forward(ctx, mri, pet, T, ok, raw):
@@ -65,30 +67,16 @@ class _OTAlignLoss(torch.autograd.Function):
         else:
             Tn = T.float().contiguous()
             ot = ops.gemm_f32(pet.float(), Tn, transpose_b=True)
-        with torch.enable_grad():
-            xd = mri.detach().float().requires_grad_(True)
-            yd = ot.detach().requires_grad_(True)
-            loss = cosine_loss(xd, yd)
-            gx, gy = torch.autograd.grad(loss, (xd, yd))
-        keep = torch.isfinite(loss.detach()) & ok
-        zero = torch.zeros((), dtype=loss.dtype, device=loss.device)
-        ctx.save_for_backward(torch.where(keep, gx, zero), torch.where(keep, gy, zero), Tn, keep)
+        loss, gx, gy, keep = ops.cosine_align(mri.detach(), ot, ok)
+        ctx.save_for_backward(gx, gy, Tn, keep)
         ctx.dtypes = (mri.dtype, pet.dtype)
         ctx.mark_non_differentiable(Tn)
-        return torch.where(keep, loss.detach(), zero), ot, Tn
+        return loss, ot, Tn
 
     @staticmethod
     def backward(ctx, g_loss, g_ot, _g_tn):
         gx, gy, Tn, keep = ctx.saved_tensors
-        if g_loss is None:
-            g_loss = torch.zeros((), dtype=gx.dtype, device=gx.device)
-        g_mri = g_loss * gx
-        gyt = g_loss * gy
-        if g_ot is not None:
-            gpet = ops.gemm_f32((gyt + g_ot).contiguous(), Tn)
-        else:   # only the loss used ot: exact zeros when it was dropped (Tn may hold NaN)
-            gpet = torch.where(keep, ops.gemm_f32(gyt.contiguous(), Tn),
-                               torch.zeros((), dtype=gyt.dtype, device=gyt.device))
+        g_mri, gpet = ops.ot_align_backward(gx, gy, Tn, g_loss=g_loss, g_ot=g_ot, keep=keep)
         return g_mri.to(ctx.dtypes[0]), gpet.to(ctx.dtypes[1]), None, None, None
 
 

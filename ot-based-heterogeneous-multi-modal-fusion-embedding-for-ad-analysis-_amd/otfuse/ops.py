@@ -379,6 +379,73 @@ def gemm_f32(A: torch.Tensor, B: torch.Tensor, transpose_b: bool = False) -> tor
     return out
 
 
+def cosine_align(X: torch.Tensor, Y: torch.Tensor, ok: torch.Tensor | None = None):
+    """``1 - mean_b cos(X_b, Y_b)`` with torch's normalize / cosine_similarity clamps
+    (cosine_loss, MRI_PET_OT_nojax.py:552-560) and its gradients, in ONE launch
+    (otf_cosine_align).  X: (B, d) float32 / bfloat16 / float16 (read as stored), Y:
+    (B, d) float32.  ``ok`` (device bool scalar, optional) and a non-finite loss give
+    an exact-zero loss and gradients (the NaN -> 0 swap of :724-725).
+    Returns ``(loss (0-dim float32), gx (B, d), gy (B, d), keep (uint8 scalar))``."""
+    _dev(X, "X")
+    _dev(Y, "Y")
+    if X.dim() == 1:
+        X = X.unsqueeze(0)
+    if Y.dim() == 1:
+        Y = Y.unsqueeze(0)
+    if X.dtype not in _EMB_DT:
+        X = X.float()
+    X = X.contiguous()
+    Y = Y.float().contiguous()
+    B, d = X.shape
+    if tuple(Y.shape) != (B, d):
+        raise ValueError(f"X {tuple(X.shape)} and Y {tuple(Y.shape)} differ")
+    dev = X.device
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    gx = torch.empty((B, d), dtype=torch.float32, device=dev)
+    gy = torch.empty((B, d), dtype=torch.float32, device=dev)
+    keep = torch.empty((), dtype=torch.uint8, device=dev)
+    okp = None
+    if ok is not None:
+        ok = _dev(ok, "ok").to(torch.uint8).reshape(())
+        okp = ok.data_ptr()
+    L.check(L.lib().otf_cosine_align(X.data_ptr(), X.stride(0), _EMB_DT[X.dtype], Y.data_ptr(),
+                                     Y.stride(0), B, d, okp, loss.data_ptr(), gx.data_ptr(), d,
+                                     gy.data_ptr(), d, keep.data_ptr(), L.stream_handle(dev)),
+            "otf_cosine_align")
+    return loss, gx, gy, keep
+
+
+def ot_align_backward(gx: torch.Tensor, gy: torch.Tensor, Tn: torch.Tensor,
+                      g_loss: torch.Tensor | None = None, g_ot: torch.Tensor | None = None,
+                      keep: torch.Tensor | None = None):
+    """Backward of ``ot = pet @ Tn^T`` under the alignment loss in ONE launch
+    (otf_ot_align_backward): ``g_pet = (g_loss * gy + g_ot) @ Tn``, ``g_mri = g_loss * gx``.
+    Without ``g_ot`` and with ``keep == 0`` g_pet is exact zeros (Tn may hold NaN)."""
+    for t, nm in ((gx, "gx"), (gy, "gy"), (Tn, "Tn")):
+        _dev(t, nm)
+    gx = gx.float().contiguous()
+    gy = gy.float().contiguous()
+    Tn = Tn.float().contiguous()
+    B, d = gy.shape
+    d_, d2 = Tn.shape
+    if d_ != d or tuple(gx.shape) != (B, d):
+        raise ValueError("gx / gy (B, d) and Tn (d, d2) do not match")
+    dev = gy.device
+    if g_loss is not None:
+        g_loss = g_loss.float().reshape(()).contiguous()
+    if g_ot is not None:
+        g_ot = g_ot.float().contiguous()
+        if tuple(g_ot.shape) != (B, d):
+            raise ValueError("g_ot must be (B, d)")
+    g_mri = torch.empty((B, d), dtype=torch.float32, device=dev)
+    g_pet = torch.empty((B, d2), dtype=torch.float32, device=dev)
+    L.check(L.lib().otf_ot_align_backward(
+        gx.data_ptr(), d, gy.data_ptr(), d, L.ptr(g_ot), d, L.ptr(g_loss), L.ptr(keep),
+        Tn.data_ptr(), Tn.stride(0), B, d, d2, g_mri.data_ptr(), d, g_pet.data_ptr(), d2,
+        L.stream_handle(dev)), "otf_ot_align_backward")
+    return g_mri, g_pet
+
+
 def plan_postprocess_apply(T: torch.Tensor, Z: torch.Tensor, nan_fill: float = 1e-8,
                            rownorm: bool = True):
     """Fused MRI_PET_OT_nojax.py:702-718 in one pass over the plan: returns
