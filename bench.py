@@ -86,6 +86,7 @@ def parse():
     p.add_argument("--profile-config5", action="store_true",
                    help="with --profile-only: run the config-5 sweep workload instead")
     p.add_argument("--no-gw", action="store_true", help="skip the per-epoch GW latency leg")
+    p.add_argument("--no-f64", action="store_true", help="skip the float64 metric leg")
     p.add_argument("--no-config5", action="store_true",
                    help="skip the N=8192 d=1024 fp16 200-iteration single-GPU leg")
     p.add_argument("--no-batch-ot", action="store_true",
@@ -267,6 +268,8 @@ def main():
         out["gw_per_epoch"] = gw_leg(dev, world == 1 and not args.no_cpu_baseline)
     if rank == 0 and not args.no_config5:
         out["sweep_config5"] = config5_leg(dev)
+    if rank == 0 and not args.no_f64:
+        out["metric_f64"] = metric_f64_leg(dev, N, d, iters, eps)
     if rank == 0 and not args.no_batch_ot:
         out["batch_ot_per_step"] = batch_ot_leg(dev, world == 1 and not args.no_cpu_baseline)
     if world > 1 or args.multi_legs:
@@ -397,6 +400,50 @@ def config5_leg(dev, N=8192, d=1024, iters=200, eps=0.1, reps=4):
                          "note": "N*N*2 B read per sweep (the fp16 cost, streamed every iteration "
                                  "from the Infinity Cache); per-sweep time = solve without the "
                                  "plan / (iters + 1); the plan write is timed separately"}}
+
+
+def metric_f64_leg(dev, N=4096, d=512, iters=100, eps=0.1, reps=3):
+    """The metric config in the reference's own precision (POT runs NumPy float64,
+    MRI_PET_OT_nojax.py:143): float64 pairwise cost from the float32 embeddings
+    (otf_cost_pairwise_f64, POT euclidean_distances order, divided by its max) and a
+    float64 POT Sinkhorn, 100 iterations, float64 plan.  The float64 cost (128 MiB) does
+    not fit the register files, so the sweep engine streams it once per iteration: its
+    roofline is the N*N*8 bytes read per sweep against HBM (the cost is Infinity-Cache
+    resident at this size).  Parity: tests/test_gpu_precision.py (1e-9 of the oracle)."""
+    import numpy as np
+    from otfuse import gw, ops
+    from otfuse.synthetic import paired_embeddings
+    X, Y, _ = paired_embeddings(N, d, seed=1234)
+    Xd = torch.from_numpy(X).to(dev)
+    Yd = torch.from_numpy(Y).to(dev)
+    a = torch.full((N,), 1.0 / N, device=dev, dtype=torch.float64)
+    ws = ops.sinkhorn_workspace(N, N, torch.float64, iters, dev)
+    P = torch.empty((N, N), dtype=torch.float64, device=dev)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tc, ts = [], []
+    res = None
+    for _ in range(reps):
+        e[0].record()
+        C, _ = gw.pairwise_cost_f64(Xd, Yd, scale_max=True)
+        e[1].record()
+        res = ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, workspace=ws, plan_out=P)
+        e[2].record()
+        torch.cuda.synchronize()
+        tc.append(e[0].elapsed_time(e[1]))
+        ts.append(e[1].elapsed_time(e[2]))
+        del C
+    k = len(tc) // 2
+    tc, ts = sorted(tc)[k], sorted(ts)[k]
+    info = res.info()
+    sweep_us = ts * 1e3 / (iters + 1)
+    gbs = N * N * 8 / (sweep_us * 1e-6) / 1e9
+    return {"N": N, "d": d, "iters": iters, "eps": eps, "dtype": "f64",
+            "engine": info["engine_name"], "status": info["status_name"],
+            "cost_ms": tc, "sinkhorn_incl_plan_ms": ts, "ms_per_step": tc + ts,
+            "pairs_per_s": N / ((tc + ts) * 1e-3), "sinkhorn_iters_per_s": iters / (ts * 1e-3),
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS,
+                         "note": "N*N*8 B per sweep (iters + 1 sweeps incl. the plan pass)"}}
 
 
 def gw_leg(dev, with_cpu, labels=2, per_label=64, d=512, eps=5e-3):

@@ -136,6 +136,8 @@ typedef struct {
     int32_t break_iter; /* iteration of the numerical break, or -1                     */
     int32_t engine;     /* engine that ran (otf_engine)                                */
     int32_t stalled;    /* persistent engines: 1 if any workgroup hit the stall timeout */
+    int32_t fallback;   /* 1 if the persistent engine could not become co-resident and
+                           the one-workgroup fallback solved the problem instead       */
 } otf_sinkhorn_info;
 
 /* Library identification; returns a static string ("otfuse <ver> gfx950"). */
@@ -238,6 +240,11 @@ int otf_coupled_cost(const float* A, int64_t a0, int64_t a1, const float* B, int
  * Layout requirements: ldc and ldp multiples of 16/sizeof(dtype) and 16-B
  * aligned rows.  Workspace: otf_sinkhorn_workspace_size() bytes.
  * Host synchronisation happens only if opts->sync_every > 0.                   */
+/* Number of solves (process-wide, since load) that the one-workgroup fallback had to
+ * finish because a persistent engine's grid could not become co-resident within
+ * OTF_REG_MS (otf_sinkhorn_info.fallback marks the solve itself).  Synchronous.     */
+int otf_sinkhorn_fallback_count(uint64_t* count);
+
 size_t otf_sinkhorn_workspace_size(int64_t n, int64_t m, int32_t dtype, int32_t max_iter);
 int otf_sinkhorn(const void* a, const void* b, const void* C, int64_t n, int64_t m, int64_t ldc,
                  int32_t dtype, const void* cost_scale, const otf_sinkhorn_opts* opts,

@@ -514,3 +514,101 @@ def sinkhorn_knopp_np(a, b, M, reg, numItermax=1000, stopThr=1e-9, check_every=1
             if err < stopThr:
                 break
     return u.reshape(-1, 1) * K * v.reshape(1, -1), u, v, {"niter": niter, "err": errs}
+
+
+def sinkhorn_scaling_np(a, b, K, numItermax=1000, stopThr=1e-9):
+    """perturbot ``sinkhorn_scaling`` (utils.py:6-115) restated: POT's scaling
+    iteration on a GIVEN kernel matrix K (no exp), revert-and-break on a zero K^T u or a
+    non-finite scaling, marginal error as the SQUARED 2-norm every 10 iterations.
+    Returns the plan u K v."""
+    a, b, K = _d(a), _d(b), _d(K)
+    u = np.ones(len(a)) / len(a)
+    v = np.ones(len(b)) / len(b)
+    Kp = (1 / a).reshape(-1, 1) * K
+    for ii in range(int(numItermax)):
+        uprev, vprev = u, v
+        ktu = K.T @ u
+        v = b / ktu
+        u = 1.0 / (Kp @ v)
+        if (np.any(ktu == 0) or np.any(np.isnan(u)) or np.any(np.isnan(v))
+                or np.any(np.isinf(u)) or np.any(np.isinf(v))):
+            u, v = uprev, vprev
+            break
+        if ii % 10 == 0:
+            err = np.sum((np.einsum("i,ij,j->j", u, K, v) - b) ** 2)
+            if not err > stopThr:   # the reference's `while err > stopThr`
+                break
+    return u.reshape(-1, 1) * K * v.reshape(1, -1)
+
+
+def beta_kernel(n, m):
+    """The random matrix of perturbot ``random_gamma_init`` (utils.py:118-122): a dense
+    scipy.sparse.random(n, m, density=1) with Beta(0.1, 0.1) entries, drawn from
+    NumPy's global generator exactly as the reference draws it."""
+    from scipy import stats
+    from scipy.sparse import random as sprandom
+    return sprandom(n, m, density=1, data_rvs=stats.beta(1e-1, 1e-1).rvs).toarray()
+
+
+def random_gamma_init_np(p, q, numItermax=1000, stopThr=1e-9):
+    return sinkhorn_scaling_np(p, q, beta_kernel(len(p), len(q)), numItermax, stopThr)
+
+
+def cotl_np(X_dict, Y_dict, eps=5e-3, niter=100, algo="sinkhorn", algo2="sinkhorn", C_lin=None,
+            random_init=False):
+    """cot_labels.py:14-225 (cotl_numpy) restated with every branch the reference has:
+    per-stage solver algo (sample plans) / algo2 (feature plan) each 'sinkhorn' (OTT
+    linear.solve on the max-scaled cost at reg, restated by the C log-domain Sinkhorn)
+    or 'emd' (pot.emd -> emd_lp); the sample-cost prior C_lin added to every M_k (:175-176);
+    random_init: Ts[k] = random_gamma_init(w1[k], w2[k]) for the labels in order, then
+    Tv = random_gamma_init(v1, v2) (:133-135).  Quirks kept: feature solve at reg (:200),
+    Tv-only delta (Tsold aliases Ts), Tv renormalisation, stop on delta < 1e-16 or
+    |cost change| < 1e-7."""
+    labels = list(X_dict.keys())
+
+    def hist(D):
+        Xc = np.concatenate([np.asarray(D[k]) for k in labels], axis=0)
+        if (Xc >= 0).all():
+            return np.asarray(Xc.sum(axis=0) / Xc.sum(), dtype=np.float64)
+        return np.ones(Xc.shape[1]) / Xc.shape[1]
+
+    v1, v2 = hist(X_dict), hist(Y_dict)
+    X = {k: np.asarray(X_dict[k], np.float32) for k in labels}
+    Y = {k: np.asarray(Y_dict[k], np.float32) for k in labels}
+    w1 = {k: np.ones(len(X[k])) / len(X[k]) for k in labels}
+    w2 = {k: np.ones(len(Y[k])) / len(Y[k]) for k in labels}
+    d, d2 = X[labels[0]].shape[1], Y[labels[0]].shape[1]
+    if random_init:
+        Ts = {k: random_gamma_init_np(w1[k], w2[k]) for k in labels}
+        Tv = random_gamma_init_np(v1, v2)
+    else:
+        Ts = {k: np.ones((len(X[k]), len(Y[k]))) / (len(X[k]) * len(Y[k])) for k in labels}
+        Tv = np.ones((d, d2)) / (d * d2)
+
+    def ott(M):
+        n, m = M.shape
+        P, *_ = sinkhorn_log(np.ones(n) / n, np.ones(m) / m, M, eps, max_iter=2000,
+                             threshold=1e-3, cscale=1.0 / M.max())
+        return P
+
+    cost, costs = np.inf, []
+    for _ in range(niter):
+        Tvold, costold = Tv, cost
+        for k in labels:
+            Mk = coupled_cost_np(X[k], Y[k], Tv, v1, v2)
+            if C_lin is not None:
+                Mk = Mk + C_lin
+            Ts[k] = emd_lp(w1[k], w2[k], Mk)[0] if algo == "emd" else ott(Mk)
+        M = 0
+        for k in labels:
+            M = M + coupled_cost_np(X[k].T, Y[k].T, Ts[k], w1[k], w2[k])
+        Tv = emd_lp(v1, v2, M)[0] if algo2 == "emd" else ott(M)
+        if not np.abs(Tv.sum() - 1.0) < 1e-8:
+            Tv = Tv / Tv.sum()
+        delta = np.linalg.norm(Tv - Tvold)
+        cost = np.sum(M * Tv)
+        costs.append(cost)
+        if delta < 1e-16 or np.abs(costold - cost) < 1e-7:
+            break
+    return Ts, Tv, cost, {"cost": costs}
+

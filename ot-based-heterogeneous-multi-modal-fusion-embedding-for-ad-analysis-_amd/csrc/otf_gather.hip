@@ -69,6 +69,7 @@ template <typename T> struct SkGatherArgs {
     void* P;
     int64_t ldp;
     unsigned long long timeout_ticks;
+    unsigned long long reg_ticks;  // the first wait (registration / first hop)
 };
 
 using I4 = __attribute__((ext_vector_type(4))) int;
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
     const int n_ = FULL ? SNWG * TR : p.n, m_ = FULL ? Cf::C : p.m;
     auto row_in = [&](int r) -> bool { return FULL || r < n_; };
     auto col_in = [&](int c) -> bool { return FULL || c < m_; };
-    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.reg_ticks;
     // Team mode: the launch has 8 x nwg workgroups; each registers on its hardware XCC
     // and the first XCC whose first nwg registrants are all resident claims the solve,
     // every other workgroup returns at once.  The team's hand-offs then stay inside one
@@ -147,6 +148,10 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
             if (keep) {
                 // wait until this XCC's team is complete or another team has claimed
                 for (;;) {
+                    if (load_agent(&p.info->stalled)) {  // another registrant gave up
+                        keep = 0;
+                        break;
+                    }
                     const int claim = load_agent(p.team + 8 * 64);
                     if (claim != 0) {
                         keep = claim == xcd + 1;
@@ -611,6 +616,7 @@ hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, co
     p.P = P_out;
     p.ldp = ldp;
     p.timeout_ticks = stall_ticks();
+    p.reg_ticks = reg_stall_ticks();
     hipError_t e = hipMemsetAsync(region, 0, gather_region_bytes<T>(n, m), s);
     if (e != hipSuccess) return e;
     const int grid = (int)gather_grid<T>(n);

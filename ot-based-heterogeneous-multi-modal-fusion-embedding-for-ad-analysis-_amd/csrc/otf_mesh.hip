@@ -83,6 +83,7 @@ struct SkMeshArgs {
     void* P;
     int64_t ldp;
     unsigned long long timeout_ticks;
+    unsigned long long reg_ticks;  // the first wait (registration / first hop)
 };
 
 // Diagnostic build only (-DOTF_MESH_STAMPS, tools/stamps_mesh.hip): per-hop wall-clock
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     __shared__ int red_cnt;           // reducer-wave ticket of this epoch
     int tid = threadIdx.x, lane = tid & 63;
     const int w = (int)threadIdx.x >> 6;
-    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.reg_ticks;
     constexpr bool FULL = SNRB != 0 && SNCB != 0;
     const int nrb = FULL ? SNRB : p.nrb, ncb = FULL ? SNCB : p.ncb;
     const int CPR = FULL ? pow2_at_least((kMeshNCH + SNRB - 1) / (SNRB > 0 ? SNRB : 1)) : p.cpr;
@@ -210,7 +211,8 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         const int xcd = xcc_id();
         if (tid == 0)
             s_reg[0] = __hip_atomic_fetch_add(p.xreg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool ok = grid_barrier(p.xreg + 8 * 64, gridDim.x, deadline, p.timeout_ticks, &s_reg[3]);
+        const bool ok = grid_barrier(p.xreg + 8 * 64, gridDim.x, deadline, p.timeout_ticks, &s_reg[3],
+                                     &p.info->stalled);
         if (tid == 0) {
             // the first ncb XCCs (by id) holding >= nrb registrants are the column tiles;
             // registrants beyond slot nrb - 1 and XCCs past the ncb-th leave
@@ -921,6 +923,7 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
     p.P = P_out;
     p.ldp = ldp;
     p.timeout_ticks = stall_ticks();
+    p.reg_ticks = reg_stall_ticks();
     if (!zeroed) {  // else the Sinkhorn init kernel zeroed it
         const hipError_t e = hipMemsetAsync(region, 0, mesh_region_bytes(n, m), s);
         if (e != hipSuccess) return e;

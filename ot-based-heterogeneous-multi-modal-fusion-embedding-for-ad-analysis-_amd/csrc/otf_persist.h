@@ -60,6 +60,19 @@ inline unsigned long long stall_ticks() {
     return ms > 0 ? (unsigned long long)ms * 100000ull : kStallTicks;
 }
 
+// The first device-wide wait of a persistent launch (its registration, or its first
+// hop) gives up much sooner: a grid that is not co-resident after OTF_REG_MS (default
+// 50 ms; a healthy launch registers within microseconds of its prologue) sets
+// info->stalled, and the one-workgroup fallback queued behind it (sk_solo_kernel)
+// solves the problem instead of the caller waiting out the 5-s stall limit.
+inline unsigned long long reg_stall_ticks() {
+    const char* e = getenv("OTF_REG_MS");
+    const long long ms = e ? atoll(e) : 50;
+    const unsigned long long t = (unsigned long long)(ms > 0 ? ms : 50) * 100000ull;
+    const unsigned long long st = stall_ticks();
+    return t < st ? t : st;
+}
+
 // XCD this wave runs on (0..7).  Only speed depends on it (replica choice, grouping).
 __device__ __forceinline__ int xcc_id() {
     int v;
@@ -97,20 +110,31 @@ __device__ __forceinline__ void store_sum_vec(__amdgpu_buffer_rsrc_t rs, uint32_
 // Device-wide flat barrier: every wave drains its own memory operations, one lane per
 // workgroup arrives on the counter and polls it.  Returns false on a stall (flag
 // broadcast via LDS); re-arms `deadline` on success.
+// abandon (nullable, the solve's info->stalled): a registration barrier's give-up word.
+// The workgroup whose deadline passes raises it; every other one -- waiting, or arriving
+// late after the others left (a grid that was not co-resident) -- sees it and fails too,
+// instead of completing the count with workgroups that are gone.
 __device__ __forceinline__ bool grid_barrier(int* bar, int target, unsigned long long& deadline,
-                                             unsigned long long stall, int* s_flag) {
+                                             unsigned long long stall, int* s_flag,
+                                             int* abandon = nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         int ok = 1;
         __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         while (load_agent(bar) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() > deadline) {
+            if (abandon && load_agent(abandon)) {
                 ok = 0;
                 break;
             }
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() > deadline) {
+                ok = 0;
+                if (abandon) store_wt(abandon, 1);
+                break;
+            }
         }
+        if (ok && abandon && load_agent(abandon)) ok = 0;
         *s_flag = ok;
     }
     __syncthreads();

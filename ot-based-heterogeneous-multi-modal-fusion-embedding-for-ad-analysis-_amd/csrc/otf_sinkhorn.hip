@@ -129,7 +129,7 @@ __device__ __forceinline__ double marginal_err(const SkArgs<T>& p, const T* vit,
 // (chunk q = tid + NT*g), R rows per row block; K values for a row block stay in
 // registers (R*G*VEC of them) between the row reduction and the column update.
 template <typename T, typename CT, bool LOG, int G, int R>
-__global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
+__device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p) {
     constexpr int VEC = Vec<T>::N;
     using V = typename Vec<T>::type;
     __shared__ __attribute__((aligned(16))) T colbuf[512 * G * VEC];  // column partials
@@ -356,6 +356,10 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
     // ---- zero the column-sum buffer of the next pass (nobody touches it now)
     for (int j = blockIdx.x * NT + tid; j <= p.m_pad; j += gridDim.x * NT) p.cs_zero[j] = 0;
 }
+template <typename T, typename CT, bool LOG, int G, int R>
+__global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
+    sk_pass_body<T, CT, LOG, G, R>(p);
+}
 
 template <typename T>
 __global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, T* a_pad, T* b_pad,
@@ -385,6 +389,7 @@ __global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, 
         info->break_iter = -1;
         info->engine = OTF_ENGINE_STREAM;
         info->stalled = 0;
+        info->fallback = 0;
     }
 }
 
@@ -404,7 +409,7 @@ __global__ __launch_bounds__(256) void sk_colmin_kernel(const CT* C, int64_t ldc
 
 // Decides the outcome of the last pass when the loop ran to max_iter.
 template <typename T, bool LOG>
-__global__ __launch_bounds__(512) void sk_finalize_kernel(SkArgs<T> p, int max_iter) {
+__device__ __forceinline__ void sk_finalize_body(const SkArgs<T>& p, int max_iter) {
     __shared__ T red[17 * 2];
     __shared__ int s_flag;
     if (threadIdx.x == 0) s_flag = __hip_atomic_load(&p.info->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -443,6 +448,10 @@ __global__ __launch_bounds__(512) void sk_finalize_kernel(SkArgs<T> p, int max_i
         if (is_conv(p, err)) status = OTF_SK_CONVERGED;
     }
     if (lead) sk_stop(p.info, it, it, status, -1);
+}
+template <typename T, bool LOG>
+__global__ __launch_bounds__(512) void sk_finalize_kernel(SkArgs<T> p, int max_iter) {
+    sk_finalize_body<T, LOG>(p, max_iter);
 }
 
 // Copies the scalings of info->last_good (or the initial ones) to the outputs.
@@ -498,6 +507,118 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const CT* C, int64_t ldc, 
 }
 
 // ============================================================================
+// Solo fallback: the whole POT solve in ONE workgroup, enqueued behind every persistent
+// engine launch on the same stream.  A persistent engine needs its whole grid
+// co-resident; when other kernels hold CUs (RCCL kernels under DDP, a second solve on
+// another stream) its registration gives up after OTF_REG_MS and sets info->stalled.
+// This kernel then returns the right answer instead of a timeout: a single workgroup is
+// always schedulable, its __syncthreads is a grid barrier, so the streaming pass runs
+// as a loop (every row block per pass, an L1 invalidate between passes for the sums the
+// memory-side atomics wrote), then the finalize / output / plan steps.  When the
+// persistent solve succeeded (stalled == 0, the normal case) it returns at once: one
+// empty dispatch per solve, no host synchronisation either way.  Every fallback bumps
+// g_sk_fallbacks (otf_sinkhorn_fallback_count) and sets info->fallback.
+// ============================================================================
+__device__ unsigned long long g_sk_fallbacks;
+
+template <typename T> struct SoloArgs {
+    T* cs;              // 3 x cs_stride column-sum ring (stream engine layout)
+    T* u2;              // 2 x n scalings by iteration parity
+    T* v2;              // 2 x m_pad
+    int64_t cs_stride;
+    int max_iter;
+    T* u_out;
+    T* v_out;
+    void* P;
+    int64_t ldp;
+    int p_f64;
+};
+
+template <typename T, typename CT, int G, int R>
+__global__ __launch_bounds__(512) void sk_solo_kernel(SkArgs<T> p, SoloArgs<T> x) {
+    __shared__ int s_go;
+    if (threadIdx.x == 0) s_go = __hip_atomic_load(&p.info->stalled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (!s_go) return;
+    const int tid = threadIdx.x, NT = blockDim.x;
+    auto sync_mem = [&]() {  // drain, barrier, and drop this CU's stale L1 lines
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    };
+    // fresh state: the abandoned persistent solve may have written the info words
+    for (int64_t j = tid; j < 3 * x.cs_stride; j += NT) x.cs[j] = 0;
+    for (int j = tid; j < 2 * p.n; j += NT) x.u2[j] = 0;
+    for (int j = tid; j < 2 * p.m_pad; j += NT) x.v2[j] = 0;
+    if (tid == 0) {
+        p.info->stop = 0;
+        p.info->last_good = -1;
+        p.info->niter = 0;
+        p.info->status = OTF_SK_RUNNING;
+        p.info->n_err = 0;
+        p.info->break_iter = -1;
+    }
+    sync_mem();
+    auto set_pass = [&](SkArgs<T>& q, int pass) {
+        const int it = pass - 1;
+        q.it = it;
+        q.cs_src = pass >= 1 ? x.cs + (size_t)((pass - 1) % 3) * x.cs_stride : nullptr;
+        q.cs_dst = x.cs + (size_t)(pass % 3) * x.cs_stride;
+        q.cs_zero = x.cs + (size_t)((pass + 1) % 3) * x.cs_stride;
+        q.u_cur = x.u2 + (size_t)(it & 1) * p.n;
+        q.v_cur = x.v2 + (size_t)(it & 1) * p.m_pad;
+        q.u_prev = x.u2 + (size_t)((it - 1) & 1) * p.n;
+        q.v_prev = x.v2 + (size_t)((it - 1) & 1) * p.m_pad;
+    };
+    for (int pass = 0; pass <= x.max_iter; ++pass) {
+        SkArgs<T> q = p;
+        set_pass(q, pass);
+        sk_pass_body<T, CT, false, G, R>(q);
+        sync_mem();
+        if (__hip_atomic_load(&p.info->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    }
+    {
+        SkArgs<T> q = p;
+        set_pass(q, x.max_iter + 1);
+        q.it = x.max_iter - 1;
+        q.v_cur = x.v2 + (size_t)(q.it & 1) * p.m_pad;
+        sk_finalize_body<T, false>(q, x.max_iter);
+    }
+    sync_mem();
+    // outputs: the scalings of last_good (or the initial ones), then the plan
+    const int lg = p.info->last_good;
+    const T u0 = (T)1 / (T)p.n_total, v0 = (T)1 / (T)p.m;
+    for (int i = tid; i < p.n; i += NT) x.u_out[i] = lg >= 0 ? x.u2[(lg & 1) * p.n + i] : u0;
+    for (int j = tid; j < p.m; j += NT) x.v_out[j] = lg >= 0 ? x.v2[(lg & 1) * p.m_pad + j] : v0;
+    sync_mem();
+    if (x.P) {
+        const double unit = exp_unit<T>();
+        double cinv = 1.0;
+        if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
+        const T ks = (T)(-unit / p.reg * cinv);
+        const CT* C = (const CT*)p.C;
+        for (int row = 0; row < p.n; ++row) {
+            const T ui = x.u_out[row];
+            for (int j = tid; j < p.m; j += NT) {
+                const T val = ui * fast_exp((T)C[(int64_t)row * p.ldc + j] * ks) * x.v_out[j];
+                if (x.p_f64) ((double*)x.P)[(int64_t)row * x.ldp + j] = (double)val;
+                else ((float*)x.P)[(int64_t)row * x.ldp + j] = (float)val;
+            }
+        }
+    }
+    if (tid == 0) {
+        p.info->engine = OTF_ENGINE_STREAM;
+        p.info->fallback = 1;
+        p.info->stalled = 0;
+        atomicAdd(&g_sk_fallbacks, 1ull);
+    }
+}
+
+// ============================================================================
 // Resident engine: ONE persistent launch for the whole solve (POT flavour).
 //
 // Workgroup w owns row block w (R rows x all m columns) and keeps K = exp(-C/reg)
@@ -538,6 +659,7 @@ template <typename T> struct SkResArgs {
     int64_t ldp;
     int p_f64;
     unsigned long long timeout_ticks;
+    unsigned long long reg_ticks;  // the first wait (registration / first hop)
 };
 
 
@@ -557,7 +679,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     const int NT = blockDim.x;
     const int nwg = gridDim.x;
     const bool lead = (blockIdx.x == 0 && tid == 0);
-    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.reg_ticks;
 
     const double unit = exp_unit<T>();
     double cinv = 1.0;
@@ -705,7 +827,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
     // register on this XCD's population, then the one flat barrier of the launch
     if (tid == 0)
         __hip_atomic_fetch_add(p.sync.reg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!grid_barrier(p.bar, nwg, deadline, p.timeout_ticks, &s_flag)) {
+    if (!grid_barrier(p.bar, nwg, deadline, p.timeout_ticks, &s_flag, &p.info->stalled)) {
         status = OTF_SK_TIMEOUT;
         done = true;
     }
@@ -976,6 +1098,7 @@ template <typename T> struct SkTileArgs {
     void* P;
     int64_t ldp;
     unsigned long long timeout_ticks;
+    unsigned long long reg_ticks;  // the first wait (registration / first hop)
 };
 
 
@@ -996,7 +1119,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nwg = gridDim.x;
     const bool lead = (blockIdx.x == 0 && tid == 0);
-    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.reg_ticks;
 
     // tile of this workgroup; groups (row blocks) on one XCD when nrb % 8 == 0
     int rb, cb;
@@ -1152,7 +1275,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
     bool done = false;
     if (tid == 0)
         __hip_atomic_fetch_add(p.sync.reg + xcd * 64, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!grid_barrier(p.bar, nwg, deadline, p.timeout_ticks, &s_flag)) {
+    if (!grid_barrier(p.bar, nwg, deadline, p.timeout_ticks, &s_flag, &p.info->stalled)) {
         status = OTF_SK_TIMEOUT;
         done = true;
     }
@@ -1413,6 +1536,17 @@ hipError_t launch_pass(const PassCfg& c, int grid, const SkArgs<T>& p, hipStream
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// OTF_FALLBACK=0 launches no solo fallback behind the persistent engines (A/B timing);
+// a persistent solve that cannot become co-resident then ends in OTF_SK_TIMEOUT
+inline bool fallback_enabled() {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = getenv("OTF_FALLBACK");
+        env = e ? atoi(e) : 1;
+    }
+    return env != 0;
+}
+
 struct Workspace {
     void* a_pad;
     void* b_pad;
@@ -1554,6 +1688,7 @@ hipError_t run_resident(const PassCfg& cfg, int grid, const CT* C, int64_t ldc, 
     p.ldp = ldp;
     p.p_f64 = P_dtype == OTF_F64;
     p.timeout_ticks = stall_ticks();
+    p.reg_ticks = reg_stall_ticks();
     hipError_t e = hipMemsetAsync(w.res, 0, w.res_bytes, s);
     if (e != hipSuccess) return e;
     if (P_out && P_dtype == OTF_F64) return launch_resident<T, CT, double>(cfg, grid, p, s);
@@ -1618,6 +1753,7 @@ hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const T* cost_scale
     p.P = P_out;
     p.ldp = ldp;
     p.timeout_ticks = stall_ticks();
+    p.reg_ticks = reg_stall_ticks();
     hipError_t e = hipMemsetAsync(w.res, 0, w.res_bytes, s);
     if (e != hipSuccess) return e;
     const int grid = (int)(w.t_nrb * w.t_ncb);
@@ -1738,6 +1874,28 @@ int sk_finish(SkArgs<T>& p, const SkSetup<T>& su, const CT* C, int64_t ldc, int6
     return OTF_OK;
 }
 
+// The one-workgroup fallback behind a persistent engine launch (sk_solo_kernel): a no-op
+// dispatch unless the persistent solve stalled.
+template <typename T, typename CT>
+hipError_t launch_solo(const SkSetup<T>& su, const CT* C, int64_t ldc, int64_t n, int64_t m,
+                       const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out,
+                       void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
+                       double* errlog, hipStream_t s) {
+    if (!fallback_enabled()) return hipSuccess;
+    SkArgs<T> p = sk_args<T, CT, false>(su, C, ldc, n, m, cost_scale, o, info, errlog, false);
+    SoloArgs<T> x{(T*)su.w.cs, (T*)su.w.u2, (T*)su.w.v2, su.w.cs_stride, o.max_iter, u_out, v_out,
+                  P_out, ldp, P_dtype == OTF_F64 ? 1 : 0};
+    const PassCfg& c = su.cfg;
+    switch (c.G) {
+        case 1: sk_solo_kernel<T, CT, 1, pass_rows<T>(1)><<<1, c.NT, 0, s>>>(p, x); break;
+        case 2: sk_solo_kernel<T, CT, 2, pass_rows<T>(2)><<<1, c.NT, 0, s>>>(p, x); break;
+        case 4: sk_solo_kernel<T, CT, 4, pass_rows<T>(4)><<<1, c.NT, 0, s>>>(p, x); break;
+        case 8: sk_solo_kernel<T, CT, 8, pass_rows<T>(8)><<<1, c.NT, 0, s>>>(p, x); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 // OTF_GATHER=0 keeps AUTO off the gather engine (A/B measurements); GATHER still forces it
 inline bool gather_enabled() {
     static int env = -1;
@@ -1791,7 +1949,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         const hipError_t e = run_gather<T, CT>(C, ldc, (int)n, (int)m, (const T*)su.w.a_pad,
                                                (const T*)su.w.b_pad, cost_scale, o, su.w.gather, u_out,
                                                v_out, P_out, ldp, P_dtype, info, errlog, s);
-        if (e == hipSuccess) return OTF_OK;
+        if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_GATHER) return check_hip(e);
     }
@@ -1808,7 +1966,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
                                               (const float*)su.w.b_pad, cost_scale, o, su.w.mesh,
                                               u_out, v_out, P_out, ldp, P_dtype, info, errlog,
                                               /*zeroed=*/mesh_pick, s);
-            if (e == hipSuccess) return OTF_OK;
+            if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
             (void)hipGetLastError();
             if (o.engine == OTF_ENGINE_MESH) return check_hip(e);
         }
@@ -1818,9 +1976,11 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         if (LOG || avg_pass_ms || !(o.engine == OTF_ENGINE_AUTO || o.engine == OTF_ENGINE_SWEEP) ||
             o.max_iter < 1 || !sweep_supported<T, CT>(n, m, ldc) || !whole)
             return OTF_EUNSUPPORTED;
-        return check_hip(run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
-                                          (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
-                                          v_out, P_out, ldp, P_dtype, info, errlog, s));
+        const hipError_t e = run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
+                                              (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
+                                              v_out, P_out, ldp, P_dtype, info, errlog, s);
+        if (e != hipSuccess) return check_hip(e);
+        return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
     }
     // resident engine: the whole solve in one persistent launch when every row block
     // gets its own CU (POT flavour, no per-pass profiling requested)
@@ -1839,7 +1999,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         Workspace w = su.w;
         const hipError_t e = run_tiled<T, CT>(C, ldc, (int)n, (int)m, cost_scale, o, w, u_out, v_out,
                                               P_out, ldp, P_dtype, info, errlog, s);
-        if (e == hipSuccess) return OTF_OK;
+        if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_TILED) return check_hip(e);
     }
@@ -1853,7 +2013,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         const hipError_t e = run_resident<T, CT>(su.cfg, su.nrb, C, ldc, (int)n, (int)m, cost_scale,
                                                  o, w, u_out, v_out, P_out, ldp, P_dtype, info,
                                                  errlog, s);
-        if (e == hipSuccess) return OTF_OK;
+        if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_RESIDENT) return check_hip(e);
         // co-residency refused (e.g. a smaller device): fall back to the sweep engine
@@ -1867,7 +2027,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         const hipError_t e = run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
                                               (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
                                               v_out, P_out, ldp, P_dtype, info, errlog, s);
-        if (e == hipSuccess) return OTF_OK;
+        if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_SWEEP) return check_hip(e);
     }
@@ -1997,6 +2157,15 @@ int dispatch(const void* a, const void* b, const void* C, int64_t n, int64_t m, 
 }  // namespace otf
 
 extern "C" {
+
+int otf_sinkhorn_fallback_count(uint64_t* count) {
+    if (!count) return OTF_EINVAL;
+    unsigned long long v = 0;
+    OTF_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(otf::g_sk_fallbacks), sizeof(v)));
+    *count = (uint64_t)v;
+    return OTF_OK;
+}
+
 
 size_t otf_sinkhorn_workspace_size(int64_t n, int64_t m, int32_t dtype, int32_t max_iter) {
     const size_t esz = dtype == OTF_F64 ? 8 : 4;

@@ -63,6 +63,7 @@ template <typename T> struct SkSweepArgs {
     void* P;
     int64_t ldp;
     unsigned long long stall_ticks;
+    unsigned long long reg_ticks;  // the first wait (registration / first hop)
     int nt_loads;       // 1: cost larger than the Infinity Cache, stream it non-temporal
     int det;            // 1: fixed-order column sums (one group = the whole grid, no atomics)
     int nres;           // row blocks per workgroup kept in LDS (< the fewest blocks any has)
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nwg = gridDim.x;
     const bool lead = (blockIdx.x == 0 && tid == 0);
-    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.stall_ticks;
+    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.reg_ticks;
 
     const double unit = exp_unit<T>();
     double cinv = 1.0;
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         s_pop[3] = __hip_atomic_fetch_add(p.sync.reg + xcd * 64, 1, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
     }
-    bool reg_ok = grid_barrier(p.bar, nwg, deadline, p.stall_ticks, &s_flag);
+    bool reg_ok = grid_barrier(p.bar, nwg, deadline, p.stall_ticks, &s_flag, &p.info->stalled);
     if (tid == 0) {
         int nact = 0, base = 0;
         unsigned mask = 0;
@@ -860,6 +861,7 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     p.P = P_out;
     p.ldp = ldp;
     p.stall_ticks = stall_ticks();
+    p.reg_ticks = reg_stall_ticks();
     p.nt_loads = (double)n * ldc * sizeof(CT) > 192.0 * (1 << 20) ? 1 : 0;
     p.det = o.deterministic ? 1 : 0;
     hipError_t e = hipMemsetAsync(region, 0, sweep_ctrl_bytes(m_pad, sizeof(T)), s);

@@ -74,8 +74,9 @@ class EmdProblem(ctypes.Structure):
 
 EMD_STATUS = {0: "optimal", 1: "max_iter", 2: "infeasible", 3: "unbounded"}
 
-INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "engine", "stalled")
-INFO_INT32S = len(INFO_FIELDS)  # otf_sinkhorn_info is 8 x int32
+INFO_FIELDS = ("stop", "last_good", "niter", "status", "n_err", "break_iter", "engine", "stalled",
+               "fallback")
+INFO_INT32S = len(INFO_FIELDS)  # otf_sinkhorn_info is 9 x int32
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -101,6 +102,7 @@ _SIGS = {
                                         _vp, _i64, _vp, _vp, _vp, _i64, _vp, ctypes.c_size_t,
                                         _vp]),
     "otf_sinkhorn_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i32, _i32]),
+    "otf_sinkhorn_fallback_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "otf_sinkhorn": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
                                     ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _i64, _i32, _vp,
                                     _vp, _vp, ctypes.c_size_t, _vp]),

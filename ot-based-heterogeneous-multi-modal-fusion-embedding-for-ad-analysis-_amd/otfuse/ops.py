@@ -8,6 +8,7 @@ checked here so the C side only sees layouts it supports; anything else raises.
 from __future__ import annotations
 
 import ctypes
+import warnings
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -252,8 +253,20 @@ class SinkhornResult:
                 raise L.OtfError("Sinkhorn: the solve reported no final status; results are "
                                  "invalid")
             d["err"] = self.errlog_dev[: max(d["n_err"], 0)].cpu().tolist()
+            if (self.flavor == "pot" and self.u.dtype == torch.float32
+                    and d["status"] == L.SK_NUMERICAL_BREAK and d["break_iter"] <= 1):
+                warnings.warn(
+                    "float32 POT Sinkhorn broke at iteration %d: a row or column of "
+                    "K = exp(-C/reg) underflows (or its scaling overflows) in float32 -- POT's "
+                    "float64 solve may not break there.  Use precision='auto' or 'fp64' for "
+                    "parity with the reference's float64 path." % d["break_iter"],
+                    RuntimeWarning, stacklevel=2)
             self._info = d
         return self._info
+
+
+def sinkhorn_workspace_bytes(n: int, m: int, dtype, max_iter: int) -> int:
+    return int(L.lib().otf_sinkhorn_workspace_size(n, m, _DT[dtype], max_iter))
 
 
 def sinkhorn_workspace(n: int, m: int, dtype, max_iter: int, device) -> torch.Tensor:
@@ -266,7 +279,7 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
              check_every: int = 10, err_squared: bool = False, sync_every: int = 0,
              want_plan: bool = True, plan_dtype=None, workspace: torch.Tensor | None = None,
              plan_out: torch.Tensor | None = None, engine: str = "auto",
-             deterministic: bool = False) -> SinkhornResult:
+             deterministic: bool = False, precision: str = "as_given") -> SinkhornResult:
     """Entropic OT on the device.  ``flavor="pot"`` is POT's sinkhorn_knopp (u, v scalings,
     revert-and-break), ``flavor="ott"`` OTT's lse-mode solver (potentials f, g).
 
@@ -276,8 +289,29 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
     reduces the column sums in a fixed order without float atomics (gather / mesh engines
     by construction, else the sweep engine's fixed-order mode; POT flavour):
     bitwise-identical results run to run.
+
+    ``precision``: "as_given" computes in C's dtype; "fp64" in float64 (the reference's
+    POT path is float64 NumPy); "auto" keeps float32 unless a POT-flavour solve would
+    break in float32 where POT's float64 does not: when some row or column of
+    K = exp(-C / (reg cost_scale)) underflows entirely in float32, K^T u = 0 (or v = b /
+    K^T u overflows) and POT reverts at iteration 0.  The test is min over every row and
+    every column of C / (reg cost_scale) > 60 (float32 exp underflows below -87 and the
+    scaling overflows near e^88): two reductions and one host read, so "auto" is opt-in.
     """
     _dev(C, "C")
+    if precision not in ("as_given", "fp64", "auto"):
+        raise ValueError(f"precision must be 'as_given', 'fp64' or 'auto', not {precision!r}")
+    if precision == "auto" and flavor == "pot" and C.dtype in (torch.float32, torch.float16):
+        cs = 1.0 if cost_scale is None else float(cost_scale.reshape(-1)[0])
+        worst = torch.maximum(C.amin(dim=0).max(), C.amin(dim=1).max()).float()
+        if float(worst) / (cs * float(reg)) > 60.0:
+            precision = "fp64"
+    if precision == "fp64" and C.dtype != torch.float64:
+        C = C.double()
+        if cost_scale is not None:
+            cost_scale = cost_scale.double()
+        if workspace is not None and workspace.numel() < sinkhorn_workspace_bytes(C.shape[0], C.shape[1], torch.float64, max_iter):
+            workspace = None
     if C.dtype not in _VEC:
         raise TypeError("C must be float16, float32 or float64")
     cost_f16 = C.dtype == torch.float16

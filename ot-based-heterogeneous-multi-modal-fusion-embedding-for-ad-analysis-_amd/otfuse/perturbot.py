@@ -72,6 +72,36 @@ def solve_ott(M: torch.Tensor, eps: float, scale_cost: str | None = "max_cost",
     return res, scale
 
 
+def random_gamma_init_device(p, q, numItermax: int = 1000, stopThr: float = 1e-9) -> torch.Tensor:
+    """perturbot ``random_gamma_init`` (utils.py:118-122) with the scaling on the device.
+
+    The random matrix is the reference's draw, from NumPy's global generator: a dense
+    ``scipy.sparse.random(len(p), len(q), density=1)`` with Beta(0.1, 0.1) entries (the
+    reference reads it with ``.A``, which SciPy >= 1.14 removed; ``.toarray()`` is the
+    same array).  ``sinkhorn_scaling(p, q, S)`` is POT's scaling iteration on the GIVEN
+    kernel S with the squared marginal error: the POT-flavour device Sinkhorn on the
+    cost -log S at reg 1 (K = exp(log S)), err_squared.  Returns the float64 plan on the
+    device."""
+    from scipy import stats
+    from scipy.sparse import random as sprandom
+    p = np.asarray(p, dtype=np.float64)
+    q = np.asarray(q, dtype=np.float64)
+    S = sprandom(len(p), len(q), density=1, data_rvs=stats.beta(1e-1, 1e-1).rvs).toarray()
+    dev = _device()
+    C = -torch.log(torch.as_tensor(S, dtype=torch.float64, device=dev))
+    res = ops.sinkhorn(torch.as_tensor(p, device=dev), torch.as_tensor(q, device=dev), C, 1.0,
+                       max_iter=int(numItermax), stop_thr=float(stopThr), flavor="pot",
+                       err_squared=True, want_plan=True)
+    return res.plan
+
+
+def random_gamma_init(p, q, **kwargs) -> np.ndarray:
+    """Drop-in for perturbot ``random_gamma_init`` (utils.py:118-122): a random coupling
+    with marginals p, q (NumPy float64)."""
+    kw = {k: kwargs[k] for k in ("numItermax", "stopThr") if k in kwargs}
+    return ops.to_host(random_gamma_init_device(p, q, **kw))
+
+
 def fot_numpy(X1, X2, Ts, v1=None, v2=None, niter=10, algo="emd", reg=0, algo2="emd", reg2=0,
               verbose=True, log=False, random_init=False, C_lin=None):
     """Feature OT given a fixed sample coupling Ts (perturbot fot.py:14-152).
@@ -82,18 +112,23 @@ def fot_numpy(X1, X2, Ts, v1=None, v2=None, niter=10, algo="emd", reg=0, algo2="
     as the reference's two iterations would.  Note the reference's weights:
     ``Ts /= Ts.sum(); w1 = Ts.sum(axis=0); w2 = Ts.sum(axis=1)`` (fot.py:108-110).
     """
-    if random_init:
-        raise NotImplementedError("random_init (random_gamma_init) is not supported")
     dev = _device()
     Ts = np.asarray(Ts, dtype=np.float64)
     Ts = Ts / Ts.sum()
+    Tv_init = None
+    if random_init:
+        # fot.py:115-116: the only effect is the first iteration's delta (the BCD still
+        # stops at i = 1 on the cost test); the draw consumes NumPy's generator as there
+        d1, d2_ = np.asarray(X1).shape[1], np.asarray(X2).shape[1]
+        Tv_init = random_gamma_init_device(np.ones(d1) / d1 if v1 is None else v1,
+                                           np.ones(d2_) / d2_ if v2 is None else v2)
     Xd = torch.as_tensor(np.asarray(X1), dtype=torch.float32, device=dev)
     Yd = torch.as_tensor(np.asarray(X2), dtype=torch.float32, device=dev)
     M = ops.feature_cost(Xd, Yd, Ts=torch.as_tensor(Ts, device=dev), weights="fot")
     res, _ = solve_ott(M, float(reg2))
     Tv = res.plan
     d, d2 = M.shape
-    Tv0 = 1.0 / (d * d2)
+    Tv0 = 1.0 / (d * d2) if Tv_init is None else Tv_init
     # cost, delta and the finiteness test on the device, one host read
     stats = torch.stack([(M * Tv).sum(), torch.linalg.norm(Tv - Tv0),
                          torch.isfinite(Tv).all().to(Tv.dtype)]).cpu().tolist()
@@ -384,30 +419,32 @@ def _feature_hist(D, labels):
     return np.ones(Xc.shape[1]) / Xc.shape[1]
 
 
-def cotl_sinkhorn(X_dict, Y_dict, eps: float = 5e-3, eps2: float | None = None,
-                  niter: int = 100, v1=None, v2=None, w1=None, w2=None, log: bool = False,
-                  algo: str = "sinkhorn", numItermax: int = 10_000_000):
-    """``cotl_numpy(X_dict, Y_dict, algo="sinkhorn", algo2="sinkhorn", reg=eps,
-    reg2=eps2)`` (perturbot/perturbot/match/cot_labels.py:14-225) on the device.
+def cotl(X_dict, Y_dict, eps: float = 5e-3, niter: int = 100, v1=None, v2=None, w1=None,
+         w2=None, log: bool = False, algo: str = "sinkhorn", algo2: str | None = None,
+         C_lin=None, random_init: bool = False, numItermax: int = 10_000_000):
+    """``cotl_numpy`` (perturbot/perturbot/match/cot_labels.py:14-225) on the device.
 
     Block-coordinate descent over per-label sample couplings Ts[k] and one feature
-    coupling Tv: the sample costs ``constC_s - X_k Tv (2 Y_k)^T`` and the feature cost
-    ``sum_k constC_v,k - X_k^T Ts[k] (2 Y_k)`` come from ``otf_coupled_cost`` (float64,
-    float32 squares), every linear problem is OTT ``linear.solve(Geometry(M, epsilon,
-    scale_cost="max_cost"), max_iterations=2000)`` -- uniform marginals, as the
-    reference's Sinkhorn branch -- on the device Sinkhorn (float64, lse mode).
-    Reference behaviour kept: the feature solve uses ``eps`` (reg), not eps2 (:200);
-    ``delta`` counts only Tv (``Tsold = Ts`` aliases the dict that is updated in place,
-    :167-172, so the Ts terms are 0); Tv is renormalised when its mass is off by 1e-8;
-    stop when delta < 1e-16 or |cost change| < 1e-7.
-    ``algo="emd"``: every linear problem is ``pot.emd(w1[k], w2[k], M_k,
-    numItermax=1e7)`` / ``pot.emd(v1, v2, M, 1e7)`` instead (cot_labels.py:178,195) —
-    the device network simplex (``otf_emd_solve``), the per-label sample plans of one
-    step in one launch.
-    Returns ``(Ts dict of numpy, Tv, cost[, {"cost": [...]}])``.
+    coupling Tv: the sample costs ``constC_s - X_k Tv (2 Y_k)^T`` (+ ``C_lin``, the
+    sample-cost prior of :175-176) and the feature cost ``sum_k constC_v,k - X_k^T Ts[k]
+    (2 Y_k)`` come from ``otf_coupled_cost`` (float64, float32 squares).  Each stage
+    takes its own solver, as the reference's independent ``algo`` (sample plans) /
+    ``algo2`` (feature plan) branches: "sinkhorn" = OTT ``linear.solve(Geometry(M,
+    epsilon=reg, scale_cost="max_cost"), max_iterations=2000)`` -- uniform marginals,
+    as there -- on the device Sinkhorn (float64, lse mode); "emd" = ``pot.emd(w, w', M,
+    numItermax=1e7)`` on the device network simplex (``otf_emd_solve``; the per-label
+    sample plans of one step in one launch).  ``random_init``: Ts[k] =
+    random_gamma_init(w1[k], w2[k]) for the labels in order, then Tv =
+    random_gamma_init(v1, v2) (:133-135, same draws from NumPy's generator).
+    Reference behaviour kept: the feature solve uses ``reg`` (:200), never reg2;
+    ``delta`` counts only Tv (``Tsold = Ts`` aliases the dict updated in place,
+    :167-172); Tv is renormalised when its mass is off by 1e-8; stop when delta < 1e-16
+    or |cost change| < 1e-7.  Returns ``(Ts dict of numpy, Tv, cost[, {"cost": [...]}])``.
     """
-    if algo not in ("sinkhorn", "emd"):
-        raise NotImplementedError(f"algo={algo!r}")
+    algo2 = algo if algo2 is None else algo2
+    for a_ in (algo, algo2):
+        if a_ not in ("sinkhorn", "emd"):
+            raise NotImplementedError(f"algo={a_!r}")
     assert sorted(X_dict.keys()) == sorted(Y_dict.keys()), "Labels don't match in y1 & y2."
     dev = _device()
     labels = list(X_dict.keys())
@@ -424,29 +461,36 @@ def cotl_sinkhorn(X_dict, Y_dict, eps: float = 5e-3, eps2: float | None = None,
                else torch.as_tensor(np.asarray(w1[k], dtype=np.float64), device=dev)) for k in labels}
     w2t = {k: (torch.full((Ys[k].shape[0],), 1.0 / Ys[k].shape[0], **f64) if w2 is None
                else torch.as_tensor(np.asarray(w2[k], dtype=np.float64), device=dev)) for k in labels}
+    Clt = None if C_lin is None else torch.as_tensor(np.asarray(C_lin, dtype=np.float64), device=dev)
     d, d2 = Xs[labels[0]].shape[1], Ys[labels[0]].shape[1]
-    Ts = {k: torch.full((Xs[k].shape[0], Ys[k].shape[0]),
-                        1.0 / (Xs[k].shape[0] * Ys[k].shape[0]), **f64) for k in labels}
-    Tv = torch.full((d, d2), 1.0 / (d * d2), **f64)
+    if random_init:
+        Ts = {k: random_gamma_init_device(w1t[k].cpu().numpy(), w2t[k].cpu().numpy()) for k in labels}
+        Tv = random_gamma_init_device(v1t.cpu().numpy(), v2t.cpu().numpy())
+    else:
+        Ts = {k: torch.full((Xs[k].shape[0], Ys[k].shape[0]),
+                            1.0 / (Xs[k].shape[0] * Ys[k].shape[0]), **f64) for k in labels}
+        Tv = torch.full((d, d2), 1.0 / (d * d2), **f64)
     cost = np.inf
     costs = []
     for _ in range(niter):
         Tvold, costold = Tv, cost
+        Ms = []
+        for k in labels:  # sample costs of every label under the current Tv
+            Mk = ops.coupled_cost(Xs[k], Ys[k], Tv, v1t, v2t)
+            Ms.append(Mk if Clt is None else Mk + Clt)
         if algo == "emd":  # sample OT per label: every label's EMD in one launch
-            Ms = [ops.coupled_cost(Xs[k], Ys[k], Tv, v1t, v2t) for k in labels]
             for k, T in zip(labels, _emd_many([(w1t[k], w2t[k], Mk) for k, Mk in zip(labels, Ms)],
                                               numItermax)):
                 Ts[k] = T
         else:
-            for k in labels:  # sample OT per label
-                Mk = ops.coupled_cost(Xs[k], Ys[k], Tv, v1t, v2t)
+            for k, Mk in zip(labels, Ms):
                 res, _ = solve_ott(Mk, eps, "max_cost", max_iterations=OTT_MAX_ITER)
                 Ts[k] = res.plan
         M = None  # global feature OT
         for k in labels:
             Mv = ops.coupled_cost(Xs[k].T, Ys[k].T, Ts[k], w1t[k], w2t[k])
             M = Mv if M is None else M + Mv
-        if algo == "emd":
+        if algo2 == "emd":
             Tv = _emd_many([(v1t, v2t, M)], numItermax)[0]
         else:
             res, _ = solve_ott(M, eps, "max_cost", max_iterations=OTT_MAX_ITER)
@@ -463,6 +507,24 @@ def cotl_sinkhorn(X_dict, Y_dict, eps: float = 5e-3, eps2: float | None = None,
     if log:
         return Ts_np, ops.to_host(Tv), cost, {"cost": costs}
     return Ts_np, ops.to_host(Tv), cost
+
+
+def cotl_numpy(X_dict, Y_dict, w1=None, w2=None, v1=None, v2=None, niter: int = 100,
+               algo: str = "emd", reg: float = 0.2, algo2: str = "emd", reg2: float = 0.2,
+               verbose: bool = True, log: bool = False, random_init: bool = False, C_lin=None):
+    """Drop-in for perturbot ``cotl_numpy`` (cot_labels.py:14-225), same signature and
+    returns; see ``cotl`` (reg2 is accepted and, as in the reference, unused)."""
+    return cotl(X_dict, Y_dict, eps=reg, niter=niter, v1=v1, v2=v2, w1=w1, w2=w2, log=log,
+                algo=algo, algo2=algo2, C_lin=C_lin, random_init=random_init)
+
+
+def cotl_sinkhorn(X_dict, Y_dict, eps: float = 5e-3, eps2: float | None = None,
+                  niter: int = 100, v1=None, v2=None, w1=None, w2=None, log: bool = False,
+                  algo: str = "sinkhorn", numItermax: int = 10_000_000):
+    """``cotl_numpy(..., algo=algo, algo2=algo, reg=eps, reg2=eps2)``: both stages on one
+    solver (kept for the r02 callers; ``cotl`` takes every combination)."""
+    return cotl(X_dict, Y_dict, eps=eps, niter=niter, v1=v1, v2=v2, w1=w1, w2=w2, log=log,
+                algo=algo, algo2=algo, numItermax=numItermax)
 
 
 def get_coupling_cotl_sinkhorn(data, eps: float = 5e-3, eps2: float | None = None):

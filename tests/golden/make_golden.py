@@ -166,6 +166,22 @@ def main():
                         Xcat=Xs, Ycat=Ys, Ts=Tsm, M=orc.feature_cost_np(Xs, Ys, Tsm), eps=5e-3,
                         u=call["u"], v=call["v"], plan=Tv4, err=np.sqrt(call["err2"]),
                         n_err=len(call["err2"]))
+    # F5: random_gamma_init (perturbot utils.py:118-122) -- a Beta(0.1, 0.1) random matrix
+    #     drawn by scipy.sparse.random from NumPy's global generator, then the reference's
+    #     own sinkhorn_scaling.  The function itself calls ``S.A``, which SciPy >= 1.14
+    #     removed (this container: 1.15); ``.A`` was ``.toarray()``, so the fixture composes
+    #     the identical draw with .toarray() and the reference scaling loop.
+    from scipy import stats
+    from scipy.sparse import random as sprandom
+    f5 = {}
+    for tag, (n5, m5, seed5) in {"a": (6, 5, 3), "b": (64, 48, 11)}.items():
+        p5, q5 = np.ones(n5) / n5, rng.random(m5) + 0.2
+        q5 = q5 / q5.sum()
+        np.random.seed(seed5)
+        S5 = sprandom(n5, m5, density=1, data_rvs=stats.beta(1e-1, 1e-1).rvs).toarray()
+        f5[f"p_{tag}"], f5[f"q_{tag}"], f5[f"seed_{tag}"] = p5, q5, seed5
+        f5[f"plan_{tag}"] = sinkhorn_scaling(p5, q5, S5)
+    np.savez_compressed(os.path.join(HERE, "f5_random_gamma_init.npz"), **f5)
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

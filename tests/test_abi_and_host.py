@@ -40,7 +40,13 @@ def test_abi_structs_and_enums_match_header():
     from otfuse import _lib as L
     src = open(L.HEADER_PATH).read()
     assert ctypes.sizeof(L.SinkhornOpts) == 56   # 2 doubles + 9 int32, 8-aligned
-    assert L.INFO_INT32S * 4 == 32
+    # otf_sinkhorn_info: the int32 fields of the header, in order, are INFO_FIELDS
+    import re
+    hdr = open(L.HEADER_PATH).read()
+    body = hdr[:hdr.index("} otf_sinkhorn_info;")]
+    body = body[body.rindex("typedef struct"):]
+    fields = re.findall(r"int32_t\s+(\w+);", body)
+    assert tuple(fields) == L.INFO_FIELDS and L.INFO_INT32S == len(fields)
     for name, val in [("OTF_F32", 0), ("OTF_F64", 1), ("OTF_F16", 2), ("OTF_BF16", 3),
                       ("OTF_ENGINE_SWEEP", 4), ("OTF_RED_SUM", 0), ("OTF_RED_MAX", 1),
                       ("OTF_FLAVOR_POT", 0),

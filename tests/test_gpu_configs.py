@@ -212,37 +212,74 @@ def test_eot_and_leot_dropins_vs_oracle(orc, dev):
         assert nrel(Td[k], Pr) < 1e-9
 
 
-@pytest.mark.parametrize("engine", ["tiled", "mesh"])
-def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch, engine):
-    """Two persistent solves (tiled engine, a full grid each) launched together on two
-    streams cannot both be co-resident: each must either complete with the right plan
-    or report the stall cleanly (OtfError from info(), status timeout) -- never hang
-    and never return a silently wrong plan.  A short stall limit keeps it quick."""
+@pytest.mark.parametrize("engine,n,dt", [("tiled", 4096, torch.float32), ("mesh", 4096, torch.float32),
+                                         ("gather", 512, torch.float64)])
+def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch, engine, n, dt):
+    """A persistent solve launched together with a full-grid persistent solve on another
+    stream (the r02 stall scenario: e.g. RCCL kernels holding CUs) cannot always become
+    co-resident.  It must never hang, never return a silently wrong plan and -- with the
+    one-workgroup fallback queued behind every persistent launch -- never lose the
+    answer: each solve ends max_iter with the reference plan, either from its engine or
+    from the fallback (info fallback = 1, counted in otf_sinkhorn_fallback_count)."""
     from otfuse import _lib as L, ops
     monkeypatch.setenv("OTF_STALL_MS", "300")
-    N = 4096
     g = torch.Generator(device=dev).manual_seed(9)
-    C = torch.rand(N, N, device=dev, generator=g)
-    a = torch.full((N,), 1.0 / N, device=dev)
+    Cb = torch.rand(4096, 4096, device=dev, generator=g)
+    ab = torch.full((4096,), 1.0 / 4096, device=dev)
+    C = Cb[:n, :n].to(dt).contiguous()
+    a = torch.full((n,), 1.0 / n, device=dev, dtype=dt)
     ref = ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine="stream").plan
+    refb = ops.sinkhorn(ab, ab, Cb, 0.1, max_iter=30, stop_thr=0.0, engine="stream").plan
     s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     torch.cuda.synchronize()
-    outs = []
-    for s in (s1, s2):
-        with torch.cuda.stream(s):
-            outs.append(ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine=engine))
+    blocker_engine = "mesh" if engine == "gather" else engine
+    with torch.cuda.stream(s1):
+        blk = ops.sinkhorn(ab, ab, Cb, 0.1, max_iter=30, stop_thr=0.0, engine=blocker_engine)
+    with torch.cuda.stream(s2):
+        res = ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine=engine)
     torch.cuda.synchronize()
-    for res in outs:
-        try:
-            info = res.info()
-        except L.OtfError:
-            continue                      # reported cleanly
-        assert info["status_name"] == "max_iter"
-        assert (res.plan - ref).abs().max() / ref.abs().max() < 1e-5
+    for r, rp in ((blk, refb), (res, ref)):
+        info = r.info()                       # no OtfError: the fallback finished it
+        assert info["status_name"] == "max_iter" and info["stalled"] == 0
+        assert (r.plan - rp).abs().max() / rp.abs().max() < 1e-5
+    import ctypes
+    cnt = ctypes.c_uint64()
+    L.check(L.lib().otf_sinkhorn_fallback_count(ctypes.byref(cnt)), "fallback_count")
+    assert cnt.value >= int(blk.info()["fallback"]) + int(res.info()["fallback"])
     # the device is healthy afterwards
-    res = ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine=engine)
-    assert res.info()["status_name"] == "max_iter"
+    r = ops.sinkhorn(a, a, C, 0.1, max_iter=30, stop_thr=0.0, engine=engine)
+    assert r.info()["status_name"] == "max_iter" and r.info()["fallback"] == 0
+    assert (r.plan - ref).abs().max() / ref.abs().max() < 1e-5
+
+
+def test_solo_fallback_when_registration_cannot_complete(dev, monkeypatch):
+    """Force the fallback: a long gather solve (its XCC team holds 8 CUs for ~0.1 s) on
+    one stream, then a mesh solve (a whole grid, one workgroup per CU) on another with a
+    1-ms registration window: 8 of its workgroups cannot start, its registration gives
+    up, the late workgroups see the give-up word and leave, and the one-workgroup
+    fallback queued behind it returns the right plan (info fallback = 1)."""
+    from otfuse import ops
+    monkeypatch.setenv("OTF_REG_MS", "1")
+    g = torch.Generator(device=dev).manual_seed(3)
+    C = torch.rand(4096, 4096, device=dev, generator=g)
+    a = torch.full((4096,), 1.0 / 4096, device=dev)
+    Cg = torch.rand(512, 512, device=dev, generator=g, dtype=torch.float64)
+    ag = torch.full((512,), 1.0 / 512, device=dev, dtype=torch.float64)
+    ref = ops.sinkhorn(a, a, C, 0.1, max_iter=20, stop_thr=0.0, engine="stream").plan
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        blocker = ops.sinkhorn(ag, ag, Cg, 0.1, max_iter=40000, stop_thr=0.0, engine="gather",
+                               want_plan=False)
+    with torch.cuda.stream(s2):
+        res = ops.sinkhorn(a, a, C, 0.1, max_iter=20, stop_thr=0.0, engine="mesh")
+    torch.cuda.synchronize()
+    info = res.info()
+    assert info["status_name"] == "max_iter" and info["niter"] == 19 and info["stalled"] == 0
     assert (res.plan - ref).abs().max() / ref.abs().max() < 1e-5
+    assert blocker.info()["status_name"] == "max_iter"
+    if info["fallback"] != 1:
+        pytest.skip("the blocker finished before the mesh launch: no contention to test")
 
 
 @pytest.mark.parametrize("engine,n,m,dt,iters", [("tiled", 4096, 4096, torch.float32, 20000),

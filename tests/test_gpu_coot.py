@@ -66,3 +66,83 @@ def test_cotl_emd_dropin_vs_oracle(orc, dev):
     np.testing.assert_allclose(log["cost"], log_r["cost"], rtol=1e-9)
     for k in Xd:
         assert np.abs(Ts[k] - Tr[k]).max() < 1e-9
+
+
+def _coot_data(seed):
+    rng = np.random.default_rng(seed)
+    Xd = {0: rng.random((14, 10)).astype(np.float32), 1: rng.random((17, 10)).astype(np.float32)}
+    Yd = {0: rng.random((15, 7)).astype(np.float32), 1: rng.random((12, 7)).astype(np.float32)}
+    return Xd, Yd
+
+
+@pytest.mark.parametrize("algo,algo2", [("emd", "sinkhorn"), ("sinkhorn", "emd")])
+def test_cotl_mixed_solvers_vs_oracle(orc, dev, algo, algo2):
+    """cotl_numpy with algo != algo2 (cot_labels.py:177-199): each stage on its own
+    solver, same BCD iterations and plans as the oracle."""
+    from otfuse import perturbot
+    Xd, Yd = _coot_data(2)
+    Ts, Tv, cost, log = perturbot.cotl_numpy(Xd, Yd, niter=200, algo=algo, algo2=algo2, reg=5e-2,
+                                             log=True)
+    Tr, Tvr, cost_r, log_r = orc.cotl_np(Xd, Yd, eps=5e-2, niter=200, algo=algo, algo2=algo2)
+    assert len(log["cost"]) == len(log_r["cost"])
+    np.testing.assert_allclose(log["cost"], log_r["cost"], rtol=1e-6)
+    assert nrel(Tv, Tvr) < 1e-6
+    for k in Xd:
+        assert nrel(Ts[k], Tr[k]) < 1e-6
+
+
+def test_cotl_sample_cost_prior_vs_oracle(orc, dev):
+    """C_lin (cot_labels.py:175-176) added to every label's sample cost."""
+    from otfuse import perturbot
+    Xd = {0: np.random.default_rng(3).random((12, 8)).astype(np.float32),
+          1: np.random.default_rng(4).random((12, 8)).astype(np.float32)}
+    Yd = {0: np.random.default_rng(5).random((12, 6)).astype(np.float32),
+          1: np.random.default_rng(6).random((12, 6)).astype(np.float32)}
+    C_lin = np.random.default_rng(7).random((12, 12)) * 0.5
+    Ts, Tv, cost, log = perturbot.cotl_numpy(Xd, Yd, niter=200, algo="emd", algo2="emd",
+                                             C_lin=C_lin, log=True)
+    Tr, Tvr, cost_r, log_r = orc.cotl_np(Xd, Yd, niter=200, algo="emd", algo2="emd", C_lin=C_lin)
+    np.testing.assert_allclose(log["cost"], log_r["cost"], rtol=1e-9)
+    for k in Xd:
+        assert np.abs(Ts[k] - Tr[k]).max() < 1e-9
+
+
+def test_random_gamma_init_device_vs_golden(golden, dev):
+    """random_gamma_init (utils.py:118-122): the reference's Beta draw from NumPy's
+    generator + the reference's own scaling loop (F5) -- the device scaling of the same
+    draw matches it."""
+    from otfuse import perturbot
+    f = golden("f5_random_gamma_init.npz")
+    for tag in ("a", "b"):
+        np.random.seed(int(f[f"seed_{tag}"]))
+        P = perturbot.random_gamma_init(f[f"p_{tag}"], f[f"q_{tag}"])
+        assert nrel(P, f[f"plan_{tag}"]) < 1e-10
+
+
+def test_cotl_random_init_vs_oracle(orc, dev):
+    """cotl_numpy(random_init=True): the Ts / Tv initial couplings drawn in the
+    reference's order (labels, then Tv) change the first sample costs; same BCD."""
+    from otfuse import perturbot
+    Xd, Yd = _coot_data(8)
+    np.random.seed(21)
+    Ts, Tv, cost, log = perturbot.cotl_numpy(Xd, Yd, niter=200, algo="emd", algo2="emd",
+                                             random_init=True, log=True)
+    np.random.seed(21)
+    Tr, Tvr, cost_r, log_r = orc.cotl_np(Xd, Yd, niter=200, algo="emd", algo2="emd",
+                                         random_init=True)
+    np.testing.assert_allclose(log["cost"], log_r["cost"], rtol=1e-8)
+    assert np.abs(Tv - Tvr).max() < 1e-8
+
+
+def test_fot_numpy_random_init(dev):
+    """fot_numpy(random_init=True) (fot.py:115-116): only the first delta changes; the
+    feature plan is the one of the uniform start."""
+    from otfuse import perturbot
+    rng = np.random.default_rng(9)
+    X = rng.random((20, 12)).astype(np.float32)
+    Y = rng.random((20, 9)).astype(np.float32)
+    Ts = np.eye(20) / 20
+    T0, c0 = perturbot.fot_numpy(X, Y, Ts, reg2=5e-2, verbose=False)
+    np.random.seed(4)
+    T1, c1 = perturbot.fot_numpy(X, Y, Ts, reg2=5e-2, verbose=False, random_init=True)
+    assert np.abs(T1 - T0).max() < 1e-14 and c1 == c0

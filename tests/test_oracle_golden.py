@@ -128,3 +128,15 @@ def test_plan_apply_matches_fixture(golden, orc):
     idx = f["idx"]
     np.testing.assert_allclose(Tn[idx[:, 0], idx[:, 1]], f["Tn_samples"], rtol=2e-5)
     np.testing.assert_allclose(out, f["ot_mri_from_pet"], rtol=2e-5, atol=1e-6)
+
+
+def test_random_gamma_init_matches_reference_draw_and_scaling(golden, orc):
+    """F5: the oracle's random_gamma_init (utils.py:118-122) draws the same Beta(0.1,
+    0.1) matrix from NumPy's global generator and scales it like the reference's own
+    sinkhorn_scaling."""
+    f = golden("f5_random_gamma_init.npz")
+    for tag in ("a", "b"):
+        np.random.seed(int(f[f"seed_{tag}"]))
+        P = orc.random_gamma_init_np(f[f"p_{tag}"], f[f"q_{tag}"])
+        np.testing.assert_allclose(P, f[f"plan_{tag}"], rtol=1e-12, atol=1e-300)
+
