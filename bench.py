@@ -725,18 +725,9 @@ def config3_leg(dev, world, B=32, d=2048, labels=2, per_label=64, eps=5e-3):
             e0.record()
             Xa, Ya, La = comm.all_gather(Xl), comm.all_gather(Yl), comm.all_gather(Ll)
             e1.record()
-            labs = La.cpu().numpy().astype(np.int64)
-            xd, yd = {}, {}
-            for k in range(labels):
-                idx = np.nonzero(labs == k)[0][:per_label]
-                if len(idx) == 0:
-                    idx = np.arange(min(per_label, len(labs)))
-                it = torch.from_numpy(idx).to(dev)
-                # the drop-ins take the reference's NumPy dicts: (PET, MRI) per label
-                xd[k] = Ya.index_select(0, it).cpu().numpy()
-                yd[k] = Xa.index_select(0, it).cpu().numpy()
-            Ts, _ = perturbot.get_coupling_egw_ott_fixed((xd, yd), eps=eps)
-            Tv, _ = perturbot.get_coupling_fot((xd, yd), Ts, eps=eps)
+            # the whole chain stays on the device (one host read: the labels)
+            Tv, _ = perturbot.per_epoch_coupling_device(Xa, Ya, La, eps=eps,
+                                                        max_per_label=per_label)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
             tg.append(e0.elapsed_time(e1))
@@ -744,8 +735,9 @@ def config3_leg(dev, world, B=32, d=2048, labels=2, per_label=64, eps=5e-3):
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         out.update({"ms_per_epoch_call": float(t[0]), "allgather_ms": float(t[1]),
-                    "plan_shape": list(np.asarray(Tv).shape) if not isinstance(Tv, int) else None,
-                    "note": "max over ranks; solve replicated on every rank after the all-gather"})
+                    "plan_shape": list(Tv.shape),
+                    "note": ("max over ranks; solve replicated on every rank after the all-gather, "
+                             "device-resident (otfuse.perturbot.per_epoch_coupling_device)")})
         comm.close()
     except Exception as e:  # noqa: BLE001
         out["error"] = repr(e)

@@ -267,6 +267,63 @@ def get_coupling_egw_ott_fixed(
     return dict(zip(labels, plans)), dict(zip(labels, logs))
 
 
+def per_epoch_coupling_device(mri: torch.Tensor, pet: torch.Tensor, labels: torch.Tensor,
+                              eps: float = 5e-3, max_per_label: int | None = 64,
+                              gw_max_iterations: int = 2000, sinkhorn_max_iterations: int = 2000):
+    """``compute_pet_to_mri_coupling`` (MRI_PET_OT_OT_per_epoch_attn.py:940-960) on device
+    tensors -- e.g. the all-gathered embedding shards of a data-parallel epoch -- without
+    the NumPy round trips of the drop-ins.
+
+    ``group_features_by_label`` (:915-937: labels in ``np.unique`` order, the first
+    ``max_per_label`` rows of each) becomes index selects from one host read of the
+    labels; ``get_coupling_egw_ott_fixed((pet, mri))`` runs every label's entropic GW in
+    one launch (:954); ``get_coupling_fot((pet, mri), Ts)`` (:959 -> perturbot fot.py:155-220)
+    builds the float64 feature cost from the block-diagonal Ts on the device (``Ts /=
+    Ts.sum()``, fot weights) and runs the OTT solve with a host poll only every 10
+    iterations (OTT's own check cadence).  Returns ``(Tv, info)``: Tv the PET->MRI feature
+    plan (d_pet x d_mri float64, on the device) and ``info`` a callable returning the
+    solver logs (it synchronises; the chain itself reads only the labels back).
+    Equivalent to the NumPy chain ``get_coupling_egw_ott_fixed`` + ``get_coupling_fot``
+    (tests/test_gpu_configs.py::test_config3_device_chain_matches_dropins)."""
+    from . import gw
+    dev = mri.device
+    lab = labels.reshape(-1).to("cpu").numpy()
+    groups = []
+    for l in np.unique(lab):
+        idx = np.nonzero(lab == l)[0]
+        if max_per_label is not None and max_per_label > 0:
+            idx = idx[:max_per_label]
+        groups.append((int(l), torch.as_tensor(idx, device=dev)))
+    pets = [torch.nan_to_num(pet.index_select(0, i).float()) for _, i in groups]
+    mris = [torch.nan_to_num(mri.index_select(0, i).float()) for _, i in groups]
+    # per-label entropic GW (PET samples x MRI samples), all labels in one launch
+    C1s, C2s = [], []
+    for x, y in zip(pets, mris):
+        C1s.append(gw.pairwise_cost_f64(x, None, metric="sqeuclidean", zero_diag=False, scale_max=True)[0])
+        C2s.append(gw.pairwise_cost_f64(y, None, metric="sqeuclidean", zero_diag=False, scale_max=True)[0])
+    egw = gw.solve_batched(C1s, C2s, gw.GW_ENTROPIC, max_iter=gw_max_iterations, min_iter=5,
+                           threshold=1e-3, eps=float(eps), sk_max_iter=sinkhorn_max_iterations,
+                           sk_inner=OTT_INNER, sk_threshold=OTT_THRESHOLD, warm_start=True,
+                           log_len=max(1, min(gw_max_iterations, 4096)))
+    # feature OT given the block-diagonal sample coupling (label order = data[0] keys)
+    n = sum(int(i.numel()) for _, i in groups)
+    Ts = torch.zeros((n, n), dtype=torch.float64, device=dev)
+    r = 0
+    for T in egw.plans:
+        Ts[r:r + T.shape[0], r:r + T.shape[1]] = T
+        r += T.shape[0]
+    Ts = Ts / Ts.sum()
+    X = torch.cat(pets)
+    Y = torch.cat(mris)
+    M = ops.feature_cost(X, Y, Ts=Ts, weights="fot")
+    res, _ = solve_ott(M, float(eps), sync_every=OTT_INNER)
+
+    def info():
+        return {"egw": egw.infos(), "fot": res.info(), "labels": [l for l, _ in groups]}
+
+    return res.plan, info
+
+
 def get_coupling_egw_ott(data, eps: float = 5e-3):
     """Per-label entropic GW, OTT defaults for the inner Sinkhorn, max_iterations=1000
     (perturbot ott_egwl.py:129-206)."""

@@ -73,6 +73,34 @@ def test_config3_get_coupling_fot_2048_vs_oracle(config3, orc):
     np.testing.assert_allclose(Tv.sum(1), 1.0 / 2048, rtol=1e-6)
 
 
+def test_config3_device_chain_matches_dropins(config3, dev):
+    """per_epoch_coupling_device (compute_pet_to_mri_coupling on device tensors, e.g. the
+    all-gathered shards) equals the NumPy drop-in chain get_coupling_egw_ott_fixed +
+    get_coupling_fot on the same rows: interleaved labels are grouped in np.unique order,
+    the first 64 of each kept."""
+    from otfuse import perturbot
+    pet, mri, Ts, _ = config3
+    Tv_ref, _ = perturbot.get_coupling_fot((pet, mri), Ts, eps=5e-3)
+    # interleave the two labels' rows and add rows beyond the 64-per-label cut
+    rng = np.random.default_rng(3)
+    extra = 10
+    lab = np.concatenate([np.zeros(64 + extra, np.int64), np.ones(64 + extra, np.int64)])
+    P = np.concatenate([pet[0], rng.random((extra, 2048), np.float32), pet[1],
+                        rng.random((extra, 2048), np.float32)])
+    Mr = np.concatenate([mri[0], rng.random((extra, 2048), np.float32), mri[1],
+                         rng.random((extra, 2048), np.float32)])
+    # rows of label 0 at even positions, label 1 at odd ones, each label's order kept
+    perm = np.empty(len(lab), np.int64)
+    perm[0::2] = np.arange(64 + extra)
+    perm[1::2] = 64 + extra + np.arange(64 + extra)
+    Tv, info = perturbot.per_epoch_coupling_device(
+        torch.as_tensor(Mr[perm], device=dev), torch.as_tensor(P[perm], device=dev),
+        torch.as_tensor(lab[perm], device=dev), eps=5e-3, max_per_label=64)
+    assert Tv.is_cuda and tuple(Tv.shape) == (2048, 2048)
+    assert nrel(Tv.cpu().numpy(), Tv_ref) < 1e-9
+    assert info()["labels"] == [0, 1]
+
+
 def test_config3_pot_form_2048_vs_oracle(config3, orc):
     """POT form of the per-epoch chain: get_feature_coupling_pot with the block-diagonal
     GW plans (MRI_PET_OT_nojax.py:91-145), 2048^2 float64, eps = 5e-3, 2000 iterations,
