@@ -636,6 +636,181 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
     }
 }
 
+// 256 x 256 output tile per 512-thread workgroup with the operands staged by LDS-DMA
+// (global_load_lds_dwordx4) into a RING of 4 stages of 16-deep K -- the hi and lo fp16
+// images of both operands, 32 KB a stage, 128 KB the ring: three stages are in flight
+// while one is computed; the waits are counted (vmcnt of the stages issued later) and
+// the barrier is the raw s_barrier, so nothing drains the ring.  cost_big_kernel stages
+// one 32-deep stage through registers (one stage in flight, an LDS write pass and a
+// full drain per barrier): 0.30 of the fp16 MFMA peak at the metric shape.
+// LDS image of an operand for one stage: 256 rows x 32 B with the two 16-B chunks of a
+// row swapped when row bit 3 is set, so the 16 lanes of every ds_read_b128 phase (rows
+// r and r + 8 alike) hit 16 distinct bank groups.  The DMA writes lane-linear (lane L:
+// row L / 2, slot L % 2 of its wave's 32 rows), so the swap is applied to each lane's
+// SOURCE chunk (cdna_hip_programming.md §5.4 rule 21).  Wave w issues the DMA of rows
+// [32 w, 32 w + 32) of each image; the fragments are read with the same swap.
+constexpr int RBK = 16, RSLOTS = 4;
+__device__ __forceinline__ int rswz(int row, int chunk) { return row * 32 + ((chunk ^ ((row >> 3) & 1)) << 4); }
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NS, typename TC>
+__global__ __launch_bounds__(512) void cost_ring_kernel(
+    const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
+    const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
+    const float* __restrict__ ys, const float* __restrict__ yy, int64_t ldxh, int64_t ldyh, int n, int m, int kpad,
+    int metric, int zero_diag, TC* __restrict__ C, int64_t ldc, unsigned int* cmax, int tiles_n,
+    const float* __restrict__ store_scale) {
+    constexpr int NI = NS == 3 ? 2 : 1;           // fp16 images per operand
+    constexpr int IMG = GBM * RBK * 2;            // 8 KB: one image of one stage
+    constexpr int STAGE = 2 * NI * IMG;
+    constexpr int PER = 2 * NI;                   // DMA instructions per wave per stage
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* sxs = reinterpret_cast<float*>(smem + RSLOTS * STAGE);
+    float* sxx = sxs + GBM;
+    float* wmx = sxx + GBM;
+
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+    int tm, tn;
+    grouped_tile(wg, nwg, tiles_n, tm, tn);
+    const int i0 = tm * GBM, j0 = tn * GBN;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    // this lane's DMA sources: row 32 wid + lane / 2 of each image, the chunk stored at
+    // slot lane % 2 (swapped on row bit 3); clamped rows past n / m are never stored
+    const int drow = 32 * wid + (lane >> 1);
+    const int dchk = (lane & 1) ^ ((drow >> 3) & 1);
+    const int gi = i0 + drow < n ? i0 + drow : n - 1;
+    const int gj = j0 + drow < m ? j0 + drow : m - 1;
+    const _Float16* pa[NI];
+    const _Float16* pb[NI];
+    pa[0] = Xh + (int64_t)gi * ldxh + dchk * 8;
+    pb[0] = Yh + (int64_t)gj * ldyh + dchk * 8;
+    if constexpr (NI == 2) {
+        pa[NI - 1] = Xl + (int64_t)gi * ldxh + dchk * 8;
+        pb[NI - 1] = Yl + (int64_t)gj * ldyh + dchk * 8;
+    }
+    auto issue = [&](int st) {
+        char* slot = smem + (st % RSLOTS) * STAGE + wid * 1024;
+        const int k0 = st * RBK;
+#pragma unroll
+        for (int h = 0; h < NI; ++h) {
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)(pa[h] + k0), (lds_void_t*)(slot + h * IMG), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)(pb[h] + k0), (lds_void_t*)(slot + (NI + h) * IMG), 16, 0, 0);
+        }
+    };
+
+    // norms first: ordinary loads, none inside the ring loop (hipcc waits vmcnt(0) at the
+    // use of an ordinary load while a DMA is in flight)
+    if (tid < GBM) {
+        const int g = i0 + tid < n ? i0 + tid : n - 1;
+        sxs[tid] = xs[g];
+        sxx[tid] = xx[g];
+    }
+    float cys[4], cyy[4];
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+        const int gj0 = j0 + wn * 128 + nj * 32 + (lane & 31);
+        const int g = gj0 < m ? gj0 : m - 1;
+        cys[nj] = ys[g];
+        cyy[nj] = yy[g];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+    const int nk = kpad / RBK;
+#pragma unroll
+    for (int st = 0; st < RSLOTS - 1; ++st)
+        if (st < nk) issue(st);
+    const int fch = lane >> 5;
+    for (int kt = 0; kt < nk; ++kt) {
+        // stage kt has landed once only the stages issued after it are outstanding
+        const int later = nk - 1 - kt < RSLOTS - 2 ? nk - 1 - kt : RSLOTS - 2;
+        if (later >= 2) wait_vm<2 * PER>();
+        else if (later == 1) wait_vm<PER>();
+        else wait_vm<0>();
+        // every wave's DMA of stage kt has landed; every wave is done reading stage kt - 1,
+        // whose slot the next issue refills
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + RSLOTS - 1 < nk) issue(kt + RSLOTS - 1);
+        const char* sl = smem + (kt % RSLOTS) * STAGE;
+        f16x8 ah[2], al[2], bh[4], bl[4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int ar = wm * 64 + t * 32 + (lane & 31);
+            ah[t] = *reinterpret_cast<const f16x8*>(sl + rswz(ar, fch));
+            if (NI == 2) al[t] = *reinterpret_cast<const f16x8*>(sl + IMG + rswz(ar, fch));
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int br = wn * 128 + t * 32 + (lane & 31);
+            bh[t] = *reinterpret_cast<const f16x8*>(sl + NI * IMG + rswz(br, fch));
+            if (NI == 2) bl[t] = *reinterpret_cast<const f16x8*>(sl + (NI + 1) * IMG + rswz(br, fch));
+        }
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int nj = 0; nj < 4; ++nj) {
+                if (NS == 3) {
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mi], bh[nj], acc[mi][nj], 0, 0, 0);
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bl[nj], acc[mi][nj], 0, 0, 0);
+                }
+                acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bh[nj], acc[mi][nj], 0, 0, 0);
+            }
+    }
+
+    const float os = store_scale ? store_scale[0] : 1.0f;
+    float lmax = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int rl = wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                const int cl = wn * 128 + nj * 32 + (lane & 31);
+                const int gi2 = i0 + rl, gj2 = j0 + cl;
+                if (gi2 < n && gj2 < m) {
+                    const float dot = acc[mi][nj][e] * sxs[rl] * cys[nj];
+                    float c = sxx[rl] + cyy[nj] - 2.f * dot;
+                    c = c > 0.f ? c : 0.f;
+                    if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
+                    if (zero_diag && gi2 == gj2) c = 0.f;
+                    const TC cs = (TC)(c * os);
+                    C[(int64_t)gi2 * ldc + gj2] = cs;
+                    lmax = fmaxf(lmax, (float)cs);
+                }
+            }
+    if (cmax) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmx[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            float v = wmx[0];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) v = fmaxf(v, wmx[w]);
+            const unsigned int u = __float_as_uint(v);
+            if (u > __hip_atomic_load(cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(cmax, u);
+        }
+    }
+}
+constexpr size_t kRingLds = (size_t)RSLOTS * 2 * 2 * (GBM * RBK * 2) + (2 * GBM + 8) * sizeof(float);
+
 }  // namespace
 }  // namespace otf
 
@@ -670,9 +845,30 @@ static bool cost_big_enabled() {
     static int env = -1;
     if (env < 0) {
         const char* e = getenv("OTF_COST_BIG");
-        env = e ? atoi(e) : 1;
+        env = e ? atoi(e) : 0;
     }
     return env != 0;
+}
+
+// OTF_COST_RING=1 selects the LDS-DMA ring kernel (A/B against the register-staged one)
+// (read per call: a test switches it in-process)
+static bool cost_ring_enabled() {
+    const char* e = getenv("OTF_COST_RING");
+    return e ? atoi(e) != 0 : false;
+}
+// the ring kernel asks for 130 KB of dynamic LDS: raise the launch limit once
+static bool ring_lds_ok() {
+    static int ok = -1;
+    if (ok < 0) {
+        ok = 1;
+        if (hipFuncSetAttribute((const void*)otf::cost_ring_kernel<3, float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kRingLds) != hipSuccess ||
+            hipFuncSetAttribute((const void*)otf::cost_ring_kernel<3, _Float16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kRingLds) != hipSuccess ||
+            hipFuncSetAttribute((const void*)otf::cost_ring_kernel<1, float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kRingLds) != hipSuccess ||
+            hipFuncSetAttribute((const void*)otf::cost_ring_kernel<1, _Float16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kRingLds) != hipSuccess)
+            ok = 0;
+        (void)hipGetLastError();
+    }
+    return ok != 0;
 }
 
 size_t otf_cost_ex_workspace_size(int64_t n, int64_t m, int64_t d, int32_t in_dtype) {
@@ -771,6 +967,7 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     const int64_t big_rounds = (big_tiles + cus - 1) / cus;
     const int64_t small_rounds = (small_tiles + 2 * cus - 1) / (2 * cus);
     const bool big = 18 * big_rounds < 10 * small_rounds && cost_big_enabled();
+    const bool ring = cost_ring_enabled() && ring_lds_ok();
     const int BMx = big ? otf::GBM : otf::BM, BNx = big ? otf::GBN : otf::BN;
     const int tiles_m = (int)((n + BMx - 1) / BMx);
     const int tiles_n = (int)((m + BNx - 1) / BNx);
@@ -778,7 +975,11 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     if (nwg > INT32_MAX) return OTF_EUNSUPPORTED;
 #define OTF_COST_LAUNCH(NS, TC)                                                                   \
     do {                                                                                          \
-        if (big)                                                                                  \
+        if (big && ring)                                                                          \
+            otf::cost_ring_kernel<NS, TC><<<(int)nwg, 512, otf::kRingLds, s>>>(                  \
+                Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
+                zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
+        else if (big)                                                                             \
             otf::cost_big_kernel<NS, TC><<<(int)nwg, 512, 0, s>>>(                               \
                 Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
                 zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
