@@ -117,39 +117,6 @@ using I4 = __attribute__((ext_vector_type(4))) int;
 #endif
 using F2 = __attribute__((ext_vector_type(2))) float;
 
-__device__ __forceinline__ I4 chunk2(float v0, float v1, int tag) {
-    I4 x;
-    x[0] = __builtin_bit_cast(int, v0);
-    x[1] = tag;
-    x[2] = __builtin_bit_cast(int, v1);
-    x[3] = tag;
-    return x;
-}
-__device__ __forceinline__ bool chunk_at(const I4 x, unsigned e) {
-    return ((unsigned)x[1] >> 2) == e && ((unsigned)x[3] >> 2) == e;
-}
-// element copies first (ROCm 7.2: a bit_cast of a vector ELEMENT reads element 0)
-__device__ __forceinline__ float chunk_v0(const I4 x) { const int w = x[0]; return __builtin_bit_cast(float, w); }
-__device__ __forceinline__ float chunk_v1(const I4 x) { const int w = x[2]; return __builtin_bit_cast(float, w); }
-
-template <int CTRL> __device__ __forceinline__ float dpp_f(float x) { return dpp_lane<CTRL>(x); }
-
-__device__ __forceinline__ I4 gload(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
-    return __builtin_bit_cast(I4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16 /* sc1 */));
-}
-__device__ __forceinline__ void gstore(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x) {
-    __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
-}
-// Column-path store: plain (xl = 1) when producer and consumers share one XCC, so the
-// line stays in that XCC's L2 -- see the tile assignment in the kernel -- else
-// write-through (sc1) like every cross-XCC hop
-__device__ __forceinline__ void gstore_col(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x, int xl) {
-    if (xl)
-        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
-    else
-        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
-}
-
 constexpr int pow2_at_least(int x) { return x <= 1 ? 1 : 2 * pow2_at_least((x + 1) / 2); }
 
 // KQ: reducer loads per lane, ceil(nrb * CPR / 64): 4 when nrb is a power of two

@@ -107,6 +107,43 @@ __device__ __forceinline__ void store_sum_vec(__amdgpu_buffer_rsrc_t rs, uint32_
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(I4, v), rs, byte_off, 0, 16 /* sc1 */);
 }
 
+// Epoch-tagged granules (mesh, gather and sweep engines): 16 B = two {value, tag}
+// pairs, tag = (epoch << 2) | flags; a consumer polls the data itself (no fence, no
+// counter).  sc1 loads; stores sc1 (write-through) across XCCs, plain within one XCC.
+using I4 = __attribute__((ext_vector_type(4))) int;
+__device__ __forceinline__ I4 chunk2(float v0, float v1, int tag) {
+    I4 x;
+    x[0] = __builtin_bit_cast(int, v0);
+    x[1] = tag;
+    x[2] = __builtin_bit_cast(int, v1);
+    x[3] = tag;
+    return x;
+}
+__device__ __forceinline__ bool chunk_at(const I4 x, unsigned e) {
+    return ((unsigned)x[1] >> 2) == e && ((unsigned)x[3] >> 2) == e;
+}
+// element copies first (ROCm 7.2: a bit_cast of a vector ELEMENT reads element 0)
+__device__ __forceinline__ float chunk_v0(const I4 x) { const int w = x[0]; return __builtin_bit_cast(float, w); }
+__device__ __forceinline__ float chunk_v1(const I4 x) { const int w = x[2]; return __builtin_bit_cast(float, w); }
+
+template <int CTRL> __device__ __forceinline__ float dpp_f(float x) { return dpp_lane<CTRL>(x); }
+
+__device__ __forceinline__ I4 gload(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(I4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16 /* sc1 */));
+}
+__device__ __forceinline__ void gstore(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x) {
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
+}
+// Column-path store: plain (xl = 1) when producer and consumers share one XCC, so the
+// line stays in that XCC's L2 -- see the tile assignment in the kernel -- else
+// write-through (sc1) like every cross-XCC hop
+__device__ __forceinline__ void gstore_col(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x, int xl) {
+    if (xl)
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
+    else
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
+}
+
 // Device-wide flat barrier: every wave drains its own memory operations, one lane per
 // workgroup arrives on the counter and polls it.  Returns false on a stall (flag
 // broadcast via LDS); re-arms `deadline` on success.

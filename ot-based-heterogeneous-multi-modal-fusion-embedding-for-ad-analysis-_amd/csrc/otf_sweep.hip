@@ -26,6 +26,22 @@
 // barrier and the atomic drain overlap the stream.  The plan is written at the end
 // from the last good (u, v) by a final sweep.
 //
+// Granule flush (float problems outside the deterministic mode, r03): step 3 above
+// without atomics, zeroing or barriers -- every hand-off is an epoch-tagged granule
+// (otf_persist.h) that the consumer polls:
+//   a. every workgroup stores its m partials into its slab row (plain stores: only its
+//      XCC reads them);
+//   b. the XCC's workgroups, ranked by blockIdx, own the 32 column slices round-robin:
+//      the owner of a slice sums it over the XCC members' rows in rank order and
+//      publishes the XCC partial (write-through, parity double-buffered);
+//   c. the same owner sums the slice over the active XCCs' partials in XCC order and
+//      stores S into its XCC's ring slot (plain): every XCC derives the same S, bit for
+//      bit, from the same partials in the same order;
+//   d. the next sweep's v-update polls the XCC-local S granules.
+// A non-finite u travels as a tag flag (slab -> XCC partial -> S) instead of the bad
+// counters.  Three hops, one of them across XCCs, instead of flush + group counter +
+// atomics + grid barrier (~11 us of a 29-us config-5 sweep in r02).
+//
 // Ring of 4 sum slots S[k] = K^T u(k-1) (slot k % 4): iteration it reads S[it] and, on
 // check iterations, S[it-1]; accumulates S[it+1]; zeroes slot (it+2) % 4 (= S[it-2],
 // last read in iteration it-1).  Exits keep S[it-2..it] intact, so the outputs can be
@@ -67,7 +83,13 @@ template <typename T> struct SkSweepArgs {
     int nt_loads;       // 1: cost larger than the Infinity Cache, stream it non-temporal
     int det;            // 1: fixed-order column sums (one group = the whole grid, no atomics)
     int nres;           // row blocks per workgroup kept in LDS (< the fewest blocks any has)
+    int gran;           // 1: granule flush (float, not deterministic mode)
+    unsigned char* gslab;  // [grid][m_pad] granules: column partials per workgroup
+    unsigned char* gxp;    // [2 parity][8 XCC][m_pad] granules: XCC partials (sc1)
+    unsigned char* gfs;    // [8 XCC][4 ring][m_pad] granules: S, read within the XCC
+    int* xl;               // [8][256] registration lists: blockIdx per XCC slot
 };
+constexpr int kSwSlices = 32;  // column slices of the granule reduction
 
 using Raw = __attribute__((ext_vector_type(4))) unsigned int;  // 16 B of cost
 
@@ -150,7 +172,10 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     __shared__ T red[2][NW][R];
     __shared__ T ered[17];
     __shared__ int s_flag;
-    __shared__ int s_pop[5];
+    __shared__ int s_pop[6];
+    __shared__ int mrow[256];     // granule flush: this XCC's members by blockIdx rank
+    __shared__ int s_or[4][NW];  // [0..1] v-update checks, [2..3] flushes (by parity)
+    const bool gran = sizeof(T) == 4 && p.gran;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nwg = gridDim.x;
@@ -260,6 +285,50 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 #pragma unroll
         for (int k2 = 0; k2 < VC; ++k2) out[k2] = acc[k2 / VT][k2 % VT];
     };
+    // granule form: S[k] of chunk g from this XCC's ring slot, polled until its tags carry
+    // epoch k + 1; flags of every granule ORed into fl, a stall clears ok
+    const int mc = p.m_pad / 2;                       // 16-B granule pairs per row
+    auto load_sums_gran = [&](int k, int g, T (&out)[VC], int& fl, bool& ok) {
+        const __amdgpu_buffer_rsrc_t rfs = sums_rsrc(p.gfs);
+        const unsigned e = (unsigned)(k + 1);
+        const uint32_t base = (uint32_t)((xcc_id() * 4 + (int)(e & 3)) * mc) * 16u + (uint32_t)(colc[g] / 2) * 16u;
+        I4 x[VC / 2];
+#pragma unroll
+        for (int h = 0; h < VC / 2; ++h) x[h] = gload(rfs, base + h * 16);
+        unsigned pend = 0;
+#pragma unroll
+        for (int h = 0; h < VC / 2; ++h)
+            if (!chunk_at(x[h], e)) pend |= 1u << h;
+        while (pend && ok) {
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int h = 0; h < VC / 2; ++h)
+                if (pend & (1u << h)) x[h] = gload(rfs, base + h * 16);
+#pragma unroll
+            for (int h = 0; h < VC / 2; ++h)
+                if ((pend & (1u << h)) && chunk_at(x[h], e)) pend &= ~(1u << h);
+            if (pend && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
+        }
+#pragma unroll
+        for (int h = 0; h < VC / 2; ++h) {
+            out[2 * h] = (T)chunk_v0(x[h]);
+            out[2 * h + 1] = (T)chunk_v1(x[h]);
+            fl |= (x[h][1] | x[h][3]) & 3;
+        }
+    };
+    // OR of 3 flag bits over the workgroup (ballots + one barrier; par alternates)
+    auto block_or = [&](int bits, int par) -> int {
+        int wv = 0;
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+            if (__ballot((bits >> b) & 1)) wv |= 1 << b;
+        if (lane == 0) s_or[par][w] = wv;
+        __syncthreads();
+        int r = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) r |= s_or[par][ww];
+        return r;
+    };
     auto load_b_chunk = [&](int g, T (&bv)[VC]) {
 #pragma unroll
         for (int h = 0; h < VC / VT; ++h) {
@@ -275,8 +344,15 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             T sk[VC], sk1[VC], bv[VC];
-            load_sums_chunk(k, g, sk);
-            load_sums_chunk(k + 1, g, sk1);
+            if (gran) {
+                int fl = 0;
+                bool ok = true;
+                load_sums_gran(k, g, sk, fl, ok);
+                load_sums_gran(k + 1, g, sk1, fl, ok);
+            } else {
+                load_sums_chunk(k, g, sk);
+                load_sums_chunk(k + 1, g, sk1);
+            }
             load_b_chunk(g, bv);
 #pragma unroll
             for (int k2 = 0; k2 < VC; ++k2) {
@@ -423,6 +499,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     if (tid == 0) {
         s_pop[3] = __hip_atomic_fetch_add(p.sync.reg + xcd * 64, 1, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
+        if (gran && s_pop[3] < 256) store_wt(p.xl + xcd * 256 + s_pop[3], (int)blockIdx.x);
     }
     bool reg_ok = grid_barrier(p.bar, nwg, deadline, p.stall_ticks, &s_flag, &p.info->stalled);
     if (tid == 0) {
@@ -444,6 +521,19 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     __syncthreads();
     const int nx = s_pop[0], nact = s_pop[1];
     const unsigned act_mask = (unsigned)s_pop[2];
+    // granule flush: the XCC's members ranked by blockIdx (a placement-independent order
+    // of the slab rows within the group)
+    if (gran) {
+        if (tid < nx && tid < 256) {
+            const int b = load_agent(p.xl + xcd * 256 + tid);
+            int rk = 0;
+            for (int j = 0; j < nx && j < 256; ++j) rk += load_agent(p.xl + xcd * 256 + j) < b ? 1 : 0;
+            mrow[rk] = b;
+            if (b == (int)blockIdx.x) s_pop[5] = rk;
+        }
+        __syncthreads();
+    }
+    const int gslot_r = gran ? s_pop[5] : 0;
     // reduction group: the workgroups of this XCD (slot = registration order), or in the
     // deterministic mode the whole grid by blockIdx (placement- and timing-independent
     // order: every column sum is added in slab-row order by one workgroup, no atomics)
@@ -544,26 +634,158 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         badu = 0;
     };
 
+    // Granule flush of S[k] (see the header): false on a stall
+    // slab rows polled per batch (fewer at G = 8, whose registers are the tightest)
+    constexpr int NBT = G >= 8 ? 4 : 8;
+    auto flush_gran = [&](int k) -> bool {
+        const __amdgpu_buffer_rsrc_t rsl = sums_rsrc(p.gslab);
+        const __amdgpu_buffer_rsrc_t rxp = sums_rsrc(p.gxp);
+        const __amdgpu_buffer_rsrc_t rfs = sums_rsrc(p.gfs);
+        const int sw = (mc + kSwSlices - 1) / kSwSlices;         // granule pairs per slice (<= 256)
+        const int swp = sw <= 64 ? 64 : sw <= 128 ? 128 : 256;   // lanes per row group
+        const int Q = kSwNT / swp, sq = tid / swp, sj = tid % swp;
+        const unsigned e = (unsigned)(k + 1);
+        bool ok = true;
+        // a. this workgroup's partials -> its slab row
+        const uint32_t rowo = (uint32_t)blockIdx.x * (uint32_t)mc * 16u;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int c0 = (tid + kSwNT * g) * VC;
+            if (c0 < p.m_pad) {
+#pragma unroll
+                for (int h = 0; h < VP2; ++h)
+                    gstore_col(rsl, rowo + (uint32_t)(c0 / 2 + h) * 16u,
+                               chunk2((float)colacc[g][h].x, (float)colacc[g][h].y, (int)(e << 2) | badu), 1);
+            }
+        }
+        badu = 0;
+        // b. owned slices: sum over the XCC's members (rank order), publish the XCC partial
+        for (int sl = gslot_r; sl < kSwSlices; sl += nx) {
+            const int cch = sl * sw + sj;
+            const bool act = sj < sw && cch < mc;
+            float a0 = 0.f, a1 = 0.f;
+            int fl = 0;
+            for (int rb = sq; rb < nx; rb += NBT * Q) {
+                I4 x[NBT];
+                unsigned pend = 0;
+#pragma unroll
+                for (int i = 0; i < NBT; ++i) {
+                    const int r = rb + i * Q;
+                    if (act && r < nx) {
+                        x[i] = gload(rsl, (uint32_t)mrow[r] * (uint32_t)mc * 16u + (uint32_t)cch * 16u);
+                        pend |= 1u << i;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < NBT; ++i)
+                    if ((pend & (1u << i)) && chunk_at(x[i], e)) pend &= ~(1u << i);
+                while (pend && ok) {
+                    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                    for (int i = 0; i < NBT; ++i)
+                        if (pend & (1u << i))
+                            x[i] = gload(rsl, (uint32_t)mrow[rb + i * Q] * (uint32_t)mc * 16u + (uint32_t)cch * 16u);
+#pragma unroll
+                    for (int i = 0; i < NBT; ++i)
+                        if ((pend & (1u << i)) && chunk_at(x[i], e)) pend &= ~(1u << i);
+                    if (pend && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
+                }
+#pragma unroll
+                for (int i = 0; i < NBT; ++i)
+                    if (act && rb + i * Q < nx) {
+                        a0 += chunk_v0(x[i]);
+                        a1 += chunk_v1(x[i]);
+                        fl |= (x[i][1] | x[i][3]) & 3;
+                    }
+            }
+            float* st = reinterpret_cast<float*>(gred);
+            st[tid * 4] = a0;
+            st[tid * 4 + 1] = a1;
+            st[tid * 4 + 2] = __builtin_bit_cast(float, fl);
+            __syncthreads();
+            if (sq == 0 && act) {
+                float s0 = st[sj * 4], s1 = st[sj * 4 + 1];
+                int f = __builtin_bit_cast(int, st[sj * 4 + 2]);
+                for (int qq = 1; qq < Q; ++qq) {
+                    s0 += st[(qq * swp + sj) * 4];
+                    s1 += st[(qq * swp + sj) * 4 + 1];
+                    f |= __builtin_bit_cast(int, st[(qq * swp + sj) * 4 + 2]);
+                }
+                gstore(rxp, (uint32_t)(((e & 1) * 8 + xcd) * mc + cch) * 16u, chunk2(s0, s1, (int)(e << 2) | f));
+            }
+            __syncthreads();
+        }
+        // c. owned slices: S = the active XCCs' partials in XCC order -> this XCC's ring slot
+        if (sq == 0) {
+            for (int sl = gslot_r; sl < kSwSlices; sl += nx) {
+                const int cch = sl * sw + sj;
+                if (!(sj < sw && cch < mc)) continue;
+                I4 x[8];
+                unsigned pend = 0;
+#pragma unroll
+                for (int xx = 0; xx < 8; ++xx)
+                    if (act_mask & (1u << xx)) {
+                        x[xx] = gload(rxp, (uint32_t)(((e & 1) * 8 + xx) * mc + cch) * 16u);
+                        pend |= 1u << xx;
+                    }
+#pragma unroll
+                for (int xx = 0; xx < 8; ++xx)
+                    if ((pend & (1u << xx)) && chunk_at(x[xx], e)) pend &= ~(1u << xx);
+                while (pend && ok) {
+                    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                    for (int xx = 0; xx < 8; ++xx)
+                        if (pend & (1u << xx)) x[xx] = gload(rxp, (uint32_t)(((e & 1) * 8 + xx) * mc + cch) * 16u);
+#pragma unroll
+                    for (int xx = 0; xx < 8; ++xx)
+                        if ((pend & (1u << xx)) && chunk_at(x[xx], e)) pend &= ~(1u << xx);
+                    if (pend && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
+                }
+                float s0 = 0.f, s1 = 0.f;
+                int f = 0;
+#pragma unroll
+                for (int xx = 0; xx < 8; ++xx)
+                    if (act_mask & (1u << xx)) {
+                        s0 += chunk_v0(x[xx]);
+                        s1 += chunk_v1(x[xx]);
+                        f |= (x[xx][1] | x[xx][3]) & 3;
+                    }
+                gstore_col(rfs, (uint32_t)((xcd * 4 + (int)(e & 3)) * mc + cch) * 16u, chunk2(s0, s1, (int)(e << 2) | f), 1);
+            }
+        }
+        ok = !block_or(ok ? 0 : 4, 2 + (int)(e & 1));
+        deadline = __builtin_amdgcn_s_memrealtime() + p.stall_ticks;
+        return ok;
+    };
+
     // ---- prologue: S[0] = K^T u0
     if (my_nb > 0) load_block(0, bufA);
     sweep(-1);
-    flush(0);
+    if (gran) {
+        if (reg_ok && !flush_gran(0)) gep = -1;
+    } else {
+        flush(0);
+    }
     int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
     bool done = false, ran_all = false;
     if (!reg_ok || gep < 0 ||
-        !xcd_barrier(p.sync, xcd, nx, nact, act_mask, 1, deadline, p.stall_ticks, &s_flag)) {
+        (!gran && !xcd_barrier(p.sync, xcd, nx, nact, act_mask, 1, deadline, p.stall_ticks, &s_flag))) {
         status = OTF_SK_TIMEOUT;
         done = true;
     }
 
     for (int it = 0; it < p.max_iter && !done; ++it) {
         OTF_STAMP(it, 0);
-        const int prev_bad = it >= 1 ? load_agent(p.bad + ((it - 1) & 3) * 64) : 0;
-        int badv = 0;
+        int prev_bad = (!gran && it >= 1) ? load_agent(p.bad + ((it - 1) & 3) * 64) : 0;
+        int badv = 0, gfl = 0;
+        bool gok = true;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             T s[VC], bv[VC];
-            load_sums_chunk(it, g, s);
+            if (gran)
+                load_sums_gran(it, g, s, gfl, gok);
+            else
+                load_sums_chunk(it, g, s);
             load_b_chunk(g, bv);
             T vv[VC];
 #pragma unroll
@@ -583,6 +805,15 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                     *reinterpret_cast<V*>(vbuf + c0 + h * VT) = wv;
                 }
             }
+        }
+        if (gran) {  // S[it]'s flags: u(it-1) not finite; a stalled poll: timeout
+            const int bits = block_or((gfl & 1) | (gok ? 0 : 4), it & 1);
+            if (bits & 4) {
+                status = OTF_SK_TIMEOUT;
+                break;
+            }
+            prev_bad = bits & 1;
+            deadline = __builtin_amdgcn_s_memrealtime() + p.stall_ticks;
         }
         if (prev_bad > 0) {  // u(it-1) not finite: revert to it-2
             last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
@@ -605,7 +836,11 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         OTF_STAMP(it, 1);
         sweep(it);
         OTF_STAMP(it, 2);
-        flush(it + 1);
+        if (gran) {
+            if (!flush_gran(it + 1)) gep = -1;
+        } else {
+            flush(it + 1);
+        }
         OTF_STAMP(it, 3);
 #ifdef OTF_STAMPS
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -613,7 +848,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         OTF_STAMP(it, 4);
 #endif
         if (gep < 0 ||
-            !xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 2, deadline, p.stall_ticks, &s_flag)) {
+            (!gran && !xcd_barrier(p.sync, xcd, nx, nact, act_mask, it + 2, deadline, p.stall_ticks, &s_flag))) {
             status = OTF_SK_TIMEOUT;
             done = true;
         }
@@ -622,7 +857,20 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     }
     if (status == OTF_SK_MAX_ITER && ran_all) {
         const int it = p.max_iter - 1;
-        if (load_agent(p.bad + (it & 3) * 64) > 0) {
+        int ubad = 0;
+        if (gran) {  // u(it)'s flag rides in S[it + 1]
+            int fl = 0;
+            bool ok = true;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                T tmp[VC];
+                load_sums_gran(it + 1, g, tmp, fl, ok);
+            }
+            ubad = block_or(fl & 1, (it + 1) & 1) & 1;
+        } else {
+            ubad = load_agent(p.bad + (it & 3) * 64) > 0;
+        }
+        if (ubad) {
             last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
         } else {
             last_good = it; niter = it;
@@ -644,7 +892,13 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         T vo[VC];
         if (last_good >= 0) {
             T sl[VC], bv[VC];
-            load_sums_chunk(last_good, g, sl);
+            if (gran) {
+                int fl = 0;
+                bool ok = true;
+                load_sums_gran(last_good, g, sl, fl, ok);
+            } else {
+                load_sums_chunk(last_good, g, sl);
+            }
             load_b_chunk(g, bv);
 #pragma unroll
             for (int k = 0; k < VC; ++k) vo[k] = k < cnt[g] ? bv[k] / sl[k] : (T)0;
@@ -804,8 +1058,11 @@ int sweep_grid(int64_t nrb) {
 
 }  // namespace
 
+// granule flush: slab rows + 2 x 8 XCC partials + 8 x 4 S slots (8 B a column) + lists
+size_t sweep_gran_bytes(int64_t m_pad) { return (size_t)(kSwMaxGrid + 16 + 32) * m_pad * 8 + 8 * 256 * 4; }
 template <typename T> size_t sweep_region_bytes(int64_t m_pad) {
-    return sweep_ctrl_bytes(m_pad, sizeof(T)) + (size_t)kSwMaxGrid * m_pad * sizeof(T);
+    return sweep_ctrl_bytes(m_pad, sizeof(T)) + (size_t)kSwMaxGrid * m_pad * sizeof(T) +
+           (sizeof(T) == 4 ? sweep_gran_bytes(m_pad) : 0);
 }
 
 template <typename T, typename CT> bool sweep_supported(int64_t n, int64_t m, int64_t ldc) {
@@ -864,7 +1121,20 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     p.reg_ticks = reg_stall_ticks();
     p.nt_loads = (double)n * ldc * sizeof(CT) > 192.0 * (1 << 20) ? 1 : 0;
     p.det = o.deterministic ? 1 : 0;
-    hipError_t e = hipMemsetAsync(region, 0, sweep_ctrl_bytes(m_pad, sizeof(T)), s);
+    // OTF_SWEEP_GRAN=0: the r02 flush (slab + group counter + atomics + grid barrier)
+    const char* ge = getenv("OTF_SWEEP_GRAN");
+    p.gran = (sizeof(T) == 4 && !p.det && !(ge && atoi(ge) == 0)) ? 1 : 0;
+    size_t zero_bytes = sweep_ctrl_bytes(m_pad, sizeof(T));
+    if (p.gran) {
+        unsigned char* gb = (unsigned char*)p.slab + (size_t)kSwMaxGrid * m_pad * sizeof(T);
+        p.gslab = gb;
+        p.gxp = gb + (size_t)kSwMaxGrid * m_pad * 8;
+        p.gfs = p.gxp + (size_t)16 * m_pad * 8;
+        p.xl = (int*)(p.gfs + (size_t)32 * m_pad * 8);
+        hipError_t e0 = hipMemsetAsync(gb, 0, sweep_gran_bytes(m_pad), s);  // tags: epoch 0
+        if (e0 != hipSuccess) return e0;
+    }
+    hipError_t e = hipMemsetAsync(region, 0, zero_bytes, s);
     if (e != hipSuccess) return e;
     int R = 1;
     switch (G) {

@@ -244,6 +244,18 @@ def test_float32_stop_and_break_all_engines(ops, orc, dev, engine):
     assert info["status_name"] == "numerical_break" and info["break_iter"] == 0
     assert info["niter"] == info2["niter"]
     assert nrel(res.plan.cpu().numpy(), P2) < 1e-5
+    # a ROW of cost 1e3: K v = 0 there, u = inf at iteration 0 (the non-finite-u path:
+    # the sweep engine's granule flags, the mesh engine's hop-A tags)
+    C3 = rng.random((n, m)).astype(np.float32)
+    C3[41, :] = 1e3
+    P3, *_, info3 = orc.sinkhorn_knopp(a, b, C3.astype(np.float64), 1.0, 100, 0.0)
+    assert info3["break_iter"] == 0
+    res = ops.sinkhorn(_t(a, dev, torch.float32), _t(b, dev, torch.float32), _t(C3, dev), 1.0,
+                       max_iter=100, stop_thr=0.0, engine=engine)
+    info = res.info()
+    assert info["status_name"] == "numerical_break" and info["break_iter"] == info3["break_iter"]
+    assert info["niter"] == info3["niter"] and info["last_good"] == -1
+    assert nrel(res.plan.cpu().numpy(), P3) < 1e-5
 
 
 @pytest.mark.parametrize("engine", ["stream", "resident", "sweep", "gather"])   # float64 (tiled: fp32 test above)

@@ -1,6 +1,6 @@
 """Pairwise-cost kernel probe: event time of ops.pairwise_cost (split-fp16 MFMA, fp32 out)
 and pairwise_cost_ex variants at the metric shape, plus max error vs float64 on a row
-sample.  python tools/bench_cost.py [N] [d]"""
+sample.  python tools/bench_cost.py [N] [d]   (OTF_COST_RING=0/1 picks the 256 x 256 kernel)"""
 import os
 import sys
 
@@ -41,5 +41,6 @@ for algo in ("split16", "f32"):
     print(f"{algo:8s} {ms * 1e3:8.1f} us  {2.0 * N * N * d / ms / 1e9:7.1f} TFLOP/s fp32-eq  "
           f"max err / max C {err:.2e}", flush=True)
 Xh, Yh = Xd.half(), Yd.half()
+C0, _, _ = ops.pairwise_cost_ex(Xh, Yh, out_dtype=torch.float16)
 ms = timeit(lambda: ops.pairwise_cost_ex(Xh, Yh, out_dtype=torch.float16))
 print(f"f16-in f16-out {ms * 1e3:8.1f} us  {2.0 * N * N * d / ms / 1e9:7.1f} TFLOP/s", flush=True)
