@@ -23,9 +23,12 @@ def test_version_and_workspace_queries_are_host_only():
     ws = lib.otf_sinkhorn_workspace_size(4096, 4096, L.OTF_F32, 100)
     # streaming buffers (~9 vectors), the persistent engines' 4-slot sum rings, the tiled
     # engine's row exchange, the sweep engine's partial slab (256 rows of N) and the mesh
-    # engine's granule slots (2 parities x 256 tiles x (4 KB column + 1.25 KB row + 256 B))
+    # engine's granule slots (2 parities x 256 tiles x (4 KB column + 1.25 KB row + 256 B)),
+    # the sweep engine's granule flush (256 slab rows + 16 XCC partials + 32 S slots, 8 B a
+    # column, + 8 KB of registration lists)
     mesh = 2 * 256 * (4096 + 1280 + 256)
-    assert 4 * 4096 * (9 + 16 + 256) + mesh < ws < 4 * 4096 * (80 + 256) + mesh
+    gran = (256 + 16 + 32) * 4096 * 8 + 8192
+    assert 4 * 4096 * (9 + 16 + 256) + mesh + gran < ws < 4 * 4096 * (80 + 256) + mesh + gran
     # only the err log grows with max_iter (the ring replaces per-iteration buffers)
     ws_long = lib.otf_sinkhorn_workspace_size(4096, 4096, L.OTF_F32, 100000)
     assert ws_long - ws <= 8 * 100000 + 512
