@@ -482,7 +482,7 @@ typedef struct {
     double* T;        /* (n x m) optimal plan out, row stride ldt                    */
     int64_t ldt;
     int32_t n;
-    int32_t m;        /* n + m + 1 <= otf_emd_max_nodes()                            */
+    int32_t m;        /* n + m + 1 <= otf_emd_max_nodes(), n * m + n + m < 2^31       */
 } otf_emd_problem;
 
 /* Written on the device, one per problem. */
@@ -493,7 +493,11 @@ typedef struct {
     double max_artificial_flow; /* 0 at a feasible optimum                              */
 } otf_emd_info;
 
+/* Largest n + m + 1 (n * m + n + m < 2^31 also holds).  Up to otf_emd_lds_nodes()
+ * the spanning tree lives in LDS; larger problems keep it in global memory (stream-
+ * ordered allocation inside otf_emd_solve), same pivots. */
 int otf_emd_max_nodes(void);
+int otf_emd_lds_nodes(void);
 /* probs: HOST array of nprob descriptors; info: device array of nprob. */
 int otf_emd_solve(int32_t nprob, const otf_emd_problem* probs, int64_t max_pivots,
                   otf_emd_info* info, otf_stream_t stream);

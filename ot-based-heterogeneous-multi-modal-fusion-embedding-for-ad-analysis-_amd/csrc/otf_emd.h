@@ -34,7 +34,11 @@
 // Tree arcs have reduced cost 0, so pricing needs no arc state; the flow of a tree
 // arc lives with its child node, so the plan is written once at the end.
 // One workgroup per problem: a batch (the per-label plans of one COOT-L step) is one
-// launch.  Per node 31 B of LDS: n + m + 1 <= kEmdMaxNodes.
+// launch.  Per node 31 B of LDS (16-bit tree indices): n + m + 1 <= kEmdMaxNodes.
+// Larger problems (POT's emd has no node ceiling: a feature plan at d + d' > 4799, or
+// a large --max-jax-samples) keep the tree in global memory instead -- 45 B per node
+// with 32-bit indices, L2-resident up to ~90 k nodes per XCC -- and only the
+// workgroup's reduction scratch in LDS; same algorithm, same pivots.
 #pragma once
 #include "otf_device.h"
 
@@ -46,13 +50,23 @@ namespace otf {
 __device__ unsigned long long g_emd_stats[8];
 #endif
 
-constexpr int kEmdMaxNodes = 4800;
+constexpr int kEmdMaxNodes = 4800;                    // LDS-resident tree (16-bit indices)
 constexpr size_t kEmdScratch = 256 * (8 + 4) + 128;  // reductions of up to 256 threads
-constexpr size_t kEmdNodeBytes = 2 * 8 + 7 * 2 + 1;  // pi, tflow | par sz pos ord tmp shift path | sgn
+// pi, tflow | par sz pos ord tmp shift path | sgn
+template <typename IX> constexpr size_t emd_node_bytes() { return 2 * 8 + 7 * sizeof(IX) + 1; }
+constexpr size_t kEmdNodeBytes = emd_node_bytes<short>();
 
-// LDS of emd_block for n + m + 1 = N nodes
+// LDS of emd_block for n + m + 1 = N nodes (tree and scratch in LDS)
 inline __host__ __device__ size_t emd_lds_bytes(int N) {
     return ((size_t)N * kEmdNodeBytes + 15) / 16 * 16 + kEmdScratch;
+}
+// global-memory tree of emd_block<NT, int> for N nodes
+inline __host__ __device__ size_t emd_tree_bytes_g(int64_t N) {
+    return ((size_t)N * emd_node_bytes<int>() + 255) / 256 * 256;
+}
+// the global-tree form: n * m real arcs + N artificial ones index as int
+inline __host__ __device__ bool emd_fits_g(int64_t n, int64_t m) {
+    return n * m + n + m + 1 < (int64_t)INT32_MAX;
 }
 
 inline __device__ void argmin_pair(double& v, int& i, double v2, int i2) {
@@ -62,26 +76,29 @@ inline __device__ void argmin_pair(double& v, int& i, double v2, int i2) {
     }
 }
 
-// One workgroup of NT threads solves one problem; every thread must call it.  esm:
-// emd_lds_bytes(n + m + 1) bytes of LDS (16-B aligned).  P.a / P.b may point to LDS.
-template <int NT>
-__device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, unsigned char* esm) {
+// One workgroup of NT threads solves one problem; every thread must call it.  tree:
+// the node arrays (N * emd_node_bytes<IX>() bytes, 16-B aligned) -- LDS for IX = short,
+// a workspace in global memory for IX = int; scr: kEmdScratch bytes of LDS.  P.a / P.b
+// may point to LDS.  Every access goes through generic pointers, and __syncthreads
+// orders global memory within the workgroup as it does LDS.
+template <int NT, typename IX = short>
+__device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, unsigned char* tree,
+                                  unsigned char* scr) {
     static_assert(NT % 64 == 0 && NT <= 256, "whole waves; kEmdScratch holds 256 lanes");
     constexpr int kNW = NT / 64;
     const int n = P.n, m = P.m, N = n + m + 1, R = N - 1;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 
-    double* pi = reinterpret_cast<double*>(esm);   // node potentials
+    double* pi = reinterpret_cast<double*>(tree);  // node potentials
     double* tflow = pi + N;                         // flow of the tree arc (u, parent u)
-    short* par = reinterpret_cast<short*>(tflow + N);
-    short* sz = par + N;                            // subtree sizes
-    short* pos = sz + N;                            // position in the pre-order
-    short* ord = pos + N;                           // the pre-order (ord[pos[x]] = x)
-    short* tmp = ord + N;                           // new pre-order of the moved subtree
-    short* shf = tmp + N;                           // the block of ord that shifts
-    short* path = shf + N;                          // u_in .. u_out
+    IX* par = reinterpret_cast<IX*>(tflow + N);
+    IX* sz = par + N;                               // subtree sizes
+    IX* pos = sz + N;                               // position in the pre-order
+    IX* ord = pos + N;                              // the pre-order (ord[pos[x]] = x)
+    IX* tmp = ord + N;                              // new pre-order of the moved subtree
+    IX* shf = tmp + N;                              // the block of ord that shifts
+    IX* path = shf + N;                             // u_in .. u_out
     signed char* sgn = reinterpret_cast<signed char*>(path + N);  // 1: supply > 0
-    unsigned char* scr = esm + ((size_t)N * kEmdNodeBytes + 15) / 16 * 16;
     double* rv = reinterpret_cast<double*>(scr);
     int* ri = reinterpret_cast<int*>(rv + NT);
     int* flag = ri + NT;      // [0] stop code, [1..7] pivot scalars
@@ -109,21 +126,21 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
     for (int k = tid; k < N - 1; k += NT) {
         const double sup = k < n ? P.a[k] : -P.b[k - n];
         sgn[k] = sup > 0.0 ? 1 : 0;
-        par[k] = (short)R;
+        par[k] = (IX)R;
         tflow[k] = fabs(sup);
         pi[k] = sup > 0.0 ? -ART : ART;
         sz[k] = 1;
-        pos[k] = (short)(k + 1);
-        ord[k + 1] = (short)k;
+        pos[k] = (IX)(k + 1);
+        ord[k + 1] = (IX)k;
     }
     if (tid == 0) {
         sgn[R] = 0;
         par[R] = -1;
         tflow[R] = 0.0;
         pi[R] = 0.0;
-        sz[R] = (short)N;
+        sz[R] = (IX)N;
         pos[R] = 0;
-        ord[0] = (short)R;
+        ord[0] = (IX)R;
         flag[0] = 0;
     }
     __syncthreads();
@@ -253,10 +270,10 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
                 }
                 const int u_in = side == 1 ? s : t, v_in = side == 1 ? t : s;
                 int k = 0;
-                path[0] = (short)u_in;
+                path[0] = (IX)u_in;
                 for (u = u_in; u != u_out;) {
                     u = par[u];
-                    path[++k] = (short)u;
+                    path[++k] = (IX)u;
                 }
                 flag[1] = k;
                 flag[2] = u_in;
@@ -304,20 +321,20 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
             // path nodes in descending order); the others save the shifting block
             if (tid == 0) {
                 const int w = par[u_out];
-                for (int x = w; x != join; x = par[x]) sz[x] = (short)(sz[x] - L);
-                for (int x = v_in; x != join; x = par[x]) sz[x] = (short)(sz[x] + L);
+                for (int x = w; x != join; x = par[x]) sz[x] = (IX)(sz[x] - L);
+                for (int x = v_in; x != join; x = par[x]) sz[x] = (IX)(sz[x] + L);
                 int acc = 0;
                 for (int i = k; i >= 1; --i) {
                     acc += sz[path[i]] - sz[path[i - 1]];
-                    sz[path[i]] = (short)acc;
+                    sz[path[i]] = (IX)acc;
                 }
-                sz[u_in] = (short)L;
+                sz[u_in] = (IX)L;
                 double carry = dsc[1];
                 int prev = v_in;
                 for (int i = 0; i <= k; ++i) {
                     const int x = path[i];
                     const double f = tflow[x];
-                    par[x] = (short)prev;
+                    par[x] = (IX)prev;
                     tflow[x] = carry;
                     carry = f;
                     prev = x;
@@ -332,13 +349,13 @@ __device__ otf_emd_info emd_block(const otf_emd_problem& P, int64_t max_pivots, 
             const double sigma = dsc[0];
             for (int e = tid; e < nb; e += NT) {
                 const int x = shf[e];
-                ord[nb0 + e] = (short)x;
-                pos[x] = (short)(nb0 + e);
+                ord[nb0 + e] = (IX)x;
+                pos[x] = (IX)(nb0 + e);
             }
             for (int e = tid; e < L; e += NT) {
                 const int x = tmp[e];
-                ord[ns0 + e] = (short)x;
-                pos[x] = (short)(ns0 + e);
+                ord[ns0 + e] = (IX)x;
+                pos[x] = (IX)(ns0 + e);
                 pi[x] += sigma;
             }
 #ifdef OTF_EMD_STAMPS

@@ -38,7 +38,11 @@
 //    <constC - 2 C1 T C2, T>.
 //
 // Everything is float64 like the reference.  Matrices live in a caller workspace
-// (L2-resident at the reference's sizes, <= 1024 per side), vectors in LDS.
+// (L2-resident at the reference's sizes, <= 1024 per side), vectors in LDS.  Problems
+// up to GW_HUGEN per side (POT has no cap) run the same loop with the vectors and the
+// network simplex's tree in the workspace too (GwHuge); CG's linear step is then
+// always the network simplex (the one-wave assignment solver keeps its columns in
+// registers, <= 1024).
 #include <float.h>
 
 #include "otf_device.h"
@@ -48,6 +52,7 @@ namespace otf {
 namespace {
 
 constexpr int GW_MAXN = 1024;
+constexpr int GW_HUGEN = 4096;
 constexpr int GW_MAXP = 16;
 constexpr double GW_INF = 1e300;
 constexpr int GW_SMALLN = 64;  // problems with n, m <= this run with all matrices in LDS
@@ -60,13 +65,17 @@ template <int NT_, int MAXV_, bool SMALL_> struct GwCfg {
     static constexpr int NW = NT_ / kWave;
     static constexpr int MAXV = MAXV_;
     static constexpr bool SMALL = SMALL_;
+    static constexpr bool GLOBAL = MAXV_ > GW_MAXN;  // shared state in the workspace
 };
 using GwBig = GwCfg<256, GW_MAXN, false>;
+using GwHuge = GwCfg<256, GW_HUGEN, false>;
 using GwSmall = GwCfg<512, GW_SMALLN, true>;
 
+template <class Cfg> constexpr size_t gw_sh_bytes();
 struct GwLaunch {
     otf_gw_problem prob[GW_MAXP];
     double* ws[GW_MAXP];
+    unsigned char* shg[GW_MAXP];   // GwHuge: GwShared, then the network simplex's tree
     int first;  // index of prob[0] in the caller's array (info / cost-log rows)
     int nprob;
 };
@@ -106,6 +115,8 @@ template <class Cfg> struct GwShared {
     int kflag[2];  // PGD inner Sinkhorn: numerical-error flags by update parity
     GwMats<Cfg::SMALL ? GW_SMALLN : 0> mat;
 };
+
+template <class Cfg> constexpr size_t gw_sh_bytes() { return (sizeof(GwShared<Cfg>) + 255) / 256 * 256; }
 
 // Diagnostic build only (-DOTF_GW_STAMPS, tools/stamps_gw.hip): per-phase wall-clock
 // totals of workgroup 0..15 (s_memrealtime ticks, 10 ns); compiled out of the library.
@@ -669,7 +680,14 @@ template <class Cfg>
 __global__ __launch_bounds__(Cfg::NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, otf_gw_info* infos,
                                                    double* costlog, int costlog_len,
                                                    unsigned long long timeout_ticks) {
-    __shared__ GwShared<Cfg> sh;
+    GwShared<Cfg>* shp;
+    if constexpr (Cfg::GLOBAL) {
+        shp = reinterpret_cast<GwShared<Cfg>*>(Lz.shg[blockIdx.x]);
+    } else {
+        __shared__ GwShared<Cfg> sh_lds;
+        shp = &sh_lds;
+    }
+    GwShared<Cfg>& sh = *shp;
     if ((int)blockIdx.x >= Lz.nprob) return;
     const otf_gw_problem P = Lz.prob[blockIdx.x];
     const int pid = Lz.first + blockIdx.x;
@@ -724,7 +742,7 @@ __global__ __launch_bounds__(Cfg::NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o,
 
     // CG on weighted or unequal groups: the linear step is the network simplex
     // (emd_block, dynamic LDS) instead of the assignment solver
-    const bool gen_cg = !Cfg::SMALL && o.solver == OTF_GW_CG && (n != m || P.p || P.q);
+    const bool gen_cg = !Cfg::SMALL && o.solver == OTF_GW_CG && (Cfg::GLOBAL || n != m || P.p || P.q);
     if (gen_cg) {
         if constexpr (!Cfg::SMALL) {
             extern __shared__ __attribute__((aligned(16))) unsigned char gw_dyn[];
@@ -785,7 +803,14 @@ __global__ __launch_bounds__(Cfg::NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o,
                 ep.n = n;
                 ep.m = m;
                 __syncthreads();
-                const otf_emd_info ei = emd_block<Cfg::NT>(ep, 100000, gw_dyn);
+                otf_emd_info ei;
+                if constexpr (Cfg::GLOBAL) {
+                    __shared__ __attribute__((aligned(16))) unsigned char emd_scr[kEmdScratch];
+                    ei = emd_block<Cfg::NT, int>(ep, 100000, Lz.shg[blockIdx.x] + gw_sh_bytes<Cfg>(), emd_scr);
+                } else {
+                    ei = emd_block<Cfg::NT>(ep, 100000, gw_dyn,
+                                            gw_dyn + ((size_t)(n + m + 1) * kEmdNodeBytes + 15) / 16 * 16);
+                }
                 __syncthreads();
                 if (ei.status == OTF_EMD_INFEASIBLE || ei.status == OTF_EMD_UNBOUNDED) {
                     status = OTF_GW_NUMERICAL;
@@ -881,9 +906,11 @@ __global__ __launch_bounds__(Cfg::NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o,
             __syncthreads();
             // Gc = assignment(Mi) / n
 { GW_TBEG();
-            if (t < kWave) {
-                const bool ok = wave_lap<(Cfg::MAXV + kWave - 1) / kWave>(Lm, ldl, n, sh.lap.sigma, sh.f, sh.lap.used);
-                if (t == 0) sh.flag = ok ? 0 : 1;
+            if constexpr (!Cfg::GLOBAL) {  // (GwHuge: the CG step is the network simplex)
+                if (t < kWave) {
+                    const bool ok = wave_lap<(Cfg::MAXV + kWave - 1) / kWave>(Lm, ldl, n, sh.lap.sigma, sh.f, sh.lap.used);
+                    if (t == 0) sh.flag = ok ? 0 : 1;
+                }
             }
             __syncthreads();
 GW_TEND(1); }
@@ -1234,47 +1261,34 @@ int otf_cost_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64_t l
     return OTF_OK;
 }
 
+namespace otf {
+namespace {
+bool gw_huge(const otf_gw_problem& P) { return P.n > GW_MAXN || P.m > GW_MAXN; }
+// per problem: 4 n x m matrices, and for GwHuge its shared state + the simplex tree
+size_t gw_prob_bytes(const otf_gw_problem& P) {
+    size_t b = align256(4 * 8 * (size_t)P.n * (size_t)P.m);
+    if (gw_huge(P)) b += gw_sh_bytes<GwHuge>() + emd_tree_bytes_g((int64_t)P.n + P.m + 1);
+    return b;
+}
+}  // namespace
+}  // namespace otf
+
 size_t otf_gw_workspace_size(int32_t nprob, const otf_gw_problem* probs) {
     if (nprob <= 0 || !probs) return 0;
     size_t tot = 0;
-    for (int b = 0; b < nprob; ++b) tot += otf::align256(4 * 8 * (size_t)(probs[b].n * probs[b].m));
+    for (int b = 0; b < nprob; ++b) tot += otf::gw_prob_bytes(probs[b]);
     return tot;
 }
 
-int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* opts,
-                 otf_gw_info* info, double* costlog, int32_t costlog_len, void* workspace,
-                 size_t ws_bytes, otf_stream_t stream) {
+static int gw_launch(const otf::GwLaunch& L, const otf_gw_opts& o, otf_gw_info* info, double* costlog,
+                     int32_t costlog_len, unsigned long long ticks, bool huge, hipStream_t s) {
     using namespace otf;
-    if (nprob <= 0 || !probs || !opts || !info || !workspace) return OTF_EINVAL;
-    const otf_gw_opts o = *opts;
-    if (o.solver != OTF_GW_CG && o.solver != OTF_GW_ENTROPIC && o.solver != OTF_GW_PGD)
-        return OTF_EINVAL;
-    if (o.max_iter < 1) return OTF_EINVAL;
-    if (o.solver != OTF_GW_CG && (!(o.eps > 0) || o.sk_inner < 1 || o.sk_max_iter < 1))
-        return OTF_EINVAL;
-    if (costlog && costlog_len < 1) return OTF_EINVAL;
-    if (ws_bytes < otf_gw_workspace_size(nprob, probs)) return OTF_EINVAL;
-    for (int b = 0; b < nprob; ++b) {
-        const otf_gw_problem& P = probs[b];
-        if (!P.C1 || !P.C2 || !P.T || P.n < 1 || P.m < 1) return OTF_EINVAL;
-        if (P.ldc1 < P.n || P.ldc2 < P.m || P.ldt < P.m) return OTF_EINVAL;
-        if (P.n > GW_MAXN || P.m > GW_MAXN) return OTF_EUNSUPPORTED;
-        if ((P.labels_a == nullptr) != (P.labels_b == nullptr)) return OTF_EINVAL;
-        if (o.solver == OTF_GW_CG && P.labels_a) return OTF_EUNSUPPORTED;
-        if (o.solver == OTF_GW_PGD && P.labels_a) return OTF_EUNSUPPORTED;
+    if (huge) {
+        gw_kernel<GwHuge><<<L.nprob, GwHuge::NT, 0, s>>>(L, o, info, costlog, costlog_len, ticks);
+        OTF_HIP(hipGetLastError());
+        return OTF_OK;
     }
-    hipStream_t s = (hipStream_t)stream;
-    char* wsp = (char*)workspace;
-    const unsigned long long ticks = 100000000ull * 20;  // 20 s at 100 MHz
-    for (int first = 0; first < nprob; first += GW_MAXP) {
-        GwLaunch L{};
-        L.first = first;
-        L.nprob = nprob - first < GW_MAXP ? nprob - first : GW_MAXP;
-        for (int b = 0; b < L.nprob; ++b) {
-            L.prob[b] = probs[first + b];
-            L.ws[b] = (double*)wsp;
-            wsp += align256(4 * 8 * (size_t)(probs[first + b].n * probs[first + b].m));
-        }
+    {
         bool small = true;
         size_t dyn = 0;  // CG on weighted / unequal groups: the network simplex's LDS
         for (int b = 0; b < L.nprob; ++b) {
@@ -1295,6 +1309,83 @@ int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* 
             gw_kernel<GwBig><<<L.nprob, GwBig::NT, dyn, s>>>(L, o, info, costlog, costlog_len, ticks);
         }
         OTF_HIP(hipGetLastError());
+    }
+    return OTF_OK;
+}
+
+int otf_gw_solve(int32_t nprob, const otf_gw_problem* probs, const otf_gw_opts* opts,
+                 otf_gw_info* info, double* costlog, int32_t costlog_len, void* workspace,
+                 size_t ws_bytes, otf_stream_t stream) {
+    using namespace otf;
+    if (nprob <= 0 || !probs || !opts || !info || !workspace) return OTF_EINVAL;
+    const otf_gw_opts o = *opts;
+    if (o.solver != OTF_GW_CG && o.solver != OTF_GW_ENTROPIC && o.solver != OTF_GW_PGD)
+        return OTF_EINVAL;
+    if (o.max_iter < 1) return OTF_EINVAL;
+    if (o.solver != OTF_GW_CG && (!(o.eps > 0) || o.sk_inner < 1 || o.sk_max_iter < 1))
+        return OTF_EINVAL;
+    if (costlog && costlog_len < 1) return OTF_EINVAL;
+    if (ws_bytes < otf_gw_workspace_size(nprob, probs)) return OTF_EINVAL;
+    for (int b = 0; b < nprob; ++b) {
+        const otf_gw_problem& P = probs[b];
+        if (!P.C1 || !P.C2 || !P.T || P.n < 1 || P.m < 1) return OTF_EINVAL;
+        if (P.ldc1 < P.n || P.ldc2 < P.m || P.ldt < P.m) return OTF_EINVAL;
+        if (P.n > GW_HUGEN || P.m > GW_HUGEN) return OTF_EUNSUPPORTED;
+        if ((P.labels_a == nullptr) != (P.labels_b == nullptr)) return OTF_EINVAL;
+        if (o.solver == OTF_GW_CG && P.labels_a) return OTF_EUNSUPPORTED;
+        if (o.solver == OTF_GW_PGD && P.labels_a) return OTF_EUNSUPPORTED;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    char* wsp = (char*)workspace;
+    // 20 s at 100 MHz per outer iteration, scaled up with the problem past 1024^2 pairs
+    // (GwHuge: one workgroup's GEMMs and simplex grow with n m (n + m))
+    unsigned long long ticks = 100000000ull * 20;
+    for (int b = 0; b < nprob; ++b) {
+        const double sc = (double)probs[b].n * probs[b].m * (probs[b].n + probs[b].m) / (2.0 * 1024.0 * 1024.0 * 1024.0);
+        if (sc > 1.0 && 100000000ull * 20 * sc > (double)ticks) ticks = (unsigned long long)(100000000.0 * 20 * sc);
+    }
+    // one launch per kernel variant (GwHuge problems separately)
+    for (int huge = 0; huge < 2; ++huge)
+    for (int first = 0; first < nprob; first += GW_MAXP) {
+        GwLaunch L{};
+        L.first = first;
+        L.nprob = 0;
+        char* w = wsp;
+        for (int b = 0; b < first; ++b) w += gw_prob_bytes(probs[b]);
+        const int last = nprob - first < GW_MAXP ? nprob - first : GW_MAXP;
+        // problems of this variant in [first, first + last): launched as one batch whose
+        // info / log rows are addressed through L.first + slot, so keep the slots dense
+        int idx[GW_MAXP];
+        for (int b = 0; b < last; ++b) {
+            const otf_gw_problem& P = probs[first + b];
+            char* mine = w;
+            w += gw_prob_bytes(P);
+            if ((int)gw_huge(P) != huge) continue;
+            idx[L.nprob] = first + b;
+            L.prob[L.nprob] = P;
+            L.ws[L.nprob] = (double*)mine;
+            L.shg[L.nprob] = (unsigned char*)mine + align256(4 * 8 * (size_t)P.n * (size_t)P.m);
+            ++L.nprob;
+        }
+        if (L.nprob == 0) continue;
+        bool dense = true;  // info / cost-log rows are first + slot: contiguous problems only
+        for (int b = 0; b < L.nprob; ++b) dense = dense && idx[b] == idx[0] + b;
+        if (!dense) {  // mixed batch: one launch per problem
+            for (int b = 0; b < L.nprob; ++b) {
+                GwLaunch L1{};
+                L1.first = idx[b];
+                L1.nprob = 1;
+                L1.prob[0] = L.prob[b];
+                L1.ws[0] = L.ws[b];
+                L1.shg[0] = L.shg[b];
+                const int rc = gw_launch(L1, o, info, costlog, costlog_len, ticks, huge != 0, s);
+                if (rc != OTF_OK) return rc;
+            }
+            continue;
+        }
+        L.first = idx[0];
+        const int rc = gw_launch(L, o, info, costlog, costlog_len, ticks, huge != 0, s);
+        if (rc != OTF_OK) return rc;
     }
     return OTF_OK;
 }

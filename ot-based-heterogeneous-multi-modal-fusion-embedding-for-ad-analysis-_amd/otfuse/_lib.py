@@ -142,6 +142,7 @@ _SIGS = {
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                              ctypes.c_void_p]),
     "otf_emd_max_nodes": (ctypes.c_int, []),
+    "otf_emd_lds_nodes": (ctypes.c_int, []),
     "otf_emd_solve": (ctypes.c_int, [_i32, ctypes.POINTER(EmdProblem), _i64, _vp, _vp]),
     "otf_gw_workspace_size": (ctypes.c_size_t, [ctypes.c_int32, ctypes.POINTER(GwProblem)]),
     "otf_gw_solve": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(GwProblem),

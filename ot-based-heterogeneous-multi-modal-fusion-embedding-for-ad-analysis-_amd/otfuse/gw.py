@@ -31,7 +31,7 @@ from . import _lib as L
 
 GW_CG, GW_ENTROPIC, GW_PGD = 0, 1, 2
 GW_STATUS = {0: "running", 1: "converged", 2: "max_iter", 3: "numerical", 4: "timeout"}
-GW_MAXN = 1024
+GW_MAXN = 4096  # per side; past 1024 the kernel keeps its vectors in the workspace
 
 
 GwOpts, GwProblem = L.GwOpts, L.GwProblem

@@ -560,7 +560,13 @@ class EmdResult:
 
 
 def emd_max_nodes() -> int:
+    """Largest n + m + 1 of an exact EMD (n * m + n + m < 2^31 must hold as well)."""
     return int(L.lib().otf_emd_max_nodes())
+
+
+def emd_lds_nodes() -> int:
+    """n + m + 1 up to which the network simplex keeps its tree in LDS."""
+    return int(L.lib().otf_emd_lds_nodes())
 
 
 def emd_batched(problems, max_pivots: int = 100000) -> EmdResult:
@@ -579,8 +585,8 @@ def emd_batched(problems, max_pivots: int = 100000) -> EmdResult:
         b = b.to(dev, torch.float64).contiguous()
         if a.numel() != n or b.numel() != m:
             raise ValueError(f"a ({a.numel()}) / b ({b.numel()}) do not match M {tuple(M.shape)}")
-        if n + m + 1 > emd_max_nodes():
-            raise NotImplementedError(f"EMD {n}x{m}: n + m + 1 must be <= {emd_max_nodes()}")
+        if n + m + 1 > emd_max_nodes() or n * m + n + m >= 2 ** 31 - 1:
+            raise NotImplementedError(f"EMD {n}x{m}: n * m + n + m must be < 2^31")
         T = torch.empty((n, m), dtype=torch.float64, device=dev)
         plans.append(T)
         keep += [a, b, M]

@@ -99,11 +99,78 @@ def test_emd_largest_size_is_feasible_and_optimal_vs_product(dev):
     """n + m + 1 at the LDS bound: feasible, basic, and no worse than the product
     plan or a north-west-corner plan."""
     from otfuse import ops, pot
-    n = ops.emd_max_nodes() // 2 - 1
-    m = ops.emd_max_nodes() - n - 1
+    n = ops.emd_lds_nodes() // 2 - 1
+    m = ops.emd_lds_nodes() - n - 1
     rng = np.random.default_rng(11)
     a, b, M = _problem(rng, n, m)
     T, log = pot.emd(a, b, M, log=True)
     _check_feasible(T, a, b, tol=1e-11)
     assert log["cost"] <= float((np.outer(a, b) * M).sum())
     assert log["result_code"] == 1
+
+
+def _dual_certificate(T, M, a, b, tol):
+    """Optimality of a feasible basic plan: potentials from the positive arcs (a spanning
+    tree of the bipartite graph for non-degenerate masses), then every reduced cost
+    M_ij - u_i - v_j >= -tol."""
+    n, m = M.shape
+    ii, jj = np.nonzero(T > 1e-15)
+    assert len(ii) == n + m - 1                        # non-degenerate: a spanning tree
+    adj_r = [[] for _ in range(n)]
+    adj_c = [[] for _ in range(m)]
+    for i, j in zip(ii, jj):
+        adj_r[i].append(j)
+        adj_c[j].append(i)
+    u = np.full(n, np.nan)
+    v = np.full(m, np.nan)
+    u[0] = 0.0
+    stack = [("r", 0)]
+    while stack:
+        kind, k = stack.pop()
+        if kind == "r":
+            for j in adj_r[k]:
+                if np.isnan(v[j]):
+                    v[j] = M[k, j] - u[k]
+                    stack.append(("c", j))
+        else:
+            for i in adj_c[k]:
+                if np.isnan(u[i]):
+                    u[i] = M[i, k] - v[k]
+                    stack.append(("r", i))
+    assert not np.isnan(u).any() and not np.isnan(v).any()
+    red = M - u[:, None] - v[None, :]
+    assert red.min() >= -tol, red.min()
+
+
+@pytest.mark.parametrize("n,m", [(13, 11), (120, 90), (300, 250)])
+def test_emd_global_tree_matches_lds_tree(orc, dev, monkeypatch, n, m):
+    """The global-memory tree (problems past the LDS) runs the same pivots: forced on
+    problems that fit the LDS, the plans and pivot counts are bit-identical."""
+    from otfuse import ops
+    rng = np.random.default_rng(n + 7 * m)
+    a, b, M = _problem(rng, n, m)
+    args = [(torch.as_tensor(a, device=dev), torch.as_tensor(b, device=dev), torch.as_tensor(M, device=dev))]
+    r0 = ops.emd_batched(args)
+    T0, i0 = r0.plans[0].cpu().numpy(), r0.infos()[0]
+    monkeypatch.setenv("OTF_EMD_TREE", "global")
+    r1 = ops.emd_batched(args)
+    T1, i1 = r1.plans[0].cpu().numpy(), r1.infos()[0]
+    assert np.array_equal(T0, T1) and i0["n_pivots"] == i1["n_pivots"] and i0["cost"] == i1["cost"]
+    Tr, cr = orc.emd_lp(a, b, M)
+    assert np.abs(T1 - Tr).max() < 1e-9
+
+
+def test_emd_past_the_lds_ceiling_is_optimal(dev):
+    """n + m + 1 = 5201 > the LDS bound (4800), where POT's emd has no ceiling: the
+    global-tree network simplex returns a feasible basic plan with a dual certificate
+    (every reduced cost >= 0 for the potentials of its tree)."""
+    from otfuse import ops, pot
+    n, m = 2700, 2500
+    assert n + m + 1 > ops.emd_lds_nodes()
+    rng = np.random.default_rng(21)
+    a, b, M = _problem(rng, n, m)
+    T, log = pot.emd(a, b, M, log=True, numItermax=10 ** 7)
+    assert log["result_code"] == 1
+    _check_feasible(T, a, b, tol=1e-11)
+    _dual_certificate(T, M, a, b, tol=1e-9)
+    assert log["cost"] == pytest.approx(float((T * M).sum()), rel=1e-12)

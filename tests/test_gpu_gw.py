@@ -313,3 +313,35 @@ def test_gw_pgd_small_inner_break_vs_oracle(orc, dev, n, m, eps):
     fin = np.isfinite(Tr)
     if fin.any() and np.abs(Tr[fin]).max() > 0:
         assert np.abs(Td[fin] - Tr[fin]).max() / np.abs(Tr[fin]).max() < 1e-9
+
+
+def test_gw_past_1024_points_vs_oracle(orc, dev):
+    """Groups past the former 1024-point cap (POT's GW has none): GwHuge keeps its
+    vectors and the simplex tree in the workspace.  CG on 1030 x 40 (linear step: the
+    network simplex) and the OTT entropic solver on 1040 x 60, against the oracle."""
+    from otfuse import gw
+    rng = np.random.default_rng(1030)
+    A = rng.standard_normal((1030, 3))
+    B = rng.standard_normal((40, 4))
+    C1 = orc.pairwise_cost(A, A, metric="euclidean", zero_diag=True, scale_max=True)[0]
+    C2 = orc.pairwise_cost(B, B, metric="euclidean", zero_diag=True, scale_max=True)[0]
+    res = gw.solve_batched([torch.as_tensor(C1, device=dev)], [torch.as_tensor(C2, device=dev)],
+                           gw.GW_CG, max_iter=10000, log_len=64)
+    info = res.infos()[0]
+    G, ref = orc.gw_cg_np(C1, C2)
+    assert info["status"] == "converged", info
+    assert info["n_iter"] == ref["n_iter"]
+    assert np.abs(res.plans[0].cpu().numpy() - G).max() < 1e-9
+    assert info["cost"] == pytest.approx(ref["gw_dist"], rel=1e-8, abs=1e-12)
+    A = rng.standard_normal((1040, 3))
+    B = rng.standard_normal((60, 3))
+    C1 = orc.pairwise_cost(A, A, scale_max=True)[0]
+    C2 = orc.pairwise_cost(B, B, scale_max=True)[0]
+    P, info = gw.entropic_gromov_wasserstein_ott(torch.as_tensor(C1, device=dev),
+                                                 torch.as_tensor(C2, device=dev), 1e-2,
+                                                 max_iterations=2000)
+    Pr, ref = orc.gw_entropic(C1, C2, 1e-2)
+    assert info["n_iter"] == ref["n_iters"]
+    assert info["converged"] == ref["converged"]
+    assert nrel(P.cpu().numpy(), Pr) < 1e-4
+    assert info["cost"] == pytest.approx(ref["reg_gw_cost"], rel=1e-6, abs=1e-9)

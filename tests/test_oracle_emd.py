@@ -54,7 +54,7 @@ def test_emd_abi_layout():
         m = re.search(rf"\b{name}\s*=\s*(-?\d+)", src)
         assert m and int(m.group(1)) == val, name
     lib = L.lib()
-    assert lib.otf_emd_max_nodes() >= 4096
+    assert lib.otf_emd_max_nodes() >= 4096 and lib.otf_emd_lds_nodes() == 4800
     probs = (L.EmdProblem * 1)()
     assert lib.otf_emd_solve(0, probs, 10, None, None) == L.OTF_EINVAL
     probs[0] = L.EmdProblem(None, None, None, 1, None, 1, 1, 1)
