@@ -286,6 +286,30 @@ int otf_sinkhorn_finish(const void* a, const void* b, const void* C, int64_t n, 
                         int64_t ldp, int32_t P_dtype, otf_sinkhorn_info* info, double* errlog,
                         void* workspace, size_t ws_bytes, otf_stream_t stream);
 
+/* Cross-rank persistent sweep (BASELINE config 5 on several GPUs of one node): one
+ * problem's rows sharded over world <= 8 ranks, each rank one persistent launch that
+ * streams its cost rows; the m column sums are exchanged INSIDE the launch as
+ * epoch-tagged granules written into every rank's exchange buffer over xGMI (no RCCL
+ * call, no host round trip per iteration).  Replaces the per-iteration all-reduce of
+ * otf_sinkhorn_row_sharded (MRI_PET_OT_OT_per_epoch_attn.py:940-960 generalised).
+ * Setup per rank: otf_xpeer_create (allocates this rank's exchange buffer, returns
+ * its IPC handle, otf_xpeer_handle_size() bytes), exchange the handles (any
+ * all-gather, rank order), otf_xpeer_connect.  Every rank then makes the SAME sequence
+ * of otf_sinkhorn_xsweep calls (the exchange's epochs advance in lock-step); the grids
+ * of all ranks must run concurrently.  float32 compute (fp32 or fp16 cost: opts.cost_f16),
+ * POT flavour; opts.n_total = rows over all ranks; u / plan: this rank's rows, v: all.
+ * A stall (a rank that never launches) ends in OTF_SK_TIMEOUT + info.stalled. */
+typedef struct otf_xpeer otf_xpeer;
+size_t otf_xpeer_handle_size(void);
+int otf_xpeer_create(int32_t rank, int32_t world, int64_t m, otf_xpeer** out, void* handle_out);
+int otf_xpeer_connect(otf_xpeer* x, const void* handles);
+int otf_xpeer_destroy(otf_xpeer* x);
+int otf_sinkhorn_xsweep(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                        int64_t ldc, int32_t dtype, const void* cost_scale,
+                        const otf_sinkhorn_opts* opts, otf_xpeer* x, void* u_out, void* v_out,
+                        void* P_out, int64_t ldp, int32_t P_dtype, otf_sinkhorn_info* info,
+                        double* errlog, void* workspace, size_t ws_bytes, otf_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * RCCL communicator.  The reference has no collectives; these
  * carry the path's two exchanges: the all-gather of per-epoch embedding shards

@@ -134,6 +134,14 @@ __device__ __forceinline__ I4 gload(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
 __device__ __forceinline__ void gstore(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x) {
     __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
 }
+// Across GPUs (peer-mapped exchange buffers): system-scope (sc0 sc1) stores reach the
+// owner's memory over xGMI; the owner polls with system-scope loads
+__device__ __forceinline__ I4 gload_sys(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(I4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 17 /* sc0 sc1 */));
+}
+__device__ __forceinline__ void gstore_sys(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x) {
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 17 /* sc0 sc1 */);
+}
 // Column-path store: plain (xl = 1) when producer and consumers share one XCC, so the
 // line stays in that XCC's L2 -- see the tile assignment in the kernel -- else
 // write-through (sc1) like every cross-XCC hop
@@ -251,11 +259,21 @@ __device__ __forceinline__ bool register_grid(const SkSync& sy, int* bar, int xc
 // the register files.  Host entry points; `region` is zeroed by the launcher.
 template <typename T> size_t sweep_region_bytes(int64_t m_pad);
 template <typename T, typename CT> bool sweep_supported(int64_t n, int64_t m, int64_t ldc);
+// Cross-rank form (otf_sinkhorn_xsweep): this rank's place, the world's exchange buffers
+// as mapped here, and the solve's epoch base (identical on every rank).
+struct XSweep {
+    int rank, world, n_total;
+    unsigned ep_base;
+    unsigned char* xr[8];
+};
+constexpr int kXMaxRanks = 8;
+inline size_t xsweep_exchange_bytes(int64_t m_pad) { return (size_t)2 * kXMaxRanks * m_pad * 8; }
 template <typename T, typename CT>
 hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T* a_pad,
                      const T* b_pad, const T* cost_scale, const otf_sinkhorn_opts& o, void* region,
                      T* u_out, T* v_out, void* P_out, int64_t ldp, int P_dtype,
-                     otf_sinkhorn_info* info, double* errlog, hipStream_t s);
+                     otf_sinkhorn_info* info, double* errlog, hipStream_t s,
+                     const XSweep* xs = nullptr);
 
 // Gather engine (otf_gather.hip): small problems (<= 16 row tiles, m <= 512), column
 // partials exchanged as epoch-tagged granules, no barrier.  `region` is zeroed by the

@@ -28,6 +28,8 @@
 // (read p-1, accumulate p, zero p+1) so a pass never races the zeroing.
 #include <stdlib.h>
 
+#include <string.h>
+
 #include "otf_persist.h"
 #include "otf_comm.h"
 
@@ -2153,10 +2155,127 @@ int dispatch(const void* a, const void* b, const void* C, int64_t n, int64_t m, 
     return OTF_EUNSUPPORTED;
 }
 
+// Cross-rank sweep (otf_sinkhorn_xsweep): this rank's rows, the exchange of its peers.
+template <typename T, typename CT>
+int run_xsweep(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_t ldc,
+               const T* cost_scale, const otf_sinkhorn_opts& o, const XSweep& xs, T* u_out, T* v_out,
+               void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info, double* errlog_user,
+               void* ws, size_t ws_bytes, hipStream_t s) {
+    constexpr int VEC = Vec<T>::N;
+    if (!u_out || !v_out) return OTF_EINVAL;
+    if (P_out && (ldp < m || ldp % VEC != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
+    if (o.max_iter < 1 || xs.n_total < n) return OTF_EINVAL;
+    if (!sweep_supported<T, CT>(n, m, ldc)) return OTF_EUNSUPPORTED;
+    SkSetup<T> su;
+    int rc = sk_prepare<T, CT>(a, b, C, n, m, ldc, o, info, ws, ws_bytes, su);
+    if (rc != OTF_OK) return rc;
+    double* errlog = errlog_user ? errlog_user : su.w.errlog;
+    rc = sk_init<T>(su, a, b, n, m, info, s);
+    if (rc != OTF_OK) return rc;
+    return check_hip(run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
+                                      (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out, v_out,
+                                      P_out, ldp, P_dtype, info, errlog, s, &xs));
+}
+
 }  // namespace
 }  // namespace otf
 
+// One rank's side of a cross-rank exchange (include/otfuse.h, otf_xpeer_*).
+struct otf_xpeer {
+    int rank, world;
+    int64_t m, m_pad;
+    void* own;
+    void* peer[otf::kXMaxRanks];
+    unsigned ep_base;
+    int connected;
+};
+
 extern "C" {
+
+size_t otf_xpeer_handle_size(void) { return sizeof(hipIpcMemHandle_t); }
+
+int otf_xpeer_create(int32_t rank, int32_t world, int64_t m, otf_xpeer** out, void* handle_out) {
+    if (!out || !handle_out || world < 1 || world > otf::kXMaxRanks || rank < 0 || rank >= world || m < 1)
+        return OTF_EINVAL;
+    otf_xpeer* x = new otf_xpeer{};
+    x->rank = rank;
+    x->world = world;
+    x->m = m;
+    x->m_pad = (int64_t)otf::align_up((size_t)m, 64);
+    const size_t bytes = otf::xsweep_exchange_bytes(x->m_pad);
+    hipError_t e = hipMalloc(&x->own, bytes);
+    if (e == hipSuccess) e = hipMemset(x->own, 0, bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipIpcGetMemHandle((hipIpcMemHandle_t*)handle_out, x->own);
+    if (e != hipSuccess) {
+        if (x->own) (void)hipFree(x->own);
+        delete x;
+        return otf::check_hip(e);
+    }
+    x->peer[rank] = x->own;
+    *out = x;
+    return OTF_OK;
+}
+
+int otf_xpeer_connect(otf_xpeer* x, const void* handles) {
+    if (!x || !handles || x->connected) return OTF_EINVAL;
+    const unsigned char* h = (const unsigned char*)handles;
+    for (int r = 0; r < x->world; ++r) {
+        if (r == x->rank) continue;
+        hipIpcMemHandle_t hr;
+        memcpy(&hr, h + (size_t)r * sizeof(hipIpcMemHandle_t), sizeof(hr));
+        const hipError_t e = hipIpcOpenMemHandle(&x->peer[r], hr, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            for (int q = 0; q < r; ++q)
+                if (q != x->rank && x->peer[q]) (void)hipIpcCloseMemHandle(x->peer[q]);
+            return otf::check_hip(e);
+        }
+    }
+    x->connected = 1;
+    return OTF_OK;
+}
+
+int otf_xpeer_destroy(otf_xpeer* x) {
+    if (!x) return OTF_EINVAL;
+    if (x->connected)
+        for (int r = 0; r < x->world; ++r)
+            if (r != x->rank && x->peer[r]) (void)hipIpcCloseMemHandle(x->peer[r]);
+    if (x->own) (void)hipFree(x->own);
+    delete x;
+    return OTF_OK;
+}
+
+int otf_sinkhorn_xsweep(const void* a, const void* b, const void* C, int64_t n, int64_t m,
+                        int64_t ldc, int32_t dtype, const void* cost_scale,
+                        const otf_sinkhorn_opts* opts, otf_xpeer* x, void* u_out, void* v_out,
+                        void* P_out, int64_t ldp, int32_t P_dtype, otf_sinkhorn_info* info,
+                        double* errlog, void* workspace, size_t ws_bytes, otf_stream_t stream) {
+    if (!opts || !x || !x->connected || dtype != OTF_F32) return OTF_EINVAL;
+    if (opts->flavor != OTF_FLAVOR_POT) return OTF_EUNSUPPORTED;
+    if (m != x->m) return OTF_EINVAL;
+    if (P_out && P_dtype != OTF_F32 && P_dtype != OTF_F64) return OTF_EINVAL;
+    // epochs live in 30 bits of a tag and 0 is the cleared state: a window that would
+    // wrap restarts at 1 (every peer slot has been rewritten many times since)
+    if ((uint64_t)x->ep_base + (uint64_t)opts->max_iter + 8 >= (1ull << 30)) x->ep_base = 0;
+    otf::XSweep xs{};
+    xs.rank = x->rank;
+    xs.world = x->world;
+    xs.n_total = opts->n_total > 0 ? opts->n_total : (int)n;
+    xs.ep_base = x->ep_base;
+    for (int r = 0; r < x->world; ++r) xs.xr[r] = (unsigned char*)x->peer[r];
+    // every rank makes the same sequence of calls: the bases stay in lock-step
+    x->ep_base = x->ep_base + (unsigned)opts->max_iter + 4u;
+    hipStream_t s = (hipStream_t)stream;
+    if (opts->cost_f16)
+        return otf::run_xsweep<float, _Float16>((const float*)a, (const float*)b, (const _Float16*)C, n,
+                                                m, ldc, (const float*)cost_scale, *opts, xs,
+                                                (float*)u_out, (float*)v_out, P_out, ldp, P_dtype,
+                                                info, errlog, workspace, ws_bytes, s);
+    return otf::run_xsweep<float, float>((const float*)a, (const float*)b, (const float*)C, n, m, ldc,
+                                         (const float*)cost_scale, *opts, xs, (float*)u_out,
+                                         (float*)v_out, P_out, ldp, P_dtype, info, errlog, workspace,
+                                         ws_bytes, s);
+}
 
 int otf_sinkhorn_fallback_count(uint64_t* count) {
     if (!count) return OTF_EINVAL;

@@ -38,6 +38,15 @@
 //      stores S into its XCC's ring slot (plain): every XCC derives the same S, bit for
 //      bit, from the same partials in the same order;
 //   d. the next sweep's v-update polls the XCC-local S granules.
+// Across GPUs (otf_sinkhorn_xsweep: one problem's rows sharded over <= 8 ranks of one
+// node, BASELINE config 5's multi-GPU form): step c sums the XCC partials into this
+// rank's partial of the slice, which the first active XCC's owner stores into EVERY
+// rank's exchange buffer (system-scope write-through over xGMI, parity double-buffered
+// like the XCC partials); step c' then sums the slice over the world's rank partials in
+// rank order -- every rank derives the same S, bit for bit -- into the XCC-local ring.
+// POT's decisions follow from S alone, so every rank takes them at the same iteration.
+// Epochs of an exchange continue across solves (ep_base, advanced by the host in
+// lock-step on every rank), so no rank ever needs to clear a peer's buffer.
 // A non-finite u travels as a tag flag (slab -> XCC partial -> S) instead of the bad
 // counters.  Three hops, one of them across XCCs, instead of flush + group counter +
 // atomics + grid barrier (~11 us of a 29-us config-5 sweep in r02).
@@ -88,6 +97,12 @@ template <typename T> struct SkSweepArgs {
     unsigned char* gxp;    // [2 parity][8 XCC][m_pad] granules: XCC partials (sc1)
     unsigned char* gfs;    // [8 XCC][4 ring][m_pad] granules: S, read within the XCC
     int* xl;               // [8][256] registration lists: blockIdx per XCC slot
+    // cross-rank exchange (world > 1): xr[r] = rank r's exchange buffer as mapped here,
+    // [2 parity][8 ranks][m_pad] granules
+    int rank, world;
+    int n_total;           // rows over all ranks (POT's u0 = 1 / n)
+    unsigned ep_base;      // epoch offset of this solve (the same on every rank)
+    unsigned char* xr[8];
 };
 constexpr int kSwSlices = 32;  // column slices of the granule reduction
 
@@ -290,7 +305,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     const int mc = p.m_pad / 2;                       // 16-B granule pairs per row
     auto load_sums_gran = [&](int k, int g, T (&out)[VC], int& fl, bool& ok) {
         const __amdgpu_buffer_rsrc_t rfs = sums_rsrc(p.gfs);
-        const unsigned e = (unsigned)(k + 1);
+        const unsigned e = (p.ep_base + (unsigned)(k + 1)) & 0x3fffffffu;
         const uint32_t base = (uint32_t)((xcc_id() * 4 + (int)(e & 3)) * mc) * 16u + (uint32_t)(colc[g] / 2) * 16u;
         I4 x[VC / 2];
 #pragma unroll
@@ -366,7 +381,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         return p.err_squared ? (double)e : sqrt((double)e);
     };
 
-    const T u0 = (T)1 / (T)p.n;
+    const T u0 = (T)1 / (T)(p.n_total > 0 ? p.n_total : p.n);
     const int xcd = xcc_id();
 #ifdef OTF_STAMPS
     if (tid == 0 && blockIdx.x < 256) g_stamps[(blockIdx.x * 16 + 15) * 8 + 7] = (unsigned long long)xcd;
@@ -639,12 +654,13 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     constexpr int NBT = G >= 8 ? 4 : 8;
     auto flush_gran = [&](int k) -> bool {
         const __amdgpu_buffer_rsrc_t rsl = sums_rsrc(p.gslab);
+        const __amdgpu_buffer_rsrc_t rxx = sums_rsrc(p.xr[p.world > 1 ? p.rank : 0]);
         const __amdgpu_buffer_rsrc_t rxp = sums_rsrc(p.gxp);
         const __amdgpu_buffer_rsrc_t rfs = sums_rsrc(p.gfs);
         const int sw = (mc + kSwSlices - 1) / kSwSlices;         // granule pairs per slice (<= 256)
         const int swp = sw <= 64 ? 64 : sw <= 128 ? 128 : 256;   // lanes per row group
         const int Q = kSwNT / swp, sq = tid / swp, sj = tid % swp;
-        const unsigned e = (unsigned)(k + 1);
+        const unsigned e = (p.ep_base + (unsigned)(k + 1)) & 0x3fffffffu;
         bool ok = true;
         // a. this workgroup's partials -> its slab row
         const uint32_t rowo = (uint32_t)blockIdx.x * (uint32_t)mc * 16u;
@@ -659,6 +675,12 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             }
         }
         badu = 0;
+#ifdef OTF_STAMPS
+        if (k >= 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            OTF_STAMP(k - 1, 6);
+        }
+#endif
         // b. owned slices: sum over the XCC's members (rank order), publish the XCC partial
         for (int sl = gslot_r; sl < kSwSlices; sl += nx) {
             const int cch = sl * sw + sj;
@@ -715,6 +737,12 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             }
             __syncthreads();
         }
+#ifdef OTF_STAMPS
+        if (k >= 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            OTF_STAMP(k - 1, 7);
+        }
+#endif
         // c. owned slices: S = the active XCCs' partials in XCC order -> this XCC's ring slot
         if (sq == 0) {
             for (int sl = gslot_r; sl < kSwSlices; sl += nx) {
@@ -750,7 +778,52 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                         s1 += chunk_v1(x[xx]);
                         f |= (x[xx][1] | x[xx][3]) & 3;
                     }
-                gstore_col(rfs, (uint32_t)((xcd * 4 + (int)(e & 3)) * mc + cch) * 16u, chunk2(s0, s1, (int)(e << 2) | f), 1);
+                if (p.world <= 1) {
+                    gstore_col(rfs, (uint32_t)((xcd * 4 + (int)(e & 3)) * mc + cch) * 16u, chunk2(s0, s1, (int)(e << 2) | f), 1);
+                } else if (xcd == __builtin_ctz(act_mask)) {
+                    // this rank's partial of the slice -> every rank's exchange buffer
+                    const uint32_t xo = (uint32_t)(((e & 1) * 8 + p.rank) * mc + cch) * 16u;
+                    for (int r = 0; r < p.world; ++r)
+                        gstore_sys(sums_rsrc(p.xr[r]), xo, chunk2(s0, s1, (int)(e << 2) | f));
+                }
+            }
+            // c'. the world's rank partials of the slice, in rank order -> S
+            if (p.world > 1) {
+                for (int sl = gslot_r; sl < kSwSlices; sl += nx) {
+                    const int cch = sl * sw + sj;
+                    if (!(sj < sw && cch < mc)) continue;
+                    I4 x[8];
+                    unsigned pend = 0;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r)
+                        if (r < p.world) {
+                            x[r] = gload_sys(rxx, (uint32_t)(((e & 1) * 8 + r) * mc + cch) * 16u);
+                            pend |= 1u << r;
+                        }
+#pragma unroll
+                    for (int r = 0; r < 8; ++r)
+                        if ((pend & (1u << r)) && chunk_at(x[r], e)) pend &= ~(1u << r);
+                    while (pend && ok) {
+                        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                        for (int r = 0; r < 8; ++r)
+                            if (pend & (1u << r)) x[r] = gload_sys(rxx, (uint32_t)(((e & 1) * 8 + r) * mc + cch) * 16u);
+#pragma unroll
+                        for (int r = 0; r < 8; ++r)
+                            if ((pend & (1u << r)) && chunk_at(x[r], e)) pend &= ~(1u << r);
+                        if (pend && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
+                    }
+                    float s0 = 0.f, s1 = 0.f;
+                    int f = 0;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r)
+                        if (r < p.world) {
+                            s0 += chunk_v0(x[r]);
+                            s1 += chunk_v1(x[r]);
+                            f |= (x[r][1] | x[r][3]) & 3;
+                        }
+                    gstore_col(rfs, (uint32_t)((xcd * 4 + (int)(e & 3)) * mc + cch) * 16u, chunk2(s0, s1, (int)(e << 2) | f), 1);
+                }
             }
         }
         ok = !block_or(ok ? 0 : 4, 2 + (int)(e & 1));
@@ -1086,7 +1159,7 @@ template <typename T, typename CT>
 hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T* a_pad,
                      const T* b_pad, const T* cost_scale, const otf_sinkhorn_opts& o, void* region,
                      T* u_out, T* v_out, void* P_out, int64_t ldp, int P_dtype,
-                     otf_sinkhorn_info* info, double* errlog, hipStream_t s) {
+                     otf_sinkhorn_info* info, double* errlog, hipStream_t s, const XSweep* xs) {
     const int G = sweep_g<CT>(m);
     if (G == 0) return hipErrorInvalidValue;
     SkSweepArgs<T> p{};
@@ -1124,6 +1197,17 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     // OTF_SWEEP_GRAN=0: the r02 flush (slab + group counter + atomics + grid barrier)
     const char* ge = getenv("OTF_SWEEP_GRAN");
     p.gran = (sizeof(T) == 4 && !p.det && !(ge && atoi(ge) == 0)) ? 1 : 0;
+    p.world = 1;
+    p.n_total = n;
+    if (xs && xs->world > 1) {  // the cross-rank form runs on the granule flush only
+        if (sizeof(T) != 4 || xs->world > kXMaxRanks) return hipErrorInvalidValue;
+        p.gran = 1;
+        p.rank = xs->rank;
+        p.world = xs->world;
+        p.n_total = xs->n_total;
+        p.ep_base = xs->ep_base;
+        for (int r = 0; r < xs->world; ++r) p.xr[r] = xs->xr[r];
+    }
     size_t zero_bytes = sweep_ctrl_bytes(m_pad, sizeof(T));
     if (p.gran) {
         unsigned char* gb = (unsigned char*)p.slab + (size_t)kSwMaxGrid * m_pad * sizeof(T);
@@ -1144,7 +1228,10 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
         default: R = sweep_rows<T, CT>(8); break;
     }
     const int nrb = (n + R - 1) / R;
-    const int grid = sweep_grid(nrb);
+    int grid = sweep_grid(nrb);
+    // OTF_SWEEP_GRID caps the grid (tests: two ranks' persistent grids on one device)
+    if (const char* gg = getenv("OTF_SWEEP_GRID"))
+        if (atoi(gg) > 0 && atoi(gg) < grid) grid = atoi(gg);
     if (P_out && P_dtype == OTF_F64) return launch_sweep<T, CT, double>(G, grid, p, s);
     return launch_sweep<T, CT, float>(G, grid, p, s);
 }
@@ -1157,14 +1244,14 @@ template bool sweep_supported<double, double>(int64_t, int64_t, int64_t);
 template hipError_t run_sweep<float, float>(const float*, int64_t, int, int, int, const float*,
                                             const float*, const float*, const otf_sinkhorn_opts&,
                                             void*, float*, float*, void*, int64_t, int,
-                                            otf_sinkhorn_info*, double*, hipStream_t);
+                                            otf_sinkhorn_info*, double*, hipStream_t, const XSweep*);
 template hipError_t run_sweep<float, _Float16>(const _Float16*, int64_t, int, int, int, const float*,
                                                const float*, const float*, const otf_sinkhorn_opts&,
                                                void*, float*, float*, void*, int64_t, int,
-                                               otf_sinkhorn_info*, double*, hipStream_t);
+                                               otf_sinkhorn_info*, double*, hipStream_t, const XSweep*);
 template hipError_t run_sweep<double, double>(const double*, int64_t, int, int, int, const double*,
                                               const double*, const double*, const otf_sinkhorn_opts&,
                                               void*, double*, double*, void*, int64_t, int,
-                                              otf_sinkhorn_info*, double*, hipStream_t);
+                                              otf_sinkhorn_info*, double*, hipStream_t, const XSweep*);
 
 }  // namespace otf

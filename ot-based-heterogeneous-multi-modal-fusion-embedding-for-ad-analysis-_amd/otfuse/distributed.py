@@ -202,14 +202,111 @@ def sinkhorn_row_sharded(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.
     return be.finish(want_plan, plan_dtype)
 
 
+class XPeer:
+    """One rank's side of the in-kernel cross-rank exchange (``otf_xpeer_*``): an
+    exchange buffer on this GPU that every rank's persistent sweep writes its column-sum
+    partials into over xGMI, and the peers' buffers mapped here (IPC handles exchanged
+    once through ``torch.distributed``, any backend).  Every rank must make the same
+    sequence of ``sinkhorn_xsweep`` calls on it."""
+
+    def __init__(self, m: int, group=None):
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.m = int(m)
+        lib = L.lib()
+        hs = int(lib.otf_xpeer_handle_size())
+        h = (ctypes.c_ubyte * hs)()
+        ptr = ctypes.c_void_p()
+        L.check(lib.otf_xpeer_create(self.rank, self.world, self.m, ctypes.byref(ptr), h),
+                "otf_xpeer_create")
+        self._h = ptr
+        mine = bytes(h)
+        if self.world > 1:
+            allh = [None] * self.world
+            dist.all_gather_object(allh, mine, group=group)
+        else:
+            allh = [mine]
+        buf = b"".join(allh)
+        rc = lib.otf_xpeer_connect(self._h, buf)
+        if rc != 0:
+            lib.otf_xpeer_destroy(self._h)
+            self._h = None
+            L.check(rc, "otf_xpeer_connect")
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RuntimeError("XPeer is closed")
+        return self._h
+
+    def close(self):
+        if self._h is not None:
+            L.lib().otf_xpeer_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # noqa: D105
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+def sinkhorn_xsweep(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.Tensor, reg: float,
+                    xpeer: XPeer, n_total: int, max_iter: int = 1000, stop_thr: float = 1e-9,
+                    cost_scale: torch.Tensor | None = None, check_every: int = 10,
+                    err_squared: bool = False, want_plan: bool = True, plan_dtype=None,
+                    workspace: torch.Tensor | None = None) -> ops.SinkhornResult:
+    """POT ``sinkhorn_knopp`` on a problem whose cost rows are split over the ranks, as
+    ONE persistent launch per rank (``otf_sinkhorn_xsweep``): the column sums are
+    exchanged inside the launch through ``xpeer`` -- no all-reduce call per iteration.
+    Same contract as ``sinkhorn_row_sharded`` (this rank's rows of u and the plan, the
+    full v); float32 compute, fp32 or fp16 cost rows."""
+    ops._dev(C_local, "C_local")
+    if C_local.dtype not in (torch.float32, torch.float16):
+        raise TypeError("sinkhorn_xsweep: float32 or float16 cost rows")
+    n, m = C_local.shape
+    if m != xpeer.m:
+        raise ValueError(f"C_local has {m} columns, the exchange was built for {xpeer.m}")
+    dev = C_local.device
+    C = ops._rowmajor(C_local, ops._VEC[C_local.dtype])
+    a = a_local.to(dev, torch.float32).contiguous()
+    bb = b.to(dev, torch.float32).contiguous()
+    if a.numel() != n or bb.numel() != m:
+        raise ValueError("a_local / b do not match C_local")
+    cs = None if cost_scale is None else cost_scale.to(dev, torch.float32).contiguous()
+    opts = L.SinkhornOpts(reg=float(reg), stop_thr=float(stop_thr), max_iter=int(max_iter),
+                          check_every=int(check_every), flavor=L.OTF_FLAVOR_POT,
+                          err_squared=int(err_squared), sync_every=0, engine=L.ENGINE_SWEEP,
+                          cost_f16=int(C.dtype == torch.float16), n_total=int(n_total))
+    if workspace is None:
+        workspace = ops.sinkhorn_workspace(n, m, torch.float32, max_iter, dev)
+    u = torch.empty(n, dtype=torch.float32, device=dev)
+    v = torch.empty(m, dtype=torch.float32, device=dev)
+    P = ops._alloc_rowmajor(n, m, plan_dtype or torch.float32, dev, 4) if want_plan else None
+    info = torch.empty(L.INFO_INT32S, dtype=torch.int32, device=dev)
+    errlog = torch.empty(max_iter // max(check_every, 1) + 2, dtype=torch.float64, device=dev)
+    L.check(L.lib().otf_sinkhorn_xsweep(
+        a.data_ptr(), bb.data_ptr(), C.data_ptr(), n, m, C.stride(0), ops._DT[torch.float32],
+        L.ptr(cs), ctypes.byref(opts), xpeer.handle, u.data_ptr(), v.data_ptr(), L.ptr(P),
+        P.stride(0) if P is not None else 0, ops._DT[P.dtype] if P is not None else 0,
+        info.data_ptr(), errlog.data_ptr(), workspace.data_ptr(), workspace.numel(),
+        L.stream_handle(dev)), "otf_sinkhorn_xsweep")
+    res = ops.SinkhornResult(u=u, v=v, plan=P, info_dev=info, errlog_dev=errlog)
+    res._keep = (C, a, bb, cs, workspace)
+    return res
+
+
 def coupled_solve_sharded(X_local: torch.Tensor, Y_local: torch.Tensor, reg: float,
                           max_iter: int = 200, stop_thr: float = 0.0, cost_dtype=torch.float16,
-                          want_plan: bool = True, sync_every: int = 0, group=None, comm=None):
+                          want_plan: bool = True, sync_every: int = 0, group=None, comm=None,
+                          xpeer: XPeer | None = None):
     """The per-epoch global OT of one large problem over the data-parallel ranks:
     all-gather the PET embedding shards (RCCL), cost rows of this rank's MRI shard
     against every PET embedding (fp16 storage by default, BASELINE config 5), one
     all-reduce(MAX) for scale_cost="max_cost", then the row-sharded Sinkhorn with
-    uniform marginals.  Returns (SinkhornResult of this rank's rows, n_total)."""
+    uniform marginals.  With an ``xpeer`` exchange the solve is the in-kernel cross-rank
+    sweep (``sinkhorn_xsweep``), otherwise the row-sharded solve with one all-reduce per
+    iteration.  Returns (SinkhornResult of this rank's rows, n_total)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     x_sizes = None
     if comm is not None and comm.nranks > 1:
@@ -239,6 +336,9 @@ def coupled_solve_sharded(X_local: torch.Tensor, Y_local: torch.Tensor, reg: flo
     m = Y_all.shape[0]
     a = torch.full((X_local.shape[0],), 1.0 / n_total, dtype=torch.float32, device=X_local.device)
     b = torch.full((m,), 1.0 / m, dtype=torch.float32, device=X_local.device)
+    if xpeer is not None:
+        return sinkhorn_xsweep(a, b, C, reg, xpeer, n_total, max_iter=max_iter, stop_thr=stop_thr,
+                               cost_scale=gmax / unit, want_plan=want_plan), n_total
     res = sinkhorn_row_sharded(a, b, C, reg, max_iter=max_iter, stop_thr=stop_thr,
                                cost_scale=gmax / unit, n_total=n_total, sync_every=sync_every,
                                want_plan=want_plan, group=group, comm=comm)

@@ -120,6 +120,45 @@ int main(int argc, char** argv) {
                             "atomics performed", "grid barrier", "loop back"};
     for (int ph = 0; ph < 6; ++ph) printf("%-28s %8.2f us\n", names[ph], span[ph] / cnt / 100.0);
     printf("sweep-end spread             %8.2f us\n", sweep_spread / 13 / 100.0);
+    // granule flush (OTF_SWEEP_GRAN != 0): slot 6 = slab row published, 7 = XCC partials
+    // published, 3 = S slices published; next iteration's slot 1 = S polled + v + checks.
+    // Latency of each hop after the LAST producer it waits for.
+    {
+        const char* ge = getenv("OTF_SWEEP_GRAN");
+        if (!(ge && atoi(ge) == 0)) {
+            double pub = 0, hb = 0, hc = 0, hs = 0, crit = 0;
+            int c2 = 0;
+            for (int it = 2; it < 14; ++it) {
+                unsigned long long last6[8] = {0}, last3[8] = {0}, last7 = 0, slow2 = 0, first1 = ~0ull;
+                for (int w = 0; w < nwg; ++w) {
+                    const unsigned long long* x = &st[(w * 16 + it) * 8];
+                    const int xc = (int)(st[(w * 16 + 15) * 8 + 7] & 7);
+                    last6[xc] = x[6] > last6[xc] ? x[6] : last6[xc];
+                    last3[xc] = x[3] > last3[xc] ? x[3] : last3[xc];
+                    last7 = x[7] > last7 ? x[7] : last7;
+                    slow2 = x[2] > slow2 ? x[2] : slow2;
+                    const unsigned long long nx1 = st[(w * 16 + it + 1) * 8 + 1];
+                    first1 = nx1 < first1 ? nx1 : first1;
+                }
+                for (int w = 0; w < nwg; ++w) {
+                    const unsigned long long* x = &st[(w * 16 + it) * 8];
+                    const int xc = (int)(st[(w * 16 + 15) * 8 + 7] & 7);
+                    pub += (double)(x[6] - x[2]);
+                    hb += (double)x[7] - (double)last6[xc];
+                    hc += (double)x[3] - (double)last7;
+                    hs += (double)st[(w * 16 + it + 1) * 8 + 1] - (double)last3[xc];
+                    ++c2;
+                }
+                crit += (double)(first1 - slow2);
+            }
+            printf("granule flush (per workgroup-iteration, us):\n");
+            printf("  slab publish (own partials)           %6.2f\n", pub / c2 / 100.0);
+            printf("  XCC slice sums, after last member     %6.2f\n", hb / c2 / 100.0);
+            printf("  S slices, after last XCC partial      %6.2f\n", hc / c2 / 100.0);
+            printf("  S polled + v, after last XCC owner    %6.2f\n", hs / c2 / 100.0);
+            printf("  slowest sweep end -> first v ready    %6.2f\n", crit / 12 / 100.0);
+        }
+    }
     printf("barrier arrival spread       %8.2f us\n", arrive_spread / 13 / 100.0);
     return 0;
 }
