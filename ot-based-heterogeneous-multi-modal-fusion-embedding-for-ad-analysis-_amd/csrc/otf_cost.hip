@@ -468,6 +468,9 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
                     if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
                     if (zero_diag && gi == gj) c = 0.f;
                     const TC cs = (TC)(c * os);
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
+                    if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
+#endif
                     C[(int64_t)gi * ldc + gj] = cs;
                     lmax = fmaxf(lmax, (float)cs);
                 }
@@ -618,6 +621,9 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
                     if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
                     if (zero_diag && gi == gj) c = 0.f;
                     const TC cs = (TC)(c * os);
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
+                    if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
+#endif
                     C[(int64_t)gi * ldc + gj] = cs;
                     lmax = fmaxf(lmax, (float)cs);
                 }
@@ -792,6 +798,9 @@ __global__ __launch_bounds__(512) void cost_ring_kernel(
                     if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
                     if (zero_diag && gi2 == gj2) c = 0.f;
                     const TC cs = (TC)(c * os);
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
+                    if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
+#endif
                     C[(int64_t)gi2 * ldc + gj2] = cs;
                     lmax = fmaxf(lmax, (float)cs);
                 }
