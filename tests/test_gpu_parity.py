@@ -58,16 +58,20 @@ def test_split16_wide_dynamic_range(ops, orc, dev):
 @pytest.mark.parametrize("n,m,d,in_dt,out_dt", [
     (4096, 4096, 512, torch.float32, torch.float32), (4100, 3999, 300, torch.float32, torch.float32),
     (8192, 8192, 256, torch.float16, torch.float16), (4096, 4096, 40, torch.float32, torch.float16)])
-def test_cost_ring_kernel_matches_register_kernel(ops, orc, dev, monkeypatch, n, m, d, in_dt, out_dt):
-    """The LDS-DMA ring kernel (OTF_COST_RING=1) runs the same products in the same
-    order as the register-staged 256 x 256 kernel: bit-identical cost, and the oracle
-    tolerance of the split-fp16 path on a sampled block."""
+@pytest.mark.parametrize("switch", ["OTF_COST_RING", "OTF_COST_WS"])
+def test_cost_ring_kernel_matches_register_kernel(ops, orc, dev, monkeypatch, n, m, d, in_dt, out_dt,
+                                                  switch):
+    """The LDS-DMA kernels -- the ring kernel (OTF_COST_RING=1) and the warp-specialised
+    persistent kernel (OTF_COST_WS=1) -- run the same products in the same order as the
+    register-staged 256 x 256 kernel: bit-identical cost, and the oracle tolerance of the
+    split-fp16 path on a sampled block."""
     g = torch.Generator(device=dev).manual_seed(n + d)
     X = torch.randn(n, d, device=dev, generator=g).to(in_dt)
     Y = (torch.randn(m, d, device=dev, generator=g) * 0.7 + 0.2).to(in_dt)
     monkeypatch.setenv("OTF_COST_RING", "0")
+    monkeypatch.setenv("OTF_COST_WS", "0")
     C0, mx0, u0 = ops.pairwise_cost_ex(X, Y, out_dtype=out_dt)
-    monkeypatch.setenv("OTF_COST_RING", "1")
+    monkeypatch.setenv(switch, "1")
     C1, mx1, u1 = ops.pairwise_cost_ex(X, Y, out_dtype=out_dt)
     torch.cuda.synchronize()
     assert torch.equal(C0, C1) and torch.equal(mx0, mx1) and torch.equal(u0, u1)
