@@ -10,4 +10,5 @@ import sys, json, torch
 sys.path.insert(0, '.'); sys.path.insert(0, 'ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd')
 import bench
 print(json.dumps(bench.sharded_config5_leg(torch.device('cuda', 0), 1)))
+print(json.dumps(bench.config3_leg(torch.device('cuda', 0), 1)))
 " > $O/sharded1.json 2>&1; rc=$?; tail -3 $O/sharded1.json; exit $rc

@@ -10,7 +10,7 @@ for cfg in "big:" "ring:OTF_COST_RING=1" "ws:OTF_COST_WS=1"; do
   name=${cfg%%:*}; envs=${cfg#*:}
   for v in "" _a1; do
     for shp in "4096 512 f32" "8192 1024 f16in"; do
-      tag=$name$v_$(echo $shp | tr ' ' '_')
+      tag=${name}${v}_$(echo $shp | tr ' ' '_')
       echo "=== $name$v $shp"
       env $envs timeout -k 10 60 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$tag -o run -- ./tools/ubench_cost$v $shp 20 > $O/$tag.log 2>&1 || exit $?
       grep "per call" $O/$tag.log
