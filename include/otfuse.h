@@ -178,6 +178,10 @@ int otf_cost_pairwise_split16(const float* X, int64_t ldx, const float* Y, int64
  * ldx, ldy elements; C rows 16-B aligned when it feeds otf_sinkhorn.
  * Workspace: otf_cost_ex_workspace_size() bytes.                                 */
 size_t otf_cost_ex_workspace_size(int64_t n, int64_t m, int64_t d, int32_t in_dtype);
+/* Profiling: with OTF_COST_PHASES=1 in the environment every otf_cost_pairwise_ex call
+ * records events around its prep (split / norms) and its cost kernel; this returns the
+ * last call's two durations (synchronises on that call). */
+int otf_cost_last_phases(float* prep_ms, float* kernel_ms);
 int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
                          int32_t in_dtype, int64_t n, int64_t m, int64_t d, int32_t metric,
                          int32_t zero_diag, void* C, int64_t ldc, int32_t c_dtype, float* cmax,

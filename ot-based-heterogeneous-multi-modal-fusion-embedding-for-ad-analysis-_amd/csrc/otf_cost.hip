@@ -753,7 +753,11 @@ __global__ __launch_bounds__(512) void cost_ring_kernel(
         // whose slot the next issue refills
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 4)
+        // diagnostic: no DMA after the prologue (the loop re-reads stale slots)
+#else
         if (kt + RSLOTS - 1 < nk) issue(kt + RSLOTS - 1);
+#endif
         const char* sl = smem + (kt % RSLOTS) * STAGE;
         f16x8 ah[2], al[2], bh[4], bl[4];
 #pragma unroll
@@ -772,11 +776,16 @@ __global__ __launch_bounds__(512) void cost_ring_kernel(
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int nj = 0; nj < 4; ++nj) {
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 2)
+                // diagnostic: no MFMAs (the fragments still feed one add each)
+                acc[mi][nj][0] += (float)ah[mi][0] + (float)bh[nj][0] + (NI == 2 ? (float)al[mi][0] + (float)bl[nj][0] : 0.f);
+#else
                 if (NS == 3) {
                     acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mi], bh[nj], acc[mi][nj], 0, 0, 0);
                     acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bl[nj], acc[mi][nj], 0, 0, 0);
                 }
                 acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bh[nj], acc[mi][nj], 0, 0, 0);
+#endif
             }
     }
 
@@ -1164,6 +1173,29 @@ size_t otf_cost_split16_workspace_size(int64_t n, int64_t m, int64_t d) {
     return otf_cost_ex_workspace_size(n, m, d, OTF_F32);
 }
 
+// OTF_COST_PHASES=1 (read per call): events around the prep and the cost kernel of
+// every otf_cost_pairwise_ex call; otf_cost_last_phases reports the last call's split
+static hipEvent_t g_cost_ev[3];
+static int g_cost_ev_state = 0;  // 0 none, 1 created, 2 recorded
+static bool cost_phases_on() {
+    const char* e = getenv("OTF_COST_PHASES");
+    if (!(e && atoi(e) != 0)) return false;
+    if (g_cost_ev_state == 0) {
+        for (auto& ev : g_cost_ev)
+            if (hipEventCreate(&ev) != hipSuccess) return false;
+        g_cost_ev_state = 1;
+    }
+    return true;
+}
+
+int otf_cost_last_phases(float* prep_ms, float* kernel_ms) {
+    if (!prep_ms || !kernel_ms || g_cost_ev_state != 2) return OTF_EINVAL;
+    OTF_HIP(hipEventSynchronize(g_cost_ev[2]));
+    OTF_HIP(hipEventElapsedTime(prep_ms, g_cost_ev[0], g_cost_ev[1]));
+    OTF_HIP(hipEventElapsedTime(kernel_ms, g_cost_ev[1], g_cost_ev[2]));
+    return OTF_OK;
+}
+
 int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
                          int32_t in_dtype, int64_t n, int64_t m, int64_t d, int32_t metric,
                          int32_t zero_diag, void* C, int64_t ldc, int32_t c_dtype, float* cmax,
@@ -1176,6 +1208,8 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     if (ws_bytes < otf_cost_ex_workspace_size(n, m, d, in_dtype)) return OTF_EINVAL;
     if (n > INT32_MAX || m > INT32_MAX || d > (1 << 20)) return OTF_EUNSUPPORTED;
     hipStream_t s = (hipStream_t)stream;
+    const bool phases = cost_phases_on();
+    if (phases) OTF_HIP(hipEventRecord(g_cost_ev[0], s));
     const bool split = in_dtype == OTF_F32;
     const int ldh = (int)((d + otf::SBK - 1) / otf::SBK * otf::SBK);
     char* p = (char*)workspace;
@@ -1281,12 +1315,17 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
                 Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
                 zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
     } while (0)
+    if (phases) OTF_HIP(hipEventRecord(g_cost_ev[1], s));
     if (split && !f16out) OTF_COST_LAUNCH(3, float);
     else if (split) OTF_COST_LAUNCH(3, _Float16);
     else if (!f16out) OTF_COST_LAUNCH(1, float);
     else OTF_COST_LAUNCH(1, _Float16);
 #undef OTF_COST_LAUNCH
     OTF_HIP(hipGetLastError());
+    if (phases) {
+        OTF_HIP(hipEventRecord(g_cost_ev[2], s));
+        g_cost_ev_state = 2;
+    }
     return OTF_OK;
 }
 

@@ -124,6 +124,7 @@ _SIGS = {
     "otf_sinkhorn_row_sharded": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
                                                 ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _vp,
                                                 _i64, _i32, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "otf_cost_last_phases": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "otf_xpeer_handle_size": (ctypes.c_size_t, []),
     "otf_xpeer_create": (ctypes.c_int, [_i32, _i32, _i64, ctypes.POINTER(ctypes.c_void_p), _vp]),
     "otf_xpeer_connect": (ctypes.c_int, [_vp, _vp]),

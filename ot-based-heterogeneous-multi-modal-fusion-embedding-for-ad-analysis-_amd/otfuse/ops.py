@@ -86,6 +86,14 @@ def pairwise_cost(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = 
     return C, cmax
 
 
+def cost_last_phases() -> tuple[float, float]:
+    """(prep_ms, kernel_ms) of the last pairwise_cost / pairwise_cost_ex call made with
+    OTF_COST_PHASES=1 in the environment (profiling; synchronises on that call)."""
+    p, k = ctypes.c_float(), ctypes.c_float()
+    L.check(L.lib().otf_cost_last_phases(ctypes.byref(p), ctypes.byref(k)), "otf_cost_last_phases")
+    return float(p.value), float(k.value)
+
+
 def pairwise_cost_ex(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = "sqeuclidean",
                      zero_diag: bool | None = None, out_dtype=torch.float32,
                      workspace: torch.Tensor | None = None, in_dtype=None):
