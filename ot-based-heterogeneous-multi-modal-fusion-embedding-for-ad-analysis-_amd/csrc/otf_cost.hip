@@ -656,6 +656,20 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
 // SOURCE chunk (cdna_hip_programming.md §5.4 rule 21).  Wave w issues the DMA of rows
 // [32 w, 32 w + 32) of each image; the fragments are read with the same swap.
 constexpr int RBK = 16, RSLOTS = 4;
+// Diagnostic build only (-DOTF_COST_STAMPS, tools/ubench_cost.hip): wave 0's wall clock
+// at the phases of the ring kernel per workgroup
+#ifdef OTF_COST_STAMPS
+__device__ unsigned long long g_cst[1024 * 8];
+#define OTF_CST(k)                                                                            \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < 1024)                                            \
+            g_cst[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                   \
+    } while (0)
+#else
+#define OTF_CST(k) \
+    do {           \
+    } while (0)
+#endif
 __device__ __forceinline__ int rswz(int row, int chunk) { return row * 32 + ((chunk ^ ((row >> 3) & 1)) << 4); }
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
@@ -680,6 +694,7 @@ __global__ __launch_bounds__(512) void cost_ring_kernel(
     float* sxx = sxs + GBM;
     float* wmx = sxx + GBM;
 
+    OTF_CST(0);
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -729,6 +744,7 @@ __global__ __launch_bounds__(512) void cost_ring_kernel(
         cyy[nj] = yy[g];
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    OTF_CST(1);
 
     f32x16 acc[2][4];
 #pragma unroll
@@ -758,6 +774,7 @@ __global__ __launch_bounds__(512) void cost_ring_kernel(
 #else
         if (kt + RSLOTS - 1 < nk) issue(kt + RSLOTS - 1);
 #endif
+        if (kt == nk / 2) OTF_CST(4);
         const char* sl = smem + (kt % RSLOTS) * STAGE;
         f16x8 ah[2], al[2], bh[4], bl[4];
 #pragma unroll
@@ -789,6 +806,7 @@ __global__ __launch_bounds__(512) void cost_ring_kernel(
             }
     }
 
+    OTF_CST(2);
     const float os = store_scale ? store_scale[0] : 1.0f;
     float lmax = 0.f;
 #pragma unroll
@@ -814,6 +832,7 @@ __global__ __launch_bounds__(512) void cost_ring_kernel(
                     lmax = fmaxf(lmax, (float)cs);
                 }
             }
+    OTF_CST(3);
     if (cmax) {
         lmax = wave_max(lmax);
         if (lane == 0) wmx[wid] = lmax;

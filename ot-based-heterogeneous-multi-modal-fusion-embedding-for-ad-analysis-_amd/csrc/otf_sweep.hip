@@ -95,7 +95,8 @@ template <typename T> struct SkSweepArgs {
     int gran;           // 1: granule flush (float, not deterministic mode)
     unsigned char* gslab;  // [grid][m_pad] granules: column partials per workgroup
     unsigned char* gxp;    // [2 parity][8 XCC][m_pad] granules: XCC partials (sc1)
-    unsigned char* gfs;    // [8 XCC][4 ring][m_pad] granules: S, read within the XCC
+    unsigned char* gfs;    // [8 XCC][4 ring][m_pad] floats: S, read within the XCC, then
+                           // [8 XCC][4 ring][32 slices] ready words: (epoch << 2) | flags
     int* xl;               // [8][256] registration lists: blockIdx per XCC slot
     // cross-rank exchange (world > 1): xr[r] = rank r's exchange buffer as mapped here,
     // [2 parity][8 ranks][m_pad] granules
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     __shared__ int s_flag;
     __shared__ int s_pop[6];
     __shared__ int mrow[256];     // granule flush: this XCC's members by blockIdx rank
-    __shared__ int s_or[4][NW];  // [0..1] v-update checks, [2..3] flushes (by parity)
+    __shared__ int s_or[6][NW];  // [0..1] v-update checks, [2..3] flushes, [4..5] S slices
     const bool gran = sizeof(T) == 4 && p.gran;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -304,31 +305,29 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     // epoch k + 1; flags of every granule ORed into fl, a stall clears ok
     const int mc = p.m_pad / 2;                       // 16-B granule pairs per row
     auto load_sums_gran = [&](int k, int g, T (&out)[VC], int& fl, bool& ok) {
+        // S[k] of chunk g: poll the ready word of its slice (one dword), then read the
+        // VC sums (plain floats: half the bytes of tagged granules)
         const __amdgpu_buffer_rsrc_t rfs = sums_rsrc(p.gfs);
         const unsigned e = (p.ep_base + (unsigned)(k + 1)) & 0x3fffffffu;
-        const uint32_t base = (uint32_t)((xcc_id() * 4 + (int)(e & 3)) * mc) * 16u + (uint32_t)(colc[g] / 2) * 16u;
-        I4 x[VC / 2];
-#pragma unroll
-        for (int h = 0; h < VC / 2; ++h) x[h] = gload(rfs, base + h * 16);
-        unsigned pend = 0;
-#pragma unroll
-        for (int h = 0; h < VC / 2; ++h)
-            if (!chunk_at(x[h], e)) pend |= 1u << h;
-        while (pend && ok) {
+        const int swc = (mc + kSwSlices - 1) / kSwSlices;
+        const int slot = xcc_id() * 4 + (int)(e & 3);
+        const uint32_t fo = (uint32_t)(32 * p.m_pad) * 4u + (uint32_t)(slot * kSwSlices + (colc[g] / 2) / swc) * 4u;
+        int fw = __builtin_amdgcn_raw_buffer_load_b32(rfs, fo, 0, 16 /* sc1 */);
+        while (((unsigned)fw >> 2) != e && ok) {
             __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-            for (int h = 0; h < VC / 2; ++h)
-                if (pend & (1u << h)) x[h] = gload(rfs, base + h * 16);
-#pragma unroll
-            for (int h = 0; h < VC / 2; ++h)
-                if ((pend & (1u << h)) && chunk_at(x[h], e)) pend &= ~(1u << h);
-            if (pend && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
+            fw = __builtin_amdgcn_raw_buffer_load_b32(rfs, fo, 0, 16 /* sc1 */);
+            if (((unsigned)fw >> 2) != e && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
         }
+        fl |= fw & 3;
+        const uint32_t base = (uint32_t)(slot * p.m_pad + colc[g]) * 4u;
 #pragma unroll
-        for (int h = 0; h < VC / 2; ++h) {
-            out[2 * h] = (T)chunk_v0(x[h]);
-            out[2 * h + 1] = (T)chunk_v1(x[h]);
-            fl |= (x[h][1] | x[h][3]) & 3;
+        for (int h = 0; h < VC / 4; ++h) {
+            using F4 = __attribute__((ext_vector_type(4))) float;
+            const F4 v4 = __builtin_bit_cast(F4, __builtin_amdgcn_raw_buffer_load_b128(rfs, base + h * 16, 0, 16 /* sc1 */));
+            out[4 * h] = (T)v4[0];
+            out[4 * h + 1] = (T)v4[1];
+            out[4 * h + 2] = (T)v4[2];
+            out[4 * h + 3] = (T)v4[3];
         }
     };
     // OR of 3 flag bits over the workgroup (ballots + one barrier; par alternates)
@@ -743,11 +742,17 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             OTF_STAMP(k - 1, 7);
         }
 #endif
-        // c. owned slices: S = the active XCCs' partials in XCC order -> this XCC's ring slot
-        if (sq == 0) {
-            for (int sl = gslot_r; sl < kSwSlices; sl += nx) {
-                const int cch = sl * sw + sj;
-                if (!(sj < sw && cch < mc)) continue;
+        // c. owned slices: S = the active XCCs' partials in XCC order (across ranks: this
+        // rank's partial to every rank, then the world's partials in rank order) -> this
+        // XCC's ring slot as plain floats; once every owner thread's stores are done, one
+        // ready word per slice carries the epoch and the OR of the flags
+        int nsl = 0;
+        for (int sl = gslot_r; sl < kSwSlices; sl += nx, ++nsl) {
+            const int cch = sl * sw + sj;
+            const bool act = sq == 0 && sj < sw && cch < mc;
+            float s0 = 0.f, s1 = 0.f;
+            int f = 0;
+            if (act) {
                 I4 x[8];
                 unsigned pend = 0;
 #pragma unroll
@@ -769,8 +774,6 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                         if ((pend & (1u << xx)) && chunk_at(x[xx], e)) pend &= ~(1u << xx);
                     if (pend && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
                 }
-                float s0 = 0.f, s1 = 0.f;
-                int f = 0;
 #pragma unroll
                 for (int xx = 0; xx < 8; ++xx)
                     if (act_mask & (1u << xx)) {
@@ -778,53 +781,59 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                         s1 += chunk_v1(x[xx]);
                         f |= (x[xx][1] | x[xx][3]) & 3;
                     }
-                if (p.world <= 1) {
-                    gstore_col(rfs, (uint32_t)((xcd * 4 + (int)(e & 3)) * mc + cch) * 16u, chunk2(s0, s1, (int)(e << 2) | f), 1);
-                } else if (xcd == __builtin_ctz(act_mask)) {
-                    // this rank's partial of the slice -> every rank's exchange buffer
-                    const uint32_t xo = (uint32_t)(((e & 1) * 8 + p.rank) * mc + cch) * 16u;
-                    for (int r = 0; r < p.world; ++r)
-                        gstore_sys(sums_rsrc(p.xr[r]), xo, chunk2(s0, s1, (int)(e << 2) | f));
-                }
-            }
-            // c'. the world's rank partials of the slice, in rank order -> S
-            if (p.world > 1) {
-                for (int sl = gslot_r; sl < kSwSlices; sl += nx) {
-                    const int cch = sl * sw + sj;
-                    if (!(sj < sw && cch < mc)) continue;
-                    I4 x[8];
-                    unsigned pend = 0;
+                if (p.world > 1) {
+                    if (xcd == __builtin_ctz(act_mask)) {
+                        // this rank's partial of the slice -> every rank's exchange buffer
+                        const uint32_t xo = (uint32_t)(((e & 1) * 8 + p.rank) * mc + cch) * 16u;
+                        for (int r = 0; r < p.world; ++r)
+                            gstore_sys(sums_rsrc(p.xr[r]), xo, chunk2(s0, s1, (int)(e << 2) | f));
+                    }
+                    // c'. the world's rank partials of the slice, in rank order
+                    I4 y[8];
+                    unsigned pr = 0;
 #pragma unroll
                     for (int r = 0; r < 8; ++r)
                         if (r < p.world) {
-                            x[r] = gload_sys(rxx, (uint32_t)(((e & 1) * 8 + r) * mc + cch) * 16u);
-                            pend |= 1u << r;
+                            y[r] = gload_sys(rxx, (uint32_t)(((e & 1) * 8 + r) * mc + cch) * 16u);
+                            pr |= 1u << r;
                         }
 #pragma unroll
                     for (int r = 0; r < 8; ++r)
-                        if ((pend & (1u << r)) && chunk_at(x[r], e)) pend &= ~(1u << r);
-                    while (pend && ok) {
+                        if ((pr & (1u << r)) && chunk_at(y[r], e)) pr &= ~(1u << r);
+                    while (pr && ok) {
                         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
                         for (int r = 0; r < 8; ++r)
-                            if (pend & (1u << r)) x[r] = gload_sys(rxx, (uint32_t)(((e & 1) * 8 + r) * mc + cch) * 16u);
+                            if (pr & (1u << r)) y[r] = gload_sys(rxx, (uint32_t)(((e & 1) * 8 + r) * mc + cch) * 16u);
 #pragma unroll
                         for (int r = 0; r < 8; ++r)
-                            if ((pend & (1u << r)) && chunk_at(x[r], e)) pend &= ~(1u << r);
-                        if (pend && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
+                            if ((pr & (1u << r)) && chunk_at(y[r], e)) pr &= ~(1u << r);
+                        if (pr && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
                     }
-                    float s0 = 0.f, s1 = 0.f;
-                    int f = 0;
+                    s0 = 0.f;
+                    s1 = 0.f;
+                    f = 0;
 #pragma unroll
                     for (int r = 0; r < 8; ++r)
                         if (r < p.world) {
-                            s0 += chunk_v0(x[r]);
-                            s1 += chunk_v1(x[r]);
-                            f |= (x[r][1] | x[r][3]) & 3;
+                            s0 += chunk_v0(y[r]);
+                            s1 += chunk_v1(y[r]);
+                            f |= (y[r][1] | y[r][3]) & 3;
                         }
-                    gstore_col(rfs, (uint32_t)((xcd * 4 + (int)(e & 3)) * mc + cch) * 16u, chunk2(s0, s1, (int)(e << 2) | f), 1);
                 }
+                using F2s = __attribute__((ext_vector_type(2))) float;
+                using U2s = __attribute__((ext_vector_type(2))) unsigned int;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2s, F2s{s0, s1}), rfs,
+                                                      (uint32_t)((xcd * 4 + (int)(e & 3)) * p.m_pad + 2 * cch) * 4u, 0, 0);
             }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int bits = block_or((f & 1) | (ok ? 0 : 4), 4 + ((nsl + (int)e) & 1));
+            if (tid == 0 && sl * sw < mc)
+                __builtin_amdgcn_raw_buffer_store_b32((int)(e << 2) | (bits & 1), rfs,
+                                                      (uint32_t)(32 * p.m_pad) * 4u +
+                                                          (uint32_t)((xcd * 4 + (int)(e & 3)) * kSwSlices + sl) * 4u,
+                                                      0, 0);
+            if (bits & 4) ok = false;
         }
         ok = !block_or(ok ? 0 : 4, 2 + (int)(e & 1));
         deadline = __builtin_amdgcn_s_memrealtime() + p.stall_ticks;

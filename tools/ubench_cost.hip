@@ -58,5 +58,29 @@ int main(int argc, char** argv) {
     const double gf = 2.0 * N * (double)N * d * (f16 ? 1 : 3) / 1e9;
     printf("N=%d d=%d %s: %.1f us per call (prep + cost), %.0f TFLOP/s of fp16 MFMA work\n", N, d,
            f16 ? "f16in" : "f32", us, gf / us * 1e3);
+#ifdef OTF_COST_STAMPS
+    {   // the last call's ring-kernel phases (wave 0 of each workgroup, 10-ns ticks)
+        std::vector<unsigned long long> st(1024 * 8);
+        (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(otf::g_cst), st.size() * 8);
+        int nw = 0;
+        unsigned long long t0 = ~0ull, t3 = 0, s0max = 0;
+        double ph[4] = {0, 0, 0, 0};
+        for (int w = 0; w < 1024; ++w) {
+            const unsigned long long* x = &st[w * 8];
+            if (x[0] == 0 || x[3] < x[0]) continue;
+            ++nw;
+            ph[0] += (double)(x[1] - x[0]);
+            ph[1] += (double)(x[4] - x[1]);
+            ph[2] += (double)(x[2] - x[4]);
+            ph[3] += (double)(x[3] - x[2]);
+            t0 = x[0] < t0 ? x[0] : t0;
+            t3 = x[3] > t3 ? x[3] : t3;
+            s0max = x[0] > s0max ? x[0] : s0max;
+        }
+        if (nw) printf("stamps: %d WGs  prologue %.2f  loop 1st half %.2f  2nd half %.2f  epilogue %.2f  "
+                       "span %.2f  start spread %.2f us\n", nw, ph[0] / nw / 100, ph[1] / nw / 100,
+                       ph[2] / nw / 100, ph[3] / nw / 100, (t3 - t0) / 100.0, (s0max - t0) / 100.0);
+    }
+#endif
     return 0;
 }
