@@ -488,6 +488,60 @@ __global__ __launch_bounds__(256) void cost_split16_kernel(
 // chunk index XORed with (row >> 2) & 3: 16 consecutive rows of one ds_read_b128 phase
 // (and 4 rows x 4 chunks of a ds_write_b128 phase) hit 16 distinct 16-B bank groups.
 constexpr int GBM = 256, GBN = 256, GBK = 32, GCPR = GBK / 8;
+
+// Cost values of one 256 x 256 tile from its 8 waves' accumulators (wave (wm, wn): rows
+// wm*64 .., columns wn*128 ..): c = max(sxx_r + cyy_c - 2 sxs_r cys_c acc, 0) as ONE fma
+// per element -- k = -2 sxs_r cys_c is exact (the row scales are powers of two), so this
+// is bit-identical to (sxx_r + cyy_c) - 2 dot -- stored through a buffer descriptor at
+// the tile's corner with the row step of element e a scalar offset (no 64-bit address
+// per element); whole off-diagonal tiles skip every per-element test.  Returns the max
+// of the stored values (the fp16 rounding is monotone: max first, round once).
+template <typename TC>
+__device__ __forceinline__ float epilogue_tile256(const f32x16 (&acc)[2][4], const float* sxs, const float* sxx,
+                                                  const float (&cys)[4], const float (&cyy)[4], int wm, int wn,
+                                                  int lane, int i0, int j0, int n, int m, int metric,
+                                                  int zero_diag, TC* C, int64_t ldc, float os) {
+    const __amdgpu_buffer_rsrc_t ct =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(C + (int64_t)i0 * ldc + j0), 0, 0x7fffffff, 0x00020000);
+    const bool whole = i0 + 256 <= n && j0 + 256 <= m && !(zero_diag && i0 == j0);
+    const int r0 = wm * 64 + 4 * (lane >> 5);
+    float lmax = 0.f;
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+        const int cl = wn * 128 + nj * 32 + (lane & 31);
+        const float cy2 = -2.f * cys[nj], cyc = cyy[nj];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t vb = (uint32_t)((r0 + mi * 32) * (int)ldc + cl) * (uint32_t)sizeof(TC);
+            asm volatile("" : "+v"(vb));
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int rl = r0 + mi * 32 + (e & 3) + 8 * (e >> 2);
+                float c = fmaf(acc[mi][nj][e], sxs[rl] * cy2, sxx[rl] + cyc);
+                c = c > 0.f ? c : 0.f;
+                if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
+                if (!whole) {
+                    if (i0 + rl >= n || j0 + cl >= m) continue;
+                    if (zero_diag && i0 + rl == j0 + cl) c = 0.f;
+                }
+                lmax = fmaxf(lmax, c);
+                const uint32_t so = (uint32_t)(((e & 3) + 8 * (e >> 2)) * (int)ldc) * (uint32_t)sizeof(TC);
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
+                if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
+#endif
+                {
+                    if constexpr (sizeof(TC) == 4)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, c * os), ct, vb, so, 0);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (TC)(c * os)), ct, vb, so, 0);
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    return (float)(TC)(lmax * os);
+}
 __device__ __forceinline__ int gswz(int row, int kc) { return row * GBK + ((kc ^ ((row >> 2) & 3)) << 3); }
 
 template <int NS, typename TC>
@@ -604,30 +658,8 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
     }
 
     const float os = store_scale ? store_scale[0] : 1.0f;
-    float lmax = 0.f;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int rl = wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-                const int cl = wn * 128 + nj * 32 + (lane & 31);
-                const int gi = i0 + rl, gj = j0 + cl;
-                if (gi < n && gj < m) {
-                    const float dot = acc[mi][nj][e] * sxs[rl] * cys[nj];
-                    float c = sxx[rl] + cyy[nj] - 2.f * dot;
-                    c = c > 0.f ? c : 0.f;
-                    if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
-                    if (zero_diag && gi == gj) c = 0.f;
-                    const TC cs = (TC)(c * os);
-#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
-                    if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
-#endif
-                    C[(int64_t)gi * ldc + gj] = cs;
-                    lmax = fmaxf(lmax, (float)cs);
-                }
-            }
+    float lmax = epilogue_tile256<TC>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, metric, zero_diag, C,
+                                      ldc, os);
     if (cmax) {
         lmax = wave_max(lmax);
         if (lane == 0) wmx[wid] = lmax;
@@ -808,30 +840,8 @@ __global__ __launch_bounds__(512) void cost_ring_kernel(
 
     OTF_CST(2);
     const float os = store_scale ? store_scale[0] : 1.0f;
-    float lmax = 0.f;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int rl = wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-                const int cl = wn * 128 + nj * 32 + (lane & 31);
-                const int gi2 = i0 + rl, gj2 = j0 + cl;
-                if (gi2 < n && gj2 < m) {
-                    const float dot = acc[mi][nj][e] * sxs[rl] * cys[nj];
-                    float c = sxx[rl] + cyy[nj] - 2.f * dot;
-                    c = c > 0.f ? c : 0.f;
-                    if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
-                    if (zero_diag && gi2 == gj2) c = 0.f;
-                    const TC cs = (TC)(c * os);
-#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
-                    if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
-#endif
-                    C[(int64_t)gi2 * ldc + gj2] = cs;
-                    lmax = fmaxf(lmax, (float)cs);
-                }
-            }
+    float lmax = epilogue_tile256<TC>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, metric, zero_diag, C,
+                                      ldc, os);
     OTF_CST(3);
     if (cmax) {
         lmax = wave_max(lmax);

@@ -675,7 +675,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         }
         badu = 0;
 #ifdef OTF_STAMPS
-        if (k >= 1) {
+        if (k >= 1 && k - 1 < 15) {  // (slot 15 * 8 + 7 holds the XCD id)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             OTF_STAMP(k - 1, 6);
         }
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             __syncthreads();
         }
 #ifdef OTF_STAMPS
-        if (k >= 1) {
+        if (k >= 1 && k - 1 < 15) {  // (slot 15 * 8 + 7 holds the XCD id)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             OTF_STAMP(k - 1, 7);
         }
