@@ -494,53 +494,78 @@ constexpr int GBM = 256, GBN = 256, GBK = 32, GCPR = GBK / 8;
 // per element -- k = -2 sxs_r cys_c is exact (the row scales are powers of two), so this
 // is bit-identical to (sxx_r + cyy_c) - 2 dot -- stored through a buffer descriptor at
 // the tile's corner with the row step of element e a scalar offset (no 64-bit address
-// per element); whole off-diagonal tiles skip every per-element test.  Returns the max
-// of the stored values (the fp16 rounding is monotone: max first, round once).
-template <typename TC>
-__device__ __forceinline__ float epilogue_tile256(const f32x16 (&acc)[2][4], const float* sxs, const float* sxx,
-                                                  const float (&cys)[4], const float (&cyy)[4], int wm, int wn,
-                                                  int lane, int i0, int j0, int n, int m, int metric,
-                                                  int zero_diag, TC* C, int64_t ldc, float os) {
+// per element).  The metric and the whole-tile test are template arguments (one uniform
+// branch per tile, not per element); a row's norm terms are read once for its 4 column
+// blocks.  Returns the max of the stored values (the fp16 rounding is monotone).
+template <typename TC, bool EUC, bool WHOLE>
+__device__ __forceinline__ float epilogue_tile256_t(const f32x16 (&acc)[2][4], const float* sxs, const float* sxx,
+                                                    const float (&cys)[4], const float (&cyy)[4], int wm, int wn,
+                                                    int lane, int i0, int j0, int n, int m, int zero_diag, TC* C,
+                                                    int64_t ldc, float os) {
     const __amdgpu_buffer_rsrc_t ct =
         __builtin_amdgcn_make_buffer_rsrc((void*)(C + (int64_t)i0 * ldc + j0), 0, 0x7fffffff, 0x00020000);
-    const bool whole = i0 + 256 <= n && j0 + 256 <= m && !(zero_diag && i0 == j0);
     const int r0 = wm * 64 + 4 * (lane >> 5);
-    float lmax = 0.f;
+    float cy2[4];
+    int cl[4];
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj) {
-        const int cl = wn * 128 + nj * 32 + (lane & 31);
-        const float cy2 = -2.f * cys[nj], cyc = cyy[nj];
+        cy2[nj] = -2.f * cys[nj];
+        cl[nj] = wn * 128 + nj * 32 + (lane & 31);
+    }
+    float lmax = 0.f;
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-            __builtin_amdgcn_sched_barrier(0);
-            uint32_t vb = (uint32_t)((r0 + mi * 32) * (int)ldc + cl) * (uint32_t)sizeof(TC);
-            asm volatile("" : "+v"(vb));
+    for (int mi = 0; mi < 2; ++mi) {
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t vb[4];
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int rl = r0 + mi * 32 + (e & 3) + 8 * (e >> 2);
-                float c = fmaf(acc[mi][nj][e], sxs[rl] * cy2, sxx[rl] + cyc);
-                c = c > 0.f ? c : 0.f;
-                if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
-                if (!whole) {
-                    if (i0 + rl >= n || j0 + cl >= m) continue;
-                    if (zero_diag && i0 + rl == j0 + cl) c = 0.f;
+        for (int nj = 0; nj < 4; ++nj) {
+            vb[nj] = (uint32_t)((r0 + mi * 32) * (int)ldc + cl[nj]) * (uint32_t)sizeof(TC);
+            asm volatile("" : "+v"(vb[nj]));
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int rl = r0 + mi * 32 + (e & 3) + 8 * (e >> 2);
+            const float a = sxs[rl], b = sxx[rl];
+            const uint32_t so = (uint32_t)(((e & 3) + 8 * (e >> 2)) * (int)ldc) * (uint32_t)sizeof(TC);
+#pragma unroll
+            for (int nj = 0; nj < 4; ++nj) {
+                float c = fmaf(acc[mi][nj][e], a * cy2[nj], b + cyy[nj]);
+                c = fmaxf(c, 0.f);  // (a NaN maps to 0 either way)
+                if constexpr (EUC) c = sqrtf(c);
+                if constexpr (!WHOLE) {
+                    if (i0 + rl >= n || j0 + cl[nj] >= m) continue;
+                    if (zero_diag && i0 + rl == j0 + cl[nj]) c = 0.f;
                 }
                 lmax = fmaxf(lmax, c);
-                const uint32_t so = (uint32_t)(((e & 3) + 8 * (e >> 2)) * (int)ldc) * (uint32_t)sizeof(TC);
 #if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
                 if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
 #endif
                 {
                     if constexpr (sizeof(TC) == 4)
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, c * os), ct, vb, so, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, c * os), ct, vb[nj], so, 0);
                     else
-                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (TC)(c * os)), ct, vb, so, 0);
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (TC)(c * os)), ct, vb[nj], so, 0);
                 }
             }
         }
     }
     __builtin_amdgcn_sched_barrier(0);
     return (float)(TC)(lmax * os);
+}
+template <typename TC>
+__device__ __forceinline__ float epilogue_tile256(const f32x16 (&acc)[2][4], const float* sxs, const float* sxx,
+                                                  const float (&cys)[4], const float (&cyy)[4], int wm, int wn,
+                                                  int lane, int i0, int j0, int n, int m, int metric,
+                                                  int zero_diag, TC* C, int64_t ldc, float os) {
+    const bool whole = i0 + 256 <= n && j0 + 256 <= m && !(zero_diag && i0 == j0);
+    if (metric == OTF_EUCLIDEAN) {
+        if (whole)
+            return epilogue_tile256_t<TC, true, true>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
+        return epilogue_tile256_t<TC, true, false>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
+    }
+    if (whole)
+        return epilogue_tile256_t<TC, false, true>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
+    return epilogue_tile256_t<TC, false, false>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
 }
 __device__ __forceinline__ int gswz(int row, int kc) { return row * GBK + ((kc ^ ((row >> 2) & 3)) << 3); }
 
