@@ -583,6 +583,7 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
     __shared__ float sxs[GBM], sxx[GBM];
     __shared__ float wmx[8];
 
+    OTF_CST(0);
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
@@ -644,11 +645,13 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
         cyy[nj] = yy[gj];
     }
 
+    OTF_CST(1);
     const int nk = kpad / GBK;
     gload(0);
     lstore(0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
+        if (kt == nk / 2) OTF_CST(4);
         const int buf = kt & 1;
         if (kt + 1 < nk) gload((kt + 1) * GBK);
 #pragma unroll
@@ -682,9 +685,11 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
         __syncthreads();
     }
 
+    OTF_CST(2);
     const float os = store_scale ? store_scale[0] : 1.0f;
     float lmax = epilogue_tile256<TC>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, metric, zero_diag, C,
                                       ldc, os);
+    OTF_CST(3);
     if (cmax) {
         lmax = wave_max(lmax);
         if (lane == 0) wmx[wid] = lmax;
