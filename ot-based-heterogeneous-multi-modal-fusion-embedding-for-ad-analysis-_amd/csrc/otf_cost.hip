@@ -569,6 +569,20 @@ __device__ __forceinline__ float epilogue_tile256(const f32x16 (&acc)[2][4], con
 }
 __device__ __forceinline__ int gswz(int row, int kc) { return row * GBK + ((kc ^ ((row >> 2) & 3)) << 3); }
 
+// Diagnostic build only (-DOTF_COST_STAMPS, tools/ubench_cost.hip): wave 0's wall clock
+// at the phases of the 256x256 cost kernels per workgroup
+#ifdef OTF_COST_STAMPS
+__device__ unsigned long long g_cst[1024 * 8];
+#define OTF_CST(k)                                                                            \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < 1024)                                            \
+            g_cst[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                   \
+    } while (0)
+#else
+#define OTF_CST(k) \
+    do {           \
+    } while (0)
+#endif
 template <int NS, typename TC>
 __global__ __launch_bounds__(512) void cost_big_kernel(
     const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
@@ -718,20 +732,6 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
 // SOURCE chunk (cdna_hip_programming.md §5.4 rule 21).  Wave w issues the DMA of rows
 // [32 w, 32 w + 32) of each image; the fragments are read with the same swap.
 constexpr int RBK = 16, RSLOTS = 4;
-// Diagnostic build only (-DOTF_COST_STAMPS, tools/ubench_cost.hip): wave 0's wall clock
-// at the phases of the ring kernel per workgroup
-#ifdef OTF_COST_STAMPS
-__device__ unsigned long long g_cst[1024 * 8];
-#define OTF_CST(k)                                                                            \
-    do {                                                                                      \
-        if (threadIdx.x == 0 && blockIdx.x < 1024)                                            \
-            g_cst[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                   \
-    } while (0)
-#else
-#define OTF_CST(k) \
-    do {           \
-    } while (0)
-#endif
 __device__ __forceinline__ int rswz(int row, int chunk) { return row * 32 + ((chunk ^ ((row >> 3) & 1)) << 4); }
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
