@@ -667,7 +667,13 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
     for (int kt = 0; kt < nk; ++kt) {
         if (kt == nk / 2) OTF_CST(4);
         const int buf = kt & 1;
-        if (kt + 1 < nk) gload((kt + 1) * GBK);
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 4)
+        // diagnostic: no operand loads after the prologue (the loop re-reads stale stages)
+        if (false)
+#else
+        if (kt + 1 < nk)
+#endif
+            gload((kt + 1) * GBK);
 #pragma unroll
         for (int ks = 0; ks < GBK / 16; ++ks) {
             const int kc = ks * 2 + (lane >> 5);
@@ -688,14 +694,24 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
             for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
                 for (int nj = 0; nj < 4; ++nj) {
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 2)
+                    // diagnostic: no MFMAs (the fragments still feed one add each)
+                    acc[mi][nj][0] += (float)ah[mi][0] + (float)bh[nj][0] + (NI == 2 ? (float)al[mi][0] + (float)bl[nj][0] : 0.f);
+#else
                     if (NS == 3) {
                         acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mi], bh[nj], acc[mi][nj], 0, 0, 0);
                         acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bl[nj], acc[mi][nj], 0, 0, 0);
                     }
                     acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bh[nj], acc[mi][nj], 0, 0, 0);
+#endif
                 }
         }
-        if (kt + 1 < nk) lstore(buf ^ 1);
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 4)
+        if (false)
+#else
+        if (kt + 1 < nk)
+#endif
+            lstore(buf ^ 1);
         __syncthreads();
     }
 
@@ -703,6 +719,222 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
     const float os = store_scale ? store_scale[0] : 1.0f;
     float lmax = epilogue_tile256<TC>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, metric, zero_diag, C,
                                       ldc, os);
+    OTF_CST(3);
+    if (cmax) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmx[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            float v = wmx[0];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) v = fmaxf(v, wmx[w]);
+            const unsigned int u = __float_as_uint(v);
+            if (u > __hip_atomic_load(cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(cmax, u);
+        }
+    }
+}
+
+// The same 256 x 256 tile on v_mfma_f32_16x16x32_f16 (OTF_COST_MFMA16): one MFMA per
+// 32-deep stage and 16 x 16 output block, so a wave's 64 x 128 block is 4 x 8 MFMA
+// blocks (128 accumulators, as before) and the LDS reads per stage are the same 24
+// ds_read_b128 per wave; the point is the clock: MFMA-dense loops hold a higher clock on
+// the 16x16 shape (MI355X_MICROARCH.md, DVFS item 7: 1.12-1.15x the FLOP/s of 32x32x16).
+// Fragment of rows r..r+15: lane l reads row r + (l & 15), 16-B chunk l >> 4 of the
+// 64-B row.  The chunk is XOR-permuted by the row quad q = (row >> 2) & 3 through
+// g(q) = {0, 2, 3, 1}: every 16-lane group of ds_read_b128 ({0-3,12-15,20-27}, ...)
+// then hits 16 distinct 16-B slots of the 256-B bank row, and the 8-lane groups of the
+// ds_write_b128 staging stores (rows 2j, 2j + 1, chunks 0..3) cover 128 B exactly.
+__device__ __forceinline__ int g16swz(int row, int kc) {
+    return row * GBK + ((kc ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3)) << 3);
+}
+template <typename TC, bool EUC, bool WHOLE>
+__device__ __forceinline__ float epilogue_tile256_16t(const f32x4 (&acc)[4][8], const float* sxs, const float* sxx,
+                                                      const float (&cys)[8], const float (&cyy)[8], int wm, int wn,
+                                                      int lane, int i0, int j0, int n, int m, int zero_diag, TC* C,
+                                                      int64_t ldc, float os) {
+    // 16x16 output block: lane l holds rows 4 (l >> 4) + e (e < 4) of column l & 15
+    const __amdgpu_buffer_rsrc_t ct =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(C + (int64_t)i0 * ldc + j0), 0, 0x7fffffff, 0x00020000);
+    const int r0 = wm * 64 + 4 * (lane >> 4);
+    float cy2[8];
+    int cl[8];
+    uint32_t vb[8];
+#pragma unroll
+    for (int nj = 0; nj < 8; ++nj) {
+        cy2[nj] = -2.f * cys[nj];
+        cl[nj] = wn * 128 + nj * 16 + (lane & 15);
+        vb[nj] = (uint32_t)(r0 * (int)ldc + cl[nj]) * (uint32_t)sizeof(TC);
+        asm volatile("" : "+v"(vb[nj]));
+    }
+    float lmax = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int rl = r0 + mi * 16 + e;
+            const float a = sxs[rl], b = sxx[rl];
+            const uint32_t so = (uint32_t)((mi * 16 + e) * (int)ldc) * (uint32_t)sizeof(TC);
+#pragma unroll
+            for (int nj = 0; nj < 8; ++nj) {
+                float c = fmaf(acc[mi][nj][e], a * cy2[nj], b + cyy[nj]);
+                c = fmaxf(c, 0.f);
+                if constexpr (EUC) c = sqrtf(c);
+                if constexpr (!WHOLE) {
+                    if (i0 + rl >= n || j0 + cl[nj] >= m) continue;
+                    if (zero_diag && i0 + rl == j0 + cl[nj]) c = 0.f;
+                }
+                lmax = fmaxf(lmax, c);
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
+                if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
+#endif
+                {
+                    if constexpr (sizeof(TC) == 4)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, c * os), ct, vb[nj], so, 0);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (TC)(c * os)), ct, vb[nj], so, 0);
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    return (float)(TC)(lmax * os);
+}
+
+template <int NS, typename TC>
+__global__ __launch_bounds__(512) void cost_big16_kernel(
+    const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
+    const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
+    const float* __restrict__ ys, const float* __restrict__ yy, int64_t ldxh, int64_t ldyh, int n, int m, int kpad,
+    int metric, int zero_diag, TC* __restrict__ C, int64_t ldc, unsigned int* cmax, int tiles_n,
+    const float* __restrict__ store_scale) {
+    constexpr int NI = NS == 3 ? 2 : 1;
+    constexpr int NCH = GBM * GCPR / 512;
+    __shared__ __attribute__((aligned(16))) _Float16 As[2][NI][GBM * GBK];
+    __shared__ __attribute__((aligned(16))) _Float16 Bs[2][NI][GBN * GBK];
+    __shared__ float sxs[GBM], sxx[GBM];
+    __shared__ float wmx[8];
+
+    OTF_CST(0);
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    int tm, tn;
+    grouped_tile(wg, nwg, tiles_n, tm, tn);
+    const int i0 = tm * GBM, j0 = tn * GBN;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    using u4 = __attribute__((ext_vector_type(4))) unsigned int;
+    u4 st[NCH][2 * NI];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int chunk = tid + 512 * c;
+            const int row = chunk / GCPR, kc = (chunk % GCPR) * 8;
+            const int gi = i0 + row < n ? i0 + row : n - 1;
+            const int gj = j0 + row < m ? j0 + row : m - 1;
+            st[c][0] = *reinterpret_cast<const u4*>(Xh + (int64_t)gi * ldxh + k0 + kc);
+            st[c][NI] = *reinterpret_cast<const u4*>(Yh + (int64_t)gj * ldyh + k0 + kc);
+            if (NI == 2) {
+                st[c][1] = *reinterpret_cast<const u4*>(Xl + (int64_t)gi * ldxh + k0 + kc);
+                st[c][NI + 1] = *reinterpret_cast<const u4*>(Yl + (int64_t)gj * ldyh + k0 + kc);
+            }
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int chunk = tid + 512 * c;
+            const int row = chunk / GCPR, kc = chunk % GCPR;
+#pragma unroll
+            for (int h = 0; h < NI; ++h) {
+                *reinterpret_cast<u4*>(&As[buf][h][g16swz(row, kc)]) = st[c][h];
+                *reinterpret_cast<u4*>(&Bs[buf][h][g16swz(row, kc)]) = st[c][NI + h];
+            }
+        }
+    };
+
+    if (tid < GBM) {
+        const int gi = i0 + tid < n ? i0 + tid : n - 1;
+        sxs[tid] = xs[gi];
+        sxx[tid] = xx[gi];
+    }
+    float cys[8], cyy[8];
+#pragma unroll
+    for (int nj = 0; nj < 8; ++nj) {
+        const int gj0 = j0 + wn * 128 + nj * 16 + (lane & 15);
+        const int gj = gj0 < m ? gj0 : m - 1;
+        cys[nj] = ys[gj];
+        cyy[nj] = yy[gj];
+    }
+
+    OTF_CST(1);
+    const int nk = kpad / GBK;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    const int kc = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt == nk / 2) OTF_CST(4);
+        const int buf = kt & 1;
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 4)
+        if (false)
+#else
+        if (kt + 1 < nk)
+#endif
+            gload((kt + 1) * GBK);
+        f16x8 ah[4], al[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int ar = wm * 64 + t * 16 + (lane & 15);
+            ah[t] = *reinterpret_cast<const f16x8*>(&As[buf][0][g16swz(ar, kc)]);
+            if (NI == 2) al[t] = *reinterpret_cast<const f16x8*>(&As[buf][NI - 1][g16swz(ar, kc)]);
+        }
+#pragma unroll
+        for (int nj = 0; nj < 8; ++nj) {
+            const int br = wn * 128 + nj * 16 + (lane & 15);
+            const f16x8 bh = *reinterpret_cast<const f16x8*>(&Bs[buf][0][g16swz(br, kc)]);
+            f16x8 bl;
+            if (NI == 2) bl = *reinterpret_cast<const f16x8*>(&Bs[buf][NI - 1][g16swz(br, kc)]);
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 2)
+                acc[mi][nj][0] += (float)ah[mi][0] + (float)bh[0] + (NI == 2 ? (float)al[mi][0] + (float)bl[0] : 0.f);
+#else
+                if (NS == 3) {
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mi], bh, acc[mi][nj], 0, 0, 0);
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bl, acc[mi][nj], 0, 0, 0);
+                }
+                acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bh, acc[mi][nj], 0, 0, 0);
+#endif
+            }
+        }
+#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 4)
+        if (false)
+#else
+        if (kt + 1 < nk)
+#endif
+            lstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    OTF_CST(2);
+    const float os = store_scale ? store_scale[0] : 1.0f;
+    const bool whole = i0 + 256 <= n && j0 + 256 <= m && !(zero_diag && i0 == j0);
+    float lmax;
+    if (metric == OTF_EUCLIDEAN)
+        lmax = whole ? epilogue_tile256_16t<TC, true, true>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os)
+                     : epilogue_tile256_16t<TC, true, false>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
+    else
+        lmax = whole ? epilogue_tile256_16t<TC, false, true>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os)
+                     : epilogue_tile256_16t<TC, false, false>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
     OTF_CST(3);
     if (cmax) {
         lmax = wave_max(lmax);
@@ -1188,6 +1420,11 @@ static bool cost_ring_enabled() {
     const char* e = getenv("OTF_COST_RING");
     return e ? atoi(e) != 0 : false;
 }
+// OTF_COST_MFMA16=1 selects the 16x16x32 form of the 256 x 256 kernel (read per call)
+static bool cost_mfma16_enabled() {
+    const char* e = getenv("OTF_COST_MFMA16");
+    return e ? atoi(e) != 0 : false;
+}
 // OTF_COST_WS=1 selects the warp-specialised persistent kernel (read per call)
 static bool cost_ws_enabled() {
     const char* e = getenv("OTF_COST_WS");
@@ -1343,6 +1580,7 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     const int64_t small_rounds = (small_tiles + 2 * cus - 1) / (2 * cus);
     const bool big = 18 * big_rounds < 10 * small_rounds && cost_big_enabled();
     const bool ring = cost_ring_enabled() && ring_lds_ok();
+    const bool mfma16 = cost_mfma16_enabled();
     const int BMx = big ? otf::GBM : otf::BM, BNx = big ? otf::GBN : otf::BN;
     const int tiles_m = (int)((n + BMx - 1) / BMx);
     const int tiles_n = (int)((m + BNx - 1) / BNx);
@@ -1363,6 +1601,10 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
                 store_scale);                                                                     \
         else if (big && ring)                                                                     \
             otf::cost_ring_kernel<NS, TC><<<(int)nwg, 512, otf::kRingLds, s>>>(                  \
+                Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
+                zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
+        else if (big && mfma16)                                                                   \
+            otf::cost_big16_kernel<NS, TC><<<(int)nwg, 512, 0, s>>>(                             \
                 Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
                 zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
         else if (big)                                                                             \

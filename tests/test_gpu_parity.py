@@ -81,6 +81,33 @@ def test_cost_ring_kernel_matches_register_kernel(ops, orc, dev, monkeypatch, n,
     assert nrel(got, Cr) < (2e-3 if out_dt == torch.float16 else 1e-5)
 
 
+@pytest.mark.parametrize("n,m,d,in_dt,out_dt,metric", [
+    (4096, 4096, 512, torch.float32, torch.float32, "sqeuclidean"),
+    (4100, 3999, 300, torch.float32, torch.float32, "euclidean"),
+    (8192, 8192, 256, torch.float16, torch.float16, "sqeuclidean"),
+    (4096, 4096, 40, torch.float32, torch.float16, "sqeuclidean")])
+def test_cost_mfma16_kernel_matches_oracle(ops, orc, dev, monkeypatch, n, m, d, in_dt, out_dt, metric):
+    """The 16x16x32 form of the 256 x 256 kernel (OTF_COST_MFMA16=1): the same three fp16
+    products in another MFMA shape, so the fp32 accumulation order differs -- within the
+    split-fp16 oracle tolerance of the register-staged kernel, cmax / unit alike."""
+    g = torch.Generator(device=dev).manual_seed(n + d + 1)
+    X = torch.randn(n, d, device=dev, generator=g).to(in_dt)
+    Y = (torch.randn(m, d, device=dev, generator=g) * 0.7 + 0.2).to(in_dt)
+    monkeypatch.setenv("OTF_COST_MFMA16", "0")
+    C0, mx0, u0 = ops.pairwise_cost_ex(X, Y, metric=metric, out_dtype=out_dt)
+    monkeypatch.setenv("OTF_COST_MFMA16", "1")
+    C1, mx1, u1 = ops.pairwise_cost_ex(X, Y, metric=metric, out_dtype=out_dt)
+    torch.cuda.synchronize()
+    assert torch.equal(u0, u1)
+    tol = 2e-3 if out_dt == torch.float16 else 2e-6
+    assert float(mx1) == pytest.approx(float(mx0), rel=tol)
+    assert (C1.double() - C0.double()).abs().max().item() <= tol * float(mx0)
+    rows = torch.cat([torch.arange(0, 300, device=dev), torch.arange(n - 40, n, device=dev)])
+    Cr, _ = orc.pairwise_cost(X[rows].double().cpu().numpy(), Y.double().cpu().numpy(), metric=metric)
+    got = C1[rows].double().cpu().numpy() * float(u1)
+    assert nrel(got, Cr) < (2e-3 if out_dt == torch.float16 else 2e-6)
+
+
 def test_pairwise_cost_euclidean_same_input_zero_diag(ops, orc, dev):
     rng = np.random.default_rng(1)
     X = rng.random((70, 33)).astype(np.float32)
