@@ -747,52 +747,74 @@ __global__ __launch_bounds__(512) void cost_big_kernel(
 __device__ __forceinline__ int g16swz(int row, int kc) {
     return row * GBK + ((kc ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3)) << 3);
 }
-template <typename TC, bool EUC, bool WHOLE>
+// Cost values of one 256 x 256 tile from the 16x16x32 kernel's accumulators.  The MFMAs
+// run with the Y fragment as the A operand, so each 16 x 16 accumulator block is the
+// TRANSPOSED cost block: lane l holds cost row (l & 15) at the four consecutive columns
+// 4 (l >> 4) + e -- one 16-B (fp32) / 8-B (fp16) store per lane per block instead of
+// four 4-B stores (the epilogue's store issue, not bandwidth, is its cost).  Column norm
+// terms come from LDS (sys / syy, four consecutive in one read).  VEC: whole tile with a
+// 16-B aligned row pitch; otherwise one element at a time with the bounds tests.
+template <typename TC, bool EUC, bool VEC>
 __device__ __forceinline__ float epilogue_tile256_16t(const f32x4 (&acc)[4][8], const float* sxs, const float* sxx,
-                                                      const float (&cys)[8], const float (&cyy)[8], int wm, int wn,
-                                                      int lane, int i0, int j0, int n, int m, int zero_diag, TC* C,
+                                                      const float* sys, const float* syy, int wm, int wn, int lane,
+                                                      int i0, int j0, int n, int m, int zero_diag, TC* C,
                                                       int64_t ldc, float os) {
-    // 16x16 output block: lane l holds rows 4 (l >> 4) + e (e < 4) of column l & 15
     const __amdgpu_buffer_rsrc_t ct =
         __builtin_amdgcn_make_buffer_rsrc((void*)(C + (int64_t)i0 * ldc + j0), 0, 0x7fffffff, 0x00020000);
-    const int r0 = wm * 64 + 4 * (lane >> 4);
-    float cy2[8];
-    int cl[8];
-    uint32_t vb[8];
-#pragma unroll
-    for (int nj = 0; nj < 8; ++nj) {
-        cy2[nj] = -2.f * cys[nj];
-        cl[nj] = wn * 128 + nj * 16 + (lane & 15);
-        vb[nj] = (uint32_t)(r0 * (int)ldc + cl[nj]) * (uint32_t)sizeof(TC);
-        asm volatile("" : "+v"(vb[nj]));
-    }
+    const int rr = wm * 64 + (lane & 15), cc = wn * 128 + 4 * (lane >> 4);
     float lmax = 0.f;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
+    for (int nj = 0; nj < 8; ++nj) {
         __builtin_amdgcn_sched_barrier(0);
+        const int cl = cc + nj * 16;
+        const f32x4 ys4 = *reinterpret_cast<const f32x4*>(&sys[cl]);
+        const f32x4 yy4 = *reinterpret_cast<const f32x4*>(&syy[cl]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int rl = r0 + mi * 16 + e;
-            const float a = sxs[rl], b = sxx[rl];
-            const uint32_t so = (uint32_t)((mi * 16 + e) * (int)ldc) * (uint32_t)sizeof(TC);
+        for (int mi = 0; mi < 4; ++mi) {
+            const int rl = rr + mi * 16;
+            const float a = -2.f * sxs[rl], b = sxx[rl];
+            uint32_t vo = (uint32_t)(rl * (int)ldc + cl) * (uint32_t)sizeof(TC);
+            float cv[4];
 #pragma unroll
-            for (int nj = 0; nj < 8; ++nj) {
-                float c = fmaf(acc[mi][nj][e], a * cy2[nj], b + cyy[nj]);
+            for (int e = 0; e < 4; ++e) {
+                float c = fmaf(acc[mi][nj][e], a * ys4[e], b + yy4[e]);
                 c = fmaxf(c, 0.f);
                 if constexpr (EUC) c = sqrtf(c);
-                if constexpr (!WHOLE) {
-                    if (i0 + rl >= n || j0 + cl[nj] >= m) continue;
-                    if (zero_diag && i0 + rl == j0 + cl[nj]) c = 0.f;
-                }
-                lmax = fmaxf(lmax, c);
+                cv[e] = c;
+            }
+            if constexpr (VEC) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) lmax = fmaxf(lmax, cv[e]);
 #if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
-                if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
+                if (cv[0] == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
 #endif
                 {
+                    if constexpr (sizeof(TC) == 4) {
+                        using U4 = __attribute__((ext_vector_type(4))) unsigned int;
+                        const U4 w = {__builtin_bit_cast(uint32_t, cv[0] * os), __builtin_bit_cast(uint32_t, cv[1] * os),
+                                      __builtin_bit_cast(uint32_t, cv[2] * os), __builtin_bit_cast(uint32_t, cv[3] * os)};
+                        __builtin_amdgcn_raw_buffer_store_b128(w, ct, vo, 0, 0);
+                    } else {
+                        using U2 = __attribute__((ext_vector_type(2))) unsigned int;
+                        const uint32_t h0 = __builtin_bit_cast(uint16_t, (TC)(cv[0] * os)) |
+                                            ((uint32_t)__builtin_bit_cast(uint16_t, (TC)(cv[1] * os)) << 16);
+                        const uint32_t h1 = __builtin_bit_cast(uint16_t, (TC)(cv[2] * os)) |
+                                            ((uint32_t)__builtin_bit_cast(uint16_t, (TC)(cv[3] * os)) << 16);
+                        __builtin_amdgcn_raw_buffer_store_b64(U2{h0, h1}, ct, vo, 0, 0);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float c = cv[e];
+                    if (i0 + rl >= n || j0 + cl + e >= m) continue;
+                    if (zero_diag && i0 + rl == j0 + cl + e) c = 0.f;
+                    lmax = fmaxf(lmax, c);
+                    const uint32_t ve = vo + (uint32_t)(e * (int)sizeof(TC));
                     if constexpr (sizeof(TC) == 4)
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, c * os), ct, vb[nj], so, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, c * os), ct, ve, 0, 0);
                     else
-                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (TC)(c * os)), ct, vb[nj], so, 0);
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (TC)(c * os)), ct, ve, 0, 0);
                 }
             }
         }
@@ -813,6 +835,7 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
     __shared__ __attribute__((aligned(16))) _Float16 As[2][NI][GBM * GBK];
     __shared__ __attribute__((aligned(16))) _Float16 Bs[2][NI][GBN * GBK];
     __shared__ float sxs[GBM], sxx[GBM];
+    __shared__ __attribute__((aligned(16))) float sys[GBN], syy[GBN];
     __shared__ float wmx[8];
 
     OTF_CST(0);
@@ -865,14 +888,11 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
         const int gi = i0 + tid < n ? i0 + tid : n - 1;
         sxs[tid] = xs[gi];
         sxx[tid] = xx[gi];
-    }
-    float cys[8], cyy[8];
-#pragma unroll
-    for (int nj = 0; nj < 8; ++nj) {
-        const int gj0 = j0 + wn * 128 + nj * 16 + (lane & 15);
-        const int gj = gj0 < m ? gj0 : m - 1;
-        cys[nj] = ys[gj];
-        cyy[nj] = yy[gj];
+    } else if (tid < GBM + GBN) {
+        const int c = tid - GBM;
+        const int gj = j0 + c < m ? j0 + c : m - 1;
+        sys[c] = ys[gj];
+        syy[c] = yy[gj];
     }
 
     OTF_CST(1);
@@ -908,11 +928,13 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
 #if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 2)
                 acc[mi][nj][0] += (float)ah[mi][0] + (float)bh[0] + (NI == 2 ? (float)al[mi][0] + (float)bl[0] : 0.f);
 #else
+                // Y fragment as the A operand: the accumulator block is the transposed
+                // cost block (row-contiguous stores in the epilogue)
                 if (NS == 3) {
-                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mi], bh, acc[mi][nj], 0, 0, 0);
-                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bl, acc[mi][nj], 0, 0, 0);
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, al[mi], acc[mi][nj], 0, 0, 0);
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, ah[mi], acc[mi][nj], 0, 0, 0);
                 }
-                acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bh, acc[mi][nj], 0, 0, 0);
+                acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, ah[mi], acc[mi][nj], 0, 0, 0);
 #endif
             }
         }
@@ -927,14 +949,16 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
 
     OTF_CST(2);
     const float os = store_scale ? store_scale[0] : 1.0f;
-    const bool whole = i0 + 256 <= n && j0 + 256 <= m && !(zero_diag && i0 == j0);
+    // vector stores: whole tile, no diagonal in it, rows 16-B (fp32) / 8-B (fp16) aligned
+    const bool vec = i0 + 256 <= n && j0 + 256 <= m && !(zero_diag && i0 == j0) && (ldc % 4) == 0 &&
+                     ((uintptr_t)C % 16) == 0;
     float lmax;
     if (metric == OTF_EUCLIDEAN)
-        lmax = whole ? epilogue_tile256_16t<TC, true, true>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os)
-                     : epilogue_tile256_16t<TC, true, false>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
+        lmax = vec ? epilogue_tile256_16t<TC, true, true>(acc, sxs, sxx, sys, syy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os)
+                   : epilogue_tile256_16t<TC, true, false>(acc, sxs, sxx, sys, syy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
     else
-        lmax = whole ? epilogue_tile256_16t<TC, false, true>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os)
-                     : epilogue_tile256_16t<TC, false, false>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
+        lmax = vec ? epilogue_tile256_16t<TC, false, true>(acc, sxs, sxx, sys, syy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os)
+                   : epilogue_tile256_16t<TC, false, false>(acc, sxs, sxx, sys, syy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
     OTF_CST(3);
     if (cmax) {
         lmax = wave_max(lmax);
