@@ -1444,10 +1444,13 @@ static bool cost_ring_enabled() {
     const char* e = getenv("OTF_COST_RING");
     return e ? atoi(e) != 0 : false;
 }
-// OTF_COST_MFMA16=1 selects the 16x16x32 form of the 256 x 256 kernel (read per call)
-static bool cost_mfma16_enabled() {
+// The 16x16x32 form of the 256 x 256 kernel for float32 cost storage (metric shape: 52
+// vs 56 us, r03 stamps); the fp16-storage config-5 cost keeps the 32x32x16 form (its
+// 8-B transposed stores measured no faster).  OTF_COST_MFMA16=0 / 1 forces either form
+// (read per call).
+static bool cost_mfma16_enabled(bool f16out) {
     const char* e = getenv("OTF_COST_MFMA16");
-    return e ? atoi(e) != 0 : false;
+    return e ? atoi(e) != 0 : !f16out;
 }
 // OTF_COST_WS=1 selects the warp-specialised persistent kernel (read per call)
 static bool cost_ws_enabled() {
@@ -1604,7 +1607,7 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     const int64_t small_rounds = (small_tiles + 2 * cus - 1) / (2 * cus);
     const bool big = 18 * big_rounds < 10 * small_rounds && cost_big_enabled();
     const bool ring = cost_ring_enabled() && ring_lds_ok();
-    const bool mfma16 = cost_mfma16_enabled();
+    const bool mfma16 = cost_mfma16_enabled(f16out);
     const int BMx = big ? otf::GBM : otf::BM, BNx = big ? otf::GBN : otf::BN;
     const int tiles_m = (int)((n + BMx - 1) / BMx);
     const int tiles_n = (int)((m + BNx - 1) / BNx);

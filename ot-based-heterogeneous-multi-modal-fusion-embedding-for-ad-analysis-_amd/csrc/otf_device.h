@@ -210,23 +210,7 @@ template <int O, typename T> __device__ __forceinline__ T swap_sum(T a, T b) {
 // R = 16 in float against ~35 here.)
 template <typename T, int R>
 __device__ __forceinline__ T wave_row_totals(const T (&x)[R], int lane) {
-    static_assert(R == 2 || R == 4 || R == 8 || R == 16, "2, 4, 8 or 16 rows per wave");
-    if constexpr (R <= 4) {
-        // lane bit 5 (and bit 4 for R = 4) by the swaps, then the lanes still to cover:
-        // bit 4 by an exchange for R = 2, the 16 of a row by mirror / half mirror / quads
-        T t;
-        if constexpr (R == 4) {
-            t = swap_sum<16>(swap_sum<32>(x[0], x[2]), swap_sum<32>(x[1], x[3]));
-        } else {
-            t = swap_sum<32>(x[0], x[1]);
-            t += wave_xor<T, 16>(t);
-        }
-        t += dpp_lane<0x140>(t);
-        t += dpp_lane<0x141>(t);
-        t += dpp_lane<0xB1>(t);
-        t += dpp_lane<0x4E>(t);
-        return t;
-    } else {
+    static_assert(R == 8 || R == 16, "8 or 16 rows per wave");
     T y[R / 2], z[R / 4];
 #pragma unroll
     for (int i = 0; i < R / 2; ++i) y[i] = swap_sum<32>(x[i], x[i + R / 2]);
@@ -251,7 +235,6 @@ __device__ __forceinline__ T wave_row_totals(const T (&x)[R], int lane) {
     t += dpp_lane<0xB1>(t);
     t += dpp_lane<0x4E>(t);
     return t;
-    }
 }
 
 // Block-wide sum of R values per thread.  `red` is LDS of >= (nwaves + 1) * R

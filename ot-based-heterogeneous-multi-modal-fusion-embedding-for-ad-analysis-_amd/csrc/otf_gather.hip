@@ -13,8 +13,8 @@
 // atomics into a shared buffer followed by a grid barrier and a re-read (three memory
 // round trips, 4.4 of 6.7 us per iteration at config 2), every workgroup PUBLISHES its
 // column partials as epoch-tagged granules (R2 form, cdna_hip_programming.md Guideline
-// 16: {value word, tag} 8-byte granules, a float per granule or a double as two, one
-// 16-B write-through store per two granules) and every workgroup GATHERS all the
+// 16: {value word, tag} 8-byte granules for float, two tagged doubles per chunk for
+// double -- see make_chunk -- one 16-B store per two columns) and every workgroup GATHERS all the
 // partials itself, polling until every tag carries the epoch it waits for.  The data
 // is its own flag: no fence, no counter, no barrier.  One memory hop per iteration.
 //
@@ -25,7 +25,7 @@
 //
 // Tags: partials of S[k] = K^T u(k-1) carry epoch k + 1 (slot k & 1) and the OR of the
 // producer's numerical-break flags of iteration k - 1 (non-finite u or v) in bit 0:
-// tag = ((k + 1) << 1) | bad.  A slot is rewritten two epochs later, which no producer
+// tag = ((k + 1) << 1) | bad (double: epoch mod 4 and bad in the values' low bits).  A slot is rewritten two epochs later, which no producer
 // can reach before every consumer has finished reading it (producing S[k + 2] needs
 // S[k + 1], which each workgroup publishes only after its gather of S[k]).  Every poll
 // is bounded by s_memrealtime (re-armed after each completed gather): a stall ends in
@@ -42,11 +42,11 @@ template <typename T> struct GatherCfg {
     static constexpr int G = sizeof(T) == 4 ? 2 : 4;    // VEC-vectors per lane: 8 columns
     static constexpr int TR = RW * NW;                  // rows per workgroup: 128 / 64
     static constexpr int C = kWave * G * VEC;           // 512 columns
-    static constexpr int CPC = 8 / (int)sizeof(T);      // columns per 16-B chunk (2 granules)
+    static constexpr int CPC = 2;                       // columns per 16-B chunk
     static constexpr int NCH = C / CPC;                 // chunks per producer row
 };
 constexpr int kGatherMaxWG = 16;
-constexpr uint32_t kGatherRow = 8192;  // bytes per producer row of one slot (512 chunks)
+constexpr uint32_t kGatherRow = 8192;  // bytes per producer row of one slot (256 chunks used)
 
 template <typename T> struct SkGatherArgs {
     const void* C;
@@ -74,9 +74,18 @@ template <typename T> struct SkGatherArgs {
 
 using I4 = __attribute__((ext_vector_type(4))) int;
 
+// A 16-B chunk carries two column partials with their epoch tag.  float: two
+// {value, tag} granules, tag = (epoch << 1) | bad.  double: two values whose three low
+// mantissa bits ARE the tag -- epoch mod 4 (a slot holds epoch e - 2 or e, or the zero
+// fill before epochs 1 and 2, so two bits tell them apart) and the bad flag -- so a chunk
+// holds two columns instead of one and a gather moves half the bytes (the one-hop gather
+// is bound by the CU's 64 B/clk port: nwg x 8 KB per workgroup per iteration).  The
+// value is truncated to a 49-bit mantissa (relative 2^-50, below the float64 rounding
+// of the sums that follow); 0 and infinities come back exact once the tag is cleared.
 template <typename T> __device__ __forceinline__ void chunk_values(const I4 x, T (&v)[GatherCfg<T>::CPC]) {
     if constexpr (sizeof(T) == 8) {
-        v[0] = __builtin_bit_cast(double, ((unsigned long long)(unsigned)x[2] << 32) | (unsigned)x[0]);
+        v[0] = __builtin_bit_cast(double, ((unsigned long long)(unsigned)x[1] << 32) | ((unsigned)x[0] & ~7u));
+        v[1] = __builtin_bit_cast(double, ((unsigned long long)(unsigned)x[3] << 32) | ((unsigned)x[2] & ~7u));
     } else {
         // element copies first: __builtin_bit_cast of a vector ELEMENT reads the vector's
         // first word (ROCm 7.2 clang; found by the float parity test)
@@ -85,19 +94,36 @@ template <typename T> __device__ __forceinline__ void chunk_values(const I4 x, T
         v[1] = __builtin_bit_cast(float, w2);
     }
 }
-template <typename T> __device__ __forceinline__ I4 make_chunk(const T (&v)[GatherCfg<T>::CPC], int tag) {
+template <typename T> __device__ __forceinline__ I4 make_chunk(const T (&v)[GatherCfg<T>::CPC], int ep, int bad) {
     I4 x;
     if constexpr (sizeof(T) == 8) {
-        const unsigned long long bits = __builtin_bit_cast(unsigned long long, v[0]);
-        x[0] = (int)(unsigned)bits;
-        x[2] = (int)(unsigned)(bits >> 32);
+        const unsigned low = (unsigned)(ep & 3) | ((unsigned)bad << 2);
+        const unsigned long long b0 = __builtin_bit_cast(unsigned long long, v[0]);
+        const unsigned long long b1 = __builtin_bit_cast(unsigned long long, v[1]);
+        x[0] = (int)(((unsigned)b0 & ~7u) | low);
+        x[1] = (int)(unsigned)(b0 >> 32);
+        x[2] = (int)(((unsigned)b1 & ~7u) | low);
+        x[3] = (int)(unsigned)(b1 >> 32);
     } else {
+        const int tag = (ep << 1) | bad;
         x[0] = __builtin_bit_cast(int, v[0]);
         x[2] = __builtin_bit_cast(int, v[1]);
+        x[1] = tag;
+        x[3] = tag;
     }
-    x[1] = tag;
-    x[3] = tag;
     return x;
+}
+template <typename T> __device__ __forceinline__ bool chunk_at_ep(const I4 x, unsigned ep) {
+    if constexpr (sizeof(T) == 8)
+        return (((unsigned)x[0] & 3u) == (ep & 3u)) && (((unsigned)x[2] & 3u) == (ep & 3u));
+    else
+        return ((unsigned)x[1] >> 1) == ep && ((unsigned)x[3] >> 1) == ep;
+}
+template <typename T> __device__ __forceinline__ int chunk_bad(const I4 x) {
+    if constexpr (sizeof(T) == 8)
+        return (((unsigned)x[0] | (unsigned)x[2]) >> 2) & 1;
+    else
+        return x[1] & 1;
 }
 
 // NQ: producers polled per pass, the grid rounded up to 4 / 8 / 16 (surplus slots
@@ -278,9 +304,9 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
             }
             const uint32_t off = (uint32_t)(k & 1) * (uint32_t)nwg * kGatherRow + my_row;
             if (xl)  // one XCC: plain store, the line stays in its L2
-                __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(val, ((k + 1) << 1) | bad), rs, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(val, k + 1, bad), rs, off, 0, 0);
             else
-                __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(val, ((k + 1) << 1) | bad), rs, off, 0,
+                __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(val, k + 1, bad), rs, off, 0,
                                                        16 /* sc1 */);
         }
     };
@@ -306,7 +332,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
                 bool ok = true;
 #pragma unroll
                 for (int q = 0; q < NQ; ++q)
-                    ok &= ((unsigned)x[q][1] >> 1) == ep && ((unsigned)x[q][3] >> 1) == ep;
+                    ok &= chunk_at_ep<T>(x[q], ep);
 #if defined(OTF_GATHER_ABLATE) && (OTF_GATHER_ABLATE & 1)
                 ok = true;  // diagnostic: one load pass, no wait for the producers
 #endif
@@ -327,7 +353,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
                     chunk_values<T>(x[q], v);
 #pragma unroll
                     for (int c = 0; c < CPC; ++c) sv[c] += v[c];
-                    fl |= x[q][1] & 1;
+                    fl |= chunk_bad<T>(x[q]);
                 }
             }
 #pragma unroll
@@ -527,500 +553,6 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
     }
 }
 
-// ============================================================================
-// Two-hop form (r03): reduce-scatter + all-gather inside the team's XCC.
-//
-// The one-hop gather above makes every workgroup read every producer's partials of all
-// columns: nwg x 8 KB per workgroup per iteration through the CU's 64 B/clk port, so
-// spreading the rows over more workgroups (less VALU per workgroup) costs as much in
-// gather bandwidth as it saves.  Here the column partials go to REDUCERS (workgroup j
-// owns chunks [j CPR, (j + 1) CPR)): one wave polls them from the nwg producers, sums
-// them in producer order, forms v = b / S for its columns, POT's break test on them and
-// its share of the marginal error, and publishes the v chunks; every workgroup then
-// gathers one chunk per thread.  Two L2-local hops instead of one, but each moves
-// 1 / nwg of the bytes, so the rows spread over 16 - 32 workgroups (R = 4 or 2 rows per
-// wave for float64: 2 - 4x less VALU per iteration than R = 8).
-//
-// Tags of the v chunks of S[k] (epoch k + 1, slot k & 1): bit 0 = a producer's u of
-// iteration k - 1 was not finite (-> break at k - 1), bit 1 = S[k] has a zero or v a
-// non-finite value (-> break at k).  The error chunk (index CPR of a reducer) carries the
-// reducer's terms of the marginal error of iterate k - 1 (v(k - 1) S[k] - b) when k - 1
-// is a check iteration.  Every workgroup sums the nwg error terms in reducer order, so all
-// take POT's decisions at the same iteration, bitwise reproducible as the one-hop form.
-// Slot reuse: a producer writes slot k & 1 again for S[k + 2] after gathering the v
-// chunks of S[k + 1], which every reducer published after reading its S[k + 1] partials,
-// after (program order) reading those of S[k]; the v-chunk slots the same way round.
-// ============================================================================
-constexpr int kG2MaxWG = 32;
-constexpr uint32_t kG2BStride = 1280;  // per reducer: <= 64 v chunks + the error chunk (256-B multiple)
-
-template <typename T> struct G2Shape {
-    int nwg, cpr, kq;
-};
-template <typename T> G2Shape<T> g2_shape(int64_t n, int R) {
-    using Cf = GatherCfg<T>;
-    G2Shape<T> g{};
-    g.nwg = (int)((n + 8 * R - 1) / (8 * R));
-    int per = (Cf::NCH + g.nwg - 1) / (g.nwg > 0 ? g.nwg : 1);
-    int cpr = 1;
-    while (cpr < per) cpr <<= 1;
-    g.cpr = cpr;
-    g.kq = (g.nwg * cpr + kWave - 1) / kWave;  // reducer loads per lane
-    return g;
-}
-
-template <typename T, typename CT, typename TP, int R, int KQ>
-__global__ __launch_bounds__(512) void sk_gather2_kernel(SkGatherArgs<T> p, int CPR, uint32_t off_b) {
-    using Cf = GatherCfg<T>;
-    constexpr int G = Cf::G, VEC = Cf::VEC, NW = Cf::NW, TR = NW * R;
-    constexpr int CPC = Cf::CPC, NCH = Cf::NCH;
-    constexpr int RSH = R == 16 ? 2 : R == 8 ? 3 : R == 4 ? 4 : 5;
-    using V = typename Vec<T>::type;
-    using VP = __attribute__((ext_vector_type(VEC))) TP;
-    __shared__ __attribute__((aligned(16))) T colbuf[NW][Cf::C];
-    __shared__ __attribute__((aligned(16))) T vcur[Cf::C];
-    __shared__ __attribute__((aligned(16))) T vhist[2][Cf::C];
-    __shared__ T uhist[2][TR];
-    __shared__ T s_err;
-    // raised flags hold the key of the step that raised them (keys only grow): [0] this
-    // workgroup's u not finite, [1] producer break flag, [2] stall, [3] v break flag,
-    // [4] reducer stall
-    __shared__ int s_ep[5];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int nwg = p.nwg, n_ = p.n, m_ = p.m;
-    auto row_in = [&](int r) -> bool { return r < n_; };
-    auto col_in = [&](int c) -> bool { return c < m_; };
-    unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.reg_ticks;
-    // team registration (as the one-hop form): the first XCC whose first nwg registrants
-    // are resident claims the solve; this form always runs as one XCC team
-    int wgi;
-    {
-        __shared__ int s_team[2];
-        const int xcd = xcc_id();
-        if (tid == 0) {
-            const int slot = __hip_atomic_fetch_add(p.team + xcd * 64, 1, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-            int keep = slot < nwg ? 1 : 0;
-            if (keep) {
-                for (;;) {
-                    if (load_agent(&p.info->stalled)) {
-                        keep = 0;
-                        break;
-                    }
-                    const int claim = load_agent(p.team + 8 * 64);
-                    if (claim != 0) {
-                        keep = claim == xcd + 1;
-                        break;
-                    }
-                    if (load_agent(p.team + xcd * 64) >= nwg && slot == 0) {
-                        int expected = 0;
-                        __hip_atomic_compare_exchange_strong(p.team + 8 * 64, &expected, xcd + 1, __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    if (__builtin_amdgcn_s_memrealtime() > deadline) {
-                        keep = 0;
-                        store_wt(&p.info->stalled, 1);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            s_team[0] = keep;
-            s_team[1] = slot;
-        }
-        __syncthreads();
-        if (!s_team[0]) return;
-        wgi = s_team[1];
-        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
-    }
-    const bool lead = (wgi == 0 && tid == 0);
-    const int row0 = wgi * TR + w * R;
-
-    const double unit = exp_unit<T>();
-    double cinv = 1.0;
-    if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
-    const T ks = (T)(-unit / p.reg * cinv);
-
-    int colc[G];
-    bool cok[G][VEC];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const int c0 = (lane + kWave * g) * VEC;
-        colc[g] = col_in(c0) ? c0 : 0;
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) cok[g][k] = col_in(c0 + k);
-    }
-    T kv[R][G][VEC];
-    {
-        const CT* crow = (const CT*)p.C + (int64_t)row0 * p.ldc;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const CT* src = row_in(row0 + r) ? crow : (const CT*)p.C;
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const V c = load_cost<T>(src + colc[g]);
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
-            }
-            crow += p.ldc;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const bool rok = row_in(row0 + r);
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int k = 0; k < VEC; ++k)
-                    kv[r][g][k] = (rok && cok[g][k]) ? fast_exp(kv[r][g][k] * ks) : (T)0;
-        }
-    }
-    const int myrow = lane >> RSH;
-    const T ia_mine = (T)1 / p.a[row_in(row0 + myrow) ? row0 + myrow : n_ - 1];
-    const T u0 = (T)1 / (T)n_, v0 = (T)1 / (T)m_;
-    if (tid < 5) s_ep[tid] = -1;
-    for (int q = tid; q < Cf::C; q += blockDim.x) vhist[0][q] = vhist[1][q] = v0;
-    if (tid < TR) uhist[0][tid] = uhist[1][tid] = u0;
-
-    const __amdgpu_buffer_rsrc_t rs = sums_rsrc(p.gran);
-    // reducer lanes (wave 0): chunk rc of this workgroup's range, producers rq + LPC k
-    const int LPC = kWave / CPR;
-    const int r_cc = lane & (CPR - 1), r_q = lane / CPR;
-    const int r_ch = wgi * CPR + r_cc;
-    const bool r_ok = r_ch < NCH;
-    T rbv[CPC];
-#pragma unroll
-    for (int c = 0; c < CPC; ++c) {
-        const int col = r_ch * CPC + c;
-        rbv[c] = (r_ok && col_in(col)) ? p.b[col] : (T)0;
-    }
-    const int nred = (NCH + CPR - 1) / CPR;  // reducers holding chunks
-
-    // partials of S[k] = K_tile^T wr, epoch k + 1, slot k & 1; bad = u not finite here
-    auto publish = [&](const T (&wr)[R], int k, int bad_local) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            V acc;
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) {
-                T sacc = 0;
-#pragma unroll
-                for (int r = 0; r < R; ++r) sacc += kv[r][g][q] * wr[r];
-                acc[q] = sacc;
-            }
-            *reinterpret_cast<V*>(&colbuf[w][(lane + kWave * g) * VEC]) = acc;
-        }
-        if (bad_local) s_ep[0] = k;
-        __syncthreads();
-        const int bad = s_ep[0] == k ? 1 : 0;
-        if (tid < NCH) {
-            T val[CPC];
-#pragma unroll
-            for (int c = 0; c < CPC; ++c) {
-                T sacc = colbuf[0][tid * CPC + c];
-#pragma unroll
-                for (int ww = 1; ww < NW; ++ww) sacc += colbuf[ww][tid * CPC + c];
-                val[c] = sacc;
-            }
-            const uint32_t off = ((uint32_t)(k & 1) * (uint32_t)nwg + (uint32_t)wgi) * kGatherRow + (uint32_t)tid * 16;
-            __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(val, ((k + 1) << 2) | bad), rs, off, 0, 0);
-        }
-    };
-    // reducer (wave 0): S[k] of this workgroup's chunks from the nwg producers (producer
-    // order), v = b / S[k], flags, and (need) the error terms of iterate k - 1 against
-    // v(k - 1) = vprev; publishes the v chunks and the error chunk, epoch k + 1.
-    // Returns false on a stall.
-    auto reduce = [&](int k, bool need, const T* vprev) -> bool {
-        const unsigned ep = (unsigned)(k + 1);
-        I4 x[KQ];
-        unsigned pend = 0;
-#pragma unroll
-        for (int q = 0; q < KQ; ++q) {
-            x[q] = I4{0, 0, 0, 0};
-            if (r_ok && r_q + LPC * q < nwg) pend |= 1u << q;
-        }
-        const uint32_t base = (uint32_t)(k & 1) * (uint32_t)nwg * kGatherRow + (uint32_t)r_ch * 16;
-        bool ok = true;
-        for (;;) {
-#pragma unroll
-            for (int q = 0; q < KQ; ++q)
-                if (pend & (1u << q))
-                    x[q] = gload(rs, base + (uint32_t)(r_q + LPC * q) * kGatherRow);
-#pragma unroll
-            for (int q = 0; q < KQ; ++q)
-                if ((pend & (1u << q)) && ((unsigned)x[q][1] >> 2) == ep && ((unsigned)x[q][3] >> 2) == ep)
-                    pend &= ~(1u << q);
-            if (!__any(pend != 0)) break;
-            if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        T sv[CPC];
-        int fl = 0;
-#pragma unroll
-        for (int c = 0; c < CPC; ++c) sv[c] = 0;
-#pragma unroll
-        for (int q = 0; q < KQ; ++q)
-            if (r_ok && r_q + LPC * q < nwg) {
-                T v[CPC];
-                chunk_values<T>(x[q], v);
-#pragma unroll
-                for (int c = 0; c < CPC; ++c) sv[c] += v[c];
-                fl |= x[q][1] & 1;
-            }
-        // lanes of one chunk: offsets CPR, 2 CPR, ..., 32 (uniform, static DPP)
-#pragma unroll
-        for (int c = 0; c < CPC; ++c) {
-            if (CPR <= 1) sv[c] += wave_xor<T, 1>(sv[c]);
-            if (CPR <= 2) sv[c] += wave_xor<T, 2>(sv[c]);
-            if (CPR <= 4) sv[c] += wave_xor<T, 4>(sv[c]);
-            if (CPR <= 8) sv[c] += wave_xor<T, 8>(sv[c]);
-            if (CPR <= 16) sv[c] += wave_xor<T, 16>(sv[c]);
-            if (CPR <= 32) sv[c] += wave_xor<T, 32>(sv[c]);
-        }
-        const int pbad = __any(fl) ? 1 : 0;
-        T vn[CPC];
-        int vb = 0;
-        T term = 0;
-#pragma unroll
-        for (int c = 0; c < CPC; ++c) {
-            const int col = r_ch * CPC + c;
-            const bool cin = r_ok && col_in(col);
-            const T val = rbv[c] / sv[c];
-            vb |= (cin && (sv[c] == (T)0 || !finite_val(val))) ? 1 : 0;
-            vn[c] = cin ? val : (T)0;
-            if (need && cin) {
-                const T rr = vprev[col] * sv[c] - rbv[c];
-                term += rr * rr;
-            }
-        }
-        const int vbad = __any(vb) ? 2 : 0;
-        const int tag = ((int)ep << 2) | pbad | vbad;
-        const uint32_t ob = off_b + ((uint32_t)(k & 1) * (uint32_t)nwg + (uint32_t)wgi) * kG2BStride;
-        if (lane < CPR && r_ok) __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(vn, tag), rs, ob + (uint32_t)lane * 16, 0, 0);
-        if (need) {
-            // lanes of one chunk hold the same term: one copy per chunk, then the wave sum
-            term = lane < CPR ? term : (T)0;
-            term = wave_sum<T>(term);
-            if (lane == 0 && wgi < nred) {
-                T ev[CPC];
-#pragma unroll
-                for (int c = 0; c < CPC; ++c) ev[c] = c == 0 ? term : (T)0;
-                __builtin_amdgcn_raw_buffer_store_b128(make_chunk<T>(ev, tag), rs, ob + (uint32_t)CPR * 16, 0, 0);
-            }
-        }
-        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
-        return ok;
-    };
-    // hop B: v of S[k] (epoch k + 1) into vcur; the summed error terms into s_err when
-    // need.  Returns bit 0 producer break, 1 stall, 2 v break.
-    auto gather = [&](int k, bool need) -> int {
-        const unsigned ep = (unsigned)(k + 1);
-        int fl = 0;
-        const uint32_t sb = off_b + (uint32_t)(k & 1) * (uint32_t)nwg * kG2BStride;
-        if (tid < NCH) {
-            const uint32_t off = sb + (uint32_t)(tid / CPR) * kG2BStride + (uint32_t)(tid & (CPR - 1)) * 16;
-            I4 x;
-            for (;;) {
-                x = gload(rs, off);
-                if (((unsigned)x[1] >> 2) == ep && ((unsigned)x[3] >> 2) == ep) break;
-                if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; x = I4{0, 0, 0, 0}; break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            fl |= (x[1] & 1) | ((x[1] & 2) << 1);  // tag bit 1 (v break) -> bit 2
-            T v[CPC];
-            chunk_values<T>(x, v);
-#pragma unroll
-            for (int c = 0; c < CPC; ++c) vcur[tid * CPC + c] = v[c];
-        }
-        if (need && w == NW - 1) {
-            // the last wave sums the reducers' error terms in reducer order
-            T e = 0;
-            if (lane < nred) {
-                const uint32_t off = sb + (uint32_t)lane * kG2BStride + (uint32_t)CPR * 16;
-                I4 x;
-                for (;;) {
-                    x = gload(rs, off);
-                    if (((unsigned)x[1] >> 2) == ep && ((unsigned)x[3] >> 2) == ep) break;
-                    if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; x = I4{0, 0, 0, 0}; break; }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                T v[CPC];
-                chunk_values<T>(x, v);
-                e = v[0];
-            }
-            e = wave_sum<T>(e);
-            if (lane == 0) s_err = e;
-        }
-        if (fl & 1) s_ep[1] = k;
-        if (fl & 2) s_ep[2] = k;
-        if (fl & 4) s_ep[3] = k;  // (bit 1 of the tag is bit 2 of fl: v break)
-        __syncthreads();
-        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
-        return (s_ep[1] == k ? 1 : 0) | (s_ep[2] == k ? 2 : 0) | (s_ep[3] == k ? 4 : 0) |
-               (s_ep[4] == k ? 2 : 0);
-    };
-    auto to_err = [&](T e) -> double { return p.err_squared ? (double)e : sqrt((double)e); };
-    auto stop_ok = [&](double err) -> bool { return p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr); };
-
-    // ---- prologue: S[0] = K^T u0, its v chunks (epoch 1)
-    {
-        T wr[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) wr[r] = row_in(row0 + r) ? u0 : (T)0;
-        publish(wr, 0, 0);
-        if (w == 0 && !reduce(0, false, vhist[0])) s_ep[4] = 0;
-    }
-    int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
-    bool done = false;
-    for (int it = 0; it < p.max_iter; ++it) {
-        OTF_STAMP(it, 0);
-        const bool check = it >= 1 && ((it - 1) % p.check_every) == 0;
-        const int fl = gather(it, check);
-        OTF_STAMP(it, 1);
-        if (fl & 2) { status = OTF_SK_TIMEOUT; done = true; break; }
-        if (fl & 1) {  // u of iteration it - 1 not finite somewhere: revert to it - 2
-            last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
-            done = true;
-            break;
-        }
-        if (check) {
-            const double err = to_err(s_err);
-            if (lead) p.errlog[(it - 1) / p.check_every] = err;
-            n_err = (it - 1) / p.check_every + 1;
-            if (stop_ok(err)) {
-                last_good = it - 1; niter = it - 1; status = OTF_SK_CONVERGED;
-                done = true;
-                break;
-            }
-        }
-        if (fl & 4) {  // S[it] has a zero or v(it) is not finite: revert to it - 1
-            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
-            done = true;
-            break;
-        }
-        T vn[G][VEC];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const V t = *reinterpret_cast<const V*>(&vcur[(lane + kWave * g) * VEC]);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) vn[g][k] = t[k];
-        }
-        OTF_STAMP(it, 2);
-        T rp[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            T acc = 0;
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) acc += kv[r][g][k] * vn[g][k];
-            rp[r] = acc;
-        }
-        const int slot = it & 1;
-        T un[R];
-        int badu = 0;
-        {
-            const T tot = wave_row_totals<T, R>(rp, lane);
-            T um = (T)1 / (tot * ia_mine);
-            if (!row_in(row0 + myrow)) um = 0;
-            badu = __any(!finite_val(um)) ? 1 : 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                un[r] = map_words(um, [&](unsigned wd) { return (unsigned)__builtin_amdgcn_readlane((int)wd, r << RSH); });
-            if ((lane & ((1 << RSH) - 1)) == 0) uhist[slot][w * R + myrow] = um;
-        }
-        if (w == 0) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                V vv;
-#pragma unroll
-                for (int q = 0; q < VEC; ++q) vv[q] = vn[g][q];
-                *reinterpret_cast<V*>(&vhist[slot][(lane + kWave * g) * VEC]) = vv;
-            }
-        }
-        OTF_STAMP(it, 3);
-        publish(un, it + 1, badu);
-        OTF_STAMP(it, 4);
-        // S[it + 1]: the error of iterate it is checked at it + 1 when it % check_every == 0
-        if (w == 0 && !reduce(it + 1, (it % p.check_every) == 0, vhist[slot])) s_ep[4] = it + 1;
-        OTF_STAMP(it, 5);
-    }
-    if (!done && p.max_iter > 0) {
-        const int it = p.max_iter - 1;
-        const bool check = (it % p.check_every) == 0;
-        const int fl = gather(p.max_iter, check);
-        if (fl & 2) {
-            status = OTF_SK_TIMEOUT;
-        } else if (fl & 1) {
-            last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
-        } else {
-            last_good = it; niter = it;
-            if (check) {
-                const double err = to_err(s_err);
-                if (lead) p.errlog[it / p.check_every] = err;
-                n_err = it / p.check_every + 1;
-                if (stop_ok(err)) status = OTF_SK_CONVERGED;
-            }
-        }
-    }
-
-    __syncthreads();
-    const int hs = last_good & 1;
-    T uo[R], vo[G][VEC];
-#pragma unroll
-    for (int r = 0; r < R; ++r) uo[r] = last_good < 0 ? u0 : uhist[hs][w * R + r];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int k = 0; k < VEC; ++k)
-            vo[g][k] = last_good < 0 ? v0 : vhist[hs][(lane + kWave * g) * VEC + k];
-    if (lane < R && row_in(row0 + lane)) {
-        T mine = uo[0];
-#pragma unroll
-        for (int r = 1; r < R; ++r) if (lane == r) mine = uo[r];
-        p.u_out[row0 + lane] = mine;
-    }
-    if (wgi == 0 && w == 0) {
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int k = 0; k < VEC; ++k)
-                if (cok[g][k]) p.v_out[colc[g] + k] = vo[g][k];
-    }
-    if (p.P) {
-        TP* P = (TP*)p.P;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (!row_in(row0 + r)) break;
-            TP* prow = P + (int64_t)(row0 + r) * p.ldp;
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const int c0 = (lane + kWave * g) * VEC;
-                if (!col_in(c0)) continue;
-                VP o;
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) o[k] = (TP)(uo[r] * kv[r][g][k] * vo[g][k]);
-                if (c0 + VEC <= m_) {
-                    *reinterpret_cast<VP*>(prow + c0) = o;
-                } else {
-#pragma unroll
-                    for (int k = 0; k < VEC; ++k)
-                        if (col_in(c0 + k)) prow[c0 + k] = o[k];
-                }
-            }
-        }
-    }
-    if (status == OTF_SK_TIMEOUT && tid == 0) store_wt(&p.info->stalled, 1);
-    if (lead) {
-        p.info->last_good = last_good;
-        p.info->niter = niter;
-        p.info->status = status;
-        p.info->break_iter = brk;
-        p.info->n_err = n_err;
-        p.info->engine = OTF_ENGINE_GATHER;
-        p.info->stop = 1;
-    }
-}
-
 template <typename T, typename CT, typename TP, int NQ>
 hipError_t launch_gather_q(int grid, SkGatherArgs<T>& p, hipStream_t s) {
     void* args[] = {&p};
@@ -1064,40 +596,6 @@ template <typename T> int64_t gather_grid(int64_t n) {
     return (n + GatherCfg<T>::TR - 1) / GatherCfg<T>::TR;
 }
 
-// Two-hop form: rows per wave (OTF_GATHER2_R, default 4), on (OTF_GATHER2, default 1)
-inline int gather2_rows() {
-    const char* e = getenv("OTF_GATHER2_R");
-    const int r = e ? atoi(e) : 4;
-    return r == 2 ? 2 : 4;
-}
-inline bool gather2_enabled() {
-    const char* e = getenv("OTF_GATHER2");
-    return e ? atoi(e) != 0 : true;
-}
-template <typename T> bool gather2_fits(int64_t n, int R) {
-    const G2Shape<T> g = g2_shape<T>(n, R);
-    return g.nwg >= 1 && g.nwg <= kG2MaxWG && g.cpr <= kWave;
-}
-
-template <typename T, typename CT, typename TP, int R, int KQ>
-hipError_t launch_gather2_t(SkGatherArgs<T>& p, int cpr, uint32_t off_b, hipStream_t s) {
-    const void* k = (const void*)sk_gather2_kernel<T, CT, TP, R, KQ>;
-    int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
-    if (e != hipSuccess) return e;
-    const int grid = 8 * p.nwg;  // one team of nwg per XCC, the first complete one claims
-    if (per_cu < 1 || grid > per_cu * device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
-    void* args[] = {&p, &cpr, &off_b};
-    return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
-}
-template <typename T, typename CT, typename TP, int R>
-hipError_t launch_gather2_r(SkGatherArgs<T>& p, const G2Shape<T>& g, uint32_t off_b, hipStream_t s) {
-    // loads per reducer lane: nwg * cpr / 64 lies in [NCH / 64, 2 NCH / 64]
-    constexpr int KLO = GatherCfg<T>::NCH / kWave;
-    if (g.kq <= KLO) return launch_gather2_t<T, CT, TP, R, KLO>(p, g.cpr, off_b, s);
-    return launch_gather2_t<T, CT, TP, R, 2 * KLO>(p, g.cpr, off_b, s);
-}
-
 }  // namespace
 
 template <typename T> bool gather_supported(int64_t n, int64_t m) {
@@ -1106,13 +604,8 @@ template <typename T> bool gather_supported(int64_t n, int64_t m) {
 
 constexpr size_t kTeamBytes = 9 * 256;  // 8 XCC registration counters + the claim word
 
-// one-hop: [2 slots][grid][kGatherRow]; two-hop: [2][<= 32 producers][kGatherRow] + the v
-// chunks [2][<= 32 reducers][kG2BStride]
 template <typename T> size_t gather_region_bytes(int64_t n, int64_t m) {
-    if (!gather_supported<T>(n, m)) return 0;
-    const size_t one = 2 * (size_t)gather_grid<T>(n) * kGatherRow;
-    const size_t two = 2 * (size_t)kG2MaxWG * kGatherRow + 2 * (size_t)kG2MaxWG * kG2BStride;
-    return kTeamBytes + (one > two ? one : two);
+    return gather_supported<T>(n, m) ? kTeamBytes + 2 * (size_t)gather_grid<T>(n) * kGatherRow : 0;
 }
 
 // OTF_GATHER_TEAM=0: one workgroup per row tile anywhere on the chip, write-through hops
@@ -1152,22 +645,6 @@ hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, co
     p.reg_ticks = reg_stall_ticks();
     hipError_t e = hipMemsetAsync(region, 0, gather_region_bytes<T>(n, m), s);
     if (e != hipSuccess) return e;
-    // two-hop form: rows spread over 2 - 4x the workgroups, one XCC team
-    const int R2 = gather2_rows();
-    if (gather2_enabled() && gather_team_mode() && gather2_fits<T>(n, R2)) {
-        const G2Shape<T> g = g2_shape<T>(n, R2);
-        SkGatherArgs<T> q = p;
-        q.nwg = g.nwg;
-        q.team_mode = 1;
-        const uint32_t off_b = 2u * (uint32_t)kG2MaxWG * kGatherRow;
-        const bool f64p = P_out && P_dtype == OTF_F64;
-        if (R2 == 2)
-            e = f64p ? launch_gather2_r<T, CT, double, 2>(q, g, off_b, s) : launch_gather2_r<T, CT, float, 2>(q, g, off_b, s);
-        else
-            e = f64p ? launch_gather2_r<T, CT, double, 4>(q, g, off_b, s) : launch_gather2_r<T, CT, float, 4>(q, g, off_b, s);
-        if (e != hipErrorCooperativeLaunchTooLarge) return e;
-        (void)hipGetLastError();
-    }
     const int grid = (int)gather_grid<T>(n);
     p.nwg = grid;
     p.team_mode = gather_team_mode();

@@ -21,19 +21,6 @@ def _t(x, dev, dt=None):
     return torch.as_tensor(np.asarray(x), device=dev, dtype=dt)
 
 
-@pytest.fixture(params=["one_hop", "two_hop_r4", "two_hop_r2"])
-def form(request, monkeypatch):
-    """The one-hop gather (every workgroup reads every producer) and the two-hop form
-    (reducers + v chunks, rows spread over 2 - 4x the workgroups; shapes it does not
-    take run the one-hop form)."""
-    if request.param == "one_hop":
-        monkeypatch.setenv("OTF_GATHER2", "0")
-    else:
-        monkeypatch.setenv("OTF_GATHER2", "1")
-        monkeypatch.setenv("OTF_GATHER2_R", request.param[-1])
-    return request.param
-
-
 def test_config2_takes_gather_and_matches_golden(golden, orc, dev):
     """AUTO picks the gather engine for the config-2 feature plan; F2 golden (reference
     get_feature_coupling_pot, 2000 iterations at eps 1e-2) to 1e-9, and the same plan
@@ -61,7 +48,7 @@ def test_config2_takes_gather_and_matches_golden(golden, orc, dev):
                                     (960, 512, torch.float64), (1023, 511, torch.float64),
                                     (129, 64, torch.float32), (2047, 512, torch.float32),
                                     (256, 3, torch.float32), (5, 500, torch.float64)])
-def test_gather_grid_sizes_vs_oracle(orc, dev, n, m, dt, form):
+def test_gather_grid_sizes_vs_oracle(orc, dev, n, m, dt):
     """1..16 workgroups (ragged last tile), ragged last chunk, non-uniform marginals."""
     from otfuse import ops
     rng = np.random.default_rng(n * 7 + m)
@@ -80,7 +67,7 @@ def test_gather_grid_sizes_vs_oracle(orc, dev, n, m, dt, form):
 
 
 @pytest.mark.parametrize("n,m,dt", [(512, 512, torch.float64), (2048, 500, torch.float32)])
-def test_gather_is_bitwise_reproducible(dev, n, m, dt, form):
+def test_gather_is_bitwise_reproducible(dev, n, m, dt):
     """Every workgroup adds the partials in workgroup order: same bits every run."""
     from otfuse import ops
     g = torch.Generator(device=dev).manual_seed(n)
@@ -94,7 +81,7 @@ def test_gather_is_bitwise_reproducible(dev, n, m, dt, form):
     assert torch.equal(outs[0].u, outs[2].u) and torch.equal(outs[0].v, outs[2].v)
 
 
-def test_gather_break_mid_solve_matches_oracle(orc, dev, form):
+def test_gather_break_mid_solve_matches_oracle(orc, dev):
     """A numerical break after some iterations (u overflows at a tiny reg) reverts to the
     same iterate as POT / the oracle."""
     from otfuse import ops
@@ -147,10 +134,8 @@ def test_two_gather_solves_on_two_streams(dev):
 def test_gather_team_mode_agrees_bitwise(dev, monkeypatch):
     """XCC team mode (8 x nwg workgroups launched, the first complete XCC team solves with
     plain stores inside its L2) and the one-workgroup-per-tile write-through launch add
-    the partials in the same order: identical bits, config-2 shape, float64 (one-hop
-    form: the two-hop form always runs as an XCC team)."""
+    the partials in the same order: identical bits, config-2 shape, float64."""
     from otfuse import ops
-    monkeypatch.setenv("OTF_GATHER2", "0")
     n = m = 512
     g = torch.Generator(device=dev).manual_seed(21)
     C = torch.rand(n, m, device=dev, generator=g, dtype=torch.float64)
@@ -160,36 +145,3 @@ def test_gather_team_mode_agrees_bitwise(dev, monkeypatch):
     r0 = ops.sinkhorn(a, a, C, 0.02, max_iter=500, stop_thr=0.0, engine="gather")
     assert r1.info()["engine_name"] == r0.info()["engine_name"] == "gather"
     assert torch.equal(r0.plan, r1.plan) and torch.equal(r0.u, r1.u) and torch.equal(r0.v, r1.v)
-
-
-@pytest.mark.parametrize("R", ["4", "2"])
-@pytest.mark.parametrize("n,m,dt,eps,iters,thr", [
-    (512, 512, torch.float64, 0.02, 500, 0.0), (512, 512, torch.float64, 1e-2, 2000, 1e-9),
-    (1000, 400, torch.float32, 0.05, 300, 0.0), (300, 500, torch.float64, 0.1, 200, 1e-7)])
-def test_gather_two_hop_matches_one_hop(orc, dev, monkeypatch, R, n, m, dt, eps, iters, thr):
-    """Two-hop form vs one-hop form (and the oracle): the same POT iterations, stop
-    decisions and error log; the plan agrees to rounding (the column sums are added over
-    a different split of the rows)."""
-    from otfuse import ops
-    rng = np.random.default_rng(n + m)
-    C = rng.random((n, m))
-    a = rng.random(n) + 0.5
-    a /= a.sum()
-    b = rng.random(m) + 0.5
-    b /= b.sum()
-    args = (_t(a, dev, dt), _t(b, dev, dt), _t(C, dev, dt), eps)
-    monkeypatch.setenv("OTF_GATHER2", "0")
-    r1 = ops.sinkhorn(*args, max_iter=iters, stop_thr=thr, engine="gather")
-    monkeypatch.setenv("OTF_GATHER2", "1")
-    monkeypatch.setenv("OTF_GATHER2_R", R)
-    r2 = ops.sinkhorn(*args, max_iter=iters, stop_thr=thr, engine="gather")
-    i1, i2 = r1.info(), r2.info()
-    assert i2["engine_name"] == "gather"
-    for k in ("niter", "status_name", "n_err", "break_iter"):
-        assert i1[k] == i2[k], k
-    tol = 1e-4 if dt == torch.float32 else 1e-11
-    np.testing.assert_allclose(i2["err"], i1["err"], rtol=tol * 10, atol=1e-300)
-    assert nrel(r2.plan.cpu().numpy(), r1.plan.cpu().numpy()) < tol
-    P_r, *_, info_r = orc.sinkhorn_knopp(a, b, C, eps, iters, thr)
-    assert i2["niter"] == info_r["niter"]
-    assert nrel(r2.plan.cpu().numpy(), P_r) < (1e-4 if dt == torch.float32 else 1e-9)
