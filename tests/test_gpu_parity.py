@@ -70,6 +70,7 @@ def test_cost_ring_kernel_matches_register_kernel(ops, orc, dev, monkeypatch, n,
     Y = (torch.randn(m, d, device=dev, generator=g) * 0.7 + 0.2).to(in_dt)
     monkeypatch.setenv("OTF_COST_RING", "0")
     monkeypatch.setenv("OTF_COST_WS", "0")
+    monkeypatch.setenv("OTF_COST_MFMA16", "0")  # the 32x32x16 register-staged kernel
     C0, mx0, u0 = ops.pairwise_cost_ex(X, Y, out_dtype=out_dt)
     monkeypatch.setenv(switch, "1")
     C1, mx1, u1 = ops.pairwise_cost_ex(X, Y, out_dtype=out_dt)
