@@ -895,22 +895,6 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
         syy[c] = yy[gj];
     }
 
-    // L2 prefetch two stages ahead: the register-staged load of stage kt + 1 is the only
-    // one in flight while stage kt computes (64 KB a stage fills the LDS twice over), so
-    // it pays the Infinity-Cache latency whenever the panel is not yet in this XCD's L2.
-    // One dword per 128-B line of the stages kt + 2, kt + 3 (a line holds two 64-B
-    // stage slices of a row): thread (row r, chunk q) touches image q of rows r, r + 128;
-    // the value is folded into pf two stages later (its wait is then long satisfied).
-    const int pf_row = tid / GCPR, pf_img = tid % GCPR;
-    const _Float16* pf_base[NCH];
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const int row = pf_row + 128 * c;
-        const int gi = i0 + row < n ? i0 + row : n - 1, gj = j0 + row < m ? j0 + row : m - 1;
-        const _Float16* img = pf_img == 0 ? Xh : pf_img == 1 ? (NI == 2 ? Xl : Xh) : pf_img == 2 ? Yh : (NI == 2 ? Yl : Yh);
-        pf_base[c] = img + (int64_t)(pf_img < 2 ? gi : gj) * (pf_img < 2 ? ldxh : ldyh);
-    }
-    unsigned pf = 0, pf_acc = 0;
     OTF_CST(1);
     const int nk = kpad / GBK;
     gload(0);
@@ -926,15 +910,6 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
         if (kt + 1 < nk)
 #endif
             gload((kt + 1) * GBK);
-#if !(defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 8))
-        if ((kt & 1) == 0 && kt + 2 < nk) {
-            pf_acc ^= pf;
-            pf = 0;
-#pragma unroll
-            for (int c = 0; c < NCH; ++c)
-                pf ^= *reinterpret_cast<const unsigned*>(pf_base[c] + (kt + 2) * GBK);
-        }
-#endif
         f16x8 ah[4], al[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -972,7 +947,6 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
         __syncthreads();
     }
 
-    asm volatile("" ::"v"(pf_acc ^ pf));  // the prefetches are not dead code
     OTF_CST(2);
     const float os = store_scale ? store_scale[0] : 1.0f;
     // vector stores: whole tile, no diagonal in it, rows 16-B (fp32) / 8-B (fp16) aligned
