@@ -232,9 +232,11 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": algo_gbs / HBM_PEAK_GBS,
                     "traffic": traffic, "algorithmic_bytes_per_launch": iter_bytes * iters}
     # the C side takes 256 x 256 tiles when they need fewer rounds of resident workgroups
-    # (otf_cost.hip: N = 4096 -> cost_big_kernel); the profile names the one that ran
-    cost_kernel = ("cost_big_kernel" if fresh and "cost_big_kernel" in tj.get("kernels", {})
-                   else "cost_big_kernel" if N >= 4096 else "cost_split16_kernel")
+    # (otf_cost.hip: N = 4096 -> the 16x16x32 form cost_big16_kernel for fp32 storage,
+    # cost_big_kernel with OTF_COST_MFMA16=0)
+    mf16 = os.environ.get("OTF_COST_MFMA16", "1") != "0"
+    cost_kernel = (("cost_big16_kernel" if mf16 else "cost_big_kernel") if N >= 4096
+                   else "cost_split16_kernel")
     cost_flops = 2.0 * N * N * d
     cost_tflops = cost_flops / (cost_ms * 1e-3) / 1e12
 

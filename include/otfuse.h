@@ -372,12 +372,15 @@ int otf_plan_postprocess_apply(const void* T, int64_t d, int64_t d2, int64_t ldt
  * loss = 1 - mean_b cos(normalize(X_b), normalize(Y_b)) with torch's normalize /
  * cosine_similarity clamps; gx = dloss/dX, gy = dloss/dY (B x d float32).  X is
  * x_dtype OTF_F32 / OTF_BF16 / OTF_F16 (the encoder output as stored), Y float32.
- * keep = (ok == NULL || *ok) && loss finite; when keep is 0 the loss and both
- * gradients are exact zeros.  keep_out (device uint8, nullable) receives keep.
- * B <= 1024.                                                                      */
+ * keep = (ok == NULL || *ok) && (sk_info == NULL || the solve finished: status neither
+ * RUNNING nor TIMEOUT, stop set, not stalled) && loss finite; when keep is 0 the loss
+ * and both gradients are exact zeros.  sk_info (device, nullable) is the
+ * otf_sinkhorn_info of the solve whose plan made Y: the check runs in this launch.
+ * keep_out (device uint8, nullable) receives keep.  B <= 1024.                    */
 int otf_cosine_align(const void* X, int64_t ldx, int32_t x_dtype, const float* Y, int64_t ldy,
-                     int64_t B, int64_t d, const uint8_t* ok, float* loss, float* gx, int64_t ldgx,
-                     float* gy, int64_t ldgy, uint8_t* keep_out, otf_stream_t stream);
+                     int64_t B, int64_t d, const uint8_t* ok, const otf_sinkhorn_info* sk_info,
+                     float* loss, float* gx, int64_t ldgx, float* gy, int64_t ldgy, uint8_t* keep_out,
+                     otf_stream_t stream);
 
 /* Backward of ot_mri_from_pet = pet @ Tn^T under the alignment loss, one launch:
  * g_pet = (g_loss * gy + g_ot) @ Tn (B x d2), g_mri = g_loss * gx (B x d).  g_loss

@@ -242,6 +242,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 template <typename TX>
 __global__ __launch_bounds__(1024) void cosine_align_kernel(const TX* X, int64_t ldx, const float* Y,
                                                             int64_t ldy, int B, int d, const uint8_t* ok,
+                                                            const otf_sinkhorn_info* sk_info,
                                                             float* loss, float* gx, int64_t ldgx,
                                                             float* gy, int64_t ldgy, uint8_t* keep_out) {
     __shared__ float s_cos[1024];
@@ -277,7 +278,12 @@ __global__ __launch_bounds__(1024) void cosine_align_kernel(const TX* X, int64_t
         float sum = 0.f;
         for (int b = 0; b < B; ++b) sum += s_cos[b];   // fixed order
         const float L = 1.f - sum / (float)B;
-        const int keep = (ok == nullptr || ok[0] != 0) && finite_val(L);
+        // the solve that made the plan finished (final status, stop set, no stalled
+        // workgroup): checked here, not by extra launches on the caller's side
+        const bool solved = sk_info == nullptr ||
+                            (sk_info->status != OTF_SK_TIMEOUT && sk_info->status != OTF_SK_RUNNING &&
+                             sk_info->stop != 0 && sk_info->stalled == 0);
+        const int keep = (ok == nullptr || ok[0] != 0) && solved && finite_val(L);
         s_keep = keep;
         loss[0] = keep ? L : 0.f;
         if (keep_out) keep_out[0] = (uint8_t)keep;
@@ -600,8 +606,9 @@ int otf_gemm_f32(const float* A, int64_t sa0, int64_t sa1, const float* B, int64
 }
 
 int otf_cosine_align(const void* X, int64_t ldx, int32_t x_dtype, const float* Y, int64_t ldy,
-                     int64_t B, int64_t d, const uint8_t* ok, float* loss, float* gx, int64_t ldgx,
-                     float* gy, int64_t ldgy, uint8_t* keep_out, otf_stream_t stream) {
+                     int64_t B, int64_t d, const uint8_t* ok, const otf_sinkhorn_info* sk_info,
+                     float* loss, float* gx, int64_t ldgx, float* gy, int64_t ldgy, uint8_t* keep_out,
+                     otf_stream_t stream) {
     if (!X || !Y || !loss || !gx || !gy || B <= 0 || d <= 0 || ldx < d || ldy < d || ldgx < d ||
         ldgy < d)
         return OTF_EINVAL;
@@ -609,13 +616,13 @@ int otf_cosine_align(const void* X, int64_t ldx, int32_t x_dtype, const float* Y
     hipStream_t s = (hipStream_t)stream;
     if (x_dtype == OTF_F32)
         otf::cosine_align_kernel<float><<<1, 1024, 0, s>>>((const float*)X, ldx, Y, ldy, (int)B, (int)d, ok,
-                                                           loss, gx, ldgx, gy, ldgy, keep_out);
+                                                           sk_info, loss, gx, ldgx, gy, ldgy, keep_out);
     else if (x_dtype == OTF_BF16)
         otf::cosine_align_kernel<otf::bf16><<<1, 1024, 0, s>>>((const otf::bf16*)X, ldx, Y, ldy, (int)B,
-                                                               (int)d, ok, loss, gx, ldgx, gy, ldgy, keep_out);
+                                                               (int)d, ok, sk_info, loss, gx, ldgx, gy, ldgy, keep_out);
     else if (x_dtype == OTF_F16)
         otf::cosine_align_kernel<_Float16><<<1, 1024, 0, s>>>((const _Float16*)X, ldx, Y, ldy, (int)B,
-                                                              (int)d, ok, loss, gx, ldgx, gy, ldgy, keep_out);
+                                                              (int)d, ok, sk_info, loss, gx, ldgx, gy, ldgy, keep_out);
     else
         return OTF_EINVAL;
     OTF_HIP(hipGetLastError());

@@ -138,8 +138,8 @@ _SIGS = {
                                                   _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "otf_gemm_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
                                     ctypes.c_float, ctypes.c_float, _vp]),
-    "otf_cosine_align": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _i64,
-                                        _vp, _i64, _vp, _vp]),
+    "otf_cosine_align": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp,
+                                        _i64, _vp, _i64, _vp, _vp]),
     "otf_ot_align_backward": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64,
                                              _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "otf_cost_pairwise_f64_workspace_size": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64]),

@@ -54,20 +54,20 @@ class _OTAlignLoss(torch.autograd.Function):
     (otf_plan_postprocess_apply, one pass; else T is applied as given), the loss and
     both its gradients come from ONE workgroup (otf_cosine_align), and the backward is
     ONE launch (otf_ot_align_backward: G @ Tn and the loss scaling).  A non-finite loss
-    -- or ``ok`` false (a stalled solve, decided on the device) -- becomes a constant 0
+    -- or a solve that did not finish (its info words, read by the loss kernel) -- becomes a constant 0
     that sends no gradient to mri_fused / pet_fused, like the reference's swap for
     torch.tensor(0.0) at :724-725; the zeroing is a select in the kernels, never
     0 * NaN, and needs no host sync."""
 
     @staticmethod
-    def forward(ctx, mri, pet, T, ok, raw):
+    def forward(ctx, mri, pet, T, info, raw):
         ctx.set_materialize_grads(False)   # an unused ot_mri_from_pet sends None, not zeros
         if raw:
             ot, Tn = ops.plan_postprocess_apply(T, pet)
         else:
             Tn = T.float().contiguous()
             ot = ops.gemm_f32(pet.float(), Tn, transpose_b=True)
-        loss, gx, gy, keep = ops.cosine_align(mri.detach(), ot, ok)
+        loss, gx, gy, keep = ops.cosine_align(mri.detach(), ot, sk_info=info)
         ctx.save_for_backward(gx, gy, Tn, keep)
         ctx.dtypes = (mri.dtype, pet.dtype)
         ctx.mark_non_differentiable(Tn)
@@ -91,19 +91,14 @@ def ot_alignment_loss(mri_fused: torch.Tensor, pet_fused: torch.Tensor,
     gradient) without a host sync; so does the loss of a solve whose device barrier
     stalled (status timeout), instead of training on an invalid plan.
     """
-    ok = torch.ones((), dtype=torch.bool, device=mri_fused.device)
     if T_feature_pet2mri is None:
         plan, res = batch_feature_plan(mri_fused, pet_fused, eps, numItermax, stopThr)
-        info = res.info_dev
-        from . import _lib as L
-        # a finished solve: final status written (not running / timeout), stop set,
-        # no stalled workgroup
-        ok = ((info[3] != L.SK_TIMEOUT) & (info[3] != L.SK_RUNNING) & (info[0] != 0)
-              & (info[7] == 0))
-        ot_loss, ot_mri_from_pet, T = _OTAlignLoss.apply(mri_fused, pet_fused, plan, ok, True)
+        # the loss kernel checks that the solve finished (final status written, not
+        # running / timeout, stop set, no stalled workgroup) from the info words itself
+        ot_loss, ot_mri_from_pet, T = _OTAlignLoss.apply(mri_fused, pet_fused, plan, res.info_dev, True)
     else:
         ot_loss, ot_mri_from_pet, T = _OTAlignLoss.apply(mri_fused, pet_fused, T_feature_pet2mri,
-                                                         ok, False)
+                                                         None, False)
     return ot_loss, ot_mri_from_pet, T
 
 

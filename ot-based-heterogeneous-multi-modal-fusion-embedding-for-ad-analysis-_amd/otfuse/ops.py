@@ -421,12 +421,15 @@ def gemm_f32(A: torch.Tensor, B: torch.Tensor, transpose_b: bool = False) -> tor
     return out
 
 
-def cosine_align(X: torch.Tensor, Y: torch.Tensor, ok: torch.Tensor | None = None):
+def cosine_align(X: torch.Tensor, Y: torch.Tensor, ok: torch.Tensor | None = None,
+                 sk_info: torch.Tensor | None = None):
     """``1 - mean_b cos(X_b, Y_b)`` with torch's normalize / cosine_similarity clamps
     (cosine_loss, MRI_PET_OT_nojax.py:552-560) and its gradients, in ONE launch
     (otf_cosine_align).  X: (B, d) float32 / bfloat16 / float16 (read as stored), Y:
     (B, d) float32.  ``ok`` (device bool scalar, optional) and a non-finite loss give
-    an exact-zero loss and gradients (the NaN -> 0 swap of :724-725).
+    an exact-zero loss and gradients (the NaN -> 0 swap of :724-725); so does a solve
+    that did not finish when ``sk_info`` (the SinkhornResult's device info words) is
+    given -- checked inside the same launch.
     Returns ``(loss (0-dim float32), gx (B, d), gy (B, d), keep (uint8 scalar))``."""
     _dev(X, "X")
     _dev(Y, "Y")
@@ -450,8 +453,13 @@ def cosine_align(X: torch.Tensor, Y: torch.Tensor, ok: torch.Tensor | None = Non
     if ok is not None:
         ok = _dev(ok, "ok").to(torch.uint8).reshape(())
         okp = ok.data_ptr()
+    infop = None
+    if sk_info is not None:
+        if sk_info.dtype != torch.int32 or sk_info.numel() < L.INFO_INT32S or not sk_info.is_contiguous():
+            raise ValueError("sk_info must be a SinkhornResult's contiguous int32 info words")
+        infop = _dev(sk_info, "sk_info").data_ptr()
     L.check(L.lib().otf_cosine_align(X.data_ptr(), X.stride(0), _EMB_DT[X.dtype], Y.data_ptr(),
-                                     Y.stride(0), B, d, okp, loss.data_ptr(), gx.data_ptr(), d,
+                                     Y.stride(0), B, d, okp, infop, loss.data_ptr(), gx.data_ptr(), d,
                                      gy.data_ptr(), d, keep.data_ptr(), L.stream_handle(dev)),
             "otf_cosine_align")
     return loss, gx, gy, keep

@@ -50,6 +50,29 @@ def test_cosine_align_zeroes_nonfinite_and_not_ok(dev):
     assert int(keep) == 0 and float(L) == 0.0 and torch.count_nonzero(gx) == 0
 
 
+@pytest.mark.parametrize("status,stop,stalled,keep", [
+    ("SK_MAX_ITER", 1, 0, 1), ("SK_CONVERGED", 1, 0, 1), ("SK_NUMERICAL_BREAK", 1, 0, 1),
+    ("SK_TIMEOUT", 1, 1, 0), ("SK_RUNNING", 0, 0, 0), ("SK_MAX_ITER", 0, 0, 0), ("SK_MAX_ITER", 1, 1, 0)])
+def test_cosine_align_checks_the_solve_info(dev, status, stop, stalled, keep):
+    """The loss kernel reads the solve's info words (sk_info): only a finished solve --
+    final status, stop set, no stalled workgroup -- keeps the loss and its gradients."""
+    from otfuse import _lib as L
+    from otfuse import ops
+    info = torch.zeros(L.INFO_INT32S, dtype=torch.int32)
+    info[L.INFO_FIELDS.index("status")] = getattr(L, status)
+    info[L.INFO_FIELDS.index("stop")] = stop
+    info[L.INFO_FIELDS.index("stalled")] = stalled
+    X = torch.randn(8, 64, device=dev)
+    Y = torch.randn(8, 64, device=dev)
+    L0, gx0, gy0, _ = ops.cosine_align(X, Y)
+    L1, gx1, gy1, k1 = ops.cosine_align(X, Y, sk_info=info.to(dev))
+    assert int(k1) == keep
+    if keep:
+        assert torch.equal(L0, L1) and torch.equal(gx0, gx1) and torch.equal(gy0, gy1)
+    else:
+        assert float(L1) == 0.0 and torch.count_nonzero(gx1) == 0 and torch.count_nonzero(gy1) == 0
+
+
 @pytest.mark.parametrize("B,d,d2", [(8, 512, 512), (3, 100, 77), (20, 2048, 2048), (9, 64, 130)])
 def test_ot_align_backward_vs_torch(dev, B, d, d2):
     from otfuse import ops

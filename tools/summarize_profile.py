@@ -21,7 +21,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 PROF = os.path.join(REPO, "profiles")
-HOT = ("sk_resident_kernel", "sk_tiled_kernel", "sk_mesh_kernel", "sk_gather_kernel", "sk_pass_kernel", "sk_sweep_kernel", "cost_big_kernel", "cost_split16_kernel",
+HOT = ("sk_resident_kernel", "sk_tiled_kernel", "sk_mesh_kernel", "sk_gather_kernel", "sk_pass_kernel", "sk_sweep_kernel", "cost_big_kernel", "cost_big16_kernel", "cost_split16_kernel",
        "split16_prep2_kernel", "cost_f16_kernel", "sk_init_kernel", "sk_plan_kernel")
 LIB = os.path.join(REPO, "ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd",
                    "otfuse", "lib", "libotfuse.so")
