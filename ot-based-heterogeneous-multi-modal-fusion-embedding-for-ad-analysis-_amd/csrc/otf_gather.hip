@@ -618,7 +618,7 @@ template <typename T, typename CT>
 hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, const T* b_pad,
                       const T* cost_scale, const otf_sinkhorn_opts& o, void* region, T* u_out,
                       T* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                      double* errlog, hipStream_t s) {
+                      double* errlog, bool zeroed, hipStream_t s) {
     if (!gather_supported<T>(n, m) || !region) return hipErrorInvalidValue;
     SkGatherArgs<T> p{};
     p.C = C;
@@ -643,8 +643,10 @@ hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, co
     p.ldp = ldp;
     p.timeout_ticks = stall_ticks();
     p.reg_ticks = reg_stall_ticks();
-    hipError_t e = hipMemsetAsync(region, 0, gather_region_bytes<T>(n, m), s);
-    if (e != hipSuccess) return e;
+    if (!zeroed) {  // else the Sinkhorn init kernel zeroed it (no memset launch)
+        const hipError_t e = hipMemsetAsync(region, 0, gather_region_bytes<T>(n, m), s);
+        if (e != hipSuccess) return e;
+    }
     const int grid = (int)gather_grid<T>(n);
     p.nwg = grid;
     p.team_mode = gather_team_mode();
@@ -665,14 +667,14 @@ template size_t gather_region_bytes<double>(int64_t, int64_t);
 template hipError_t run_gather<float, float>(const float*, int64_t, int, int, const float*, const float*,
                                              const float*, const otf_sinkhorn_opts&, void*, float*,
                                              float*, void*, int64_t, int, otf_sinkhorn_info*, double*,
-                                             hipStream_t);
+                                             bool, hipStream_t);
 template hipError_t run_gather<float, _Float16>(const _Float16*, int64_t, int, int, const float*,
                                                 const float*, const float*, const otf_sinkhorn_opts&,
                                                 void*, float*, float*, void*, int64_t, int,
-                                                otf_sinkhorn_info*, double*, hipStream_t);
+                                                otf_sinkhorn_info*, double*, bool, hipStream_t);
 template hipError_t run_gather<double, double>(const double*, int64_t, int, int, const double*,
                                                const double*, const double*, const otf_sinkhorn_opts&,
                                                void*, double*, double*, void*, int64_t, int,
-                                               otf_sinkhorn_info*, double*, hipStream_t);
+                                               otf_sinkhorn_info*, double*, bool, hipStream_t);
 
 }  // namespace otf

@@ -277,14 +277,15 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
 
 // Gather engine (otf_gather.hip): small problems (<= 16 row tiles, m <= 512), column
 // partials exchanged as epoch-tagged granules, no barrier.  `region` is zeroed by the
-// launcher; gather_region_bytes is 0 for shapes it does not take.
+// launcher unless `zeroed` (the Sinkhorn init kernel did it); gather_region_bytes is 0
+// for shapes it does not take.
 template <typename T> bool gather_supported(int64_t n, int64_t m);
 template <typename T> size_t gather_region_bytes(int64_t n, int64_t m);
 template <typename T, typename CT>
 hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, const T* b_pad,
                       const T* cost_scale, const otf_sinkhorn_opts& o, void* region, T* u_out,
                       T* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                      double* errlog, hipStream_t s);
+                      double* errlog, bool zeroed, hipStream_t s);
 
 // Mesh engine (otf_mesh.hip): float32 problems of 4..64 row tiles x 1..8 column tiles
 // of K in registers, row and column reductions as epoch-tagged granule hops (no atomics,

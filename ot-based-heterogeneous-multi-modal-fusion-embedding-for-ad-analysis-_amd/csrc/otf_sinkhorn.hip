@@ -1938,19 +1938,21 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
                     mesh_supported(n, m) &&
                     (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled() &&
                                                      !(gather_supported<T>(n, m) && su.w.gather_bytes > 0)));
-    rc = sk_init<T>(su, a, b, n, m, info, s, mesh_pick ? su.w.mesh : nullptr,
-                    mesh_pick ? su.w.mesh_bytes : 0);
-    if (rc != OTF_OK) return rc;
-
     // gather engine: small problems, one granule hop per iteration, no barrier (and
-    // deterministic by construction)
+    // deterministic by construction); its region is zeroed by the init kernel too
     const bool gfits = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && gather_supported<T>(n, m) &&
                        su.w.gather_bytes > 0;
+    const bool gather_pick = gfits && (o.engine == OTF_ENGINE_GATHER || (o.engine == OTF_ENGINE_AUTO && gather_enabled()));
+    rc = sk_init<T>(su, a, b, n, m, info, s, mesh_pick ? su.w.mesh : gather_pick ? su.w.gather : nullptr,
+                    mesh_pick ? su.w.mesh_bytes : gather_pick ? su.w.gather_bytes : 0);
+    if (rc != OTF_OK) return rc;
+
     if (o.engine == OTF_ENGINE_GATHER && !gfits) return OTF_EUNSUPPORTED;
-    if (gfits && (o.engine == OTF_ENGINE_GATHER || (o.engine == OTF_ENGINE_AUTO && gather_enabled()))) {
+    if (gather_pick) {
         const hipError_t e = run_gather<T, CT>(C, ldc, (int)n, (int)m, (const T*)su.w.a_pad,
                                                (const T*)su.w.b_pad, cost_scale, o, su.w.gather, u_out,
-                                               v_out, P_out, ldp, P_dtype, info, errlog, s);
+                                               v_out, P_out, ldp, P_dtype, info, errlog,
+                                               /*zeroed=*/true, s);
         if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_GATHER) return check_hip(e);

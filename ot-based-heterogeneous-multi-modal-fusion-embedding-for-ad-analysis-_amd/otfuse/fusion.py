@@ -40,7 +40,7 @@ def batch_feature_plan(mri_fused: torch.Tensor, pet_fused: torch.Tensor, eps: fl
     """PET->MRI feature coupling of one batch, Ts = eye(B)/B (MRI_PET_OT_nojax.py:683-699).
     Returns the raw float64 plan (d, d) and the SinkhornResult."""
     B = mri_fused.shape[0]
-    ts_diag = torch.full((B,), 1.0 / B, dtype=torch.float64, device=mri_fused.device)
+    ts_diag = ops.uniform(B, torch.float64, mri_fused.device)   # Ts = eye(B) / B
     res = feature_coupling_pot_device(mri_fused.detach(), pet_fused.detach(), ts_diag=ts_diag,
                                       eps=eps, numItermax=numItermax, stopThr=stopThr,
                                       sync_every=sync_every)

@@ -277,6 +277,19 @@ def sinkhorn_workspace_bytes(n: int, m: int, dtype, max_iter: int) -> int:
     return int(L.lib().otf_sinkhorn_workspace_size(n, m, _DT[dtype], max_iter))
 
 
+_UNIFORM: dict = {}
+
+
+def uniform(n: int, dtype, device) -> torch.Tensor:
+    """The uniform marginal 1/n as a cached device tensor (read-only: the solves copy it
+    into their workspace), so a training step does not pay a fill launch per marginal."""
+    key = (int(n), dtype, torch.device(device))
+    t = _UNIFORM.get(key)
+    if t is None:
+        t = _UNIFORM[key] = torch.full((int(n),), 1.0 / int(n), dtype=dtype, device=device)
+    return t
+
+
 def sinkhorn_workspace(n: int, m: int, dtype, max_iter: int, device) -> torch.Tensor:
     wsb = L.lib().otf_sinkhorn_workspace_size(n, m, _DT[dtype], max_iter)
     return torch.empty(wsb, dtype=torch.uint8, device=device)

@@ -199,8 +199,8 @@ def feature_coupling_pot_device(X: torch.Tensor, Y: torch.Tensor, Ts=None, ts_di
     float64 feature cost + POT-flavour float64 Sinkhorn.  Returns ``ops.SinkhornResult``."""
     M = ops.feature_cost(X, Y, Ts=Ts, ts_diag=ts_diag, weights="pot")
     d, d2 = M.shape
-    a = torch.full((d,), 1.0 / d, dtype=torch.float64, device=M.device)
-    b = torch.full((d2,), 1.0 / d2, dtype=torch.float64, device=M.device)
+    a = ops.uniform(d, torch.float64, M.device)
+    b = ops.uniform(d2, torch.float64, M.device)
     return ops.sinkhorn(a, b, M, float(eps), max_iter=numItermax, stop_thr=stopThr, flavor="pot",
                         sync_every=sync_every, want_plan=True)
 
