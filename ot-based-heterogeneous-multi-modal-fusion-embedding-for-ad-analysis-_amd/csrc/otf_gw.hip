@@ -1163,6 +1163,43 @@ __global__ void sqnorm_f64_kernel(const float* X, int64_t ldx, int n, int d, dou
     if (lane == 0) out[i] = s;
 }
 
+// C[i][j] = -2 x_i . y_j + |x_i|^2 + |y_j|^2 for small outputs with long rows (the
+// per-label GW costs: 64 x 64 samples of d = 2048): one wave per output, the float32
+// rows read as 16-B vectors, the products summed in float64 over the wave (a fixed
+// order), then the gemm epilogue's order (-2 acc, + row term, + column term).  The
+// 64 x 64 gemm tile put the whole 64 x 64 x 2048 contraction on ONE workgroup
+// (~290 us per cost, 4 per config-3 epoch call); this spreads it over n m waves.
+__global__ __launch_bounds__(512) void dot_cost_f64_kernel(const float* X, int64_t ldx, const float* Y,
+                                                           int64_t ldy, int n, int m, int d, int vec,
+                                                           const double* nx, const double* ny, double* C,
+                                                           int64_t ldc) {
+    const int64_t o = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (o >= (int64_t)n * m) return;
+    const int i = (int)(o / m), j = (int)(o % m);
+    const float* x = X + (int64_t)i * ldx;
+    const float* y = Y + (int64_t)j * ldy;
+    double s = 0;
+    int k0 = 0;
+    if (vec) {
+        using F4 = __attribute__((ext_vector_type(4))) float;
+        for (; k0 + 4 * kWave <= d; k0 += 4 * kWave) {
+            const F4 a = *reinterpret_cast<const F4*>(x + k0 + 4 * lane);
+            const F4 b = *reinterpret_cast<const F4*>(y + k0 + 4 * lane);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s = fma((double)a[q], (double)b[q], s);
+        }
+    }
+    for (int k = k0 + lane; k < d; k += kWave) s = fma((double)x[k], (double)y[k], s);
+    s = wave_sum(s);
+    if (lane == 0) {
+        double v = -2.0 * s;
+        v += nx[i];
+        v += ny[j];
+        C[(int64_t)i * ldc + j] = v;
+    }
+}
+
 // clamp >= 0, sqrt (euclidean), zero diagonal; per-block max to part[blockIdx.x]
 __global__ __launch_bounds__(256) void dist_finalize_kernel(double* C, int64_t ldc, int n, int m,
                                                             int euclid, int zero_diag, double* part) {
@@ -1247,10 +1284,18 @@ int otf_cost_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64_t l
     otf::sqnorm_f64_kernel<<<(unsigned)((n + 3) / 4), 256, 0, s>>>(X, ldx, (int)n, (int)d, nx);
     otf::sqnorm_f64_kernel<<<(unsigned)((m + 3) / 4), 256, 0, s>>>(Y, ldy, (int)m, (int)d, ny);
     OTF_HIP(hipGetLastError());
-    // C = -2 X Y^T + |x|^2 + |y|^2   (POT euclidean_distances order)
-    int rc = otf::launch_gemm<float, float, double, double>(X, ldx, 1, Y, 1, ldy, C, ldc, (int)n,
-                                                            (int)m, (int)d, -2.0, 0.0, nx, ny, s);
-    if (rc != OTF_OK) return rc;
+    // C = -2 X Y^T + |x|^2 + |y|^2   (POT euclidean_distances order); outputs too few to
+    // fill the chip with 64 x 64 gemm tiles: one wave per output
+    if (n * m <= 16384) {
+        const int vec = (ldx % 4 == 0) && (ldy % 4 == 0) && ((uintptr_t)X % 16 == 0) && ((uintptr_t)Y % 16 == 0);
+        otf::dot_cost_f64_kernel<<<(unsigned)((n * m + 7) / 8), 512, 0, s>>>(X, ldx, Y, ldy, (int)n, (int)m,
+                                                                             (int)d, vec, nx, ny, C, ldc);
+        OTF_HIP(hipGetLastError());
+    } else {
+        int rc = otf::launch_gemm<float, float, double, double>(X, ldx, 1, Y, 1, ldy, C, ldc, (int)n,
+                                                                (int)m, (int)d, -2.0, 0.0, nx, ny, s);
+        if (rc != OTF_OK) return rc;
+    }
     const int64_t tot = n * m;
     int grid = (int)((tot + 255) / 256);
     if (grid > otf::DIST_PARTS) grid = otf::DIST_PARTS;
