@@ -145,3 +145,25 @@ def test_gather_team_mode_agrees_bitwise(dev, monkeypatch):
     r0 = ops.sinkhorn(a, a, C, 0.02, max_iter=500, stop_thr=0.0, engine="gather")
     assert r1.info()["engine_name"] == r0.info()["engine_name"] == "gather"
     assert torch.equal(r0.plan, r1.plan) and torch.equal(r0.u, r1.u) and torch.equal(r0.v, r1.v)
+
+
+@pytest.mark.parametrize("dt", [torch.float64, torch.float32])
+def test_gather_zero_column_sum_breaks_like_pot(orc, dev, dt):
+    """A column whose K underflows entirely (S_j = 0): POT reverts at iteration 0.  The
+    float64 chunks carry their tag in the values' low mantissa bits -- an exact zero must
+    come back as zero once the tag is cleared, or the break would be missed."""
+    from otfuse import ops
+    rng = np.random.default_rng(11)
+    n, m = 512, 512
+    C = rng.random((n, m))
+    C[:, 37] = 2e3   # exp(-2e3 / 0.5) = 0 in float32 and float64
+    a = np.full(n, 1.0 / n)
+    b = np.full(m, 1.0 / m)
+    P_r, *_, info_r = orc.sinkhorn_knopp(a, b, C, 0.5, 50, 0.0)
+    res = ops.sinkhorn(_t(a, dev, dt), _t(b, dev, dt), _t(C, dev, dt), 0.5, max_iter=50,
+                       stop_thr=0.0, engine="gather")
+    info = res.info()
+    assert info["engine_name"] == "gather"
+    assert info["status_name"] == ("numerical_break" if info_r["break_iter"] >= 0 else "max_iter")
+    assert info["niter"] == info_r["niter"] and info["break_iter"] == info_r["break_iter"]
+    assert nrel(res.plan.cpu().numpy(), P_r) < (1e-5 if dt == torch.float32 else 1e-12)
