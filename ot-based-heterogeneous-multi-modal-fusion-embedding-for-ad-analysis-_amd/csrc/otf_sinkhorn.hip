@@ -662,6 +662,14 @@ template <typename T> struct SkResArgs {
     int p_f64;
     unsigned long long timeout_ticks;
     unsigned long long reg_ticks;  // the first wait (registration / first hop)
+    // OTT flavour in scaling form (float64 only; otf_sinkhorn_opts.engine = RESIDENT):
+    // U = exp(f / eps), V = exp(g / eps) with f = g = 0 at the start, so the updates are
+    // POT's (V = b / K^T U, U = a / K V) from U = 1; OTT's L1 marginal error after every
+    // check_every-th update; outputs f = eps ln U, g = eps ln V; a zero U or V (f or g =
+    // -inf in the log form) is a numerical break like a non-finite one.  Valid while
+    // K = exp(-C / (eps s)) does not underflow (the caller's contract: max C / (eps s)
+    // well inside float64's exponent range, e.g. <= 300 with scale_cost = max_cost).
+    int ott;
 };
 
 
@@ -731,11 +739,19 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
         ia[r] = (T)1 / p.a[row];
     }
 
-    // iteration history in LDS, slot = iteration & 1 (slots start as u0 = 1/n, v0 = 1/m):
-    // iteration it reads v(it-1) from slot (it-1)&1 and writes u(it), v(it) into slot it&1
-    // only after its checks pass, so slot it&1 still holds iteration it-2 when a
-    // numerical break in it-1 has to revert two iterations.
-    const T u0 = (T)1 / (T)p.n, v0 = (T)1 / (T)p.m;
+    // iteration history in LDS, slot = iteration & 1 (slots start as u0 = 1/n, v0 = 1/m;
+    // OTT: U = V = 1): iteration it reads v(it-1) from slot (it-1)&1 and writes u(it),
+    // v(it) into slot it&1 only after its checks pass, so slot it&1 still holds
+    // iteration it-2 when a numerical break in it-1 has to revert two iterations.
+    const bool ott = p.ott != 0;
+    const T u0 = ott ? (T)1 : (T)1 / (T)p.n, v0 = ott ? (T)1 : (T)1 / (T)p.m;
+    // the iteration whose marginal error is checked: POT it % ce == 0, OTT after every
+    // ce-th update ((it + 1) % ce == 0); its error-log slot
+    auto checked = [&](int it) -> bool { return ((it + (ott ? 1 : 0)) % p.check_every) == 0; };
+    auto err_slot = [&](int it) -> int { return ott ? (it + 1) / p.check_every - 1 : it / p.check_every; };
+    auto finish_err = [&](T e) -> double {
+        return ott ? (double)e : (p.err_squared ? (double)e : sqrt((double)e));
+    };
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -865,7 +881,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
             for (int k = 0; k < VEC; ++k) {
                 const T bj = bcol[g][k];
                 const T val = bj / s[g][k];
-                badv |= (cok[g][k] && ((s[g][k] == (T)0) || !finite_val(val))) ? 1 : 0;
+                badv |= (cok[g][k] && ((s[g][k] == (T)0) || !finite_val(val) || (ott && val == (T)0))) ? 1 : 0;
                 vn[g][k] = cok[g][k] ? val : (T)0;
             }
         // numerical break in u(it-1) -> revert to it-2
@@ -873,8 +889,8 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
             last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
             break;
         }
-        // marginal error of iteration it-1: v(it-1) * K^T u(it-1) - b
-        if (it >= 1 && ((it - 1) % p.check_every) == 0) {
+        // marginal error of iteration it-1: v(it-1) * K^T u(it-1) - b (POT: L2, OTT: L1)
+        if (it >= 1 && checked(it - 1)) {
             T e = 0;
 #pragma unroll
             for (int g = 0; g < G; ++g)
@@ -882,12 +898,12 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
                 for (int k = 0; k < VEC; ++k) {
                     const T vb = vhist[(it - 1) & 1][(tid + NT * g) * VEC + k];
                     const T rr = vb * s[g][k] - bcol[g][k];
-                    e += cok[g][k] ? rr * rr : (T)0;
+                    e += cok[g][k] ? (ott ? fabs(rr) : rr * rr) : (T)0;
                 }
             e = block_sum<T>(e, red);
-            const double err = p.err_squared ? (double)e : sqrt((double)e);
-            if (lead) p.errlog[(it - 1) / p.check_every] = err;
-            n_err = (it - 1) / p.check_every + 1;
+            const double err = finish_err(e);
+            if (lead) p.errlog[err_slot(it - 1)] = err;
+            n_err = err_slot(it - 1) + 1;
             if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) {
                 last_good = it - 1; niter = it - 1; status = OTF_SK_CONVERGED;
                 break;
@@ -917,7 +933,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
         for (int r = 0; r < R; ++r) {
             const bool rok = r0 + r < p.n;
             un[r] = (T)1 / (un[r] * ia[r]);
-            badu |= (rok && !finite_val(un[r])) ? 1 : 0;
+            badu |= (rok && (!finite_val(un[r]) || (ott && un[r] == (T)0))) ? 1 : 0;
             if (!rok) un[r] = 0;
         }
         if (badu && tid == 0) atomicAdd(p.bad_cnt + (it & 3) * 64, 1);
@@ -953,7 +969,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
             last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
         } else {
             last_good = it; niter = it;
-            if ((it % p.check_every) == 0) {
+            if (checked(it)) {
                 const T* cs_last = p.cs + (size_t)(p.max_iter & 3) * it_stride;
                 T e = 0, sl[G][VEC];
                 load_sums(cs_last, sl, (T)0);
@@ -964,12 +980,12 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
                         const T sk = sl[g][k];
                         const T vb = vhist[it & 1][(tid + NT * g) * VEC + k];
                         const T rr = vb * sk - bcol[g][k];
-                        e += cok[g][k] ? rr * rr : (T)0;
+                        e += cok[g][k] ? (ott ? fabs(rr) : rr * rr) : (T)0;
                     }
                 e = block_sum<T>(e, red);
-                const double err = p.err_squared ? (double)e : sqrt((double)e);
-                if (lead) p.errlog[it / p.check_every] = err;
-                n_err = it / p.check_every + 1;
+                const double err = finish_err(e);
+                if (lead) p.errlog[err_slot(it)] = err;
+                n_err = err_slot(it) + 1;
                 if (p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr)) status = OTF_SK_CONVERGED;
             }
         }
@@ -994,19 +1010,21 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
 #pragma unroll
             for (int k = 0; k < VEC; ++k) vo[g][k] = v0;
     }
+    // OTT: the potentials f = eps ln U, g = eps ln V (units of the scaled cost)
+    const T epsu = (T)(p.reg / unit);
     if (tid < R && r0 + tid < p.n) {
         T mine = uo[0];
 #pragma unroll
         for (int r = 1; r < R; ++r)
             if (tid == r) mine = uo[r];
-        p.u_out[r0 + tid] = mine;
+        p.u_out[r0 + tid] = ott ? epsu * unit_log(mine) : mine;
     }
     if (blockIdx.x == 0) {
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int k = 0; k < VEC; ++k)
-                if (cok[g][k]) p.v_out[colc[g] + k] = vo[g][k];
+                if (cok[g][k]) p.v_out[colc[g] + k] = ott ? epsu * unit_log(vo[g][k]) : vo[g][k];
     }
     if (p.P) {
         TP* P = (TP*)p.P;
@@ -1662,8 +1680,9 @@ template <typename T, typename CT>
 hipError_t run_resident(const PassCfg& cfg, int grid, const CT* C, int64_t ldc, int n, int m,
                         const T* cost_scale, const otf_sinkhorn_opts& o, Workspace& w, T* u_out,
                         T* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                        double* errlog, hipStream_t s) {
+                        double* errlog, hipStream_t s, bool ott = false) {
     SkResArgs<T> p{};
+    p.ott = ott ? 1 : 0;
     p.C = C;
     p.ldc = ldc;
     p.n = n;
@@ -2011,6 +2030,16 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     // or co-residency refused), so the row-block resident engine is the next choice
     const bool want_res = !LOG && !avg_pass_ms && fits && o.max_iter >= 1 &&
                           (o.engine == OTF_ENGINE_RESIDENT || o.engine == OTF_ENGINE_AUTO);
+    // OTT flavour, float64, on request: the resident engine in scaling form (see
+    // SkResArgs::ott for the range contract).  No one-workgroup fallback is queued (that
+    // one is POT-flavour): a grid that cannot become co-resident ends in OTF_SK_TIMEOUT.
+    if (LOG && o.engine == OTF_ENGINE_RESIDENT) {
+        if (sizeof(T) != 8 || !fits || !whole || avg_pass_ms || o.max_iter < 1) return OTF_EUNSUPPORTED;
+        Workspace w = su.w;
+        return check_hip(run_resident<T, CT>(su.cfg, su.nrb, C, ldc, (int)n, (int)m, cost_scale, o, w,
+                                             u_out, v_out, P_out, ldp, P_dtype, info, errlog, s,
+                                             /*ott=*/true));
+    }
     if (o.engine == OTF_ENGINE_RESIDENT && (LOG || !fits)) return OTF_EUNSUPPORTED;
     if (want_res) {
         Workspace w = su.w;

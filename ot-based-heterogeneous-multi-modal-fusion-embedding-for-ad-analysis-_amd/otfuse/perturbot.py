@@ -49,6 +49,13 @@ def mdict_to_matrix(M_dict, source_labels, target_labels):
     return Mtot
 
 
+# float64 OTT solves with scale_cost="max_cost" run in the resident engine's scaling form
+# (one persistent launch: U = exp(f / eps), V = exp(g / eps)) when 1 / eps keeps
+# K = exp(-C / (eps max C)) and the scalings far inside float64's range; else (and when
+# that engine does not take the shape) the log-domain streaming passes.
+OTT_SCALING_MAX = 300.0
+
+
 def solve_ott(M: torch.Tensor, eps: float, scale_cost: str | None = "max_cost",
               a: torch.Tensor | None = None, b: torch.Tensor | None = None,
               threshold: float = OTT_THRESHOLD, max_iterations: int = OTT_MAX_ITER,
@@ -58,17 +65,24 @@ def solve_ott(M: torch.Tensor, eps: float, scale_cost: str | None = "max_cost",
     n, m = M.shape
     dt = M.dtype
     if a is None:
-        a = torch.full((n,), 1.0 / n, dtype=dt, device=M.device)
+        a = ops.uniform(n, dt, M.device)
     if b is None:
-        b = torch.full((m,), 1.0 / m, dtype=dt, device=M.device)
+        b = ops.uniform(m, dt, M.device)
     scale = None
     if scale_cost == "max_cost":
         scale = M.max().reshape(1)
     elif scale_cost not in (None, 1.0):
         raise NotImplementedError(f"scale_cost={scale_cost!r}")
-    res = ops.sinkhorn(a, b, M, float(eps), max_iter=max_iterations, stop_thr=threshold,
-                       flavor="ott", cost_scale=scale, check_every=OTT_INNER,
-                       sync_every=sync_every, want_plan=True)
+    kw = dict(max_iter=max_iterations, stop_thr=threshold, flavor="ott", cost_scale=scale,
+              check_every=OTT_INNER, sync_every=sync_every, want_plan=True)
+    if dt == torch.float64 and scale_cost == "max_cost" and 1.0 / float(eps) <= OTT_SCALING_MAX:
+        try:
+            res = ops.sinkhorn(a, b, M, float(eps), engine="resident", **kw)
+            if res.info_dev[3].item() != ops.L.SK_TIMEOUT:   # the grid was co-resident
+                return res, scale
+        except ops.L.OtfError:
+            pass                              # shape not taken by the resident engine
+    res = ops.sinkhorn(a, b, M, float(eps), **kw)
     return res, scale
 
 
