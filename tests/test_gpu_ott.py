@@ -54,3 +54,33 @@ def test_solve_ott_takes_the_resident_form_and_matches_oracle(orc, dev):
                                         max_iter=2000, threshold=1e-3, cscale=1.0 / M.max())
     assert info["niter"] + 1 == info_r["n_iters"]
     assert nrel(res.plan.cpu().numpy(), Pr) < 1e-9
+
+
+def test_solve_ott_falls_back_to_log_passes_when_the_grid_is_not_co_resident(dev, monkeypatch):
+    """The scaling form has no one-workgroup fallback (that one is POT-flavour): a resident
+    OTT grid that cannot register (8 CUs held by a long gather solve on another stream,
+    1-ms registration window) ends in OTF_SK_TIMEOUT, and solve_ott re-solves with the
+    log-domain passes -- the same plan as an uncontended solve."""
+    from otfuse import ops, perturbot
+    g = torch.Generator(device=dev).manual_seed(5)
+    M = torch.rand(2048, 2048, device=dev, generator=g, dtype=torch.float64) ** 2
+    ref, _ = perturbot.solve_ott(M, 5e-3)
+    assert ref.info()["engine_name"] == "resident"
+    Cg = torch.rand(512, 512, device=dev, generator=g, dtype=torch.float64)
+    ag = torch.full((512,), 1.0 / 512, device=dev, dtype=torch.float64)
+    monkeypatch.setenv("OTF_REG_MS", "1")
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        blocker = ops.sinkhorn(ag, ag, Cg, 0.1, max_iter=40000, stop_thr=0.0, engine="gather",
+                               want_plan=False)
+    with torch.cuda.stream(s2):
+        res, _ = perturbot.solve_ott(M, 5e-3)
+    torch.cuda.synchronize()
+    info = res.info()
+    assert info["status_name"] in ("converged", "max_iter") and info["stalled"] == 0
+    assert info["niter"] == ref.info()["niter"]
+    assert nrel(res.plan.cpu().numpy(), ref.plan.cpu().numpy()) < 1e-9
+    assert blocker.info()["status_name"] == "max_iter"
+    if info["engine_name"] == "resident":
+        pytest.skip("the blocker finished before the OTT launch: no contention to test")
