@@ -210,7 +210,16 @@ template <int O, typename T> __device__ __forceinline__ T swap_sum(T a, T b) {
 // R = 16 in float against ~35 here.)
 template <typename T, int R>
 __device__ __forceinline__ T wave_row_totals(const T (&x)[R], int lane) {
-    static_assert(R == 8 || R == 16, "8 or 16 rows per wave");
+    static_assert(R == 4 || R == 8 || R == 16, "4, 8 or 16 rows per wave");
+    if constexpr (R == 4) {
+        // lane bits 5 and 4 by the swaps (lane L: row L >> 4), then the 16 of a row
+        T t = swap_sum<16>(swap_sum<32>(x[0], x[2]), swap_sum<32>(x[1], x[3]));
+        t += dpp_lane<0x140>(t);
+        t += dpp_lane<0x141>(t);
+        t += dpp_lane<0xB1>(t);
+        t += dpp_lane<0x4E>(t);
+        return t;
+    } else {
     T y[R / 2], z[R / 4];
 #pragma unroll
     for (int i = 0; i < R / 2; ++i) y[i] = swap_sum<32>(x[i], x[i + R / 2]);
@@ -235,6 +244,7 @@ __device__ __forceinline__ T wave_row_totals(const T (&x)[R], int lane) {
     t += dpp_lane<0xB1>(t);
     t += dpp_lane<0x4E>(t);
     return t;
+    }
 }
 
 // Block-wide sum of R values per thread.  `red` is LDS of >= (nwaves + 1) * R

@@ -35,9 +35,13 @@
 namespace otf {
 namespace {
 
+// rows per wave of a float64 tile (A/B build switch; 8: 64-row tiles, 4: 32-row tiles)
+#ifndef OTF_GATHER_RW64
+#define OTF_GATHER_RW64 8
+#endif
 template <typename T> struct GatherCfg {
     static constexpr int NW = 8;                        // waves per workgroup
-    static constexpr int RW = sizeof(T) == 4 ? 16 : 8;  // rows per wave
+    static constexpr int RW = sizeof(T) == 4 ? 16 : OTF_GATHER_RW64;  // rows per wave
     static constexpr int VEC = Vec<T>::N;
     static constexpr int G = sizeof(T) == 4 ? 2 : 4;    // VEC-vectors per lane: 8 columns
     static constexpr int TR = RW * NW;                  // rows per workgroup: 128 / 64
@@ -254,7 +258,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
         }
     }
     // the row whose total this lane holds after wave_row_totals: lane >> RSH
-    constexpr int RSH = R == 16 ? 2 : 3;
+    constexpr int RSH = R == 16 ? 2 : R == 8 ? 3 : 4;
     const int myrow = lane >> RSH;
     const T ia_mine = (T)1 / p.a[row_in(row0 + myrow) ? row0 + myrow : n_ - 1];
     // this thread's gathered columns (chunk tid): their target marginal
@@ -559,8 +563,9 @@ hipError_t launch_gather_q(int grid, SkGatherArgs<T>& p, hipStream_t s) {
     // BASELINE config 2 (8 whole row tiles x 512 columns of float64) has its own
     // compiled-in instance
     const bool whole = p.n == p.nwg * GatherCfg<T>::TR && p.m == GatherCfg<T>::C;
-    const void* k = (sizeof(T) == 8 && NQ == 8 && p.nwg == 8 && whole)
-                        ? (const void*)sk_gather_kernel<T, CT, TP, NQ, (sizeof(T) == 8 && NQ == 8) ? 8 : 0>
+    constexpr int S2 = 512 / GatherCfg<T>::TR;  // config 2's 512 rows in whole tiles
+    const void* k = (sizeof(T) == 8 && NQ == S2 && p.nwg == S2 && whole)
+                        ? (const void*)sk_gather_kernel<T, CT, TP, NQ, (sizeof(T) == 8 && NQ == S2) ? S2 : 0>
                         : (const void*)sk_gather_kernel<T, CT, TP, NQ, 0>;
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
