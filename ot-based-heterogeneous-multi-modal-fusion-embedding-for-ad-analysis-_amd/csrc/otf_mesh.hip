@@ -461,12 +461,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             if (t < nch) {
                 const uint32_t off = colb(e, t / CPR) + (uint32_t)(t & (CPR - 1)) * 16;
                 I4 x;
-                for (;;) {
-                    x = gload(rs, off);
-                    if (chunk_at(x, (unsigned)e)) break;
-                    if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; break; }
-                    __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
-                }
+                if (!poll_chunk<OTF_MESH_SLEEP>(rs, off, (unsigned)e, deadline, x)) fl |= 2;
                 OTF_MSTAMP(e - 1, 8, 256);
                 fl |= x[1] & 1;
                 const T s0 = chunk_v0(x), s1 = chunk_v1(x);
@@ -481,12 +476,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             if (lane < nred) {
                 const uint32_t off = colb(e, lane) + (uint32_t)CPR * 16;
                 I4 x;
-                for (;;) {
-                    x = gload(rs, off);
-                    if (chunk_at(x, (unsigned)e)) break;
-                    if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; break; }
-                    __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
-                }
+                if (!poll_chunk<OTF_MESH_SLEEP>(rs, off, (unsigned)e, deadline, x)) fl |= 2;
                 ep = chunk_v0(x);
             }
             ep = wave_sum<T>(ep);
@@ -507,12 +497,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         if (lane < ncb) {
             const uint32_t off = rowx(er, lane) + 64 * 16;
             I4 x;
-            for (;;) {
-                x = gload(rs, off);
-                if (chunk_at(x, (unsigned)er)) break;
-                if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
-                __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
-            }
+            ok = poll_chunk<OTF_MESH_SLEEP>(rs, off, (unsigned)er, deadline, x);
             ev = chunk_v0(x);
         }
         ev += wave_xor<T, 1>(ev);
@@ -611,12 +596,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             I4 x = I4{0, 0, 0, 0};
             if (act) {
                 const uint32_t off = rowx(e, q) + (uint32_t)(w * 8 + rc) * 16;
-                for (;;) {
-                    x = gload(rs, off);
-                    if (chunk_at(x, (unsigned)e)) break;
-                    if (__builtin_amdgcn_s_memrealtime() > deadline) { stall = 1; break; }
-                    __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
-                }
+                if (!poll_chunk<OTF_MESH_SLEEP>(rs, off, (unsigned)e, deadline, x)) stall = 1;
             }
             OTF_MSTAMP(it, 3, 0);
             OTF_MSTAMP(it, 9, 448);

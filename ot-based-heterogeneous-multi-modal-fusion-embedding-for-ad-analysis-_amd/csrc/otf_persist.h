@@ -134,6 +134,20 @@ __device__ __forceinline__ I4 gload(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
 __device__ __forceinline__ void gstore(__amdgpu_buffer_rsrc_t rs, uint32_t off, I4 x) {
     __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
 }
+// Polls one chunk until both its tags carry epoch e: load - wait - reload.  (Two loads in
+// flight, the next issued before the previous is examined, measured slower in r03: the
+// mesh's hops 0.72 -> 0.80 us -- the extra request traffic costs more than the finer
+// sampling gains.)  False on a stall (deadline passed); x holds the last value loaded.
+template <int SLEEP>
+__device__ __forceinline__ bool poll_chunk(__amdgpu_buffer_rsrc_t rs, uint32_t off, unsigned e,
+                                           unsigned long long deadline, I4& x) {
+    for (;;) {
+        x = gload(rs, off);
+        if (chunk_at(x, e)) return true;
+        if (__builtin_amdgcn_s_memrealtime() > deadline) return false;
+        __builtin_amdgcn_s_sleep(SLEEP);
+    }
+}
 // Across GPUs (peer-mapped exchange buffers): system-scope (sc0 sc1) stores reach the
 // owner's memory over xGMI; the owner polls with system-scope loads
 __device__ __forceinline__ I4 gload_sys(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
