@@ -115,6 +115,10 @@ using I4 = __attribute__((ext_vector_type(4))) int;
 #ifndef OTF_MESH_SLEEP
 #define OTF_MESH_SLEEP 1
 #endif
+// reducer polls: reload only the producers not yet seen (1) or all of them (0)
+#ifndef OTF_MESH_RED_PEND
+#define OTF_MESH_RED_PEND 1
+#endif
 using F2 = __attribute__((ext_vector_type(2))) float;
 
 constexpr int pow2_at_least(int x) { return x <= 1 ? 1 : 2 * pow2_at_least((x + 1) / 2); }
@@ -372,12 +376,27 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         }
         bool ok = true;
         for (;;) {
+#if OTF_MESH_RED_PEND
 #pragma unroll
             for (int k = 0; k < KQW; ++k)
                 if (pend & (1u << k)) x[k] = gload(rs, cola(e, r_qlo + LPC * (k0 + k)) + (uint32_t)r_ch * 16);
 #pragma unroll
             for (int k = 0; k < KQW; ++k)
                 if ((pend & (1u << k)) && chunk_at(x[k], (unsigned)e)) pend &= ~(1u << k);
+#else
+            // every pass reloads all KQW producers (unconditional loads, all in flight);
+            // inactive slots (past nrb) re-read producer 0 and are ignored
+#pragma unroll
+            for (int k = 0; k < KQW; ++k) {
+                const int q = r_qlo + LPC * (k0 + k);
+                x[k] = gload(rs, cola(e, act[k] ? q : 0) + (uint32_t)(r_ok ? r_ch : 0) * 16);
+            }
+            unsigned np = 0;
+#pragma unroll
+            for (int k = 0; k < KQW; ++k)
+                if (act[k] && !chunk_at(x[k], (unsigned)e)) np |= 1u << k;
+            pend = np;
+#endif
             if (!__any(pend != 0)) break;
             if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
             __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
