@@ -117,7 +117,7 @@ using I4 = __attribute__((ext_vector_type(4))) int;
 #endif
 // reducer polls: reload only the producers not yet seen (1) or all of them (0)
 #ifndef OTF_MESH_RED_PEND
-#define OTF_MESH_RED_PEND 1
+#define OTF_MESH_RED_PEND 0
 #endif
 using F2 = __attribute__((ext_vector_type(2))) float;
 
