@@ -311,7 +311,7 @@ def test_solo_fallback_when_registration_cannot_complete(dev, monkeypatch):
 
 
 @pytest.mark.parametrize("engine,n,m,dt,iters", [("tiled", 4096, 4096, torch.float32, 20000),
-                                                 ("mesh", 4096, 4096, torch.float32, 20000),
+                                                 ("mesh", 4096, 4096, torch.float32, 40000),
                                                  ("resident", 512, 512, torch.float64, 30000),
                                                  ("gather", 512, 512, torch.float64, 60000),
                                                  ("sweep", 1024, 8192, torch.float32, 20000)])
