@@ -124,6 +124,18 @@ typedef struct {
     int32_t deterministic; /* 1: bitwise-reproducible column sums (fixed-order reduction,
                            no float atomics; gather, mesh or sweep engine, POT flavour),
                            e.g. for parity runs; other engines: OTF_EUNSUPPORTED     */
+    int32_t shift;      /* 1: shifted kernel for float32 POT at small reg (C/reg beyond
+                           float32's exp range, e.g. reg < 0.0115 on a max-normalised
+                           cost): the same POT iterates computed as
+                             K~_ij = 2^(C_ij*cscale*(-log2 e)/reg + A_i + B_j),
+                             u = 2^A * u~,  v = 2^B * v~,  P = u~ K~ v~ = u K v,
+                           A, B from a log-domain first half-iteration (one column
+                           log-sum-exp pass + one row max pass over C before the solve).
+                           u_out / v_out receive u~, v~; the base-2 offsets A (n), B (m)
+                           stay in the workspace at otf_sinkhorn_shift_offsets().
+                           Engines: mesh, sweep, stream (AUTO picks among them; forcing
+                           gather / tiled / resident: OTF_EUNSUPPORTED).  float64 or OTT
+                           flavour: OTF_EUNSUPPORTED.                                 */
 } otf_sinkhorn_opts;
 
 /* Written on the device by otf_sinkhorn (read it after the stream completes). */
@@ -250,6 +262,11 @@ int otf_coupled_cost(const float* A, int64_t a0, int64_t a1, const float* B, int
 int otf_sinkhorn_fallback_count(uint64_t* count);
 
 size_t otf_sinkhorn_workspace_size(int64_t n, int64_t m, int32_t dtype, int32_t max_iter);
+/* Byte offsets, inside an otf_sinkhorn workspace of this shape, of the shifted kernel's
+ * float32 offsets A (n values) and B (m values, base-2 logarithms): POT's scalings are
+ * u_i = 2^A_i u~_i, v_j = 2^B_j v~_j.  Written by a solve with opts.shift = 1.      */
+int otf_sinkhorn_shift_offsets(int64_t n, int64_t m, int32_t dtype, int32_t max_iter,
+                               size_t* off_a, size_t* off_b);
 int otf_sinkhorn(const void* a, const void* b, const void* C, int64_t n, int64_t m, int64_t ldc,
                  int32_t dtype, const void* cost_scale, const otf_sinkhorn_opts* opts,
                  void* u_out, void* v_out, void* P_out, int64_t ldp, int32_t P_dtype,

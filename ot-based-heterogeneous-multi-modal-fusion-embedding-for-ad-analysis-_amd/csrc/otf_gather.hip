@@ -176,15 +176,14 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
                                                     __HIP_MEMORY_SCOPE_AGENT);
             int keep = slot < nwg ? 1 : 0;
             if (keep) {
-                // wait until this XCC's team is complete or another team has claimed
+                // wait until this XCC's team is complete or another team has claimed.
+                // The claim word takes exactly one value: a team (xcd + 1), or -1 when a
+                // registrant whose deadline passed gave the launch up -- both by a
+                // compare-and-swap from 0, so a solve is never both claimed and abandoned
                 for (;;) {
-                    if (load_agent(&p.info->stalled)) {  // another registrant gave up
-                        keep = 0;
-                        break;
-                    }
-                    const int claim = load_agent(p.team + 8 * 64);
+                    int claim = load_agent(p.team + 8 * 64);
                     if (claim != 0) {
-                        keep = claim == xcd + 1;
+                        keep = claim == xcd + 1;  // -1: abandoned
                         break;
                     }
                     if (load_agent(p.team + xcd * 64) >= nwg) {
@@ -196,12 +195,19 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
                         }
                     }
                     if (__builtin_amdgcn_s_memrealtime() > deadline) {
-                        // no XCC team ever claimed the solve (a slot already left, or
-                        // another persistent grid holds the CUs): report the stall, or
-                        // the untouched u / v / plan would read as a finished solve
-                        keep = 0;
-                        store_wt(&p.info->stalled, 1);
-                        break;
+                        // no XCC team claimed the solve in time (a slot already left, or
+                        // another persistent grid holds the CUs): abandon it for the
+                        // one-workgroup fallback, or the untouched u / v / plan would read
+                        // as a finished solve -- unless a team claimed it meanwhile
+                        int expected = 0;
+                        if (__hip_atomic_compare_exchange_strong(p.team + 8 * 64, &expected, -1,
+                                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+                            keep = 0;
+                            mark_stalled(&p.info->stalled, kStallRegistration);
+                            break;
+                        }
+                        continue;  // claimed: the next pass reads the owner
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
@@ -545,7 +551,7 @@ __global__ __launch_bounds__(512) void sk_gather_kernel(SkGatherArgs<T> p) {
             }
         }
     }
-    if (status == OTF_SK_TIMEOUT && tid == 0) store_wt(&p.info->stalled, 1);
+    if (status == OTF_SK_TIMEOUT && tid == 0) mark_stalled(&p.info->stalled, kStallMid);
     if (lead) {
         p.info->last_good = last_good;
         p.info->niter = niter;

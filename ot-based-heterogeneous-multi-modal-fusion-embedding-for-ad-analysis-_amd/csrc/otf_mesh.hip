@@ -84,6 +84,7 @@ struct SkMeshArgs {
     int64_t ldp;
     unsigned long long timeout_ticks;
     unsigned long long reg_ticks;  // the first wait (registration / first hop)
+    ShiftArgs sh;                  // shifted kernel (SH instances): offsets + initial scalings
 };
 
 // Diagnostic build only (-DOTF_MESH_STAMPS, tools/stamps_mesh.hip): per-hop wall-clock
@@ -129,7 +130,9 @@ constexpr int pow2_at_least(int x) { return x <= 1 ? 1 : 2 * pow2_at_least((x + 
 // is a mesh of WHOLE tiles (n = SNRB * 128, m = SNCB * 512): every row / column bound
 // test and every derived count folds away, which also frees the scalar registers whose
 // spills (v_readlane / v_writelane per branch) lengthened every phase of the generic form.
-template <typename CT, typename TP, int KQ, int SNRB, int SNCB>
+// SH: the shifted POT kernel K~ = 2^(C ks + A_i + B_j) (otf_persist.h ShiftArgs), formed
+// once in the prologue like K; the loop is unchanged.
+template <typename CT, typename TP, int KQ, int SNRB, int SNCB, bool SH>
 __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     using T = float;
     constexpr int G = 2, VEC = 4, R = kMeshRW, NW = kMeshNW, TR = kMeshTR, TC = kMeshTC;
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         // take XCC roles: it reports the stall and leaves; the rest then stall on its
         // missing data and report it too -- never a plan from mixed roles
         if (!s_reg[3]) {
-            if (tid == 0) store_wt(&p.info->stalled, 1);
+            if (tid == 0) mark_stalled(&p.info->stalled, kStallRegistration);
             return;
         }
         if (s_reg[1]) {
@@ -260,10 +263,17 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             colc[g] = col_in(c0) ? c0 : 0;
         }
         const CT* crow = (const CT*)p.C + (int64_t)row0 * p.ldc;
+        V shb[G];  // B of this lane's columns (SH)
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            shb[g] = V{0, 0, 0, 0};
+            if (SH) shb[g] = *reinterpret_cast<const V*>(p.sh.B + colc[g]);
+        }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const CT* src = row_in(row0 + r) ? crow : (const CT*)p.C;
             const bool rok = row_in(row0 + r);
+            const T sha = SH && rok ? p.sh.A[row0 + r] : (T)0;
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const V c = load_cost<T>(src + colc[g]);
@@ -271,7 +281,9 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
                     const bool ok = rok && col_in(col0 + (lane + kWave * g) * VEC + k);
-                    e[k] = ok ? fast_exp(c[k] * ks) : (T)0;
+                    T z = c[k] * ks;
+                    if (SH) z += sha + shb[g][k];
+                    e[k] = ok ? fast_exp(z) : (T)0;
                 }
                 kv[r][g][0] = F2{e[0], e[1]};
                 kv[r][g][1] = F2{e[2], e[3]};
@@ -534,7 +546,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     {
         T wr[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) wr[r] = row_in(row0 + r) ? u0 : (T)0;
+        for (int r = 0; r < R; ++r) wr[r] = row_in(row0 + r) ? (SH ? p.sh.u0[row0 + r] : u0) : (T)0;
         col_partials(wr);
         __syncthreads();
         publish_cols(1, 0);
@@ -727,12 +739,16 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     const int hs = last_good & 1;
     T uo[R], vo[G][VEC];
 #pragma unroll
-    for (int r = 0; r < R; ++r) uo[r] = last_good < 0 ? u0 : uhist[hs][w * R + r];
+    for (int r = 0; r < R; ++r)
+        uo[r] = last_good >= 0 ? uhist[hs][w * R + r] : SH ? (row_in(row0 + r) ? p.sh.u0[row0 + r] : (T)0) : u0;
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int k = 0; k < VEC; ++k)
-            vo[g][k] = last_good < 0 ? v0 : vhist[hs][(lane + kWave * g) * VEC + k];
+        for (int k = 0; k < VEC; ++k) {
+            const int c = col0 + (lane + kWave * g) * VEC + k;
+            vo[g][k] = last_good >= 0 ? vhist[hs][(lane + kWave * g) * VEC + k]
+                                      : SH ? (col_in(c) ? p.sh.v0[c] : (T)0) : v0;
+        }
     if (cb == 0 && lane < R && row_in(row0 + lane)) {
         T mine = uo[0];
 #pragma unroll
@@ -771,7 +787,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             }
         }
     }
-    if (status == OTF_SK_TIMEOUT && tid == 0) store_wt(&p.info->stalled, 1);
+    if (status == OTF_SK_TIMEOUT && tid == 0) mark_stalled(&p.info->stalled, kStallMid);
     if (lead) {
         p.info->last_good = last_good;
         p.info->niter = niter;
@@ -783,15 +799,20 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     }
 }
 
-template <typename CT, typename TP>
-hipError_t launch_mesh_t(int grid, SkMeshArgs& p, hipStream_t s) {
-    void* args[] = {&p};
+template <typename CT, typename TP, bool SH>
+const void* mesh_kernel_for(const SkMeshArgs& p) {
     const bool pow2 = (p.nrb & (p.nrb - 1)) == 0;
     // the N = 4096 metric shape (32 x 8 whole tiles) has its own compiled-in instance
     const bool whole = p.n == p.nrb * kMeshTR && p.m == p.ncb * kMeshTC;
-    const void* k = (whole && p.nrb == 32 && p.ncb == 8) ? (const void*)sk_mesh_kernel<CT, TP, 4, 32, 8>
-                    : pow2 ? (const void*)sk_mesh_kernel<CT, TP, 4, 0, 0>
-                           : (const void*)sk_mesh_kernel<CT, TP, 8, 0, 0>;
+    return (whole && p.nrb == 32 && p.ncb == 8) ? (const void*)sk_mesh_kernel<CT, TP, 4, 32, 8, SH>
+           : pow2 ? (const void*)sk_mesh_kernel<CT, TP, 4, 0, 0, SH>
+                  : (const void*)sk_mesh_kernel<CT, TP, 8, 0, 0, SH>;
+}
+
+template <typename CT, typename TP>
+hipError_t launch_mesh_t(int grid, SkMeshArgs& p, hipStream_t s) {
+    void* args[] = {&p};
+    const void* k = p.sh.A ? mesh_kernel_for<CT, TP, true>(p) : mesh_kernel_for<CT, TP, false>(p);
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
     if (e != hipSuccess) return e;
@@ -851,7 +872,7 @@ template <typename CT>
 hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                    double* errlog, bool zeroed, hipStream_t s) {
+                    double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* shift) {
     if (!mesh_supported(n, m) || !region) return hipErrorInvalidValue;
     const MeshShape sh = mesh_shape(n, m);
     if (sh.nrb * sh.ncb > device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
@@ -890,6 +911,7 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
     p.ldp = ldp;
     p.timeout_ticks = stall_ticks();
     p.reg_ticks = reg_stall_ticks();
+    if (shift) p.sh = *shift;
     if (!zeroed) {  // else the Sinkhorn init kernel zeroed it
         const hipError_t e = hipMemsetAsync(region, 0, mesh_region_bytes(n, m), s);
         if (e != hipSuccess) return e;
@@ -906,10 +928,10 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
 template hipError_t run_mesh<float>(const float*, int64_t, int, int, const float*, const float*,
                                     const float*, const otf_sinkhorn_opts&, void*, float*, float*,
                                     void*, int64_t, int, otf_sinkhorn_info*, double*, bool,
-                                    hipStream_t);
+                                    hipStream_t, const ShiftArgs*);
 template hipError_t run_mesh<_Float16>(const _Float16*, int64_t, int, int, const float*, const float*,
                                        const float*, const otf_sinkhorn_opts&, void*, float*, float*,
                                        void*, int64_t, int, otf_sinkhorn_info*, double*, bool,
-                                       hipStream_t);
+                                       hipStream_t, const ShiftArgs*);
 
 }  // namespace otf

@@ -166,13 +166,28 @@ __device__ __forceinline__ void gstore_col(__amdgpu_buffer_rsrc_t rs, uint32_t o
         __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 16 /* sc1 */);
 }
 
+// otf_sinkhorn_info.stalled values.  A mid-solve stall (a hop or barrier that made no
+// progress for the stall limit) is reported as OTF_SK_TIMEOUT and never re-solved; only
+// a launch whose grid did not become co-resident at its registration is handed to the
+// one-workgroup fallback (sk_solo_kernel), which clears the word again.
+constexpr int kStallMid = 1;
+constexpr int kStallRegistration = 2;
+// raise the stalled word to at least v (a registration give-up is never downgraded by a
+// workgroup that reports its own timeout afterwards)
+__device__ __forceinline__ void mark_stalled(int* stalled, int v) {
+    __hip_atomic_fetch_max(stalled, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int kBarPoison = -(1 << 30);
+
 // Device-wide flat barrier: every wave drains its own memory operations, one lane per
 // workgroup arrives on the counter and polls it.  Returns false on a stall (flag
 // broadcast via LDS); re-arms `deadline` on success.
-// abandon (nullable, the solve's info->stalled): a registration barrier's give-up word.
-// The workgroup whose deadline passes raises it; every other one -- waiting, or arriving
-// late after the others left (a grid that was not co-resident) -- sees it and fails too,
-// instead of completing the count with workgroups that are gone.
+// abandon (nullable, the solve's info->stalled): a REGISTRATION barrier may give up.  The
+// give-up is a compare-and-swap that poisons the counter (a large negative value) only
+// while it is still short of the target, so every workgroup sees exactly one outcome:
+// the count completed (nobody can poison it any more) or it was poisoned (waiters and
+// late arrivals fail).  The poisoning workgroup then raises abandon to
+// kStallRegistration, which queues the solve for the one-workgroup fallback.
 __device__ __forceinline__ bool grid_barrier(int* bar, int target, unsigned long long& deadline,
                                              unsigned long long stall, int* s_flag,
                                              int* abandon = nullptr) {
@@ -180,20 +195,24 @@ __device__ __forceinline__ bool grid_barrier(int* bar, int target, unsigned long
     __syncthreads();
     if (threadIdx.x == 0) {
         int ok = 1;
-        __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (load_agent(bar) < target) {
-            if (abandon && load_agent(abandon)) {
-                ok = 0;
-                break;
-            }
+        const int old = __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old < 0) ok = 0;  // arrived after the launch gave up
+        while (ok) {
+            int c = load_agent(bar);
+            if (c >= target) break;
+            if (c < 0) { ok = 0; break; }
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() > deadline) {
-                ok = 0;
-                if (abandon) store_wt(abandon, 1);
-                break;
+                if (!abandon) { ok = 0; break; }
+                if (__hip_atomic_compare_exchange_strong(bar, &c, kBarPoison, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    mark_stalled(abandon, kStallRegistration);
+                    ok = 0;
+                    break;
+                }
+                // the count moved since the load: look again (it may have completed)
             }
         }
-        if (ok && abandon && load_agent(abandon)) ok = 0;
         *s_flag = ok;
     }
     __syncthreads();
@@ -269,6 +288,16 @@ __device__ __forceinline__ bool register_grid(const SkSync& sy, int* bar, int xc
     return ok;
 }
 
+// Shifted POT kernel (opts.shift, float32 compute; otf_sinkhorn.hip sk_shift_prepass):
+// K~_ij = 2^(C_ij ks + A_i + B_j), initial scalings u~0 = 2^-A / n, v~0 = 2^-B / m.
+// Passed to the persistent engines that support it (mesh, sweep); null = plain POT kernel.
+struct ShiftArgs {
+    const float* A;
+    const float* B;
+    const float* u0;
+    const float* v0;
+};
+
 // Sweep engine (otf_sweep.hip): persistent streaming solve for costs that do not fit
 // the register files.  Host entry points; `region` is zeroed by the launcher.
 template <typename T> size_t sweep_region_bytes(int64_t m_pad);
@@ -287,7 +316,7 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
                      const T* b_pad, const T* cost_scale, const otf_sinkhorn_opts& o, void* region,
                      T* u_out, T* v_out, void* P_out, int64_t ldp, int P_dtype,
                      otf_sinkhorn_info* info, double* errlog, hipStream_t s,
-                     const XSweep* xs = nullptr);
+                     const XSweep* xs = nullptr, const ShiftArgs* sh = nullptr);
 
 // Gather engine (otf_gather.hip): small problems (<= 16 row tiles, m <= 512), column
 // partials exchanged as epoch-tagged granules, no barrier.  `region` is zeroed by the
@@ -311,6 +340,6 @@ template <typename CT>
 hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                    double* errlog, bool zeroed, hipStream_t s);
+                    double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* sh = nullptr);
 
 }  // namespace otf

@@ -64,6 +64,12 @@ template <typename T> struct SkArgs {
     int check_off;         // POT checks at ii % 10 == 0, OTT after every 10th update
     int err_squared;
     int m_pad;
+    // shifted POT kernel (opts.shift, float): K~_ij = exp2(C_ij ks + shA_i + shB_j), the
+    // scalings start from u0v (u~0 = 2^-shA / n); null otherwise
+    const T* shA;
+    const T* shB;
+    const T* u0v;
+    const T* v0v;          // v~0 = 2^-shB / m (the initial iterate POT reverts to)
 };
 
 __device__ __forceinline__ void sk_stop(otf_sinkhorn_info* info, int last_good, int niter,
@@ -130,8 +136,9 @@ __device__ __forceinline__ double marginal_err(const SkArgs<T>& p, const T* vit,
 // One fused Sinkhorn pass.  NT threads own G chunks of VEC contiguous columns each
 // (chunk q = tid + NT*g), R rows per row block; K values for a row block stay in
 // registers (R*G*VEC of them) between the row reduction and the column update.
-template <typename T, typename CT, bool LOG, int G, int R>
+template <typename T, typename CT, bool LOG, int G, int R, bool SH = false>
 __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p) {
+    static_assert(!(LOG && SH), "the shifted kernel is a POT-flavour form");
     constexpr int VEC = Vec<T>::N;
     using V = typename Vec<T>::type;
     __shared__ __attribute__((aligned(16))) T colbuf[512 * G * VEC];  // column partials
@@ -240,7 +247,7 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p) {
                             vw[g][k] = 1;
                         } else {
                             vw[g][k] = val;
-                            go[g][k] = 0;
+                            go[g][k] = SH && cok[g][k] ? p.shB[colc[g] + k] : (T)0;
                         }
                         if (blockIdx.x == 0 && cok[g][k]) p.v_cur[colc[g] + k] = val;
                     }
@@ -256,7 +263,7 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p) {
 #pragma unroll
                     for (int k = 0; k < VEC; ++k) {
                         vw[g][k] = 1;
-                        go[g][k] = 0;
+                        go[g][k] = SH && cok[g][k] ? p.shB[colc[g] + k] : (T)0;
                         if (LOG) {  // g_{-1} = column minima of the scaled cost: terms <= 1
                             const T h = (T)((double)key_val(p.cmin_key[colc[g] + k]) * cinv);
                             go[g][k] = cok[g][k] ? h * gl : (T)0;
@@ -270,7 +277,7 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int row = r0 + r < p.n ? r0 + r : p.n - 1;
-            fo[r] = (LOG && p.it >= 0) ? p.u_prev[row] * gl : (T)0;
+            fo[r] = (LOG && p.it >= 0) ? p.u_prev[row] * gl : SH ? p.shA[row] : (T)0;
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -280,7 +287,7 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p) {
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
                     T z = kv[r][g][k] * ks;
-                    if (LOG) z += fo[r] + go[g][k];
+                    if (LOG || SH) z += fo[r] + go[g][k];
                     kv[r][g][k] = (rok && cok[g][k]) ? fast_exp(z) : (T)0;
                 }
         }
@@ -329,7 +336,10 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p) {
         } else {
             const T u0 = LOG ? (T)1 : (T)1 / (T)p.n_total;
 #pragma unroll
-            for (int r = 0; r < R; ++r) ur[r] = u0;
+            for (int r = 0; r < R; ++r) {
+                ur[r] = u0;
+                if (SH) ur[r] = r0 + r < p.n ? p.u0v[r0 + r] : (T)0;  // u~0 = 2^-shA / n
+            }
         }
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -358,9 +368,9 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p) {
     // ---- zero the column-sum buffer of the next pass (nobody touches it now)
     for (int j = blockIdx.x * NT + tid; j <= p.m_pad; j += gridDim.x * NT) p.cs_zero[j] = 0;
 }
-template <typename T, typename CT, bool LOG, int G, int R>
+template <typename T, typename CT, bool LOG, int G, int R, bool SH>
 __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
-    sk_pass_body<T, CT, LOG, G, R>(p);
+    sk_pass_body<T, CT, LOG, G, R, SH>(p);
 }
 
 template <typename T>
@@ -407,6 +417,138 @@ __global__ __launch_bounds__(256) void sk_colmin_kernel(const CT* C, int64_t ldc
     float mn = INFINITY;
     for (int i = i0; i < i1; ++i) mn = fminf(mn, (float)C[(int64_t)i * ldc + j]);
     if (i0 < i1) atomicMin(cmin_key + j, ord_key(mn));
+}
+
+// ---- Shifted POT kernel (opts.shift, float32 compute) -------------------------------
+// POT's K = exp(-C/reg) leaves float32's normal range once C/reg > 87 (reg < 0.0115 on a
+// max-normalised cost): v_exp_f32 flushes those entries to zero, and POT's scalings,
+// which grow like exp(C/reg), overflow past 88.  Both matter: at reg = 0.01 on the
+// metric shape the flushed entries alone move the plan by 2.2e-3 (normwise) after 100
+// iterations, and at reg = 5e-3 whole columns of K vanish (a break at iteration 0).
+// The shifted form runs POT's iteration on
+//     K~_ij = 2^(C_ij ks + A_i + B_j),   u = 2^A u~,   v = 2^B v~,
+// which in exact arithmetic is the same sequence of iterates (the offsets cancel in
+// v = b / K^T u and u = a / K v, and P = u~ K~ v~ = u K v), with offsets taken from a
+// log-domain first half-iteration:
+//     B_j = log2 b_j - log2 sum_i 2^(C_ij ks) / n     (= log2 of POT's first v, exactly)
+//     A_i = -max_j (C_ij ks + B_j)                    (every row of K~ peaks at 1)
+// and the start u~0 = 2^-A / n (POT's u0 = 1/n).  K~ is then the first half-step's plan up
+// to row factors: its entries that underflow are those far below their row's mass, so
+// no plan entry that matters is ever formed from a flushed value, and u~, v~ stay near 1
+// (|log2| < 60 over 100 iterations at reg = 2e-3 on the metric shape).  Cost: one column
+// log-sum-exp pass and one row max pass over C before the solve.
+constexpr int kShChunkMax = 128;  // row chunks of the column pass (partials in the workspace)
+inline int shift_chunks(int64_t n) {
+    const int64_t c = (n + 31) / 32;
+    return (int)(c < 1 ? 1 : c > kShChunkMax ? kShChunkMax : c);
+}
+
+__device__ __forceinline__ float shift_ks(const float* cost_scale, double reg) {
+    double cinv = 1.0;
+    if (cost_scale) cinv = 1.0 / (double)cost_scale[0];
+    return (float)(-exp_unit<float>() / reg * cinv);
+}
+
+// (max, sum 2^(z - max)) of z = C_ij ks over one row chunk, 4 columns per thread
+template <typename CT>
+__global__ __launch_bounds__(256) void sk_shift_cols_kernel(const CT* C, int64_t ldc, int n, int m,
+                                                            int m_pad, const float* cost_scale,
+                                                            double reg, float* pmax, float* psum) {
+    using V = Vec<float>::type;
+    const float ks = shift_ks(cost_scale, reg);
+    const int c0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (c0 >= m_pad) return;
+    const int rows_per = (n + gridDim.y - 1) / gridDim.y;
+    const int i0 = blockIdx.y * rows_per;
+    const int i1 = i0 + rows_per < n ? i0 + rows_per : n;
+    const CT* col = C + (c0 < m ? c0 : 0);
+    float mx[4], sm[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        mx[k] = -3.0e38f;
+        sm[k] = 0.f;
+    }
+    int i = i0;
+    for (; i + 4 <= i1; i += 4) {
+        V c[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] = load_cost<float>(col + (int64_t)(i + r) * ldc);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float z[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[r] = c[r][k] * ks;
+            const float bm = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
+            const float nm = fmaxf(mx[k], bm);
+            float t = sm[k] * fast_exp(mx[k] - nm);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t += fast_exp(z[r] - nm);
+            sm[k] = t;
+            mx[k] = nm;
+        }
+    }
+    for (; i < i1; ++i) {
+        const V c = load_cost<float>(col + (int64_t)i * ldc);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float z = c[k] * ks, nm = fmaxf(mx[k], z);
+            sm[k] = sm[k] * fast_exp(mx[k] - nm) + fast_exp(z - nm);
+            mx[k] = nm;
+        }
+    }
+    const int64_t o = (int64_t)blockIdx.y * m_pad + c0;
+    *reinterpret_cast<V*>(pmax + o) = V{mx[0], mx[1], mx[2], mx[3]};
+    *reinterpret_cast<V*>(psum + o) = V{sm[0], sm[1], sm[2], sm[3]};
+}
+
+// B_j from the chunk partials; v~0_j = 2^-B_j / m.  Columns past m: B = 0, v~0 = 0.
+__global__ void sk_shift_merge_kernel(const float* pmax, const float* psum, int nch, int m, int m_pad,
+                                      const float* b_pad, int n_total, float* shB, float* v0v) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m_pad) return;
+    if (j >= m) {
+        shB[j] = 0.f;
+        v0v[j] = 0.f;
+        return;
+    }
+    float M = -3.0e38f;
+    for (int q = 0; q < nch; ++q) M = fmaxf(M, pmax[(int64_t)q * m_pad + j]);
+    float S = 0.f;
+    for (int q = 0; q < nch; ++q) S += psum[(int64_t)q * m_pad + j] * fast_exp(pmax[(int64_t)q * m_pad + j] - M);
+    const float bj = b_pad[j];
+    // a zero marginal keeps v = 0 in POT; its shift only has to be finite
+    const float B = (bj > 0.f ? __builtin_amdgcn_logf(bj) : 0.f) + __builtin_amdgcn_logf((float)n_total) -
+                    (M + __builtin_amdgcn_logf(S));
+    shB[j] = B;
+    v0v[j] = fast_exp(-B - __builtin_amdgcn_logf((float)m));
+}
+
+// A_i = -max_j (C_ij ks + B_j), u~0_i = 2^-A_i / n: one wave per row
+template <typename CT>
+__global__ __launch_bounds__(256) void sk_shift_rows_kernel(const CT* C, int64_t ldc, int n, int m,
+                                                            const float* cost_scale, double reg,
+                                                            const float* shB, int n_total,
+                                                            float* shA, float* u0v) {
+    using V = Vec<float>::type;
+    const float ks = shift_ks(cost_scale, reg);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const float ln = __builtin_amdgcn_logf((float)n_total);
+    for (int row = blockIdx.x * 4 + wv; row < n; row += gridDim.x * 4) {
+        const CT* crow = C + (int64_t)row * ldc;
+        float mx = -3.0e38f;
+        for (int c0 = lane * 4; c0 < m; c0 += 256) {
+            const V c = load_cost<float>(crow + c0);
+            const V b = *reinterpret_cast<const V*>(shB + c0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (c0 + k < m) mx = fmaxf(mx, fmaf(c[k], ks, b[k]));
+        }
+        mx = wave_max(mx);
+        if (lane == 0) {
+            shA[row] = -mx;
+            u0v[row] = fast_exp(mx - ln);
+        }
+    }
 }
 
 // Decides the outcome of the last pass when the loop ran to max_iter.
@@ -457,23 +599,27 @@ __global__ __launch_bounds__(512) void sk_finalize_kernel(SkArgs<T> p, int max_i
 }
 
 // Copies the scalings of info->last_good (or the initial ones) to the outputs.
+// (shifted kernel: the initial scalings are the vectors u0v, v0v)
 template <typename T, bool LOG>
 __global__ void sk_output_kernel(const T* u2, const T* v2, int n, int n_total, int m, int m_pad,
-                                 const otf_sinkhorn_info* info, T* u_out, T* v_out) {
+                                 const otf_sinkhorn_info* info, T* u_out, T* v_out,
+                                 const T* u0v, const T* v0v) {
     const int lg = info->last_good;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int stride = gridDim.x * blockDim.x;
     const T u0 = LOG ? (T)0 : (T)1 / (T)n_total;
     const T v0 = LOG ? (T)0 : (T)1 / (T)m;
-    for (int i = t; i < n; i += stride) u_out[i] = lg >= 0 ? u2[(lg & 1) * n + i] : u0;
-    for (int j = t; j < m; j += stride) v_out[j] = lg >= 0 ? v2[(lg & 1) * m_pad + j] : v0;
+    for (int i = t; i < n; i += stride) u_out[i] = lg >= 0 ? u2[(lg & 1) * n + i] : u0v ? u0v[i] : u0;
+    for (int j = t; j < m; j += stride) v_out[j] = lg >= 0 ? v2[(lg & 1) * m_pad + j] : v0v ? v0v[j] : v0;
 }
 
 // POT: P_ij = u_i exp(-C_ij/reg') v_j;  OTT: P_ij = exp((f_i + g_j - C_ij/scale)/reg).
+// (shifted kernel, shA != null: P_ij = u_i exp2(C_ij ks + shA_i + shB_j) v_j)
 template <typename T, typename CT, typename TP, bool LOG>
 __global__ __launch_bounds__(256) void sk_plan_kernel(const CT* C, int64_t ldc, int n, int m,
                                                       const T* u, const T* v, const T* cost_scale,
-                                                      double reg, TP* P, int64_t ldp) {
+                                                      double reg, TP* P, int64_t ldp,
+                                                      const T* shA, const T* shB) {
     const double unit = exp_unit<T>();
     double cinv = 1.0;
     if (cost_scale) cinv = 1.0 / (double)cost_scale[0];
@@ -484,6 +630,7 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const CT* C, int64_t ldc, 
     using VP = __attribute__((ext_vector_type(VEC))) TP;
     for (int row = blockIdx.x; row < n; row += gridDim.x) {
         const T ui = u[row];
+        const T ai = shA ? shA[row] : (T)0;
         const CT* crow = C + (int64_t)row * ldc;
         TP* prow = P + (int64_t)row * ldp;
         for (int j0 = threadIdx.x * VEC; j0 < m; j0 += blockDim.x * VEC) {
@@ -492,9 +639,10 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const CT* C, int64_t ldc, 
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
                 const T vj = j0 + k < m ? v[j0 + k] : (T)0;
+                const T bj = (shB && j0 + k < m) ? shB[j0 + k] : (T)0;
                 T val;
                 if (LOG) val = fast_exp(c[k] * ks + (ui + vj) * gl);
-                else val = ui * fast_exp(c[k] * ks) * vj;
+                else val = ui * fast_exp(c[k] * ks + (ai + bj)) * vj;
                 out[k] = (TP)val;
             }
             if (j0 + VEC <= m) {
@@ -512,7 +660,9 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const CT* C, int64_t ldc, 
 // Solo fallback: the whole POT solve in ONE workgroup, enqueued behind every persistent
 // engine launch on the same stream.  A persistent engine needs its whole grid
 // co-resident; when other kernels hold CUs (RCCL kernels under DDP, a second solve on
-// another stream) its registration gives up after OTF_REG_MS and sets info->stalled.
+// another stream) its registration gives up after OTF_REG_MS and sets info->stalled to
+// kStallRegistration (a stall in the middle of a solve sets kStallMid and is reported as
+// OTF_SK_TIMEOUT, never re-solved: it means a broken exchange, not a busy device).
 // This kernel then returns the right answer instead of a timeout: a single workgroup is
 // always schedulable, its __syncthreads is a grid barrier, so the streaming pass runs
 // as a loop (every row block per pass, an L1 invalidate between passes for the sums the
@@ -534,12 +684,16 @@ template <typename T> struct SoloArgs {
     void* P;
     int64_t ldp;
     int p_f64;
+    const T* v0v;       // shifted kernel: the initial column scalings (else null)
 };
 
-template <typename T, typename CT, int G, int R>
+template <typename T, typename CT, int G, int R, bool SH>
 __global__ __launch_bounds__(512) void sk_solo_kernel(SkArgs<T> p, SoloArgs<T> x) {
     __shared__ int s_go;
-    if (threadIdx.x == 0) s_go = __hip_atomic_load(&p.info->stalled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // only a grid that never became co-resident (registration give-up) is re-solved here;
+    // a mid-solve stall stays an OTF_SK_TIMEOUT for the caller to see
+    if (threadIdx.x == 0)
+        s_go = __hip_atomic_load(&p.info->stalled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kStallRegistration;
     __syncthreads();
     if (!s_go) return;
     const int tid = threadIdx.x, NT = blockDim.x;
@@ -579,7 +733,7 @@ __global__ __launch_bounds__(512) void sk_solo_kernel(SkArgs<T> p, SoloArgs<T> x
     for (int pass = 0; pass <= x.max_iter; ++pass) {
         SkArgs<T> q = p;
         set_pass(q, pass);
-        sk_pass_body<T, CT, false, G, R>(q);
+        sk_pass_body<T, CT, false, G, R, SH>(q);
         sync_mem();
         if (__hip_atomic_load(&p.info->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     }
@@ -594,8 +748,8 @@ __global__ __launch_bounds__(512) void sk_solo_kernel(SkArgs<T> p, SoloArgs<T> x
     // outputs: the scalings of last_good (or the initial ones), then the plan
     const int lg = p.info->last_good;
     const T u0 = (T)1 / (T)p.n_total, v0 = (T)1 / (T)p.m;
-    for (int i = tid; i < p.n; i += NT) x.u_out[i] = lg >= 0 ? x.u2[(lg & 1) * p.n + i] : u0;
-    for (int j = tid; j < p.m; j += NT) x.v_out[j] = lg >= 0 ? x.v2[(lg & 1) * p.m_pad + j] : v0;
+    for (int i = tid; i < p.n; i += NT) x.u_out[i] = lg >= 0 ? x.u2[(lg & 1) * p.n + i] : SH ? p.u0v[i] : u0;
+    for (int j = tid; j < p.m; j += NT) x.v_out[j] = lg >= 0 ? x.v2[(lg & 1) * p.m_pad + j] : SH ? x.v0v[j] : v0;
     sync_mem();
     if (x.P) {
         const double unit = exp_unit<T>();
@@ -605,8 +759,10 @@ __global__ __launch_bounds__(512) void sk_solo_kernel(SkArgs<T> p, SoloArgs<T> x
         const CT* C = (const CT*)p.C;
         for (int row = 0; row < p.n; ++row) {
             const T ui = x.u_out[row];
+            const T ai = SH ? p.shA[row] : (T)0;
             for (int j = tid; j < p.m; j += NT) {
-                const T val = ui * fast_exp((T)C[(int64_t)row * p.ldc + j] * ks) * x.v_out[j];
+                const T z = (T)C[(int64_t)row * p.ldc + j] * ks + (SH ? ai + p.shB[j] : (T)0);
+                const T val = ui * fast_exp(z) * x.v_out[j];
                 if (x.p_f64) ((double*)x.P)[(int64_t)row * x.ldp + j] = (double)val;
                 else ((float*)x.P)[(int64_t)row * x.ldp + j] = (float)val;
             }
@@ -1049,7 +1205,7 @@ __global__ __launch_bounds__(512) void sk_resident_kernel(SkResArgs<T> p) {
             }
         }
     }
-    if (status == OTF_SK_TIMEOUT && threadIdx.x == 0) store_wt(&p.info->stalled, 1);
+    if (status == OTF_SK_TIMEOUT && threadIdx.x == 0) mark_stalled(&p.info->stalled, kStallMid);
     if (lead) {
         p.info->last_good = last_good;
         p.info->niter = niter;
@@ -1498,7 +1654,7 @@ __global__ __launch_bounds__(512) void sk_tiled_kernel(SkTileArgs<T> p) {
             }
         }
     }
-    if (status == OTF_SK_TIMEOUT && threadIdx.x == 0) store_wt(&p.info->stalled, 1);
+    if (status == OTF_SK_TIMEOUT && threadIdx.x == 0) mark_stalled(&p.info->stalled, kStallMid);
     if (lead) {
         p.info->last_good = last_good;
         p.info->niter = niter;
@@ -1542,16 +1698,23 @@ template <typename T> int64_t row_blocks(int64_t n, int64_t m) {
     return (n + c.R - 1) / c.R;
 }
 
-template <typename T, typename CT, bool LOG>
-hipError_t launch_pass(const PassCfg& c, int grid, const SkArgs<T>& p, hipStream_t s) {
+template <typename T, typename CT, bool LOG, bool SH>
+hipError_t launch_pass_sh(const PassCfg& c, int grid, const SkArgs<T>& p, hipStream_t s) {
     switch (c.G) {
-        case 1: sk_pass_kernel<T, CT, LOG, 1, pass_rows<T>(1)><<<grid, c.NT, 0, s>>>(p); break;
-        case 2: sk_pass_kernel<T, CT, LOG, 2, pass_rows<T>(2)><<<grid, c.NT, 0, s>>>(p); break;
-        case 4: sk_pass_kernel<T, CT, LOG, 4, pass_rows<T>(4)><<<grid, c.NT, 0, s>>>(p); break;
-        case 8: sk_pass_kernel<T, CT, LOG, 8, pass_rows<T>(8)><<<grid, c.NT, 0, s>>>(p); break;
+        case 1: sk_pass_kernel<T, CT, LOG, 1, pass_rows<T>(1), SH><<<grid, c.NT, 0, s>>>(p); break;
+        case 2: sk_pass_kernel<T, CT, LOG, 2, pass_rows<T>(2), SH><<<grid, c.NT, 0, s>>>(p); break;
+        case 4: sk_pass_kernel<T, CT, LOG, 4, pass_rows<T>(4), SH><<<grid, c.NT, 0, s>>>(p); break;
+        case 8: sk_pass_kernel<T, CT, LOG, 8, pass_rows<T>(8), SH><<<grid, c.NT, 0, s>>>(p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+// the shifted-kernel instance when the args carry offsets (float POT only)
+template <typename T, typename CT, bool LOG>
+hipError_t launch_pass(const PassCfg& c, int grid, const SkArgs<T>& p, hipStream_t s) {
+    if constexpr (!LOG && sizeof(T) == 4)
+        if (p.shA) return launch_pass_sh<T, CT, LOG, true>(c, grid, p, s);
+    return launch_pass_sh<T, CT, LOG, false>(c, grid, p, s);
 }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -1584,6 +1747,13 @@ struct Workspace {
     size_t gather_bytes;
     void* mesh;       // mesh engine granules (otf_mesh.hip); 0 bytes if not taken
     size_t mesh_bytes;
+    // shifted kernel (float only): row / column exponent offsets, initial scalings, and the
+    // column pass's chunk partials
+    float* shA;
+    float* shB;
+    float* u0v;
+    float* v0v;
+    float* shpart;
     int nrep;
     size_t bytes;
     int64_t m_pad;
@@ -1643,6 +1813,13 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.gather = take(w.gather_bytes);
     w.mesh_bytes = esz == 4 ? mesh_region_bytes(n, m) : 0;
     w.mesh = take(w.mesh_bytes);
+    if (esz == 4) {
+        w.shA = (float*)take(sizeof(float) * (size_t)n);
+        w.u0v = (float*)take(sizeof(float) * (size_t)n);
+        w.shB = (float*)take(sizeof(float) * (size_t)w.m_pad);
+        w.v0v = (float*)take(sizeof(float) * (size_t)w.m_pad);
+        w.shpart = (float*)take(2 * sizeof(float) * (size_t)shift_chunks(n) * w.m_pad);
+    }
     w.bytes = off;
     return w;
 }
@@ -1833,6 +2010,14 @@ SkArgs<T> sk_args(const SkSetup<T>& su, const CT* C, int64_t ldc, int64_t n, int
     p.check_off = LOG ? 1 : 0;
     p.err_squared = LOG ? 0 : o.err_squared;
     p.m_pad = su.m_pad;
+    if constexpr (!LOG && sizeof(T) == 4) {
+        if (o.shift) {
+            p.shA = (const T*)su.w.shA;
+            p.shB = (const T*)su.w.shB;
+            p.u0v = (const T*)su.w.u0v;
+            p.v0v = (const T*)su.w.v0v;
+        }
+    }
     return p;
 }
 
@@ -1879,17 +2064,19 @@ int sk_finish(SkArgs<T>& p, const SkSetup<T>& su, const CT* C, int64_t ldc, int6
     sk_finalize_kernel<T, LOG><<<1, 512, 0, s>>>(p, o.max_iter);
     OTF_HIP(hipGetLastError());
     sk_output_kernel<T, LOG><<<64, 256, 0, s>>>((const T*)su.w.u2, (const T*)su.w.v2, (int)n,
-                                                p.n_total, (int)m, su.m_pad, info, u_out, v_out);
+                                                p.n_total, (int)m, su.m_pad, info, u_out, v_out,
+                                                p.u0v, p.v0v);
     OTF_HIP(hipGetLastError());
     if (P_out) {
         const int pgrid = n < 4096 ? (int)n : 4096;
         if (P_dtype == OTF_F32)
             sk_plan_kernel<T, CT, float, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out, v_out,
-                                                                   cost_scale, o.reg, (float*)P_out, ldp);
+                                                                   cost_scale, o.reg, (float*)P_out, ldp,
+                                                                   p.shA, p.shB);
         else
             sk_plan_kernel<T, CT, double, LOG><<<pgrid, 256, 0, s>>>(C, ldc, (int)n, (int)m, u_out,
                                                                     v_out, cost_scale, o.reg,
-                                                                    (double*)P_out, ldp);
+                                                                    (double*)P_out, ldp, p.shA, p.shB);
         OTF_HIP(hipGetLastError());
     }
     return OTF_OK;
@@ -1905,16 +2092,51 @@ hipError_t launch_solo(const SkSetup<T>& su, const CT* C, int64_t ldc, int64_t n
     if (!fallback_enabled()) return hipSuccess;
     SkArgs<T> p = sk_args<T, CT, false>(su, C, ldc, n, m, cost_scale, o, info, errlog, false);
     SoloArgs<T> x{(T*)su.w.cs, (T*)su.w.u2, (T*)su.w.v2, su.w.cs_stride, o.max_iter, u_out, v_out,
-                  P_out, ldp, P_dtype == OTF_F64 ? 1 : 0};
+                  P_out, ldp, P_dtype == OTF_F64 ? 1 : 0, p.v0v};
     const PassCfg& c = su.cfg;
+    if (p.shA) {
+        if constexpr (sizeof(T) == 4) {
+            switch (c.G) {
+                case 1: sk_solo_kernel<T, CT, 1, pass_rows<T>(1), true><<<1, c.NT, 0, s>>>(p, x); break;
+                case 2: sk_solo_kernel<T, CT, 2, pass_rows<T>(2), true><<<1, c.NT, 0, s>>>(p, x); break;
+                case 4: sk_solo_kernel<T, CT, 4, pass_rows<T>(4), true><<<1, c.NT, 0, s>>>(p, x); break;
+                case 8: sk_solo_kernel<T, CT, 8, pass_rows<T>(8), true><<<1, c.NT, 0, s>>>(p, x); break;
+                default: return hipErrorInvalidValue;
+            }
+            return hipGetLastError();
+        }
+    }
     switch (c.G) {
-        case 1: sk_solo_kernel<T, CT, 1, pass_rows<T>(1)><<<1, c.NT, 0, s>>>(p, x); break;
-        case 2: sk_solo_kernel<T, CT, 2, pass_rows<T>(2)><<<1, c.NT, 0, s>>>(p, x); break;
-        case 4: sk_solo_kernel<T, CT, 4, pass_rows<T>(4)><<<1, c.NT, 0, s>>>(p, x); break;
-        case 8: sk_solo_kernel<T, CT, 8, pass_rows<T>(8)><<<1, c.NT, 0, s>>>(p, x); break;
+        case 1: sk_solo_kernel<T, CT, 1, pass_rows<T>(1), false><<<1, c.NT, 0, s>>>(p, x); break;
+        case 2: sk_solo_kernel<T, CT, 2, pass_rows<T>(2), false><<<1, c.NT, 0, s>>>(p, x); break;
+        case 4: sk_solo_kernel<T, CT, 4, pass_rows<T>(4), false><<<1, c.NT, 0, s>>>(p, x); break;
+        case 8: sk_solo_kernel<T, CT, 8, pass_rows<T>(8), false><<<1, c.NT, 0, s>>>(p, x); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+// The shifted kernel's offsets (opts.shift): column log-sum-exp pass, merge, row max pass.
+// Runs after sk_init (b_pad holds b).  float compute only.
+template <typename CT>
+int sk_shift_prepass(const SkSetup<float>& su, const CT* C, int64_t ldc, int64_t n, int64_t m,
+                     int n_total, const float* cost_scale, double reg, hipStream_t s) {
+    const int nch = shift_chunks(n);
+    const int m_pad = su.m_pad;
+    float* pmax = su.w.shpart;
+    float* psum = su.w.shpart + (size_t)nch * m_pad;
+    sk_shift_cols_kernel<CT><<<dim3((unsigned)((m_pad + 1023) / 1024), (unsigned)nch), 256, 0, s>>>(
+        C, ldc, (int)n, (int)m, m_pad, cost_scale, reg, pmax, psum);
+    OTF_HIP(hipGetLastError());
+    sk_shift_merge_kernel<<<(m_pad + 255) / 256, 256, 0, s>>>(pmax, psum, nch, (int)m, m_pad,
+                                                              (const float*)su.w.b_pad, n_total,
+                                                              su.w.shB, su.w.v0v);
+    OTF_HIP(hipGetLastError());
+    const int64_t rg = (n + 3) / 4;
+    sk_shift_rows_kernel<CT><<<(unsigned)(rg < 2048 ? rg : 2048), 256, 0, s>>>(
+        C, ldc, (int)n, (int)m, cost_scale, reg, su.w.shB, n_total, su.w.shA, su.w.u0v);
+    OTF_HIP(hipGetLastError());
+    return OTF_OK;
 }
 
 // OTF_GATHER=0 keeps AUTO off the gather engine (A/B measurements); GATHER still forces it
@@ -1950,6 +2172,9 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     if (rc != OTF_OK) return rc;
     double* errlog = errlog_user ? errlog_user : su.w.errlog;
     const bool whole = o.n_total <= 0 || o.n_total == n;
+    // shifted kernel: float32 POT on the whole problem, mesh / sweep / stream engines
+    const bool sh = o.shift != 0;
+    if (sh && (LOG || sizeof(T) != 4 || !whole)) return OTF_EUNSUPPORTED;
     // the mesh engine's region is zeroed by the init kernel (no memset launch)
     bool mesh_pick = false;
     if constexpr (sizeof(T) == 4)
@@ -1959,12 +2184,21 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
                                                      !(gather_supported<T>(n, m) && su.w.gather_bytes > 0)));
     // gather engine: small problems, one granule hop per iteration, no barrier (and
     // deterministic by construction); its region is zeroed by the init kernel too
-    const bool gfits = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && gather_supported<T>(n, m) &&
-                       su.w.gather_bytes > 0;
+    const bool gfits = !LOG && !sh && !avg_pass_ms && whole && o.max_iter >= 1 &&
+                       gather_supported<T>(n, m) && su.w.gather_bytes > 0;
     const bool gather_pick = gfits && (o.engine == OTF_ENGINE_GATHER || (o.engine == OTF_ENGINE_AUTO && gather_enabled()));
     rc = sk_init<T>(su, a, b, n, m, info, s, mesh_pick ? su.w.mesh : gather_pick ? su.w.gather : nullptr,
                     mesh_pick ? su.w.mesh_bytes : gather_pick ? su.w.gather_bytes : 0);
     if (rc != OTF_OK) return rc;
+    ShiftArgs shargs{};
+    if constexpr (sizeof(T) == 4) {
+        if (sh) {
+            rc = sk_shift_prepass<CT>(su, C, ldc, n, m, (int)n, (const float*)cost_scale, o.reg, s);
+            if (rc != OTF_OK) return rc;
+            shargs = ShiftArgs{su.w.shA, su.w.shB, su.w.u0v, su.w.v0v};
+        }
+    }
+    const ShiftArgs* shp = sh ? &shargs : nullptr;
 
     if (o.engine == OTF_ENGINE_GATHER && !gfits) return OTF_EUNSUPPORTED;
     if (gather_pick) {
@@ -1988,7 +2222,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
             const hipError_t e = run_mesh<CT>(C, ldc, (int)n, (int)m, (const float*)su.w.a_pad,
                                               (const float*)su.w.b_pad, cost_scale, o, su.w.mesh,
                                               u_out, v_out, P_out, ldp, P_dtype, info, errlog,
-                                              /*zeroed=*/mesh_pick, s);
+                                              /*zeroed=*/mesh_pick, s, shp);
             if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
             (void)hipGetLastError();
             if (o.engine == OTF_ENGINE_MESH) return check_hip(e);
@@ -2001,7 +2235,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
             return OTF_EUNSUPPORTED;
         const hipError_t e = run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
                                               (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
-                                              v_out, P_out, ldp, P_dtype, info, errlog, s);
+                                              v_out, P_out, ldp, P_dtype, info, errlog, s, nullptr, shp);
         if (e != hipSuccess) return check_hip(e);
         return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
     }
@@ -2014,10 +2248,10 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     // AUTO takes it for float only: for float64 (64-row tiles) it measured no faster
     // than the row-block resident engine (config 2, d = 512: 12.8 vs 12.3 ms per step --
     // both sit on the ~5 us grid-sync round trip per iteration); TILED forces it
-    const bool want_tiled = !LOG && !avg_pass_ms && tfits && o.max_iter >= 1 &&
+    const bool want_tiled = !LOG && !sh && !avg_pass_ms && tfits && o.max_iter >= 1 &&
                             (o.engine == OTF_ENGINE_TILED ||
                              (o.engine == OTF_ENGINE_AUTO && sizeof(T) == 4));
-    if (o.engine == OTF_ENGINE_TILED && (LOG || !tfits)) return OTF_EUNSUPPORTED;
+    if (o.engine == OTF_ENGINE_TILED && (LOG || sh || !tfits)) return OTF_EUNSUPPORTED;
     if (want_tiled) {
         Workspace w = su.w;
         const hipError_t e = run_tiled<T, CT>(C, ldc, (int)n, (int)m, cost_scale, o, w, u_out, v_out,
@@ -2028,7 +2262,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     }
     // AUTO reaches here only when the tiled engine did not take the solve (shape, dtype
     // or co-residency refused), so the row-block resident engine is the next choice
-    const bool want_res = !LOG && !avg_pass_ms && fits && o.max_iter >= 1 &&
+    const bool want_res = !LOG && !sh && !avg_pass_ms && fits && o.max_iter >= 1 &&
                           (o.engine == OTF_ENGINE_RESIDENT || o.engine == OTF_ENGINE_AUTO);
     // OTT flavour, float64, on request: the resident engine in scaling form (see
     // SkResArgs::ott for the range contract).  No one-workgroup fallback is queued (that
@@ -2040,7 +2274,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
                                              u_out, v_out, P_out, ldp, P_dtype, info, errlog, s,
                                              /*ott=*/true));
     }
-    if (o.engine == OTF_ENGINE_RESIDENT && (LOG || !fits)) return OTF_EUNSUPPORTED;
+    if (o.engine == OTF_ENGINE_RESIDENT && (LOG || sh || !fits)) return OTF_EUNSUPPORTED;
     if (want_res) {
         Workspace w = su.w;
         const hipError_t e = run_resident<T, CT>(su.cfg, su.nrb, C, ldc, (int)n, (int)m, cost_scale,
@@ -2059,7 +2293,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     if (sfits && (o.engine == OTF_ENGINE_SWEEP || o.engine == OTF_ENGINE_AUTO)) {
         const hipError_t e = run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
                                               (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
-                                              v_out, P_out, ldp, P_dtype, info, errlog, s);
+                                              v_out, P_out, ldp, P_dtype, info, errlog, s, nullptr, shp);
         if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_SWEEP) return check_hip(e);
@@ -2121,7 +2355,7 @@ int sk_pass_api(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64
                 const T* cost_scale, const otf_sinkhorn_opts& o, int pass,
                 otf_sinkhorn_info* info, double* errlog, void* ws, size_t ws_bytes, void** colsum,
                 int64_t* colsum_len, hipStream_t s) {
-    if (o.flavor != OTF_FLAVOR_POT) return OTF_EUNSUPPORTED;
+    if (o.flavor != OTF_FLAVOR_POT || o.shift) return OTF_EUNSUPPORTED;
     if (pass < 0 || pass > o.max_iter) return OTF_EINVAL;
     SkSetup<T> su;
     int rc = sk_prepare<T, CT>(a, b, C, n, m, ldc, o, info, ws, ws_bytes, su);
@@ -2144,7 +2378,7 @@ int sk_finish_api(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int
                   int64_t ldp, int P_dtype, otf_sinkhorn_info* info, double* errlog, void* ws,
                   size_t ws_bytes, hipStream_t s) {
     constexpr int VEC = Vec<T>::N;
-    if (o.flavor != OTF_FLAVOR_POT) return OTF_EUNSUPPORTED;
+    if (o.flavor != OTF_FLAVOR_POT || o.shift) return OTF_EUNSUPPORTED;
     if (!u_out || !v_out) return OTF_EINVAL;
     if (P_out && (ldp < m || ldp % VEC != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
     SkSetup<T> su;
@@ -2196,7 +2430,7 @@ int run_xsweep(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_
     if (!u_out || !v_out) return OTF_EINVAL;
     if (P_out && (ldp < m || ldp % VEC != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
     if (o.max_iter < 1 || xs.n_total < n) return OTF_EINVAL;
-    if (!sweep_supported<T, CT>(n, m, ldc)) return OTF_EUNSUPPORTED;
+    if (!sweep_supported<T, CT>(n, m, ldc) || o.shift) return OTF_EUNSUPPORTED;
     SkSetup<T> su;
     int rc = sk_prepare<T, CT>(a, b, C, n, m, ldc, o, info, ws, ws_bytes, su);
     if (rc != OTF_OK) return rc;
@@ -2321,6 +2555,19 @@ size_t otf_sinkhorn_workspace_size(int64_t n, int64_t m, int32_t dtype, int32_t 
     const size_t esz = dtype == OTF_F64 ? 8 : 4;
     const int64_t nrb = dtype == OTF_F64 ? otf::row_blocks<double>(n, m) : otf::row_blocks<float>(n, m);
     return otf::carve(nullptr, n, m, esz, max_iter < 0 ? 0 : max_iter, nrb).bytes;
+}
+
+int otf_sinkhorn_shift_offsets(int64_t n, int64_t m, int32_t dtype, int32_t max_iter,
+                               size_t* off_a, size_t* off_b) {
+    if (!off_a || !off_b || n <= 0 || m <= 0) return OTF_EINVAL;
+    if (dtype != OTF_F32) return OTF_EUNSUPPORTED;
+    const int64_t nrb = otf::row_blocks<float>(n, m);
+    // carve against a non-null stand-in base (it hands out null pointers for a null one)
+    char* const base = (char*)(uintptr_t)4096;
+    const otf::Workspace w = otf::carve(base, n, m, 4, max_iter < 0 ? 0 : max_iter, nrb);
+    *off_a = (size_t)((char*)w.shA - base);
+    *off_b = (size_t)((char*)w.shB - base);
+    return OTF_OK;
 }
 
 int otf_sinkhorn(const void* a, const void* b, const void* C, int64_t n, int64_t m, int64_t ldc,

@@ -104,6 +104,7 @@ template <typename T> struct SkSweepArgs {
     int n_total;           // rows over all ranks (POT's u0 = 1 / n)
     unsigned ep_base;      // epoch offset of this solve (the same on every rank)
     unsigned char* xr[8];
+    ShiftArgs sh;          // shifted kernel (SH instances): offsets + initial scalings
 };
 constexpr int kSwSlices = 32;  // column slices of the granule reduction
 
@@ -168,7 +169,9 @@ __device__ __forceinline__ double bcast_lane(double x, int r) {
 }
 
 
-template <typename T, typename CT, typename TP, int G, int R, int NREP>
+// SH (float only): the shifted POT kernel e = 2^(C ks + A_i + B_j) (otf_persist.h
+// ShiftArgs); B of the columns and A of the workgroup's rows sit in LDS beside 1 / a.
+template <typename T, typename CT, typename TP, int G, int R, int NREP, bool SH>
 __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     constexpr int VC = RawN<CT>::N;            // cost elements per 16-B chunk
     constexpr int VT = Vec<T>::N;              // compute elements per 16-B sum load
@@ -184,7 +187,9 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     T* gred = ialds + kSwRowMax;                                     // [kSwNT * VT] group reduce
     // the workgroup's last nres row blocks (sanitized raw cost, thread-private 16-B slots):
     // read from LDS instead of the memory system on every sweep after the prologue
-    Raw* resb = reinterpret_cast<Raw*>(gred + kSwNT * VT);
+    T* shBl = gred + kSwNT * VT;                                     // SH: B, m_pad
+    T* shAl = shBl + (SH ? p.m_pad : 0);                             // SH: A of own rows
+    Raw* resb = reinterpret_cast<Raw*>(shAl + (SH ? kSwRowMax : 0));
     __shared__ T red[2][NW][R];
     __shared__ T ered[17];
     __shared__ int s_flag;
@@ -244,7 +249,11 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     for (int i = tid; i < my_nb * R; i += kSwNT) {
         const int row = ((int)blockIdx.x + (i / R) * nwg) * R + i % R;
         ialds[i] = (T)1 / p.a[row < p.n ? row : 0];
+        if (SH) shAl[i] = row < p.n ? (T)p.sh.A[row] : (T)0;
     }
+    if (SH)
+        for (int j = tid; j < p.m_pad; j += kSwNT) shBl[j] = (T)p.sh.B[j];  // zero past m
+    if (SH) __syncthreads();
 
     // R cost rows of block bi via one SGPR descriptor (rows past n read as 0).  A cost
     // larger than the Infinity Cache is loaded non-temporal (7.3 vs 6.4 TB/s from HBM,
@@ -417,6 +426,12 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                 for (int r = 0; r < R; ++r) {
                     T2 c[VP2];
                     scaled_pairs<T, CT>(buf[r][g], ks, c);
+                    if constexpr (SH) {
+                        const T sa = shAl[bi * R + r];
+#pragma unroll
+                        for (int k = 0; k < VP2; ++k)
+                            c[k] += T2{sa, sa} + *reinterpret_cast<const T2*>(shBl + colc[g] + 2 * k);
+                    }
 #pragma unroll
                     for (int k = 0; k < VP2; ++k) {
 #if defined(OTF_SWEEP_ABLATE) && (OTF_SWEEP_ABLATE & 1)
@@ -491,7 +506,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                 for (int r = 0; r < R; ++r) u[r] = bcast_lane(um, r);
             } else {
 #pragma unroll
-                for (int r = 0; r < R; ++r) u[r] = r < nrow ? u0 : (T)0;
+                for (int r = 0; r < R; ++r) u[r] = r < nrow ? (SH ? (T)p.sh.u0[r0 + r] : u0) : (T)0;
             }
 #pragma unroll
             for (int g = 0; g < G; ++g)
@@ -986,7 +1001,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             for (int k = 0; k < VC; ++k) vo[k] = k < cnt[g] ? bv[k] / sl[k] : (T)0;
         } else {
 #pragma unroll
-            for (int k = 0; k < VC; ++k) vo[k] = v0;
+            for (int k = 0; k < VC; ++k) vo[k] = SH ? (k < cnt[g] ? (T)p.sh.v0[colc[g] + k] : (T)0) : v0;
         }
 #pragma unroll
         for (int k = 0; k < VC; ++k) colacc[g][k / 2][k & 1] = vo[k];  // v(last_good) from here on
@@ -999,7 +1014,8 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     const T* uh = uhist + (last_good & 1) * kSwRowMax;
     for (int bi = 0; bi < my_nb; ++bi) {
         const int r0 = ((int)blockIdx.x + bi * nwg) * R;
-        if (tid < R && r0 + tid < p.n) p.u_out[r0 + tid] = last_good >= 0 ? uh[bi * R + tid] : u0;
+        if (tid < R && r0 + tid < p.n)
+            p.u_out[r0 + tid] = last_good >= 0 ? uh[bi * R + tid] : SH ? (T)p.sh.u0[r0 + tid] : u0;
     }
     if (p.P) {
         TP* P = (TP*)p.P;
@@ -1011,7 +1027,8 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (r0 + r >= p.n) break;
-                const T ur = last_good >= 0 ? uh[bi * R + r] : u0;
+                const T ur = last_good >= 0 ? uh[bi * R + r] : SH ? (T)p.sh.u0[r0 + r] : u0;
+                const T sa = SH ? shAl[bi * R + r] : (T)0;
                 TP* prow = P + (int64_t)(r0 + r) * p.ldp;
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
@@ -1021,7 +1038,11 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                     widen<T, CT>(bufA[r][g], c);
                     TP o[VC];
 #pragma unroll
-                    for (int k = 0; k < VC; ++k) o[k] = (TP)(ur * fast_exp(c[k] * ks) * colacc[g][k / 2][k & 1]);
+                    for (int k = 0; k < VC; ++k) {
+                        T z = c[k] * ks;
+                        if (SH) z += sa + shBl[c0 + k];
+                        o[k] = (TP)(ur * fast_exp(z) * colacc[g][k / 2][k & 1]);
+                    }
                     if (cnt[g] == VC) {
 #pragma unroll
                         for (int h = 0; h < VC / VP; ++h) {
@@ -1039,7 +1060,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
             }
         }
     }
-    if (status == OTF_SK_TIMEOUT && tid == 0) store_wt(&p.info->stalled, 1);
+    if (status == OTF_SK_TIMEOUT && tid == 0) mark_stalled(&p.info->stalled, kStallMid);
     if (lead) {
         p.info->last_good = last_good;
         p.info->niter = niter;
@@ -1078,8 +1099,9 @@ template <typename CT> int sweep_g(int64_t m) {
 constexpr int kSwMaxGrid = 256;  // slab rows in the workspace (one per workgroup)
 
 // LDS: vbuf | u history | 1 / a | group-reduce staging (T), then the resident blocks
-template <typename T> size_t sweep_lds_base(int64_t m_pad) {
-    return ((size_t)m_pad + 3 * kSwRowMax + (size_t)kSwNT * Vec<T>::N) * sizeof(T);
+template <typename T> size_t sweep_lds_base(int64_t m_pad, bool sh = false) {
+    return ((size_t)m_pad + 3 * kSwRowMax + (size_t)kSwNT * Vec<T>::N +
+            (sh ? (size_t)m_pad + kSwRowMax : 0)) * sizeof(T);
 }
 size_t sweep_block_lds(int R, int G) { return (size_t)R * G * kSwNT * 16; }
 constexpr size_t kSwLdsMax = 160 * 1024 - 4096;  // the CU's LDS less the static arrays
@@ -1087,21 +1109,22 @@ constexpr size_t kSwLdsMax = 160 * 1024 - 4096;  // the CU's LDS less the static
 #define OTF_SWEEP_MAXRES 4
 #endif
 
-template <typename T, typename CT, typename TP, int G>
-hipError_t launch_sweep_g(int grid, SkSweepArgs<T>& p, hipStream_t s) {
+template <typename T, typename CT, typename TP, int G, bool SH>
+hipError_t launch_sweep_gs(int grid, SkSweepArgs<T>& p, hipStream_t s) {
     constexpr int R = sweep_rows<T, CT>(G);
     // as many whole row blocks in LDS as fit, fewer than the smallest per-workgroup count
     const int nrb = (p.n + R - 1) / R;
     const int min_nb = nrb / grid;
-    const size_t base = sweep_lds_base<T>(p.m_pad);
+    const size_t base = sweep_lds_base<T>(p.m_pad, SH);
     int nres = base < kSwLdsMax ? (int)((kSwLdsMax - base) / sweep_block_lds(R, G)) : 0;
     if (nres > OTF_SWEEP_MAXRES) nres = OTF_SWEEP_MAXRES;
     if (nres > min_nb - 1) nres = min_nb - 1 > 0 ? min_nb - 1 : 0;
     if (const char* e = getenv("OTF_SWEEP_NRES")) nres = atoi(e) < nres ? atoi(e) : nres;
     p.nres = nres;
     void* args[] = {&p};
-    const void* k = (const void*)sk_sweep_kernel<T, CT, TP, G, R, OTF_SWEEP_NREP>;
-    const size_t lds = sweep_lds_base<T>(p.m_pad) + (size_t)p.nres * sweep_block_lds(R, G);
+    const void* k = (const void*)sk_sweep_kernel<T, CT, TP, G, R, OTF_SWEEP_NREP, SH>;
+    const size_t lds = base + (size_t)p.nres * sweep_block_lds(R, G);
+    if (lds > kSwLdsMax + 4096) return hipErrorInvalidValue;
     if ((int64_t)((nrb + grid - 1) / grid) * R > kSwRowMax) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -1110,6 +1133,13 @@ hipError_t launch_sweep_g(int grid, SkSweepArgs<T>& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     if (per_cu < 1 || grid > per_cu * device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
     return hipLaunchKernel(k, dim3(grid), dim3(kSwNT), args, lds, s);
+}
+
+template <typename T, typename CT, typename TP, int G>
+hipError_t launch_sweep_g(int grid, SkSweepArgs<T>& p, hipStream_t s) {
+    if constexpr (sizeof(T) == 4)
+        if (p.sh.A) return launch_sweep_gs<T, CT, TP, G, true>(grid, p, s);
+    return launch_sweep_gs<T, CT, TP, G, false>(grid, p, s);
 }
 
 template <typename T, typename CT, typename TP>
@@ -1168,7 +1198,8 @@ template <typename T, typename CT>
 hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T* a_pad,
                      const T* b_pad, const T* cost_scale, const otf_sinkhorn_opts& o, void* region,
                      T* u_out, T* v_out, void* P_out, int64_t ldp, int P_dtype,
-                     otf_sinkhorn_info* info, double* errlog, hipStream_t s, const XSweep* xs) {
+                     otf_sinkhorn_info* info, double* errlog, hipStream_t s, const XSweep* xs,
+                     const ShiftArgs* sh) {
     const int G = sweep_g<CT>(m);
     if (G == 0) return hipErrorInvalidValue;
     SkSweepArgs<T> p{};
@@ -1208,6 +1239,10 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     p.gran = (sizeof(T) == 4 && !p.det && !(ge && atoi(ge) == 0)) ? 1 : 0;
     p.world = 1;
     p.n_total = n;
+    if (sh) {
+        if (sizeof(T) != 4 || (xs && xs->world > 1)) return hipErrorInvalidValue;
+        p.sh = *sh;
+    }
     if (xs && xs->world > 1) {  // the cross-rank form runs on the granule flush only
         if (sizeof(T) != 4 || xs->world > kXMaxRanks) return hipErrorInvalidValue;
         p.gran = 1;
@@ -1253,14 +1288,17 @@ template bool sweep_supported<double, double>(int64_t, int64_t, int64_t);
 template hipError_t run_sweep<float, float>(const float*, int64_t, int, int, int, const float*,
                                             const float*, const float*, const otf_sinkhorn_opts&,
                                             void*, float*, float*, void*, int64_t, int,
-                                            otf_sinkhorn_info*, double*, hipStream_t, const XSweep*);
+                                            otf_sinkhorn_info*, double*, hipStream_t, const XSweep*,
+                                            const ShiftArgs*);
 template hipError_t run_sweep<float, _Float16>(const _Float16*, int64_t, int, int, int, const float*,
                                                const float*, const float*, const otf_sinkhorn_opts&,
                                                void*, float*, float*, void*, int64_t, int,
-                                               otf_sinkhorn_info*, double*, hipStream_t, const XSweep*);
+                                               otf_sinkhorn_info*, double*, hipStream_t, const XSweep*,
+                                            const ShiftArgs*);
 template hipError_t run_sweep<double, double>(const double*, int64_t, int, int, int, const double*,
                                               const double*, const double*, const otf_sinkhorn_opts&,
                                               void*, double*, double*, void*, int64_t, int,
-                                              otf_sinkhorn_info*, double*, hipStream_t, const XSweep*);
+                                              otf_sinkhorn_info*, double*, hipStream_t, const XSweep*,
+                                            const ShiftArgs*);
 
 }  // namespace otf

@@ -44,7 +44,7 @@ class SinkhornOpts(ctypes.Structure):
                 ("flavor", ctypes.c_int32), ("err_squared", ctypes.c_int32),
                 ("sync_every", ctypes.c_int32), ("engine", ctypes.c_int32),
                 ("cost_f16", ctypes.c_int32), ("n_total", ctypes.c_int32),
-                ("deterministic", ctypes.c_int32)]
+                ("deterministic", ctypes.c_int32), ("shift", ctypes.c_int32)]
 
 
 class GwOpts(ctypes.Structure):
@@ -102,6 +102,8 @@ _SIGS = {
                                         _vp, _i64, _vp, _vp, _vp, _i64, _vp, ctypes.c_size_t,
                                         _vp]),
     "otf_sinkhorn_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i32, _i32]),
+    "otf_sinkhorn_shift_offsets": (ctypes.c_int, [_i64, _i64, _i32, _i32, ctypes.POINTER(ctypes.c_size_t),
+                                                  ctypes.POINTER(ctypes.c_size_t)]),
     "otf_sinkhorn_fallback_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "otf_sinkhorn": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp,
                                     ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _i64, _i32, _vp,

@@ -237,13 +237,33 @@ def to_host(t: torch.Tensor) -> np.ndarray:
 # --------------------------------------------------------------------------- Sinkhorn
 @dataclass
 class SinkhornResult:
-    u: torch.Tensor                 # POT: scaling u; OTT: potential f
-    v: torch.Tensor                 # POT: scaling v; OTT: potential g
+    u: torch.Tensor                 # POT: scaling u (u~ of the shifted kernel); OTT: potential f
+    v: torch.Tensor                 # POT: scaling v (v~ of the shifted kernel); OTT: potential g
     plan: torch.Tensor | None
     info_dev: torch.Tensor          # int32[8] otf_sinkhorn_info on the device
     errlog_dev: torch.Tensor        # float64 marginal errors on the device
     flavor: str = "pot"
+    # shifted kernel (opts.shift): base-2 exponent offsets A (n), B (m) in the workspace,
+    # POT's scalings are u = 2^A u~, v = 2^B v~ (see pot_scalings)
+    shift_a: torch.Tensor | None = None
+    shift_b: torch.Tensor | None = None
     _info: dict | None = field(default=None, repr=False)
+
+    @property
+    def shifted(self) -> bool:
+        return self.shift_a is not None
+
+    def pot_scalings(self):
+        """POT's scaling vectors ``(u, v)`` in float64 -- identical to ``(u, v)`` for a
+        plain solve, ``(2^A u~, 2^B v~)`` for a shifted one (whose scalings can leave
+        float32's range at small reg: v ~ exp(0.5 / reg) on a max-normalised cost)."""
+        if self.flavor != "pot":
+            raise ValueError("pot_scalings: POT-flavour results only")
+        u, v = self.u.double(), self.v.double()
+        if self.shifted:
+            u = u * torch.exp2(self.shift_a.double())
+            v = v * torch.exp2(self.shift_b.double())
+        return u, v
 
     def info(self) -> dict:
         """Reads the device-side outcome (synchronises on first call)."""
@@ -253,21 +273,28 @@ class SinkhornResult:
             d["status_name"] = L.STATUS_NAMES.get(d["status"], "?")
             d["engine_name"] = L.ENGINE_NAMES.get(d["engine"], "?")
             if d["status"] == L.SK_TIMEOUT or d["stalled"]:
-                raise L.OtfError("persistent Sinkhorn: a device-wide barrier made no progress "
-                                 "(grid not co-resident?); results are invalid")
+                raise L.OtfError("persistent Sinkhorn: a device-wide exchange made no progress "
+                                 "for the stall limit (stalled=%d); results are invalid" % d["stalled"])
+            if d["fallback"]:
+                warnings.warn(
+                    "persistent Sinkhorn engine could not become co-resident within OTF_REG_MS "
+                    "(another persistent kernel held the CUs); the one-workgroup fallback "
+                    "solved the problem instead (same POT result, much slower)",
+                    RuntimeWarning, stacklevel=2)
             if d["status"] == L.SK_RUNNING or not d["stop"]:
                 # every engine writes a final status and stop = 1; a solve that left
                 # them untouched never ran to its end (u, v, plan are uninitialised)
                 raise L.OtfError("Sinkhorn: the solve reported no final status; results are "
                                  "invalid")
             d["err"] = self.errlog_dev[: max(d["n_err"], 0)].cpu().tolist()
-            if (self.flavor == "pot" and self.u.dtype == torch.float32
+            if (self.flavor == "pot" and self.u.dtype == torch.float32 and not self.shifted
                     and d["status"] == L.SK_NUMERICAL_BREAK and d["break_iter"] <= 1):
                 warnings.warn(
                     "float32 POT Sinkhorn broke at iteration %d: a row or column of "
                     "K = exp(-C/reg) underflows (or its scaling overflows) in float32 -- POT's "
-                    "float64 solve may not break there.  Use precision='auto' or 'fp64' for "
-                    "parity with the reference's float64 path." % d["break_iter"],
+                    "float64 solve may not break there.  Use shift=True (the shifted kernel, "
+                    "float32) or precision='fp64' for parity with the reference's float64 "
+                    "path." % d["break_iter"],
                     RuntimeWarning, stacklevel=2)
             self._info = d
         return self._info
@@ -295,12 +322,33 @@ def sinkhorn_workspace(n: int, m: int, dtype, max_iter: int, device) -> torch.Te
     return torch.empty(wsb, dtype=torch.uint8, device=device)
 
 
+# float32 POT switches to the shifted kernel when max(C / cost_scale) / reg exceeds
+# SHIFT_RANGE: K = exp(-C/reg) stays in float32's normal range up to 87, the scalings
+# (~exp(0.5 / reg) on a max-normalised cost) up to ~170; 64 keeps a margin to both.  Past
+# SHIFT_RANGE_F64 POT's own float64 K has exact zeros (exp underflows below -745) and
+# POT breaks on them; the plain float32 kernel reproduces that break, so it stays plain.
+SHIFT_RANGE = 64.0
+SHIFT_RANGE_F64 = 700.0
+_SHIFT_ENGINES = ("auto", "mesh", "sweep", "stream")
+
+
+def _want_shift(C: torch.Tensor, reg: float, cost_scale, flavor: str, dt, engine: str) -> bool:
+    if flavor != "pot" or dt != torch.float32 or engine not in _SHIFT_ENGINES:
+        return False
+    if cost_scale is not None:       # scale_cost = "max_cost": C / cost_scale <= 1
+        r = 1.0 / float(reg)
+    else:
+        r = (float(C.amax()) if C.numel() else 0.0) / float(reg)  # one reduction + host read
+    return SHIFT_RANGE < r <= SHIFT_RANGE_F64
+
+
 def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_iter: int = 1000,
              stop_thr: float = 1e-9, flavor: str = "pot", cost_scale: torch.Tensor | None = None,
              check_every: int = 10, err_squared: bool = False, sync_every: int = 0,
              want_plan: bool = True, plan_dtype=None, workspace: torch.Tensor | None = None,
              plan_out: torch.Tensor | None = None, engine: str = "auto",
-             deterministic: bool = False, precision: str = "as_given") -> SinkhornResult:
+             deterministic: bool = False, precision: str = "as_given",
+             shift: bool | None = None) -> SinkhornResult:
     """Entropic OT on the device.  ``flavor="pot"`` is POT's sinkhorn_knopp (u, v scalings,
     revert-and-break), ``flavor="ott"`` OTT's lse-mode solver (potentials f, g).
 
@@ -311,22 +359,25 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
     by construction, else the sweep engine's fixed-order mode; POT flavour):
     bitwise-identical results run to run.
 
-    ``precision``: "as_given" computes in C's dtype; "fp64" in float64 (the reference's
-    POT path is float64 NumPy); "auto" keeps float32 unless a POT-flavour solve would
-    break in float32 where POT's float64 does not: when some row or column of
-    K = exp(-C / (reg cost_scale)) underflows entirely in float32, K^T u = 0 (or v = b /
-    K^T u overflows) and POT reverts at iteration 0.  The test is min over every row and
-    every column of C / (reg cost_scale) > 60 (float32 exp underflows below -87 and the
-    scaling overflows near e^88): two reductions and one host read, so "auto" is opt-in.
+    ``precision``: "as_given" (and its alias "auto") computes in C's dtype; "fp64" in
+    float64 (the reference's POT path is float64 NumPy).
+
+    ``shift`` (float32 POT only): run POT's iteration on the shifted kernel
+    K~ = 2^(C ks + A_i + B_j) (include/otfuse.h opts.shift) -- the same iterates, with
+    offsets from a log-domain first half-iteration, so that no plan entry that matters is
+    formed from a flushed float32 exp and the scalings stay in range.  None (default)
+    turns it on when SHIFT_RANGE (64) < max(C / cost_scale) / reg <= SHIFT_RANGE_F64 (700)
+    on an engine that runs it (mesh, sweep, stream, AUTO): with ``cost_scale`` the ratio is
+    taken as 1 / reg (C / cost_scale <= 1, scale_cost = "max_cost"), without it from
+    C.amax() (one reduction and a host read).  Plain float32 kernel-domain POT
+    moves the plan by 2.2e-3 at reg = 0.01 on the metric shape and breaks at iteration 0
+    at reg = 5e-3; the shifted form holds 1e-4 of the float64 reference at both
+    (tests/test_gpu_precision.py).  ``u``/``v`` of a shifted result are u~, v~;
+    ``pot_scalings()`` gives POT's.
     """
     _dev(C, "C")
     if precision not in ("as_given", "fp64", "auto"):
         raise ValueError(f"precision must be 'as_given', 'fp64' or 'auto', not {precision!r}")
-    if precision == "auto" and flavor == "pot" and C.dtype in (torch.float32, torch.float16):
-        cs = 1.0 if cost_scale is None else float(cost_scale.reshape(-1)[0])
-        worst = torch.maximum(C.amin(dim=0).max(), C.amin(dim=1).max()).float()
-        if float(worst) / (cs * float(reg)) > 60.0:
-            precision = "fp64"
     if precision == "fp64" and C.dtype != torch.float64:
         C = C.double()
         if cost_scale is not None:
@@ -337,6 +388,10 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
         raise TypeError("C must be float16, float32 or float64")
     cost_f16 = C.dtype == torch.float16
     dt = torch.float32 if cost_f16 else C.dtype
+    if shift is None:
+        shift = _want_shift(C, reg, cost_scale, flavor, dt, engine)
+    elif shift and (flavor != "pot" or dt != torch.float32):
+        raise ValueError("shift: float32 POT-flavour solves only")
     n, m = C.shape
     C = _rowmajor(C, _VEC[C.dtype])
     a = _dev(a, "a").to(dt).contiguous()
@@ -364,13 +419,22 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
                           flavor=L.OTF_FLAVOR_OTT if flavor == "ott" else L.OTF_FLAVOR_POT,
                           err_squared=int(err_squared), sync_every=int(sync_every),
                           engine=L.ENGINES[engine], cost_f16=int(cost_f16),
-                          deterministic=int(bool(deterministic)))
+                          deterministic=int(bool(deterministic)), shift=int(bool(shift)))
     L.check(L.lib().otf_sinkhorn(
         a.data_ptr(), b.data_ptr(), C.data_ptr(), n, m, C.stride(0), _DT[dt], L.ptr(cost_scale),
         ctypes.byref(opts), u.data_ptr(), v.data_ptr(), L.ptr(P), P.stride(0) if P is not None else 0,
         _DT[P.dtype] if P is not None else 0, info.data_ptr(), errlog.data_ptr(),
         workspace.data_ptr(), workspace.numel(), L.stream_handle(dev)), "otf_sinkhorn")
-    return SinkhornResult(u=u, v=v, plan=P, info_dev=info, errlog_dev=errlog, flavor=flavor)
+    sa = sb = None
+    if shift:
+        oa, ob = ctypes.c_size_t(), ctypes.c_size_t()
+        L.check(L.lib().otf_sinkhorn_shift_offsets(n, m, _DT[dt], int(max_iter), ctypes.byref(oa),
+                                                   ctypes.byref(ob)), "otf_sinkhorn_shift_offsets")
+        # views into the workspace: valid until the workspace is reused by another solve
+        sa = workspace[oa.value: oa.value + 4 * n].view(torch.float32)
+        sb = workspace[ob.value: ob.value + 4 * m].view(torch.float32)
+    return SinkhornResult(u=u, v=v, plan=P, info_dev=info, errlog_dev=errlog, flavor=flavor,
+                          shift_a=sa, shift_b=sb)
 
 
 def sinkhorn_profile(a, b, C, reg, iters, cost_scale=None, flavor="pot", workspace=None) -> float:

@@ -1,8 +1,12 @@
 """Precision coverage at the metric shape (N = 4096, d = 512, 100
-iterations, max-normalised sq-Euclid cost) for the harder eps sweep {0.05, 0.01}, the
-float64 form, and the regime where POT's float64 kernel-domain Sinkhorn
-(MRI_PET_OT_nojax.py:143 -> sinkhorn_knopp) does not break but a float32 one would:
-eps = 5e-3 (the reference's per-epoch eps, MRI_PET_OT_nojax.py:94).  The oracle is the
+iterations, max-normalised sq-Euclid cost) over the eps sweep {0.05, 0.01} and the
+reference's per-epoch eps 5e-3 (MRI_PET_OT_nojax.py:94), where POT's float64
+kernel-domain Sinkhorn (MRI_PET_OT_nojax.py:143 -> sinkhorn_knopp) runs on but a plain
+float32 one does not: at eps = 0.01 float32 exp flushes the entries of K below 2^-126
+(moving the plan by 2.2e-3 normwise), at 5e-3 whole columns of K vanish (a break at
+iteration 0).  The float32 path therefore switches to the shifted kernel
+K~ = 2^(C ks + A_i + B_j) (include/otfuse.h opts.shift) -- the same POT iterates --
+below reg = 1/64, and holds the north star's 1e-4 at every eps here.  The oracle is the
 float64 C restatement (pinned on the golden vectors, tests/test_oracle_golden.py)."""
 import warnings
 
@@ -13,6 +17,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 N, D = 4096, 512
+TOL32 = 1e-4     # the north star's plan tolerance (normwise relative) for float32 compute
 
 
 def nrel(x, ref):
@@ -33,75 +38,128 @@ def metric_inputs(orc, dev):
     return X, Y, C, cmax, Cr
 
 
-# Normwise plan error of the float32 path (split-fp16 cost, float32 kernel-domain solve)
-# against the float64 oracle, measured on MI355X (r03): eps 0.1 -> < 1e-5, 0.05 -> < 1e-4,
-# 0.01 -> 2.2e-3.  Kernel-domain Sinkhorn at small eps amplifies float32 rounding over
-# the iterations; the float64 path (float64 cost + float64 solve) holds 1e-9 there.
-@pytest.mark.parametrize("eps,tol32", [(0.05, 1e-4), (0.01, 5e-3)])
-def test_metric_shape_harder_eps_float32_vs_float64_oracle(orc, dev, metric_inputs, eps, tol32):
-    """The headline fp32 path (split-fp16 cost, mesh engine) at the harder eps of the
-    sweep against the float64 oracle, and the float64 path at the same eps."""
-    from otfuse import gw, ops
+@pytest.fixture(scope="module")
+def oracle_plans(orc, metric_inputs):
+    cache = {}
+
+    def get(eps):
+        if eps not in cache:
+            Cr = metric_inputs[4]
+            cache[eps] = orc.sinkhorn_knopp(np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cr, eps, 100, 0.0)
+        return cache[eps]
+    return get
+
+
+@pytest.mark.parametrize("eps", [0.05, 0.01, 5e-3])
+def test_metric_shape_float32_vs_float64_oracle(dev, metric_inputs, oracle_plans, eps):
+    """The headline float32 path (split-fp16 cost, AUTO engine = mesh) against the float64
+    oracle at 1e-4 for every eps of the sweep: plain kernel at 0.05, the shifted kernel
+    (chosen automatically below reg = 1/64) at 0.01 and 5e-3 -- no float64 detour."""
+    from otfuse import ops
     X, Y, C, cmax, Cr = metric_inputs
     a = torch.full((N,), 1.0 / N, device=dev)
     res = ops.sinkhorn(a, a, C, eps, max_iter=100, stop_thr=0.0, cost_scale=cmax)
     info = res.info()
     assert info["status_name"] == "max_iter" and info["niter"] == 99
-    Pr, _, _, info_r = orc.sinkhorn_knopp(np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cr, eps, 100, 0.0)
+    assert info["engine_name"] == "mesh" and res.u.dtype == torch.float32
+    assert res.shifted == (eps < 1.0 / 64)
+    Pr, _, _, info_r = oracle_plans(eps)
     assert info_r["break_iter"] == -1
-    assert nrel(res.plan.cpu().numpy(), Pr) < tol32
-    C64, _ = gw.pairwise_cost_f64(torch.as_tensor(X, device=dev), torch.as_tensor(Y, device=dev),
-                                  scale_max=True)
-    a64 = a.double()
-    r64 = ops.sinkhorn(a64, a64, C64, eps, max_iter=100, stop_thr=0.0)
-    assert r64.info()["niter"] == 99
-    assert nrel(r64.plan.cpu().numpy(), Pr) < 1e-9
+    assert nrel(res.plan.cpu().numpy(), Pr) < TOL32
+    # the marginal-error log: same checks as POT's, values to float32 accuracy
+    assert info["n_err"] == len(info_r["err"])
+    np.testing.assert_allclose(info["err"], info_r["err"], rtol=2e-3, atol=1e-9)
 
 
-def test_metric_shape_float64_leg_vs_oracle(orc, dev, metric_inputs):
-    """The float64 leg of the metric config (bench.py metric_f64): float64 cost from the
-    embeddings and a float64 solve, held to 1e-9 of the float64 oracle."""
+@pytest.mark.parametrize("engine", ["mesh", "sweep", "stream"])
+def test_shifted_kernel_every_engine_vs_oracle(dev, metric_inputs, oracle_plans, engine):
+    """The shifted kernel on each engine that runs it (register-resident mesh, persistent
+    sweep, per-iteration streaming pass) at reg = 0.01: 1e-4 of the float64 oracle, and
+    POT's scalings recovered from (u~, v~, A, B) match the oracle's up to POT's scale
+    mode (u c, v / c)."""
     from otfuse import ops
+    X, Y, C, cmax, Cr = metric_inputs
+    eps = 0.01
+    a = torch.full((N,), 1.0 / N, device=dev)
+    res = ops.sinkhorn(a, a, C, eps, max_iter=100, stop_thr=0.0, cost_scale=cmax, engine=engine,
+                       shift=True)
+    info = res.info()
+    assert info["engine_name"] == engine and info["status_name"] == "max_iter" and info["niter"] == 99
+    Pr, ur, vr, _ = oracle_plans(eps)
+    assert nrel(res.plan.cpu().numpy(), Pr) < TOL32
+    u, v = (t.cpu().numpy() for t in res.pot_scalings())
+    c = np.median(u / ur)
+    np.testing.assert_allclose(u / c, ur, rtol=5e-4)
+    np.testing.assert_allclose(v * c, vr, rtol=5e-4)
+
+
+def test_plain_float32_kernel_flushes_below_reg_one_over_64(dev, metric_inputs, oracle_plans):
+    """Why the shift exists: the plain float32 kernel at reg = 0.01 is outside the north
+    star's tolerance (K entries below 2^-126 are flushed by v_exp_f32; the CPU emulation of
+    that flush gives the same 2.2e-3), and at 5e-3 it breaks at iteration 0 with a warning
+    naming the remedy."""
+    from otfuse import ops
+    X, Y, C, cmax, Cr = metric_inputs
+    a = torch.full((N,), 1.0 / N, device=dev)
+    r = ops.sinkhorn(a, a, C, 0.01, max_iter=100, stop_thr=0.0, cost_scale=cmax, shift=False)
+    assert r.info()["status_name"] == "max_iter" and not r.shifted
+    Pr, *_ = oracle_plans(0.01)
+    assert nrel(r.plan.cpu().numpy(), Pr) > 5 * TOL32
+    r = ops.sinkhorn(a, a, C, 5e-3, max_iter=100, stop_thr=0.0, cost_scale=cmax, shift=False)
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        i32 = r.info()
+    assert i32["status_name"] == "numerical_break" and i32["break_iter"] <= 1
+    assert any("shift=True" in str(w.message) for w in rec)
+
+
+def test_shift_is_a_reparametrisation_in_the_plain_regime(dev, metric_inputs):
+    """At reg = 0.1 (no float32 range issue) the shifted kernel reproduces the plain one:
+    same iterates in exact arithmetic, plans within float32 rounding."""
+    from otfuse import ops
+    X, Y, C, cmax, Cr = metric_inputs
+    a = torch.full((N,), 1.0 / N, device=dev)
+    r0 = ops.sinkhorn(a, a, C, 0.1, max_iter=100, stop_thr=0.0, cost_scale=cmax)
+    r1 = ops.sinkhorn(a, a, C, 0.1, max_iter=100, stop_thr=0.0, cost_scale=cmax, shift=True)
+    assert not r0.shifted and r1.shifted
+    assert r1.info()["niter"] == r0.info()["niter"] == 99
+    assert nrel(r1.plan.cpu().numpy(), r0.plan.cpu().numpy()) < 1e-5
+
+
+def test_shifted_fp16_storage_sweep_vs_oracle(orc, dev):
+    """BASELINE config 5's storage (fp16 cost, power-of-two scaled, fp32 compute) at
+    reg = 0.01 on the sweep engine with the shifted kernel, against the float64 oracle on
+    the same stored values (4096 x 8192, 60 iterations)."""
+    from otfuse import ops
+    from otfuse.synthetic import paired_embeddings
+    X, Y, _ = paired_embeddings(8192, 256, seed=77)
+    Xd = torch.as_tensor(X[:4096], device=dev).half()
+    Yd = torch.as_tensor(Y, device=dev).half()
+    C, cmax, unit = ops.pairwise_cost_ex(Xd, Yd, out_dtype=torch.float16)
+    a = torch.full((4096,), 1.0 / 4096, device=dev)
+    b = torch.full((8192,), 1.0 / 8192, device=dev)
+    res = ops.sinkhorn(a, b, C, 0.01, max_iter=60, stop_thr=0.0, cost_scale=cmax, engine="sweep")
+    info = res.info()
+    assert res.shifted and info["engine_name"] == "sweep" and info["niter"] == 59
+    Pr, *_ = orc.sinkhorn_knopp(np.full(4096, 1.0 / 4096), np.full(8192, 1.0 / 8192),
+                                C.double().cpu().numpy(), 0.01, 60, 0.0, cscale=1.0 / float(cmax))
+    assert nrel(res.plan.cpu().numpy(), Pr) < TOL32
+
+
+def test_metric_shape_float64_leg_vs_oracle(orc, dev, metric_inputs, oracle_plans):
+    """The float64 leg of the metric config (bench.py metric_f64): float64 cost from the
+    embeddings and a float64 solve, held to 1e-9 of the float64 oracle -- at the bench's
+    reg = 0.1 and at the reference's per-epoch reg = 5e-3."""
+    from otfuse import gw, ops
     X, Y, _, _, Cr = metric_inputs
     Xd = torch.as_tensor(X, device=dev)
     Yd = torch.as_tensor(Y, device=dev)
-    from otfuse import gw
     C64, _ = gw.pairwise_cost_f64(Xd, Yd, scale_max=True)
     assert nrel(C64.cpu().numpy(), Cr) < 1e-12
     a = torch.full((N,), 1.0 / N, device=dev, dtype=torch.float64)
-    res = ops.sinkhorn(a, a, C64, 0.1, max_iter=100, stop_thr=0.0)
-    assert res.info()["status_name"] == "max_iter"
-    Pr, *_ = orc.sinkhorn_knopp(np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cr, 0.1, 100, 0.0)
-    assert nrel(res.plan.cpu().numpy(), Pr) < 1e-9
-
-
-def test_float32_underflow_regime_auto_takes_float64(orc, dev, metric_inputs):
-    """eps = 5e-3 on the max-normalised cost: some column's smallest C / eps exceeds
-    float32's exp range, so a float32 kernel-domain solve breaks at iteration 0 (and
-    warns), while POT's float64 solve runs on; precision='auto' detects it and solves in
-    float64: same iteration count, plan within the north star's 1e-4 (the float32 cost's
-    rounding, amplified by C / eps ~ 200, bounds it: 1.2e-5 measured); from a float64
-    cost the float64 solve holds 1e-9."""
-    from otfuse import gw, ops
-    X, Y, C, cmax, Cr = metric_inputs
-    eps = 5e-3
-    Pr, _, _, info_r = orc.sinkhorn_knopp(np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cr, eps, 100, 0.0)
-    a = torch.full((N,), 1.0 / N, device=dev)
-    r32 = ops.sinkhorn(a, a, C, eps, max_iter=100, stop_thr=0.0, cost_scale=cmax)
-    with warnings.catch_warnings(record=True) as rec:
-        warnings.simplefilter("always")
-        i32 = r32.info()
-    if info_r["break_iter"] == -1 and i32["status_name"] == "numerical_break":
-        assert any("float32 POT Sinkhorn broke" in str(w.message) for w in rec)
-    res = ops.sinkhorn(a, a, C, eps, max_iter=100, stop_thr=0.0, cost_scale=cmax, precision="auto")
-    info = res.info()
-    if i32["status_name"] == "numerical_break" and info_r["break_iter"] == -1:
-        assert res.u.dtype == torch.float64      # the detector routed it to float64
-    assert info["niter"] == info_r["niter"]
-    assert nrel(res.plan.cpu().numpy(), Pr) < 1e-4
-    C64, _ = gw.pairwise_cost_f64(torch.as_tensor(X, device=dev), torch.as_tensor(Y, device=dev),
-                                  scale_max=True)
-    a64 = a.double()
-    r64 = ops.sinkhorn(a64, a64, C64, eps, max_iter=100, stop_thr=0.0)
-    assert r64.info()["niter"] == info_r["niter"]
-    assert nrel(r64.plan.cpu().numpy(), Pr) < 1e-9
+    for eps in (0.1, 5e-3):
+        res = ops.sinkhorn(a, a, C64, eps, max_iter=100, stop_thr=0.0)
+        assert res.info()["status_name"] == "max_iter" and not res.shifted
+        Pr, *_ = oracle_plans(eps) if eps != 0.1 else orc.sinkhorn_knopp(
+            np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cr, 0.1, 100, 0.0)
+        assert nrel(res.plan.cpu().numpy(), Pr) < 1e-9
