@@ -324,6 +324,10 @@ typedef struct otf_xpeer otf_xpeer;
 size_t otf_xpeer_handle_size(void);
 int otf_xpeer_create(int32_t rank, int32_t world, int64_t m, otf_xpeer** out, void* handle_out);
 int otf_xpeer_connect(otf_xpeer* x, const void* handles);
+/* Synchronises the device, unmaps the peers' buffers and frees this rank's.  Every rank
+ * must have finished ALL its xsweep solves on this exchange first (e.g. a barrier across
+ * the ranks after a device sync): a peer's grid still running would store into the freed
+ * buffer. */
 int otf_xpeer_destroy(otf_xpeer* x);
 int otf_sinkhorn_xsweep(const void* a, const void* b, const void* C, int64_t n, int64_t m,
                         int64_t ldc, int32_t dtype, const void* cost_scale,

@@ -307,10 +307,15 @@ template <typename T, typename CT> bool sweep_supported(int64_t n, int64_t m, in
 struct XSweep {
     int rank, world, n_total;
     unsigned ep_base;
+    int solve_par;  // parity of this solve in the exchange's sequence (slot set)
     unsigned char* xr[8];
 };
 constexpr int kXMaxRanks = 8;
-inline size_t xsweep_exchange_bytes(int64_t m_pad) { return (size_t)2 * kXMaxRanks * m_pad * 8; }
+// [2 solve parities][2 epoch parities][8 ranks][m_pad] granules: consecutive solves use
+// disjoint slot sets, so a rank that starts solve s + 1 can never overwrite a partial of
+// solve s that a slower peer has still to read (solve s + 2 cannot start before every
+// peer finished solve s: its first exchange needs their solve-(s + 1) partials)
+inline size_t xsweep_exchange_bytes(int64_t m_pad) { return (size_t)4 * kXMaxRanks * m_pad * 8; }
 template <typename T, typename CT>
 hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T* a_pad,
                      const T* b_pad, const T* cost_scale, const otf_sinkhorn_opts& o, void* region,

@@ -2452,6 +2452,7 @@ struct otf_xpeer {
     void* own;
     void* peer[otf::kXMaxRanks];
     unsigned ep_base;
+    unsigned solves;  // solves issued on this exchange (their parity picks the slot set)
     int connected;
 };
 
@@ -2502,6 +2503,9 @@ int otf_xpeer_connect(otf_xpeer* x, const void* handles) {
 
 int otf_xpeer_destroy(otf_xpeer* x) {
     if (!x) return OTF_EINVAL;
+    // this rank's own solves are finished before its exchange buffer goes away; the
+    // caller's contract (include/otfuse.h) covers the peers' solves that store into it
+    (void)hipDeviceSynchronize();
     if (x->connected)
         for (int r = 0; r < x->world; ++r)
             if (r != x->rank && x->peer[r]) (void)hipIpcCloseMemHandle(x->peer[r]);
@@ -2527,6 +2531,8 @@ int otf_sinkhorn_xsweep(const void* a, const void* b, const void* C, int64_t n, 
     xs.world = x->world;
     xs.n_total = opts->n_total > 0 ? opts->n_total : (int)n;
     xs.ep_base = x->ep_base;
+    xs.solve_par = (int)(x->solves & 1u);
+    ++x->solves;
     for (int r = 0; r < x->world; ++r) xs.xr[r] = (unsigned char*)x->peer[r];
     // every rank makes the same sequence of calls: the bases stay in lock-step
     x->ep_base = x->ep_base + (unsigned)opts->max_iter + 4u;

@@ -103,6 +103,7 @@ template <typename T> struct SkSweepArgs {
     int rank, world;
     int n_total;           // rows over all ranks (POT's u0 = 1 / n)
     unsigned ep_base;      // epoch offset of this solve (the same on every rank)
+    int solve_par;         // the exchange's slot set for this solve (XSweep::solve_par)
     unsigned char* xr[8];
     ShiftArgs sh;          // shifted kernel (SH instances): offsets + initial scalings
 };
@@ -675,6 +676,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         const int swp = sw <= 64 ? 64 : sw <= 128 ? 128 : 256;   // lanes per row group
         const int Q = kSwNT / swp, sq = tid / swp, sj = tid % swp;
         const unsigned e = (p.ep_base + (unsigned)(k + 1)) & 0x3fffffffu;
+        const int xsp = 2 * (p.solve_par & 1);  // exchange slot set of this solve
         bool ok = true;
         // a. this workgroup's partials -> its slab row
         const uint32_t rowo = (uint32_t)blockIdx.x * (uint32_t)mc * 16u;
@@ -799,7 +801,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                 if (p.world > 1) {
                     if (xcd == __builtin_ctz(act_mask)) {
                         // this rank's partial of the slice -> every rank's exchange buffer
-                        const uint32_t xo = (uint32_t)(((e & 1) * 8 + p.rank) * mc + cch) * 16u;
+                        const uint32_t xo = (uint32_t)(((xsp + (e & 1)) * 8 + p.rank) * mc + cch) * 16u;
                         for (int r = 0; r < p.world; ++r)
                             gstore_sys(sums_rsrc(p.xr[r]), xo, chunk2(s0, s1, (int)(e << 2) | f));
                     }
@@ -809,7 +811,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 #pragma unroll
                     for (int r = 0; r < 8; ++r)
                         if (r < p.world) {
-                            y[r] = gload_sys(rxx, (uint32_t)(((e & 1) * 8 + r) * mc + cch) * 16u);
+                            y[r] = gload_sys(rxx, (uint32_t)(((xsp + (e & 1)) * 8 + r) * mc + cch) * 16u);
                             pr |= 1u << r;
                         }
 #pragma unroll
@@ -819,7 +821,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
                         for (int r = 0; r < 8; ++r)
-                            if (pr & (1u << r)) y[r] = gload_sys(rxx, (uint32_t)(((e & 1) * 8 + r) * mc + cch) * 16u);
+                            if (pr & (1u << r)) y[r] = gload_sys(rxx, (uint32_t)(((xsp + (e & 1)) * 8 + r) * mc + cch) * 16u);
 #pragma unroll
                         for (int r = 0; r < 8; ++r)
                             if ((pr & (1u << r)) && chunk_at(y[r], e)) pr &= ~(1u << r);
@@ -1250,6 +1252,7 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
         p.world = xs->world;
         p.n_total = xs->n_total;
         p.ep_base = xs->ep_base;
+        p.solve_par = xs->solve_par;
         for (int r = 0; r < xs->world; ++r) p.xr[r] = xs->xr[r];
     }
     size_t zero_bytes = sweep_ctrl_bytes(m_pad, sizeof(T));

@@ -239,14 +239,25 @@ class XPeer:
             raise RuntimeError("XPeer is closed")
         return self._h
 
-    def close(self):
+    def close(self, group=None):
+        """Collective: every rank must call it after its last solve on this exchange.
+        The device is synchronised (this rank's grids are done) and the ranks meet at a
+        barrier (every peer's grids are done storing into this rank's buffer) before the
+        buffer is freed."""
         if self._h is not None:
+            torch.cuda.synchronize()
+            if dist.is_available() and dist.is_initialized():
+                dist.barrier(group=group)
             L.lib().otf_xpeer_destroy(self._h)
             self._h = None
 
     def __del__(self):  # noqa: D105
+        # garbage collection is not collective: free without the barrier only if the
+        # caller never closed it (the device sync in otf_xpeer_destroy still runs)
         try:
-            self.close()
+            if self._h is not None:
+                L.lib().otf_xpeer_destroy(self._h)
+                self._h = None
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
 

@@ -76,12 +76,18 @@ def solve_ott(M: torch.Tensor, eps: float, scale_cost: str | None = "max_cost",
     kw = dict(max_iter=max_iterations, stop_thr=threshold, flavor="ott", cost_scale=scale,
               check_every=OTT_INNER, sync_every=sync_every, want_plan=True)
     if dt == torch.float64 and scale_cost == "max_cost" and 1.0 / float(eps) <= OTT_SCALING_MAX:
-        try:
-            res = ops.sinkhorn(a, b, M, float(eps), engine="resident", **kw)
-            if res.info_dev[3].item() != ops.L.SK_TIMEOUT:   # the grid was co-resident
-                return res, scale
-        except ops.L.OtfError:
-            pass                              # shape not taken by the resident engine
+        # the scaling form's range contract holds for 0 <= M / max M <= 1 only: a cost with
+        # negative entries (COOT-L with a user C_lin) or max M <= 0 takes the passes
+        mn, mx = (float(t) for t in torch.aminmax(M))
+        if mn >= 0.0 and mx > 0.0:
+            try:
+                res = ops.sinkhorn(a, b, M, float(eps), engine="resident", **kw)
+                # a timeout (grid not co-resident) or a break of the scaling form (a U or V
+                # out of float64's range, which OTT's lse mode does not hit): the passes
+                if res.info_dev[3].item() not in (ops.L.SK_TIMEOUT, ops.L.SK_NUMERICAL_BREAK):
+                    return res, scale
+            except ops.L.OtfError:
+                pass                          # shape not taken by the resident engine
     res = ops.sinkhorn(a, b, M, float(eps), **kw)
     return res, scale
 
