@@ -603,7 +603,10 @@ def cpu_baseline(X, Y, N, iters, eps, threads):
     # times 10 iterations and scales the loop to `iters` to stay within the bench budget
     used, tot, tc, tl = _cpu_port_run(orc, X, Y, N, iters, eps, share)
     runs["cpu_share"] = {"threads": used, "seconds": tot, "cost_s": tc, "loop_plan_s": tl}
-    if all_threads != share:
+    # the box grants this process `share` CPUs (OMP_NUM_THREADS) of the host's nproc: an
+    # all-core run is oversubscribed there (r03: 33 s on 256 threads against 0.52 s on 16),
+    # so it runs only when asked for (--cpu-threads) or when the share is the whole host
+    if all_threads != share and (threads or share >= nproc):
         used, tot, tc, tl = _cpu_port_run(orc, X, Y, N, 10, eps, all_threads, reps=1)
         tl *= iters / 10.0
         runs["all_cores"] = {"threads": used, "seconds": tc + tl, "cost_s": tc, "loop_plan_s": tl,
@@ -643,6 +646,10 @@ def cpu_baseline(X, Y, N, iters, eps, threads):
     orc.set_threads(best["threads"])
     return {"value": N / best["seconds"], "unit": "pairs/s", "cores": best["threads"], "kind": "port",
             "nproc": nproc, "affinity_cpus": affinity, "omp_share": share, "chosen": best_key,
+            "host_cpu_quota": {"granted_cpus": share, "nproc": nproc,
+                               "note": f"the GPU box grants this process {share} of the host's "
+                                       f"{nproc} CPUs (OMP_NUM_THREADS); the baseline runs on "
+                                       f"that share"},
             "sinkhorn_iters_per_sec": iters / best["loop_plan_s"], "seconds": best["seconds"],
             "sample": f"full workload, median of 3: N={N} d={X.shape[1]} {iters} iters float64 "
                       f"(cost {best['cost_s']:.2f}s + loop/plan {best['loop_plan_s']:.2f}s) with "

@@ -823,7 +823,13 @@ __device__ __forceinline__ float epilogue_tile256_16t(const f32x4 (&acc)[4][8], 
     return (float)(TC)(lmax * os);
 }
 
-template <int NS, typename TC>
+// F32IN (split-fp16 only): X / Y are the float32 embeddings themselves (Xh / Yh cast back,
+// ldxh / ldyh in floats, d a multiple of the 64-deep image padding, rows 16-B aligned);
+// every stage is split into its hi / lo fp16 images in registers on the way to LDS with
+// the row's power-of-two scale 1 / xs (the prep kernel then writes only the norms and
+// scales): the same images as split16_prep2_kernel's, so the same bits, without their
+// 33.7 MB HBM round trip (fp32 operand bytes = hi + lo image bytes).
+template <int NS, typename TC, bool F32IN = false>
 __global__ __launch_bounds__(512) void cost_big16_kernel(
     const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
     const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
@@ -855,7 +861,18 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
         for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     using u4 = __attribute__((ext_vector_type(4))) unsigned int;
+    static_assert(!F32IN || NI == 2, "float32 operands are split into two images");
     u4 st[NCH][2 * NI];
+    // F32IN: the row scales of this thread's staging rows (fixed across stages)
+    float scx[NCH], scy[NCH];
+    if constexpr (F32IN) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int row = (tid + 512 * c) / GCPR;
+            scx[c] = 1.0f / xs[i0 + row < n ? i0 + row : n - 1];
+            scy[c] = 1.0f / ys[j0 + row < m ? j0 + row : m - 1];
+        }
+    }
     auto gload = [&](int k0) {
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
@@ -863,23 +880,56 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
             const int row = chunk / GCPR, kc = (chunk % GCPR) * 8;
             const int gi = i0 + row < n ? i0 + row : n - 1;
             const int gj = j0 + row < m ? j0 + row : m - 1;
-            st[c][0] = *reinterpret_cast<const u4*>(Xh + (int64_t)gi * ldxh + k0 + kc);
-            st[c][NI] = *reinterpret_cast<const u4*>(Yh + (int64_t)gj * ldyh + k0 + kc);
-            if (NI == 2) {
-                st[c][1] = *reinterpret_cast<const u4*>(Xl + (int64_t)gi * ldxh + k0 + kc);
-                st[c][NI + 1] = *reinterpret_cast<const u4*>(Yl + (int64_t)gj * ldyh + k0 + kc);
+            if constexpr (F32IN) {
+                // 8 consecutive floats = the same 32 B the two fp16 images would take
+                const float* xr = reinterpret_cast<const float*>(Xh) + (int64_t)gi * ldxh + k0 + kc;
+                const float* yr = reinterpret_cast<const float*>(Yh) + (int64_t)gj * ldyh + k0 + kc;
+                st[c][0] = *reinterpret_cast<const u4*>(xr);
+                st[c][1] = *reinterpret_cast<const u4*>(xr + 4);
+                st[c][NI] = *reinterpret_cast<const u4*>(yr);
+                st[c][NI + 1] = *reinterpret_cast<const u4*>(yr + 4);
+            } else {
+                st[c][0] = *reinterpret_cast<const u4*>(Xh + (int64_t)gi * ldxh + k0 + kc);
+                st[c][NI] = *reinterpret_cast<const u4*>(Yh + (int64_t)gj * ldyh + k0 + kc);
+                if (NI == 2) {
+                    st[c][1] = *reinterpret_cast<const u4*>(Xl + (int64_t)gi * ldxh + k0 + kc);
+                    st[c][NI + 1] = *reinterpret_cast<const u4*>(Yl + (int64_t)gj * ldyh + k0 + kc);
+                }
             }
         }
+    };
+    // x s = hi + lo, hi = fp16(x s), lo = fp16(x s - hi): split16_prep2_kernel's images
+    auto split8 = [&](u4 a, u4 b, float sc, u4& h, u4& l) {
+        using H8 = __attribute__((ext_vector_type(8))) _Float16;
+        H8 hv, lv;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float w = __builtin_bit_cast(float, q < 4 ? a[q] : b[q - 4]) * sc;
+            hv[q] = (_Float16)w;
+            lv[q] = (_Float16)(w - (float)hv[q]);
+        }
+        h = __builtin_bit_cast(u4, hv);
+        l = __builtin_bit_cast(u4, lv);
     };
     auto lstore = [&](int buf) {
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
             const int chunk = tid + 512 * c;
             const int row = chunk / GCPR, kc = chunk % GCPR;
+            if constexpr (F32IN) {
+                u4 h, l;
+                split8(st[c][0], st[c][1], scx[c], h, l);
+                *reinterpret_cast<u4*>(&As[buf][0][g16swz(row, kc)]) = h;
+                *reinterpret_cast<u4*>(&As[buf][1][g16swz(row, kc)]) = l;
+                split8(st[c][NI], st[c][NI + 1], scy[c], h, l);
+                *reinterpret_cast<u4*>(&Bs[buf][0][g16swz(row, kc)]) = h;
+                *reinterpret_cast<u4*>(&Bs[buf][1][g16swz(row, kc)]) = l;
+            } else {
 #pragma unroll
-            for (int h = 0; h < NI; ++h) {
-                *reinterpret_cast<u4*>(&As[buf][h][g16swz(row, kc)]) = st[c][h];
-                *reinterpret_cast<u4*>(&Bs[buf][h][g16swz(row, kc)]) = st[c][NI + h];
+                for (int h = 0; h < NI; ++h) {
+                    *reinterpret_cast<u4*>(&As[buf][h][g16swz(row, kc)]) = st[c][h];
+                    *reinterpret_cast<u4*>(&Bs[buf][h][g16swz(row, kc)]) = st[c][NI + h];
+                }
             }
         }
     };
@@ -1452,6 +1502,12 @@ static bool cost_mfma16_enabled(bool f16out) {
     const char* e = getenv("OTF_COST_MFMA16");
     return e ? atoi(e) != 0 : !f16out;
 }
+// OTF_COST_F32IN=0 keeps the fp16 images in the workspace for the 16x16x32 kernel instead of
+// splitting the float32 operands in it (A/B and the bit-identity test; read per call)
+static bool cost_f32in_enabled() {
+    const char* e = getenv("OTF_COST_F32IN");
+    return e ? atoi(e) != 0 : true;
+}
 // OTF_COST_WS=1 selects the warp-specialised persistent kernel (read per call)
 static bool cost_ws_enabled() {
     const char* e = getenv("OTF_COST_WS");
@@ -1554,6 +1610,19 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     const bool alias = !split && d % otf::SBK == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
                        (uintptr_t)X % 16 == 0 && (uintptr_t)Y % 16 == 0;
     int64_t ldxh = ldh, ldyh = ldh;
+    // float32 operands split inside the 256 x 256 16x16x32 kernel (F32IN): decided before
+    // the prep, which then writes only the norms and the row scales
+    // Tile choice by rounds of resident workgroups (two 128 x 128 per CU, one 256 x 256):
+    // a round of 256 x 256 tiles took 1.8x a round of 128 x 128 ones at N = 4096
+    // (68 vs 38 us), so big tiles win when they need fewer than 1 / 1.8 of the rounds
+    // (N = 4096: 1 vs 2 rounds; config 5: 4 vs 8), not for a ragged 17 x 16 grid (2 vs 3).
+    const int64_t cus0 = otf::device_cu_count();
+    const int64_t big_rounds = (((n + otf::GBM - 1) / otf::GBM) * ((m + otf::GBN - 1) / otf::GBN) + cus0 - 1) / cus0;
+    const int64_t small_rounds = (((n + otf::BM - 1) / otf::BM) * ((m + otf::BN - 1) / otf::BN) + 2 * cus0 - 1) / (2 * cus0);
+    const bool big0 = 18 * big_rounds < 10 * small_rounds && cost_big_enabled();
+    const bool f32in = split && big0 && cost_mfma16_enabled(c_dtype == OTF_F16) && cost_f32in_enabled() &&
+                       !cost_ring_enabled() && !cost_ws_enabled() && d % otf::SBK == 0 && ldx % 4 == 0 &&
+                       ldy % 4 == 0 && (uintptr_t)X % 16 == 0 && (uintptr_t)Y % 16 == 0;
     {
         const int rows = (int)n + (same ? 0 : (int)m);
         const int nblk = (rows + 3) / 4 < 1024 ? (rows + 3) / 4 : 1024;
@@ -1561,9 +1630,9 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
         const int vec = (ldx * isz % 16 == 0 && ldy * isz % 16 == 0 && (uintptr_t)X % 16 == 0 &&
                          (uintptr_t)Y % 16 == 0) ? 1 : 0;
         if (split) {
-            const otf::PrepSide<float> A{(const float*)X, ldx, (int)n, Xh, Xl, xs, xx, mn};
-            const otf::PrepSide<float> B{(const float*)Y, ldy, same ? 0 : (int)m, Yh, Yl, ys, yy,
-                                         mn ? mn + 1 : nullptr};
+            const otf::PrepSide<float> A{(const float*)X, ldx, (int)n, f32in ? nullptr : Xh, Xl, xs, xx, mn};
+            const otf::PrepSide<float> B{(const float*)Y, ldy, same ? 0 : (int)m, f32in ? nullptr : Yh, Yl,
+                                         ys, yy, mn ? mn + 1 : nullptr};
             otf::split16_prep2_kernel<float, true><<<nblk, 256, 0, s>>>(A, B, (int)d, ldh, vec,
                                                                        (unsigned int*)cmax,
                                                                        f16out ? nullptr : c_unit);
@@ -1596,16 +1665,8 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
         store_scale = small + 2;
     }
     // cmax = 0 and c_unit = 1 (fp32 storage) were written by the prep kernel
-    // Tile choice by rounds of resident workgroups (two 128 x 128 per CU, one 256 x 256):
-    // a round of 256 x 256 tiles took 1.8x a round of 128 x 128 ones at N = 4096
-    // (68 vs 38 us), so big tiles win when they need fewer than 1 / 1.8 of the rounds
-    // (N = 4096: 1 vs 2 rounds; config 5: 4 vs 8), not for a ragged 17 x 16 grid (2 vs 3).
-    const int64_t cus = otf::device_cu_count();
-    const int64_t big_tiles = ((n + otf::GBM - 1) / otf::GBM) * ((m + otf::GBN - 1) / otf::GBN);
-    const int64_t small_tiles = ((n + otf::BM - 1) / otf::BM) * ((m + otf::BN - 1) / otf::BN);
-    const int64_t big_rounds = (big_tiles + cus - 1) / cus;
-    const int64_t small_rounds = (small_tiles + 2 * cus - 1) / (2 * cus);
-    const bool big = 18 * big_rounds < 10 * small_rounds && cost_big_enabled();
+    const int64_t cus = cus0;
+    const bool big = big0;
     const bool ring = cost_ring_enabled() && ring_lds_ok();
     const bool mfma16 = cost_mfma16_enabled(f16out);
     const int BMx = big ? otf::GBM : otf::BM, BNx = big ? otf::GBN : otf::BN;
@@ -1630,6 +1691,11 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
             otf::cost_ring_kernel<NS, TC><<<(int)nwg, 512, otf::kRingLds, s>>>(                  \
                 Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
                 zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
+        else if (big && mfma16 && f32in)                                                          \
+            otf::cost_big16_kernel<NS, TC, NS == 3><<<(int)nwg, 512, 0, s>>>(                    \
+                (const _Float16*)X, nullptr, xs, xx, (const _Float16*)Y, nullptr, ys, yy, ldx,   \
+                ldy, (int)n, (int)m, (int)d, metric, zero_diag, (TC*)C, ldc, (unsigned int*)cmax, \
+                tiles_n, store_scale);                                                            \
         else if (big && mfma16)                                                                   \
             otf::cost_big16_kernel<NS, TC><<<(int)nwg, 512, 0, s>>>(                             \
                 Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \

@@ -109,6 +109,29 @@ def test_cost_mfma16_kernel_matches_oracle(ops, orc, dev, monkeypatch, n, m, d, 
     assert nrel(got, Cr) < (2e-3 if out_dt == torch.float16 else 2e-6)
 
 
+@pytest.mark.parametrize("n,m,d,out_dt,metric,same", [
+    (4096, 4096, 512, torch.float32, "sqeuclidean", False),
+    (4100, 3999, 256, torch.float32, "euclidean", False),
+    (3000, 3000, 128, torch.float32, "sqeuclidean", True),
+    (8192, 8192, 256, torch.float16, "sqeuclidean", False),
+    (4096, 4096, 300, torch.float32, "sqeuclidean", False)])   # d % 64 != 0: image path
+def test_cost_f32in_split_in_kernel_is_bit_identical(ops, dev, monkeypatch, n, m, d, out_dt, metric, same):
+    """The 16x16x32 kernel splitting the float32 operands into hi / lo fp16 in registers
+    (OTF_COST_F32IN, default) builds the same images as split16_prep2_kernel: the same
+    cost bits, cmax and unit as the prep-image path (OTF_COST_F32IN=0), ragged tiles,
+    the Euclidean metric, X is Y (zero diagonal) and fp16 storage included."""
+    g = torch.Generator(device=dev).manual_seed(n + d + 7)
+    X = torch.randn(n, d, device=dev, generator=g) * torch.logspace(-2, 2, n, device=dev)[:, None]
+    Y = X if same else (torch.randn(m, d, device=dev, generator=g) * 0.7 + 0.2)
+    monkeypatch.setenv("OTF_COST_MFMA16", "1")
+    monkeypatch.setenv("OTF_COST_F32IN", "0")
+    C0, mx0, u0 = ops.pairwise_cost_ex(X, Y, metric=metric, out_dtype=out_dt)
+    monkeypatch.setenv("OTF_COST_F32IN", "1")
+    C1, mx1, u1 = ops.pairwise_cost_ex(X, Y, metric=metric, out_dtype=out_dt)
+    torch.cuda.synchronize()
+    assert torch.equal(C0, C1) and torch.equal(mx0, mx1) and torch.equal(u0, u1)
+
+
 def test_pairwise_cost_euclidean_same_input_zero_diag(ops, orc, dev):
     rng = np.random.default_rng(1)
     X = rng.random((70, 33)).astype(np.float32)

@@ -141,8 +141,10 @@ def test_shifted_fp16_storage_sweep_vs_oracle(orc, dev):
     res = ops.sinkhorn(a, b, C, 0.01, max_iter=60, stop_thr=0.0, cost_scale=cmax, engine="sweep")
     info = res.info()
     assert res.shifted and info["engine_name"] == "sweep" and info["niter"] == 59
+    Cs = C.float().cpu().numpy().astype(np.float64)
+    assert float(cmax) == Cs.max()       # stored values <= 1, cmax = their max
     Pr, *_ = orc.sinkhorn_knopp(np.full(4096, 1.0 / 4096), np.full(8192, 1.0 / 8192),
-                                C.double().cpu().numpy(), 0.01, 60, 0.0, cscale=1.0 / float(cmax))
+                                Cs / float(cmax), 0.01, 60, 0.0)
     assert nrel(res.plan.cpu().numpy(), Pr) < TOL32
 
 
