@@ -454,83 +454,132 @@ __device__ int blk_sinkhorn_knopp(const double* K, int64_t ldk, int n, int m, co
     return cur;
 }
 
-// The same sinkhorn_knopp for n, m <= 64 with two workgroup barriers per update (the
-// block version above spends four, plus LDS round trips for u and v; at <= 64 points
-// the barriers dominate).  K is a zero-padded 64 x 65 LDS image (entries outside
-// n x m are 0).  Every wavefront holds the whole u (lane i) and v (lane j) in
-// registers: wavefront w forms the partial column sums of K^T u over its RPW rows
-// and, after a barrier, every wavefront sums the NW partials of its lane's column in
-// the same order, so all of them compute the same v; the row sums (Kp v) go the same
-// way over column slices.  Identical values in every wavefront make the numerical-
-// error ballot and the stop test uniform, so the barrier counts always agree.  The
-// previous pair stays in registers for the revert-on-error rule.  u ends in sh.f,
-// v in sh.g (slot 0); conv / iters are uniform.
+// The same sinkhorn_knopp for n, m <= 64 (the reference's per-label groups) at the
+// latency of two workgroup barriers per update and no LDS traffic for K: the PGD outer
+// loop runs ~1000 inner updates per outer iteration in one serial chain (562 k updates
+// for the 64 x 64, eps = 5e-3 bench problem), so the update latency is the solve time.
+// K (a zero-padded 64 x 65 LDS image, entries outside n x m are 0) is read into
+// registers once per call, in both orientations the two half-updates need:
+//   V half, v = b / K^T u:  wave w owns columns 8w .. 8w + 7; lane (q, s) = (l & 7, l >> 3)
+//                           holds K[8s + r][8w + q], r < 8, and sums them against
+//                           u[8s .. 8s + 7] (LDS, 4 broadcast reads), then xor 8 / 16 / 32;
+//   U half, u = 1 / (Kp v): wave w owns rows 8w .. 8w + 7, lane (q, s) holds
+//                           Kp[8w + q][8s + c] = K / a and sums them against v[8s ..].
+// Every lane of a column (row) group ends with the same sum, so every lane has the new v
+// (u) of its column (row) and keeps the previous one for POT's revert-on-error rule.
+// POT's error check after update ii (every `every` updates: tmp2 = sum_i u_i K_ij v_j,
+// err = ||tmp2 - b||) reuses the V half of update ii + 1 (tmp2_j = (K^T u)_j v_j, the same
+// K^T u), so a check costs one wave sum and one LDS word per wave; on convergence the v
+// that half computed is dropped.  u ends in sh.f, v in sh.g; conv / iters are uniform.
 constexpr int GW_WLD = GW_SMALLN + 1;
 
 template <class Cfg>
 __device__ void small_sinkhorn_knopp(const double* K, int n, int m, const double* a, const double* b,
                                      double thr, int maxit, int every, GwShared<Cfg>& sh,
                                      bool& conv, int& iters) {
-    static_assert(GW_SMALLN % Cfg::NW == 0 && Cfg::NT <= 8 * GW_SMALLN, "row slices");
-    constexpr int RPW = GW_SMALLN / Cfg::NW;
+    static_assert(GW_SMALLN == 64, "8 columns / rows per wave");
+    if constexpr (Cfg::NW != 8) {  // only the GwSmall kernel calls it (n, m <= 64)
+        __builtin_trap();
+    } else {
+    __shared__ __attribute__((aligned(16))) double s_u[GW_SMALLN];
+    __shared__ __attribute__((aligned(16))) double s_v[GW_SMALLN];
+    __shared__ double s_e[8];
+    __shared__ int s_kf[2];
     const int l = threadIdx.x & (kWave - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const bool rl = l < n, cl = l < m;
-    const double ia = rl ? 1.0 / marg(a, l, n) : 0.0;
-    const double bj = cl ? marg(b, l, m) : 0.0;
-    const double* kcol = K + (w * RPW) * GW_WLD + l;  // rows w*RPW.., column l
-    const double* krow = K + l * GW_WLD + w * RPW;    // row l, columns w*RPW..
-    double* pc = sh.ps;                               // NW x 64 column partials
-    double* pr = sh.pm;                               // NW x 64 row partials
-    double u = rl ? 1.0 / (double)n : 0.0, v = cl ? 1.0 / (double)m : 0.0;
+    const int q = l & 7, sg = l >> 3;
+    const int jc = 8 * w + q;  // V half: this lane's column
+    const int ir = 8 * w + q;  // U half: this lane's row
+    const bool cl = jc < m, rl = ir < n;
+    const double bj = cl ? marg(b, jc, m) : 0.0;
+    const double ia = rl ? 1.0 / marg(a, ir, n) : 0.0;
+    double kv[8], ku[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) kv[r] = K[(8 * sg + r) * GW_WLD + jc];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) ku[c] = ia * K[ir * GW_WLD + 8 * sg + c];  // Kp = K / a (POT)
+    if (threadIdx.x < GW_SMALLN) s_u[threadIdx.x] = (int)threadIdx.x < n ? 1.0 / (double)n : 0.0;
+    if (threadIdx.x < 2) s_kf[threadIdx.x] = 0;
+    double u = rl ? 1.0 / (double)n : 0.0, v = cl ? 1.0 / (double)m : 0.0;  // last good pair
+    __syncthreads();
     conv = false;
     iters = maxit;
-    for (int ii = 0; ii < maxit; ++ii) {
-        // v = b / K^T u
-        double s = 0.0;
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) s += kcol[r * GW_WLD] * readlane_f64(u, w * RPW + r);
-        pc[w * kWave + l] = s;
-        __syncthreads();
-        s = 0.0;
-#pragma unroll
-        for (int q = 0; q < Cfg::NW; ++q) s += pc[q * kWave + l];
+    bool check = false;  // POT's error check of the previous update is pending
+    using D2 = __attribute__((ext_vector_type(2))) double;
+    for (int ii = 0;; ++ii) {
+        if (ii == maxit && !check) break;
+        // ---- V half: s = (K^T u)_jc; v = b / s
+        double s;
+        {
+            const D2* up = reinterpret_cast<const D2*>(&s_u[8 * sg]);
+            const D2 u01 = up[0], u23 = up[1], u45 = up[2], u67 = up[3];
+            s = kv[0] * u01[0];
+            s = fma(kv[1], u01[1], s);
+            s = fma(kv[2], u23[0], s);
+            s = fma(kv[3], u23[1], s);
+            s = fma(kv[4], u45[0], s);
+            s = fma(kv[5], u45[1], s);
+            s = fma(kv[6], u67[0], s);
+            s = fma(kv[7], u67[1], s);
+            s += wave_xor<double, 8>(s);
+            s += wave_xor<double, 16>(s);
+            s += wave_xor<double, 32>(s);
+        }
+        if (check) {
+            // err of the previous update: tmp2_j = (K^T u)_j v_j
+            const double d = cl ? s * v - bj : 0.0;
+            double e = sg == 0 ? d * d : 0.0;
+            e += wave_xor<double, 1>(e);
+            e += wave_xor<double, 2>(e);
+            e += wave_xor<double, 4>(e);
+            if (l == 0) s_e[w] = e;
+        }
         const double vn = cl ? bj / s : 0.0;
-        bool bad = cl && (s == 0.0 || !finite_val(vn));
-        // u = 1 / (Kp v)
-        s = 0.0;
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) s += (ia * krow[r]) * readlane_f64(vn, w * RPW + r);
-        pr[w * kWave + l] = s;
+        const bool badv = cl && (s == 0.0 || !finite_val(vn));
+        if (sg == 0) s_v[jc] = vn;
+        if (__ballot(badv) != 0 && l == 0) s_kf[ii & 1] = 1;
         __syncthreads();
-        s = 0.0;
+        if (check) {
+            double e2 = s_e[0];
 #pragma unroll
-        for (int q = 0; q < Cfg::NW; ++q) s += pr[q * kWave + l];
+            for (int k = 1; k < 8; ++k) e2 += s_e[k];
+            if (sqrt(e2) < thr) { conv = true; iters = ii; break; }  // the checked update's pair
+        }
+        if (ii == maxit) break;  // the last update's check only
+        // every reader of the other parity's flag (update ii - 1) is past this barrier
+        if (threadIdx.x == 0) s_kf[(ii + 1) & 1] = 0;
+        // ---- U half: s = (Kp v)_ir; u = 1 / s
+        {
+            const D2* vp = reinterpret_cast<const D2*>(&s_v[8 * sg]);
+            const D2 v01 = vp[0], v23 = vp[1], v45 = vp[2], v67 = vp[3];
+            s = ku[0] * v01[0];
+            s = fma(ku[1], v01[1], s);
+            s = fma(ku[2], v23[0], s);
+            s = fma(ku[3], v23[1], s);
+            s = fma(ku[4], v45[0], s);
+            s = fma(ku[5], v45[1], s);
+            s = fma(ku[6], v67[0], s);
+            s = fma(ku[7], v67[1], s);
+            s += wave_xor<double, 8>(s);
+            s += wave_xor<double, 16>(s);
+            s += wave_xor<double, 32>(s);
+        }
         const double un = rl ? 1.0 / s : 0.0;
-        bad = bad || (rl && !finite_val(un));
-        if (__ballot(bad) != 0) { iters = ii + 1; break; }  // keep the previous pair
+        const bool badu = rl && !finite_val(un);
+        if (sg == 0) s_u[ir] = un;
+        if (__ballot(badu) != 0 && l == 0) s_kf[ii & 1] = 1;
+        __syncthreads();
+        if (s_kf[ii & 1]) { iters = ii + 1; break; }  // numerical error: keep the previous pair
         u = un;
         v = vn;
-        if (ii % every == 0) {
-            s = 0.0;
-#pragma unroll
-            for (int r = 0; r < RPW; ++r) s += kcol[r * GW_WLD] * readlane_f64(u, w * RPW + r);
-            pc[w * kWave + l] = s;  // every column-partial read of this update is done
-            __syncthreads();
-            s = 0.0;
-#pragma unroll
-            for (int q = 0; q < Cfg::NW; ++q) s += pc[q * kWave + l];
-            const double d = cl ? s * v - bj : 0.0;
-            const double e2 = wave_reduce_f64<0>(d * d);
-            __syncthreads();  // reads done before the next update rewrites pc
-            if (sqrt(e2) < thr) { conv = true; iters = ii + 1; break; }
-        }
+        check = (ii % every) == 0;
     }
-    if (w == 0) {
-        sh.f[l] = u;
-        sh.g[l] = v;
+    if (sg == 0) {
+        sh.f[ir] = u;
+        sh.g[jc] = v;
     }
     __syncthreads();
+    }
 }
 
 // Minimum-cost assignment of the n x n matrix A (row stride lda), ONE wavefront:

@@ -321,7 +321,8 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
                      const T* b_pad, const T* cost_scale, const otf_sinkhorn_opts& o, void* region,
                      T* u_out, T* v_out, void* P_out, int64_t ldp, int P_dtype,
                      otf_sinkhorn_info* info, double* errlog, hipStream_t s,
-                     const XSweep* xs = nullptr, const ShiftArgs* sh = nullptr);
+                     const XSweep* xs = nullptr, const ShiftArgs* sh = nullptr,
+                     void* kbuf = nullptr);
 
 // Gather engine (otf_gather.hip): small problems (<= 16 row tiles, m <= 512), column
 // partials exchanged as epoch-tagged granules, no barrier.  `region` is zeroed by the

@@ -1755,7 +1755,9 @@ struct Workspace {
     float* v0v;
     float* shpart;
     int nrep;
-    size_t bytes;
+    size_t bytes;     // required: every engine but the float64 K stream
+    void* kbuf;       // float64: K (n x m_pad) for the sweep engine's K stream, past `bytes`
+    size_t bytes_k;   // bytes + the K buffer (what otf_sinkhorn_workspace_size asks for)
     int64_t m_pad;
     int64_t t_nrb, t_ncb;  // tiled engine: row / column tiles
     size_t t_xch_off;      // tiled engine: exchange region offset inside res
@@ -1821,6 +1823,11 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
         w.shpart = (float*)take(2 * sizeof(float) * (size_t)shift_chunks(n) * w.m_pad);
     }
     w.bytes = off;
+    // float64: the sweep engine streams K = exp(-C / reg) written once by its prologue
+    // (POT materialises K too) when the caller's workspace reaches this far; a workspace of
+    // `bytes` still runs every engine (the sweep then recomputes the exp per sweep)
+    w.kbuf = esz == 8 ? take((size_t)n * (size_t)w.m_pad * esz) : nullptr;
+    w.bytes_k = off;
     return w;
 }
 
@@ -2159,6 +2166,14 @@ inline bool mesh_enabled() {
     return env != 0;
 }
 
+// float64 sweep engine: K streamed from the workspace (written by the prologue sweep) when
+// the caller's workspace holds it; OTF_SWEEP_KSTREAM=0 recomputes the exp per sweep (A/B)
+template <typename T> void* kstream_buf(const SkSetup<T>& su, size_t ws_bytes) {
+    if (sizeof(T) != 8 || !su.w.kbuf || ws_bytes < su.w.bytes_k) return nullptr;
+    const char* e = getenv("OTF_SWEEP_KSTREAM");  // read per call (a test switches it)
+    return (e && atoi(e) == 0) ? nullptr : su.w.kbuf;
+}
+
 template <typename T, typename CT, bool LOG>
 int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_t ldc,
                  const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out, void* P_out,
@@ -2235,7 +2250,8 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
             return OTF_EUNSUPPORTED;
         const hipError_t e = run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
                                               (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
-                                              v_out, P_out, ldp, P_dtype, info, errlog, s, nullptr, shp);
+                                              v_out, P_out, ldp, P_dtype, info, errlog, s, nullptr, shp,
+                                              kstream_buf(su, ws_bytes));
         if (e != hipSuccess) return check_hip(e);
         return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
     }
@@ -2293,7 +2309,8 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     if (sfits && (o.engine == OTF_ENGINE_SWEEP || o.engine == OTF_ENGINE_AUTO)) {
         const hipError_t e = run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
                                               (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
-                                              v_out, P_out, ldp, P_dtype, info, errlog, s, nullptr, shp);
+                                              v_out, P_out, ldp, P_dtype, info, errlog, s, nullptr, shp,
+                                              kstream_buf(su, ws_bytes));
         if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
         (void)hipGetLastError();
         if (o.engine == OTF_ENGINE_SWEEP) return check_hip(e);
@@ -2560,7 +2577,7 @@ int otf_sinkhorn_fallback_count(uint64_t* count) {
 size_t otf_sinkhorn_workspace_size(int64_t n, int64_t m, int32_t dtype, int32_t max_iter) {
     const size_t esz = dtype == OTF_F64 ? 8 : 4;
     const int64_t nrb = dtype == OTF_F64 ? otf::row_blocks<double>(n, m) : otf::row_blocks<float>(n, m);
-    return otf::carve(nullptr, n, m, esz, max_iter < 0 ? 0 : max_iter, nrb).bytes;
+    return otf::carve(nullptr, n, m, esz, max_iter < 0 ? 0 : max_iter, nrb).bytes_k;
 }
 
 int otf_sinkhorn_shift_offsets(int64_t n, int64_t m, int32_t dtype, int32_t max_iter,

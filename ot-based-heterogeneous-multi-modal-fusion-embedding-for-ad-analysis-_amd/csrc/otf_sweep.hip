@@ -106,6 +106,8 @@ template <typename T> struct SkSweepArgs {
     int solve_par;         // the exchange's slot set for this solve (XSweep::solve_par)
     unsigned char* xr[8];
     ShiftArgs sh;          // shifted kernel (SH instances): offsets + initial scalings
+    T* kbuf;               // KS instances: K = exp(-C / reg) written by the prologue sweep,
+                           // n rows x m_pad, streamed by every later sweep instead of C
 };
 constexpr int kSwSlices = 32;  // column slices of the granule reduction
 
@@ -172,7 +174,13 @@ __device__ __forceinline__ double bcast_lane(double x, int r) {
 
 // SH (float only): the shifted POT kernel e = 2^(C ks + A_i + B_j) (otf_persist.h
 // ShiftArgs); B of the columns and A of the workgroup's rows sit in LDS beside 1 / a.
-template <typename T, typename CT, typename TP, int G, int R, int NREP, bool SH>
+// KS (float64 only): POT's own form -- K = exp(-M / reg) materialised once (ot.bregman
+// sinkhorn_knopp, perturbot/perturbot/match/utils.py:46) -- the prologue sweep writes the
+// K of the workgroup's row blocks to p.kbuf and every later sweep (and the plan) streams
+// K instead of recomputing a float64 exp per element per sweep: the float64 exp (~20 FMA
+// -class instructions) was the largest cost of a float64 sweep.  Same exp, same values:
+// the same iterates bit for bit.
+template <typename T, typename CT, typename TP, int G, int R, int NREP, bool SH, bool KS = false>
 __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     constexpr int VC = RawN<CT>::N;            // cost elements per 16-B chunk
     constexpr int VT = Vec<T>::N;              // compute elements per 16-B sum load
@@ -247,6 +255,8 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     const int my_nb = nrb > (int)blockIdx.x ? (nrb - 1 - (int)blockIdx.x) / nwg + 1 : 0;
     const int res0 = my_nb - p.nres;  // first LDS-resident block (nres < every my_nb)
     const int64_t ld_bytes = p.ldc * (int64_t)sizeof(CT);
+    static_assert(!KS || (sizeof(T) == 8 && sizeof(CT) == 8 && !SH), "K stream: float64 only");
+    const int64_t ldk_bytes = (int64_t)p.m_pad * (int64_t)sizeof(T);
     for (int i = tid; i < my_nb * R; i += kSwNT) {
         const int row = ((int)blockIdx.x + (i / R) * nwg) * R + i % R;
         ialds[i] = (T)1 / p.a[row < p.n ? row : 0];
@@ -260,9 +270,21 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     // larger than the Infinity Cache is loaded non-temporal (7.3 vs 6.4 TB/s from HBM,
     // tools/ubench_mall.hip; N = 16384 fp32: 195 -> 184 us per sweep); a cost that fits
     // keeps the default policy (nt measured 26.2 vs 22.3 us per config-5 sweep).
-    auto load_block = [&](int bi, Raw (&buf)[R][G]) {
+    // fromK (KS): the block of K from p.kbuf (written by this workgroup's prologue sweep)
+    auto load_block = [&](int bi, Raw (&buf)[R][G], bool fromK = false) {
         const int r0 = ((int)blockIdx.x + bi * nwg) * R;
         const int nrow = p.n - r0 < R ? p.n - r0 : R;
+        if (KS && fromK) {
+            const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)((char*)p.kbuf + (int64_t)r0 * ldk_bytes), 0, (int)(nrow * ldk_bytes), 0x00020000);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    buf[r][g] = __builtin_amdgcn_raw_buffer_load_b128(
+                        kr, (uint32_t)(colc[g] * (int)sizeof(T)), (uint32_t)(r * ldk_bytes), 0);
+            return;
+        }
         const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
             (void*)((const char*)p.C + (int64_t)r0 * ld_bytes), 0, (int)(nrow * ld_bytes), 0x00020000);
         if (p.nt_loads) {
@@ -413,14 +435,26 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         auto process = [&](int bi, Raw (&buf)[R][G], int next) {
             const int r0 = ((int)blockIdx.x + bi * nwg) * R;
             const int nrow = p.n - r0 < R ? p.n - r0 : R;
+            T2 e[R][G][VP2];
+            if (KS && it >= 0) {
+                // the block holds K (from p.kbuf or the LDS-resident copy)
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        T kk[VC];
+                        widen<T, CT>(buf[r][g], kk);
+#pragma unroll
+                        for (int k = 0; k < VP2; ++k) e[r][g][k] = T2{kk[2 * k], kk[2 * k + 1]};
+                    }
+            } else {
             sanitize(buf);
-            if (it < 0 && bi >= res0) {  // prologue: keep this block in LDS
+            if (!KS && it < 0 && bi >= res0) {  // prologue: keep this block in LDS
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
                     for (int g = 0; g < G; ++g) resb[(((bi - res0) * R + r) * G + g) * kSwNT + tid] = buf[r][g];
             }
-            T2 e[R][G][VP2];
 #pragma unroll
             for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -442,6 +476,29 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
 #endif
                     }
                 }
+            if constexpr (KS) {
+                // prologue: K of this block to p.kbuf (rows < n, chunks inside m) and to LDS
+                // when the block is LDS-resident
+                char* krow = (char*)p.kbuf + (int64_t)r0 * ldk_bytes;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        T kk[VC];
+#pragma unroll
+                        for (int k = 0; k < VP2; ++k) {
+                            kk[2 * k] = e[r][g][k].x;
+                            kk[2 * k + 1] = e[r][g][k].y;
+                        }
+                        Raw kr2;
+                        static_assert(sizeof(kk) == sizeof(Raw), "one 16-B chunk");
+                        __builtin_memcpy(&kr2, kk, sizeof(Raw));
+                        if (r < nrow && cnt[g] > 0)
+                            *reinterpret_cast<Raw*>(krow + r * ldk_bytes + colc[g] * (int)sizeof(T)) = kr2;
+                        if (bi >= res0) resb[(((bi - res0) * R + r) * G + g) * kSwNT + tid] = kr2;
+                    }
+            }
+            }
             // single-buffer pipeline: the raw block is dead once widened, so the next
             // block's loads go out now and fly during this block's reductions
             // LDS-resident blocks come from LDS once the prologue sweep has put them there
@@ -454,6 +511,11 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                 for (int r = 0; r < R; ++r)
 #pragma unroll
                     for (int g = 0; g < G; ++g) buf[r][g] = resb[(((next - res0) * R + r) * G + g) * kSwNT + tid];
+            } else if (KS && (it >= 0 || bi + 1 >= my_nb)) {
+                // K: every sweep after the prologue, and the prologue's look-ahead of the
+                // first sweep's block 0 (stored by this thread earlier in this sweep)
+                if (it < 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                load_block(next, buf, true);
             } else {
                 load_block(next, buf);
             }
@@ -1025,7 +1087,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         using PV = __attribute__((ext_vector_type(VP))) TP;
         for (int bi = 0; bi < my_nb; ++bi) {
             const int r0 = ((int)blockIdx.x + bi * nwg) * R;
-            load_block(bi, bufA);
+            load_block(bi, bufA, KS);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (r0 + r >= p.n) break;
@@ -1043,7 +1105,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                     for (int k = 0; k < VC; ++k) {
                         T z = c[k] * ks;
                         if (SH) z += sa + shBl[c0 + k];
-                        o[k] = (TP)(ur * fast_exp(z) * colacc[g][k / 2][k & 1]);
+                        o[k] = (TP)(ur * (KS ? c[k] : fast_exp(z)) * colacc[g][k / 2][k & 1]);
                     }
                     if (cnt[g] == VC) {
 #pragma unroll
@@ -1111,7 +1173,7 @@ constexpr size_t kSwLdsMax = 160 * 1024 - 4096;  // the CU's LDS less the static
 #define OTF_SWEEP_MAXRES 4
 #endif
 
-template <typename T, typename CT, typename TP, int G, bool SH>
+template <typename T, typename CT, typename TP, int G, bool SH, bool KS = false>
 hipError_t launch_sweep_gs(int grid, SkSweepArgs<T>& p, hipStream_t s) {
     constexpr int R = sweep_rows<T, CT>(G);
     // as many whole row blocks in LDS as fit, fewer than the smallest per-workgroup count
@@ -1124,7 +1186,7 @@ hipError_t launch_sweep_gs(int grid, SkSweepArgs<T>& p, hipStream_t s) {
     if (const char* e = getenv("OTF_SWEEP_NRES")) nres = atoi(e) < nres ? atoi(e) : nres;
     p.nres = nres;
     void* args[] = {&p};
-    const void* k = (const void*)sk_sweep_kernel<T, CT, TP, G, R, OTF_SWEEP_NREP, SH>;
+    const void* k = (const void*)sk_sweep_kernel<T, CT, TP, G, R, OTF_SWEEP_NREP, SH, KS>;
     const size_t lds = base + (size_t)p.nres * sweep_block_lds(R, G);
     if (lds > kSwLdsMax + 4096) return hipErrorInvalidValue;
     if ((int64_t)((nrb + grid - 1) / grid) * R > kSwRowMax) return hipErrorInvalidValue;
@@ -1141,6 +1203,8 @@ template <typename T, typename CT, typename TP, int G>
 hipError_t launch_sweep_g(int grid, SkSweepArgs<T>& p, hipStream_t s) {
     if constexpr (sizeof(T) == 4)
         if (p.sh.A) return launch_sweep_gs<T, CT, TP, G, true>(grid, p, s);
+    if constexpr (sizeof(T) == 8 && sizeof(CT) == 8)
+        if (p.kbuf) return launch_sweep_gs<T, CT, TP, G, false, true>(grid, p, s);
     return launch_sweep_gs<T, CT, TP, G, false>(grid, p, s);
 }
 
@@ -1201,7 +1265,7 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
                      const T* b_pad, const T* cost_scale, const otf_sinkhorn_opts& o, void* region,
                      T* u_out, T* v_out, void* P_out, int64_t ldp, int P_dtype,
                      otf_sinkhorn_info* info, double* errlog, hipStream_t s, const XSweep* xs,
-                     const ShiftArgs* sh) {
+                     const ShiftArgs* sh, void* kbuf) {
     const int G = sweep_g<CT>(m);
     if (G == 0) return hipErrorInvalidValue;
     SkSweepArgs<T> p{};
@@ -1241,6 +1305,8 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     p.gran = (sizeof(T) == 4 && !p.det && !(ge && atoi(ge) == 0)) ? 1 : 0;
     p.world = 1;
     p.n_total = n;
+    // float64: stream K (written by the prologue) when the caller's workspace holds it
+    if (sizeof(T) == 8 && kbuf && !(xs && xs->world > 1)) p.kbuf = (T*)kbuf;
     if (sh) {
         if (sizeof(T) != 4 || (xs && xs->world > 1)) return hipErrorInvalidValue;
         p.sh = *sh;
@@ -1292,16 +1358,16 @@ template hipError_t run_sweep<float, float>(const float*, int64_t, int, int, int
                                             const float*, const float*, const otf_sinkhorn_opts&,
                                             void*, float*, float*, void*, int64_t, int,
                                             otf_sinkhorn_info*, double*, hipStream_t, const XSweep*,
-                                            const ShiftArgs*);
+                                            const ShiftArgs*, void*);
 template hipError_t run_sweep<float, _Float16>(const _Float16*, int64_t, int, int, int, const float*,
                                                const float*, const float*, const otf_sinkhorn_opts&,
                                                void*, float*, float*, void*, int64_t, int,
                                                otf_sinkhorn_info*, double*, hipStream_t, const XSweep*,
-                                            const ShiftArgs*);
+                                            const ShiftArgs*, void*);
 template hipError_t run_sweep<double, double>(const double*, int64_t, int, int, int, const double*,
                                               const double*, const double*, const otf_sinkhorn_opts&,
                                               void*, double*, double*, void*, int64_t, int,
                                               otf_sinkhorn_info*, double*, hipStream_t, const XSweep*,
-                                            const ShiftArgs*);
+                                            const ShiftArgs*, void*);
 
 }  // namespace otf

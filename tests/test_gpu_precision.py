@@ -148,6 +148,27 @@ def test_shifted_fp16_storage_sweep_vs_oracle(orc, dev):
     assert nrel(res.plan.cpu().numpy(), Pr) < TOL32
 
 
+@pytest.mark.parametrize("n,m,eps", [(4096, 4096, 0.1), (3000, 2501, 0.05), (1500, 8190, 2e-2)])
+def test_float64_sweep_k_stream_is_bit_identical(dev, monkeypatch, n, m, eps):
+    """The float64 sweep engine streams K = exp(-C / reg) written once by its prologue
+    sweep (POT's own K, ot.bregman) instead of recomputing the float64 exp per element per
+    sweep: the same exp of the same values, so the same plan, scalings, iteration count and
+    error log bit for bit as the recomputing form (OTF_SWEEP_KSTREAM=0); ragged shapes
+    and LDS-resident blocks included."""
+    from otfuse import ops
+    g = torch.Generator(device=dev).manual_seed(n + m)
+    C = torch.rand(n, m, device=dev, generator=g, dtype=torch.float64)
+    a = torch.full((n,), 1.0 / n, device=dev, dtype=torch.float64)
+    b = torch.full((m,), 1.0 / m, device=dev, dtype=torch.float64)
+    r1 = ops.sinkhorn(a, b, C, eps, max_iter=60, stop_thr=1e-12, engine="sweep")
+    monkeypatch.setenv("OTF_SWEEP_KSTREAM", "0")
+    r0 = ops.sinkhorn(a, b, C, eps, max_iter=60, stop_thr=1e-12, engine="sweep")
+    i0, i1 = r0.info(), r1.info()
+    assert i0["engine_name"] == i1["engine_name"] == "sweep"
+    assert (i0["niter"], i0["status"], i0["err"]) == (i1["niter"], i1["status"], i1["err"])
+    assert torch.equal(r0.plan, r1.plan) and torch.equal(r0.u, r1.u) and torch.equal(r0.v, r1.v)
+
+
 def test_metric_shape_float64_leg_vs_oracle(orc, dev, metric_inputs, oracle_plans):
     """The float64 leg of the metric config (bench.py metric_f64): float64 cost from the
     embeddings and a float64 solve, held to 1e-9 of the float64 oracle -- at the bench's
