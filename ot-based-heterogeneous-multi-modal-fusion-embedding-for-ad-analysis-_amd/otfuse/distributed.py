@@ -88,6 +88,46 @@ def gather_epoch_features(mri_local: torch.Tensor, pet_local: torch.Tensor,
             all_gather_rows(labels_local, group))
 
 
+# --------------------------------------------------------------------------- per-epoch label split
+def split_label_plans(pets, mris, comm, solve):
+    """The per-label sample couplings of one epoch (get_coupling_egw_ott_fixed,
+    MRI_PET_OT_OT_per_epoch_attn.py:954: one independent entropic GW per label) with the
+    labels dealt over the ranks: rank r solves labels r, r + W, r + 2W, ... (``solve(pets,
+    mris) -> (plans, result)`` on its share) and ONE all-reduce(SUM) of an L x P x P
+    float64 buffer (P = the largest group, zeros where a rank does not own the label)
+    gives every rank every plan.  Each plan has exactly one nonzero contribution, so the
+    sum reproduces it bit for bit: the result equals the unsplit solve.  Returns
+    ``(plans, result of this rank's solve or None)``."""
+    L = len(pets)
+    world, rank = comm.nranks, comm.rank
+    own = list(range(rank, L, world))
+    sizes = [(int(p.shape[0]), int(m.shape[0])) for p, m in zip(pets, mris)]
+    P = max(max(a, b) for a, b in sizes) if sizes else 0
+    dev = pets[0].device if pets else torch.device("cpu")
+    buf = torch.zeros((L, P, P), dtype=torch.float64, device=dev)
+    res = None
+    if own:
+        plans_own, res = solve([pets[k] for k in own], [mris[k] for k in own])
+        for k, T in zip(own, plans_own):
+            buf[k, : T.shape[0], : T.shape[1]] = T
+    comm.all_reduce(buf)
+    return [buf[k, : sizes[k][0], : sizes[k][1]] for k in range(L)], res
+
+
+def per_epoch_coupling_split(mri: torch.Tensor, pet: torch.Tensor, labels: torch.Tensor, comm,
+                             eps: float = 5e-3, max_per_label: int | None = 64, **kw):
+    """``compute_pet_to_mri_coupling`` (MRI_PET_OT_OT_per_epoch_attn.py:940-960) of the
+    all-gathered epoch features with the per-label GW work split over the ranks
+    (``split_label_plans``).  The feature stage after it -- the 2048 x 2048 fot cost from
+    all plans (a ~0.5 GFLOP float64 GEMM pair) and its OTT solve -- stays replicated: it is
+    one latency-bound resident launch (~1 ms), where a row-sharded solve would add one
+    cross-rank all-reduce per Sinkhorn iteration and an all-reduce of the 32 MiB cost
+    partials would cost more than building the cost.  Returns ``(Tv, info)``."""
+    from .perturbot import per_epoch_coupling_device
+    return per_epoch_coupling_device(mri, pet, labels, eps=eps, max_per_label=max_per_label,
+                                     comm=comm, **kw)
+
+
 # --------------------------------------------------------------------------- row-sharded solve
 class DevicePasses:
     """HIP backend of ``sinkhorn_row_sharded``: otf_sinkhorn_pass / otf_sinkhorn_finish

@@ -287,9 +287,58 @@ def get_coupling_egw_ott_fixed(
     return dict(zip(labels, plans)), dict(zip(labels, logs))
 
 
+def epoch_label_groups(labels: torch.Tensor, max_per_label: int | None = 64):
+    """``group_features_by_label`` (MRI_PET_OT_OT_per_epoch_attn.py:915-937) as row index
+    sets: labels in ``np.unique`` order, the first ``max_per_label`` rows of each (one
+    host read of the labels).  Returns ``[(label, int64 index array), ...]``."""
+    lab = labels.reshape(-1).to("cpu").numpy()
+    groups = []
+    for l in np.unique(lab):
+        idx = np.nonzero(lab == l)[0]
+        if max_per_label is not None and max_per_label > 0:
+            idx = idx[:max_per_label]
+        groups.append((int(l), idx))
+    return groups
+
+
+def egw_label_plans(pets, mris, eps: float = 5e-3, gw_max_iterations: int = 2000,
+                    sinkhorn_max_iterations: int = 2000):
+    """``get_coupling_egw_ott_fixed`` (:954) on device tensors: every label's entropic GW
+    (PET samples x MRI samples) in one launch.  Returns ``(plans, result)``."""
+    from . import gw
+    C1s, C2s = [], []
+    for x, y in zip(pets, mris):
+        C1s.append(gw.pairwise_cost_f64(x, None, metric="sqeuclidean", zero_diag=False, scale_max=True)[0])
+        C2s.append(gw.pairwise_cost_f64(y, None, metric="sqeuclidean", zero_diag=False, scale_max=True)[0])
+    egw = gw.solve_batched(C1s, C2s, gw.GW_ENTROPIC, max_iter=gw_max_iterations, min_iter=5,
+                           threshold=1e-3, eps=float(eps), sk_max_iter=sinkhorn_max_iterations,
+                           sk_inner=OTT_INNER, sk_threshold=OTT_THRESHOLD, warm_start=True,
+                           log_len=max(1, min(gw_max_iterations, 4096)))
+    return list(egw.plans), egw
+
+
+def fot_from_label_plans(pets, mris, plans, eps: float = 5e-3):
+    """``get_coupling_fot((pet, mri), Ts)`` (:959 -> perturbot fot.py:155-220) given the
+    per-label sample plans: block-diagonal Ts (label order = data[0] keys), ``Ts /=
+    Ts.sum()``, the fot-weighted float64 feature cost and the OTT solve with a host poll
+    every 10 iterations.  Returns the ``SinkhornResult`` (plan = Tv, d_pet x d_mri)."""
+    n = sum(int(T.shape[0]) for T in plans)
+    dev = pets[0].device
+    Ts = torch.zeros((n, n), dtype=torch.float64, device=dev)
+    r = 0
+    for T in plans:
+        Ts[r:r + T.shape[0], r:r + T.shape[1]] = T
+        r += T.shape[0]
+    Ts = Ts / Ts.sum()
+    M = ops.feature_cost(torch.cat(pets), torch.cat(mris), Ts=Ts, weights="fot")
+    res, _ = solve_ott(M, float(eps), sync_every=OTT_INNER)
+    return res
+
+
 def per_epoch_coupling_device(mri: torch.Tensor, pet: torch.Tensor, labels: torch.Tensor,
                               eps: float = 5e-3, max_per_label: int | None = 64,
-                              gw_max_iterations: int = 2000, sinkhorn_max_iterations: int = 2000):
+                              gw_max_iterations: int = 2000, sinkhorn_max_iterations: int = 2000,
+                              comm=None):
     """``compute_pet_to_mri_coupling`` (MRI_PET_OT_OT_per_epoch_attn.py:940-960) on device
     tensors -- e.g. the all-gathered embedding shards of a data-parallel epoch -- without
     the NumPy round trips of the drop-ins.
@@ -304,42 +353,29 @@ def per_epoch_coupling_device(mri: torch.Tensor, pet: torch.Tensor, labels: torc
     plan (d_pet x d_mri float64, on the device) and ``info`` a callable returning the
     solver logs (it synchronises; the chain itself reads only the labels back).
     Equivalent to the NumPy chain ``get_coupling_egw_ott_fixed`` + ``get_coupling_fot``
-    (tests/test_gpu_configs.py::test_config3_device_chain_matches_dropins)."""
-    from . import gw
+    (tests/test_gpu_configs.py::test_config3_device_chain_matches_dropins).
+
+    ``comm`` (an ``otfuse.comm.Communicator`` or anything with ``rank``, ``nranks`` and
+    ``all_reduce``): the label split of ``otfuse.distributed.per_epoch_coupling_split`` --
+    rank r solves the entropic GW of labels r, r + W, ... and one all-reduce assembles
+    every label's plan on every rank; the same plans bit for bit."""
+    groups = epoch_label_groups(labels, max_per_label)
     dev = mri.device
-    lab = labels.reshape(-1).to("cpu").numpy()
-    groups = []
-    for l in np.unique(lab):
-        idx = np.nonzero(lab == l)[0]
-        if max_per_label is not None and max_per_label > 0:
-            idx = idx[:max_per_label]
-        groups.append((int(l), torch.as_tensor(idx, device=dev)))
-    pets = [torch.nan_to_num(pet.index_select(0, i).float()) for _, i in groups]
-    mris = [torch.nan_to_num(mri.index_select(0, i).float()) for _, i in groups]
-    # per-label entropic GW (PET samples x MRI samples), all labels in one launch
-    C1s, C2s = [], []
-    for x, y in zip(pets, mris):
-        C1s.append(gw.pairwise_cost_f64(x, None, metric="sqeuclidean", zero_diag=False, scale_max=True)[0])
-        C2s.append(gw.pairwise_cost_f64(y, None, metric="sqeuclidean", zero_diag=False, scale_max=True)[0])
-    egw = gw.solve_batched(C1s, C2s, gw.GW_ENTROPIC, max_iter=gw_max_iterations, min_iter=5,
-                           threshold=1e-3, eps=float(eps), sk_max_iter=sinkhorn_max_iterations,
-                           sk_inner=OTT_INNER, sk_threshold=OTT_THRESHOLD, warm_start=True,
-                           log_len=max(1, min(gw_max_iterations, 4096)))
-    # feature OT given the block-diagonal sample coupling (label order = data[0] keys)
-    n = sum(int(i.numel()) for _, i in groups)
-    Ts = torch.zeros((n, n), dtype=torch.float64, device=dev)
-    r = 0
-    for T in egw.plans:
-        Ts[r:r + T.shape[0], r:r + T.shape[1]] = T
-        r += T.shape[0]
-    Ts = Ts / Ts.sum()
-    X = torch.cat(pets)
-    Y = torch.cat(mris)
-    M = ops.feature_cost(X, Y, Ts=Ts, weights="fot")
-    res, _ = solve_ott(M, float(eps), sync_every=OTT_INNER)
+    idx = [torch.as_tensor(i, device=dev) for _, i in groups]
+    pets = [torch.nan_to_num(pet.index_select(0, i).float()) for i in idx]
+    mris = [torch.nan_to_num(mri.index_select(0, i).float()) for i in idx]
+    if comm is not None and comm.nranks > 1:
+        from .distributed import split_label_plans
+        plans, egw = split_label_plans(
+            pets, mris, comm,
+            lambda p, m: egw_label_plans(p, m, eps, gw_max_iterations, sinkhorn_max_iterations))
+    else:
+        plans, egw = egw_label_plans(pets, mris, eps, gw_max_iterations, sinkhorn_max_iterations)
+    res = fot_from_label_plans(pets, mris, plans, eps)
 
     def info():
-        return {"egw": egw.infos(), "fot": res.info(), "labels": [l for l, _ in groups]}
+        return {"egw": egw.infos() if egw is not None else [], "fot": res.info(),
+                "labels": [l for l, _ in groups]}
 
     return res.plan, info
 

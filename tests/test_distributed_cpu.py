@@ -215,3 +215,49 @@ def test_coupled_solve_unequal_shards_through_communicator_world2(tmp_path):
     world = 2
     mp.spawn(_coupled_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     assert all((tmp_path / f"coupled{r}").exists() for r in range(world))
+
+
+def _label_split_worker(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as orc
+    import otfuse.distributed as D
+
+    # per-label sample couplings from the oracle's entropic GW (the device solver's CPU
+    # restatement) on squared-Euclidean costs / max, as egw_label_plans builds them
+    def solve(pets, mris):
+        plans = []
+        for x, y in zip(pets, mris):
+            c1, _ = orc.pairwise_cost(x.numpy(), x.numpy(), scale_max=True)
+            c2, _ = orc.pairwise_cost(y.numpy(), y.numpy(), scale_max=True)
+            T, _ = orc.gw_entropic(c1, c2, 5e-2, max_iter=40)
+            plans.append(torch.from_numpy(T))
+        return plans, len(plans)
+
+    rng = np.random.default_rng(5)
+    sizes = [9, 14, 6, 11, 8]            # 5 labels over 2 ranks: 3 + 2, ragged groups
+    pets = [torch.from_numpy(rng.random((s, 4)).astype(np.float32)) for s in sizes]
+    mris = [torch.from_numpy(rng.random((s, 5)).astype(np.float32)) for s in sizes]
+    plans, mine = D.split_label_plans(pets, mris, GlooComm(), solve)
+    assert mine == len(range(rank, len(sizes), world))
+    ref, _ = solve(pets, mris)
+    assert len(plans) == len(ref)
+    for T, R in zip(plans, ref):
+        assert T.shape == R.shape and torch.equal(T, R)   # one contribution per plan: exact
+    open(os.path.join(out_dir, f"labels{rank}"), "w").write("ok")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_per_epoch_label_split_world2(tmp_path):
+    """Config 3's per-epoch chain split over ranks (otfuse.distributed.split_label_plans):
+    labels dealt round-robin, one all-reduce of the padded plan stack; every rank ends with
+    every label's plan, bit-identical to the unsplit per-label solve."""
+    world = 2
+    mp.spawn(_label_split_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert all((tmp_path / f"labels{r}").exists() for r in range(world))

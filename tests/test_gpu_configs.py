@@ -101,6 +101,50 @@ def test_config3_device_chain_matches_dropins(config3, dev):
     assert info()["labels"] == [0, 1]
 
 
+class _PairComm:
+    """Two ranks of a world-2 communicator simulated in one process (one device): rank 1's
+    all_reduce contribution is recorded, rank 0's call adds it -- the all-reduce(SUM) of
+    otfuse.distributed.split_label_plans without a second process."""
+
+    def __init__(self, rank, store):
+        self.rank, self.nranks, self.store = rank, 2, store
+
+    def all_reduce(self, t, op="sum"):
+        if self.rank == 1:
+            self.store.append(t.clone())
+        else:
+            t += self.store[0]
+        return t
+
+
+def test_config3_label_split_matches_unsplit(config3, dev):
+    """Config 3's per-epoch chain with the per-label entropic GW split over two ranks
+    (labels dealt round-robin, one all-reduce of the padded plan stack,
+    otfuse.distributed.split_label_plans): every label's plan and the PET->MRI feature plan
+    bit-identical to the single-rank device chain."""
+    from otfuse import distributed, perturbot
+    pet, mri, _, _ = config3
+    lab = np.repeat([0, 1], 64)
+    P = torch.as_tensor(np.concatenate([pet[0], pet[1]]), device=dev)
+    M = torch.as_tensor(np.concatenate([mri[0], mri[1]]), device=dev)
+    L = torch.as_tensor(lab, device=dev)
+    Tv1, info1 = perturbot.per_epoch_coupling_device(M, P, L, eps=5e-3)
+    pets = [P[:64].float(), P[64:].float()]
+    mris = [M[:64].float(), M[64:].float()]
+    ref, _ = perturbot.egw_label_plans(pets, mris, 5e-3)
+    store = []
+    solve = lambda p, m: perturbot.egw_label_plans(p, m, 5e-3)  # noqa: E731
+    distributed.split_label_plans(pets, mris, _PairComm(1, store), solve)
+    plans, _ = distributed.split_label_plans(pets, mris, _PairComm(0, store), solve)
+    for T, R in zip(plans, ref):
+        assert torch.equal(T, R)
+    # the whole chain at rank 0, rank 1's share (label 1) as its all-reduce contribution
+    other = torch.zeros((2, 64, 64), dtype=torch.float64, device=dev)
+    other[1] = ref[1]
+    Tv2, _ = distributed.per_epoch_coupling_split(M, P, L, _PairComm(0, [other]), eps=5e-3)
+    assert torch.equal(Tv1, Tv2)
+
+
 def test_config3_pot_form_2048_vs_oracle(config3, orc):
     """POT form of the per-epoch chain: get_feature_coupling_pot with the block-diagonal
     GW plans (MRI_PET_OT_nojax.py:91-145), 2048^2 float64, eps = 5e-3, 2000 iterations,
