@@ -865,7 +865,9 @@ bool mesh_supported(int64_t n, int64_t m) {
 size_t mesh_region_bytes(int64_t n, int64_t m) {
     if (!mesh_supported(n, m)) return 0;
     const MeshShape s = mesh_shape(n, m);
-    return kMeshRegBytes + s.row_bytes + s.cola_bytes + s.colb_bytes;
+    const size_t b = kMeshRegBytes + s.row_bytes + s.cola_bytes + s.colb_bytes;
+    const size_t b2 = mesh2_region_bytes(n, m);  // the two-hop form shares the region
+    return b > b2 ? b : b2;
 }
 
 template <typename CT>
@@ -874,6 +876,9 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                     double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* shift) {
     if (!mesh_supported(n, m) || !region) return hipErrorInvalidValue;
+    if (mesh2_enabled() && mesh2_supported(n, m))
+        return run_mesh2<CT>(C, ldc, n, m, a_pad, b_pad, cost_scale, o, region, u_out, v_out, P_out, ldp,
+                             P_dtype, info, errlog, zeroed, s, shift);
     const MeshShape sh = mesh_shape(n, m);
     if (sh.nrb * sh.ncb > device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
     SkMeshArgs p{};

@@ -120,8 +120,8 @@ class _PairComm:
 def test_config3_label_split_matches_unsplit(config3, dev):
     """Config 3's per-epoch chain with the per-label entropic GW split over two ranks
     (labels dealt round-robin, one all-reduce of the padded plan stack,
-    otfuse.distributed.split_label_plans): every label's plan and the PET->MRI feature plan
-    bit-identical to the single-rank device chain."""
+    otfuse.distributed.split_label_plans): every label's plan bit-identical to the
+    single-rank solve, the PET->MRI feature plan to 1e-12."""
     from otfuse import distributed, perturbot
     pet, mri, _, _ = config3
     lab = np.repeat([0, 1], 64)
@@ -142,7 +142,9 @@ def test_config3_label_split_matches_unsplit(config3, dev):
     other = torch.zeros((2, 64, 64), dtype=torch.float64, device=dev)
     other[1] = ref[1]
     Tv2, _ = distributed.per_epoch_coupling_split(M, P, L, _PairComm(0, [other]), eps=5e-3)
-    assert torch.equal(Tv1, Tv2)
+    # the same plans feed the same OTT solve (its column sums use float atomics, so two
+    # runs agree to rounding, not bitwise)
+    assert nrel(Tv1.cpu().numpy(), Tv2.cpu().numpy()) < 1e-12
 
 
 def test_config3_pot_form_2048_vs_oracle(config3, orc):

@@ -153,16 +153,18 @@ def test_float64_sweep_k_stream_is_bit_identical(dev, monkeypatch, n, m, eps):
     """The float64 sweep engine streams K = exp(-C / reg) written once by its prologue
     sweep (POT's own K, ot.bregman) instead of recomputing the float64 exp per element per
     sweep: the same exp of the same values, so the same plan, scalings, iteration count and
-    error log bit for bit as the recomputing form (OTF_SWEEP_KSTREAM=0); ragged shapes
-    and LDS-resident blocks included."""
+    error log bit for bit as the recomputing form (OTF_SWEEP_KSTREAM=0) in the
+    deterministic mode (the default flush adds float64 partials with atomics, whose order
+    varies run to run); ragged shapes and LDS-resident blocks included."""
     from otfuse import ops
     g = torch.Generator(device=dev).manual_seed(n + m)
     C = torch.rand(n, m, device=dev, generator=g, dtype=torch.float64)
     a = torch.full((n,), 1.0 / n, device=dev, dtype=torch.float64)
     b = torch.full((m,), 1.0 / m, device=dev, dtype=torch.float64)
-    r1 = ops.sinkhorn(a, b, C, eps, max_iter=60, stop_thr=1e-12, engine="sweep")
+    # deterministic mode: fixed-order column sums, so the two forms can be compared bitwise
+    r1 = ops.sinkhorn(a, b, C, eps, max_iter=60, stop_thr=1e-12, engine="sweep", deterministic=True)
     monkeypatch.setenv("OTF_SWEEP_KSTREAM", "0")
-    r0 = ops.sinkhorn(a, b, C, eps, max_iter=60, stop_thr=1e-12, engine="sweep")
+    r0 = ops.sinkhorn(a, b, C, eps, max_iter=60, stop_thr=1e-12, engine="sweep", deterministic=True)
     i0, i1 = r0.info(), r1.info()
     assert i0["engine_name"] == i1["engine_name"] == "sweep"
     assert (i0["niter"], i0["status"], i0["err"]) == (i1["niter"], i1["status"], i1["err"])
