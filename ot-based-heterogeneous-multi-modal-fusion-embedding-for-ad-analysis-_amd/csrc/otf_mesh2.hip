@@ -74,6 +74,25 @@ struct SkMesh2Args {
 using F2 = __attribute__((ext_vector_type(2))) float;
 using F4 = __attribute__((ext_vector_type(4))) float;
 
+// Diagnostic build only (-DOTF_MESH2_STAMPS, tools/stamps_mesh2.hip): wall-clock stamps per
+// role (rb * NCB + cb), iteration 0..15, slot: 0 start, 1 column gather loaded (wave 0),
+// 2 v ready (after the barrier), 3 row chunks published (wave 0), 4 row hop done (wave 0),
+// 5 column partials reduced (after the barrier), 6 column chunks published, 9 / 10 the row
+// hop done / published by wave 7
+#ifdef OTF_MESH2_STAMPS
+__device__ unsigned long long g_m2stamps[256 * 16 * 16];
+__device__ int g_m2role[256 * 4];
+#define OTF_M2STAMP(it, slot, who)                                                            \
+    do {                                                                                      \
+        if (threadIdx.x == (who) && (it) >= 0 && (it) < 16)                                   \
+            g_m2stamps[((rb * NCB + cb) * 16 + (it)) * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define OTF_M2STAMP(it, slot, who) \
+    do {                           \
+    } while (0)
+#endif
+
 // value with the tag in its three low mantissa bits: (epoch & 3) | flag << 2
 __device__ __forceinline__ int tag_val(float v, int tag) {
     const unsigned b = __builtin_bit_cast(unsigned, v);
@@ -192,6 +211,14 @@ __global__ __launch_bounds__(512) void sk_mesh2_kernel(SkMesh2Args p) {
         cb = bi % NCB;
     }
     const bool lead = (rb == 0 && cb == 0 && tid == 0);
+#ifdef OTF_MESH2_STAMPS
+    if (tid == 0) {
+        g_m2role[(rb * NCB + cb) * 4 + 0] = rb;
+        g_m2role[(rb * NCB + cb) * 4 + 1] = cb;
+        g_m2role[(rb * NCB + cb) * 4 + 2] = xcc_id();
+        g_m2role[(rb * NCB + cb) * 4 + 3] = 1 + NCB * 1000 + NRB * 100000;
+    }
+#endif
     const int row0 = rb * TT + w * RW;   // this wave's first row
     const int col0 = cb * TT + 4 * lane; // this lane's first column
     const int n_ = NRB * TT, m_ = NCB * TT;
@@ -273,6 +300,7 @@ __global__ __launch_bounds__(512) void sk_mesh2_kernel(SkMesh2Args p) {
     // column hop of epoch e: S of this tile's columns -> sums into s4 of every lane
     // (its 4 columns); returns bit 0 = a producer's u flag, bit 1 = stall
     auto gather_cols = [&](int e, F4& s4) -> int {
+        (void)e;
         const int q0 = w, q1 = w + 8;
         I4 x0 = I4{0, 0, 0, 0}, x1 = I4{0, 0, 0, 0};
         int fl = 0;
@@ -286,6 +314,7 @@ __global__ __launch_bounds__(512) void sk_mesh2_kernel(SkMesh2Args p) {
             if (__builtin_amdgcn_s_memrealtime() > deadline) { fl |= 2; break; }
             __builtin_amdgcn_s_sleep(1);
         }
+        OTF_M2STAMP(e - 1, 1, 0);
         F4 ps = chunk4_vals(x0);
         int f = chunk4_flag(x0);
         if (q1 < NRB) {
@@ -330,8 +359,10 @@ __global__ __launch_bounds__(512) void sk_mesh2_kernel(SkMesh2Args p) {
         asm volatile("" : "+v"(tid), "+v"(lane));
         const int e = it + 1;
         const bool check = it >= 1 && chk == 0;
+        OTF_M2STAMP(it, 0, 0);
         F4 s4;
         const int gf = gather_cols(e, s4);
+        OTF_M2STAMP(it, 2, 0);
         if (gf & 2) { status = OTF_SK_TIMEOUT; done = true; break; }
         if (gf & 1) {  // a non-finite u in iteration it - 1 -> revert to it - 2
             last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
@@ -371,6 +402,8 @@ __global__ __launch_bounds__(512) void sk_mesh2_kernel(SkMesh2Args p) {
                 gstore(rs, rowx(e, cb) + (uint32_t)(w * 8 + (lane >> 3)) * 16,
                        chunk4(F4{tot, t1, t2, t3}, (e & 3) | (vbad << 2)));
         }
+        OTF_M2STAMP(it, 3, 0);
+        OTF_M2STAMP(it, 10, 448);
         if (check && w == 0 && lane == 1) gstore(rs, rowx(e, cb) + 64 * 16, chunk4(F4{eterm, 0.f, 0.f, 0.f}, e & 3));
         // row hop: members mq, mq + 8 of chunk rc
         I4 x0 = I4{0, 0, 0, 0}, x1 = I4{0, 0, 0, 0};
@@ -388,6 +421,8 @@ __global__ __launch_bounds__(512) void sk_mesh2_kernel(SkMesh2Args p) {
                 __builtin_amdgcn_s_sleep(1);
             }
         }
+        OTF_M2STAMP(it, 4, 0);
+        OTF_M2STAMP(it, 9, 448);
         F4 rt = F4{0, 0, 0, 0};
         int rflag = 0;
         if (mq < NCB) { rt = chunk4_vals(x0); rflag |= chunk4_flag(x0); }
@@ -448,6 +483,7 @@ __global__ __launch_bounds__(512) void sk_mesh2_kernel(SkMesh2Args p) {
         if (badu) s_ep[0] = it;
         if (stall) s_ep[1] = it;
         __syncthreads();
+        OTF_M2STAMP(it, 5, 0);
         if (s_ep[1] == it) { status = OTF_SK_TIMEOUT; done = true; break; }
         if (check) {
             if (lead) p.errlog[n_err] = err;
@@ -464,6 +500,7 @@ __global__ __launch_bounds__(512) void sk_mesh2_kernel(SkMesh2Args p) {
             break;
         }
         publish_cols(e + 1, s_ep[0] == it ? 1 : 0);
+        OTF_M2STAMP(it, 6, 0);
 #pragma unroll
         for (int k = 0; k < 4; ++k) vprev[k] = vn[k];
     }
