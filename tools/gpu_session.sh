@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 stop_if_fatal() { if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "fatal rc=$1 in $2, stopping"; exit "$1"; fi; }
 
 if [ "${TESTS:-1}" = "1" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 180 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/gpu_tests.log; stop_if_fatal $rc pytest
 fi
 if [ "${BENCH:-1}" = "1" ]; then
