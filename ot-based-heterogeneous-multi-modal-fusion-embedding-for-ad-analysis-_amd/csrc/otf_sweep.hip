@@ -1150,6 +1150,16 @@ template <typename T, typename CT> constexpr int sweep_rows(int G) {
                       ((int)sizeof(T) + (int)sizeof(CT)));
 }
 constexpr int kSwMaxG = 8;
+// The float64 K stream (KS) carries no exp / scaling temporaries per element: its row
+// blocks may be OTF_SWEEP_KS_RMUL times taller (fewer per-block row-sum barriers per sweep;
+// 2 spills 32-37 VGPRs at G = 2..4 with this register budget, so the default is 1)
+#ifndef OTF_SWEEP_KS_RMUL
+#define OTF_SWEEP_KS_RMUL 1
+#endif
+template <typename T, typename CT> constexpr int sweep_rows_ks(int G, bool ks) {
+    return ks ? (sweep_rows<T, CT>(G) * OTF_SWEEP_KS_RMUL > 16 ? 16 : sweep_rows<T, CT>(G) * OTF_SWEEP_KS_RMUL)
+              : sweep_rows<T, CT>(G);
+}
 
 template <typename CT> int sweep_g(int64_t m) {
     int g = 1;
@@ -1175,7 +1185,7 @@ constexpr size_t kSwLdsMax = 160 * 1024 - 4096;  // the CU's LDS less the static
 
 template <typename T, typename CT, typename TP, int G, bool SH, bool KS = false>
 hipError_t launch_sweep_gs(int grid, SkSweepArgs<T>& p, hipStream_t s) {
-    constexpr int R = sweep_rows<T, CT>(G);
+    constexpr int R = sweep_rows_ks<T, CT>(G, KS);
     // as many whole row blocks in LDS as fit, fewer than the smallest per-workgroup count
     const int nrb = (p.n + R - 1) / R;
     const int min_nb = nrb / grid;
@@ -1333,12 +1343,13 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     }
     hipError_t e = hipMemsetAsync(region, 0, zero_bytes, s);
     if (e != hipSuccess) return e;
+    const bool ks = sizeof(T) == 8 && p.kbuf != nullptr;
     int R = 1;
     switch (G) {
-        case 1: R = sweep_rows<T, CT>(1); break;
-        case 2: R = sweep_rows<T, CT>(2); break;
-        case 4: R = sweep_rows<T, CT>(4); break;
-        default: R = sweep_rows<T, CT>(8); break;
+        case 1: R = sweep_rows_ks<T, CT>(1, ks); break;
+        case 2: R = sweep_rows_ks<T, CT>(2, ks); break;
+        case 4: R = sweep_rows_ks<T, CT>(4, ks); break;
+        default: R = sweep_rows_ks<T, CT>(8, ks); break;
     }
     const int nrb = (n + R - 1) / R;
     int grid = sweep_grid(nrb);
