@@ -24,7 +24,11 @@ def _emb(n, d, seed):
 
 @pytest.mark.parametrize("metric,zero_diag,n,m,d", [("euclidean", True, 64, 64, 512),
                                                     ("sqeuclidean", False, 130, 77, 33),
-                                                    ("euclidean", False, 1, 5, 3)])
+                                                    ("euclidean", False, 1, 5, 3),
+                                                    # 128 x 128 float64 tiles, fused epilogue
+                                                    ("euclidean", True, 1000, 1000, 64),
+                                                    ("sqeuclidean", False, 1030, 777, 300),
+                                                    ("sqeuclidean", False, 2048, 300, 1027)])
 def test_pairwise_cost_f64_vs_oracle(orc, dev, metric, zero_diag, n, m, d):
     from otfuse import gw
     X, _, _ = _emb(n, d, 1)
