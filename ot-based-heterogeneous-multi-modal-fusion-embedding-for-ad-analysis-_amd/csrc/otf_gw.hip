@@ -505,6 +505,7 @@ __device__ void small_sinkhorn_knopp(const double* K, int n, int m, const double
     conv = false;
     iters = maxit;
     bool check = false;  // POT's error check of the previous update is pending
+    int cnt = 0;         // ii % every
     using D2 = __attribute__((ext_vector_type(2))) double;
     for (int ii = 0;; ++ii) {
         if (ii == maxit && !check) break;
@@ -572,7 +573,8 @@ __device__ void small_sinkhorn_knopp(const double* K, int n, int m, const double
         if (s_kf[ii & 1]) { iters = ii + 1; break; }  // numerical error: keep the previous pair
         u = un;
         v = vn;
-        check = (ii % every) == 0;
+        check = cnt == 0;  // ii % every == 0, as a counter (no integer division per update)
+        cnt = cnt + 1 == every ? 0 : cnt + 1;
     }
     if (sg == 0) {
         sh.f[ir] = u;
@@ -725,10 +727,14 @@ __device__ bool wave_lap(const double* A, int64_t lda, int n, int* sigma, double
 }
 
 // ---------------------------------------------------------------------- the kernel
-template <class Cfg>
+// SOLV >= 0 compiles ONE solver in (the others' state leaves the register allocation: the
+// small PGD instance spilled ~270 SGPRs to VGPR lanes, reloaded in its inner loop);
+// SOLV = -1 takes o.solver at run time.
+template <class Cfg, int SOLV = -1>
 __global__ __launch_bounds__(Cfg::NT) void gw_kernel(GwLaunch Lz, otf_gw_opts o, otf_gw_info* infos,
                                                    double* costlog, int costlog_len,
                                                    unsigned long long timeout_ticks) {
+    if constexpr (SOLV >= 0) o.solver = SOLV;
     GwShared<Cfg>* shp;
     if constexpr (Cfg::GLOBAL) {
         shp = reinterpret_cast<GwShared<Cfg>*>(Lz.shg[blockIdx.x]);
@@ -1524,7 +1530,10 @@ static int gw_launch(const otf::GwLaunch& L, const otf_gw_opts& o, otf_gw_info* 
             }
         }
         if (small) {
-            gw_kernel<GwSmall><<<L.nprob, GwSmall::NT, 0, s>>>(L, o, info, costlog, costlog_len, ticks);
+            if (o.solver == OTF_GW_PGD)
+                gw_kernel<GwSmall, OTF_GW_PGD><<<L.nprob, GwSmall::NT, 0, s>>>(L, o, info, costlog, costlog_len, ticks);
+            else
+                gw_kernel<GwSmall><<<L.nprob, GwSmall::NT, 0, s>>>(L, o, info, costlog, costlog_len, ticks);
         } else {
             if (dyn)
                 OTF_HIP(hipFuncSetAttribute((const void*)gw_kernel<GwBig>,
