@@ -163,13 +163,17 @@ def main():
             dist.destroy_process_group()
         return
 
-    # per-phase split of extra steps (events on the current stream = the kernels' stream)
-    cost_l, sk_l = [], []
-    for _ in range(5):
+    # per-phase split of extra steps (events on the current stream = the kernels' stream),
+    # the steps enqueued back to back as in the timed loop and synchronised once: a sync per
+    # step would leave the GPU idle while the host enqueues the next call, and the events
+    # would time the host's Python overhead instead of the device
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(6)]
+    for k in range(6):
+        ev[:] = evs[k]
         step(True)
-        torch.cuda.synchronize()
-        cost_l.append(ev[0].elapsed_time(ev[1]))
-        sk_l.append(ev[1].elapsed_time(ev[2]))
+    torch.cuda.synchronize()
+    cost_l = [e[0].elapsed_time(e[1]) for e in evs[1:]]
+    sk_l = [e[1].elapsed_time(e[2]) for e in evs[1:]]
     cost_ms = sorted(cost_l)[2]
     sk_ms = sorted(sk_l)[2]
     # the cost op split into its prep (split / norms) and the MFMA kernel (device events
