@@ -1825,8 +1825,10 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.bytes = off;
     // float64: the sweep engine streams K = exp(-C / reg) written once by its prologue
     // (POT materialises K too) when the caller's workspace reaches this far; a workspace of
-    // `bytes` still runs every engine (the sweep then recomputes the exp per sweep)
-    w.kbuf = esz == 8 ? take((size_t)n * (size_t)w.m_pad * esz) : nullptr;
+    // `bytes` still runs every engine (the sweep then recomputes the exp per sweep).  Only
+    // for costs past 64 MiB: below that the register-resident engines take float64 K
+    const size_t kb = (size_t)n * (size_t)w.m_pad * esz;
+    w.kbuf = (esz == 8 && kb > ((size_t)64 << 20)) ? take(kb) : nullptr;
     w.bytes_k = off;
     return w;
 }
