@@ -56,6 +56,7 @@ METRIC = "MRI+PET pairs/sec + Sinkhorn iters/sec, N=4096 d=512 100 iters"
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 / bf16 MFMA (same table; 2:1 sparsity excluded)
 VALU_F32_PEAK_TFMA = 78.6     # 157.3 TFLOP/s fp32 vector = 78.6 T FMA/s
+F64_VALU_TFLOPS = 78.6        # float64 vector peak (39.3 T FMA/s)
 LIB = os.path.join(PKG, "otfuse", "lib", "libotfuse.so")
 
 
@@ -428,10 +429,11 @@ def metric_f64_leg(dev, N=4096, d=512, iters=100, eps=0.1, reps=3):
     """The metric config in the reference's own precision (POT runs NumPy float64,
     MRI_PET_OT_nojax.py:143): float64 pairwise cost from the float32 embeddings
     (otf_cost_pairwise_f64, POT euclidean_distances order, divided by its max) and a
-    float64 POT Sinkhorn, 100 iterations, float64 plan.  The float64 cost (128 MiB) does
-    not fit the register files, so the sweep engine streams it once per iteration: its
-    roofline is the N*N*8 bytes read per sweep against HBM (the cost is Infinity-Cache
-    resident at this size).  Parity: tests/test_gpu_precision.py (1e-9 of the oracle)."""
+    float64 POT Sinkhorn, 100 iterations, float64 plan.  AUTO runs the float64 mesh
+    (csrc/otf_mesh64.hip: the 128 MiB K split between the register files and LDS for the
+    whole solve, latency-bound); with the mesh off (OTF_MESH=0) the sweep engine streams K
+    once per iteration, roofline N*N*8 bytes per sweep against HBM.  Parity:
+    tests/test_gpu_precision.py, tests/test_gpu_mesh64.py (1e-9 of the oracle)."""
     import numpy as np
     from otfuse import gw, ops
     from otfuse.synthetic import paired_embeddings
@@ -459,13 +461,27 @@ def metric_f64_leg(dev, N=4096, d=512, iters=100, eps=0.1, reps=3):
     info = res.info()
     sweep_us = ts * 1e3 / (iters + 1)
     gbs = N * N * 8 / (sweep_us * 1e-6) / 1e9
+    if info["engine_name"] == "mesh":
+        # K on chip for the whole solve (csrc/otf_mesh64.hip): latency-bound like the
+        # headline mesh; floor = the two N^2 float64 FMA passes per iteration at the
+        # 78.6 TFLOP/s float64 vector peak
+        it_us = ts * 1e3 / iters
+        floor_us = 2.0 * N * N / (F64_VALU_TFLOPS / 2 * 1e12) * 1e6
+        roof = {"bound": "latency", "kernel": "sk_mesh64_kernel", "achieved": it_us, "peak": floor_us,
+                "unit": "us per iteration", "frac": floor_us / it_us, "hbm_equivalent_GBs": gbs,
+                "note": "float64 K = exp(-C/eps) held in the register files (24 of every 32 rows) "
+                        "and LDS (8) for the whole solve, C read once; per iteration three granule "
+                        "hops (row hop, column partials to reducers, sums back) against a VALU floor "
+                        "(peak) of 2 N^2 float64 FMAs"}
+    else:
+        roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS,
+                "note": "N*N*8 B per sweep (iters + 1 sweeps incl. the plan pass)"}
     return {"N": N, "d": d, "iters": iters, "eps": eps, "dtype": "f64",
             "engine": info["engine_name"], "status": info["status_name"],
             "cost_ms": tc, "sinkhorn_incl_plan_ms": ts, "ms_per_step": tc + ts,
             "pairs_per_s": N / ((tc + ts) * 1e-3), "sinkhorn_iters_per_s": iters / (ts * 1e-3),
-            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS,
-                         "note": "N*N*8 B per sweep (iters + 1 sweeps incl. the plan pass)"}}
+            "roofline": roof}
 
 
 def gw_leg(dev, with_cpu, labels=2, per_label=64, d=512, eps=5e-3):

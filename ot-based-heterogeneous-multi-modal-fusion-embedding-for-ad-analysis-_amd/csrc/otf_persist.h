@@ -352,6 +352,14 @@ hipError_t run_mesh2(const CT* C, int64_t ldc, int n, int m, const float* a_pad,
                      const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
                      float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                      double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* shift);
+// float64 form (otf_mesh64.hip): whole 128 x 512 tiles, 4..32 (a power of two) x 1..8, K
+// split between the register files and LDS
+bool mesh64_supported(int64_t n, int64_t m);
+size_t mesh64_region_bytes(int64_t n, int64_t m);
+hipError_t run_mesh64(const double* C, int64_t ldc, int n, int m, const double* a_pad, const double* b_pad,
+                      const double* cost_scale, const otf_sinkhorn_opts& o, void* region, double* u_out,
+                      double* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
+                      double* errlog, bool zeroed, hipStream_t s);
 template <typename CT>
 hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,

@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include "otf_persist.h"
+#include <type_traits>
 #include "otf_comm.h"
 
 namespace otf {
@@ -1813,7 +1814,7 @@ Workspace carve(void* base, int64_t n, int64_t m, size_t esz, int max_iter, int6
     w.sweep = take(w.sweep_bytes);
     w.gather_bytes = esz == 8 ? gather_region_bytes<double>(n, m) : gather_region_bytes<float>(n, m);
     w.gather = take(w.gather_bytes);
-    w.mesh_bytes = esz == 4 ? mesh_region_bytes(n, m) : 0;
+    w.mesh_bytes = esz == 4 ? mesh_region_bytes(n, m) : mesh64_region_bytes(n, m);
     w.mesh = take(w.mesh_bytes);
     if (esz == 4) {
         w.shA = (float*)take(sizeof(float) * (size_t)n);
@@ -2193,10 +2194,15 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     const bool sh = o.shift != 0;
     if (sh && (LOG || sizeof(T) != 4 || !whole)) return OTF_EUNSUPPORTED;
     // the mesh engine's region is zeroed by the init kernel (no memset launch)
+    // float64: the mesh engine's float64 form on a float64 cost of whole 128 x 512 tiles
+    constexpr bool kMesh64 = sizeof(T) == 8 && std::is_same<CT, double>::value;
+    bool mesh_shape_ok = false;
+    if constexpr (sizeof(T) == 4) mesh_shape_ok = mesh_supported(n, m);
+    else if constexpr (kMesh64) mesh_shape_ok = !sh && mesh64_supported(n, m);
     bool mesh_pick = false;
-    if constexpr (sizeof(T) == 4)
+    if constexpr (sizeof(T) == 4 || kMesh64)
         mesh_pick = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && su.w.mesh_bytes > 0 &&
-                    mesh_supported(n, m) &&
+                    mesh_shape_ok &&
                     (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled() &&
                                                      !(gather_supported<T>(n, m) && su.w.gather_bytes > 0)));
     // gather engine: small problems, one granule hop per iteration, no barrier (and
@@ -2230,10 +2236,21 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     // mesh engine: float32 tiles of K in registers, three granule hops per iteration, no
     // atomics or barrier (deterministic by construction)
     bool mfits = false;
-    if constexpr (sizeof(T) == 4)
-        mfits = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && mesh_supported(n, m) &&
+    if constexpr (sizeof(T) == 4 || kMesh64)
+        mfits = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && mesh_shape_ok &&
                 su.w.mesh_bytes > 0;
     if (o.engine == OTF_ENGINE_MESH && !mfits) return OTF_EUNSUPPORTED;
+    if constexpr (kMesh64) {
+        if (mfits && (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled()))) {
+            const hipError_t e = run_mesh64((const double*)C, ldc, (int)n, (int)m, (const double*)su.w.a_pad,
+                                            (const double*)su.w.b_pad, (const double*)cost_scale, o, su.w.mesh,
+                                            (double*)u_out, (double*)v_out, P_out, ldp, P_dtype, info, errlog,
+                                            /*zeroed=*/mesh_pick, s);
+            if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
+            (void)hipGetLastError();
+            if (o.engine == OTF_ENGINE_MESH) return check_hip(e);
+        }
+    }
     if constexpr (sizeof(T) == 4) {
         if (mfits && (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled()))) {
             const hipError_t e = run_mesh<CT>(C, ldc, (int)n, (int)m, (const float*)su.w.a_pad,

@@ -192,7 +192,8 @@ def test_mesh_float64_plan_output(dev):
 def test_mesh_unsupported_shapes_are_refused(dev):
     from otfuse import ops
     for n, m, dt in [(300, 200, torch.float32), (1024, 4097, torch.float32),
-                     (8193, 512, torch.float32), (1024, 1024, torch.float64)]:
+                     (8193, 512, torch.float32), (1000, 1024, torch.float64),
+                     (1024, 1000, torch.float64), (384, 512, torch.float64)]:
         C = torch.rand(n, m, device=dev, dtype=dt)
         a = torch.full((n,), 1.0 / n, device=dev, dtype=dt)
         b = torch.full((m,), 1.0 / m, device=dev, dtype=dt)
