@@ -126,6 +126,30 @@ __device__ __forceinline__ double lane0_f64(double x) {
     return __builtin_bit_cast(double, ((ull)hi << 32) | lo);
 }
 
+// Diagnostic build only (-DOTF_M64_STAMPS, tools/stamps_mesh64.hip): wave 0's wall clock
+// at the phases of iterations 0..15, keyed by the workgroup's role rb * ncb + cb
+#ifdef OTF_M64_STAMPS
+__device__ unsigned long long g_m64st[256 * 16 * 8];
+__device__ unsigned long long g_m64pro[256 * 4];  // kernel start, roles known, K formed, loop end
+#define OTF_M64PRO(ph)                                                                          \
+    do {                                                                                        \
+        if (threadIdx.x == 0 && rb * ncb + cb < 256)                                            \
+            g_m64pro[(rb * ncb + cb) * 4 + (ph)] = __builtin_amdgcn_s_memrealtime();           \
+    } while (0)
+#define OTF_M64ST(it, ph)                                                                       \
+    do {                                                                                        \
+        if (threadIdx.x == 0 && (it) >= 0 && (it) < 16 && rb * ncb + cb < 256)                  \
+            g_m64st[((rb * ncb + cb) * 16 + (it)) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define OTF_M64ST(it, ph) \
+    do {                  \
+    } while (0)
+#define OTF_M64PRO(ph) \
+    do {               \
+    } while (0)
+#endif
+
 constexpr int pow2_ceil(int x) { return x <= 1 ? 1 : 2 * pow2_ceil((x + 1) / 2); }
 
 // SNRB, SNCB: the shape compiled in (0 = from the arguments).  Every shape is a mesh of
@@ -149,6 +173,9 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
     int tid = threadIdx.x, lane = tid & 63;
     const int w = (int)threadIdx.x >> 6;
     unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.reg_ticks;
+#ifdef OTF_M64_STAMPS
+    const unsigned long long t_start = deadline - p.reg_ticks;
+#endif
     const int nrb = FULL ? SNRB : p.nrb, ncb = FULL ? SNCB : p.ncb;
     const int CPR = FULL ? pow2_ceil(kM64NCH / SNRB) : p.cpr;
     const int m_ = FULL ? SNCB * TC : p.m;
@@ -194,6 +221,10 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
         cb = bi % ncb;
     }
     const bool lead = (rb == 0 && cb == 0 && tid == 0);
+#ifdef OTF_M64_STAMPS
+    if (threadIdx.x == 0 && rb * ncb + cb < 256) g_m64pro[(rb * ncb + cb) * 4] = t_start;
+#endif
+    OTF_M64PRO(1);
     const int row0 = rb * TR + w * R;
     const int col0 = cb * TC;
     const int nch = kM64NCH;
@@ -218,8 +249,12 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
                 else sK[w][r - RR][j][lane] = e;
             }
             crow += p.ldc;
+            // one row's loads in flight at a time: hoisting all 32 rows' loads needs 512
+            // registers on top of K and spills the prologue to scratch
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
+    OTF_M64PRO(2);
     auto kget = [&](int r, int j) -> D2 { return r < RR ? kv[r][j] : sK[w][r - RR][j][lane]; };
     // 1 / a of the rows this lane group finishes after the row hop: chunk c = lane >> 3
     // of each half (rows 2c, 2c + 1 and 16 + 2c, 16 + 2c + 1 of the wave's 32)
@@ -410,7 +445,9 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
         asm volatile("" : "+v"(tid), "+v"(lane));
         const int e = it + 1;
         const bool check = it >= 1 && chk == 0;
+        OTF_M64ST(it, 0);
         const int fl = gather_b(e, check);
+        OTF_M64ST(it, 1);
         if (fl & 2) { status = OTF_SK_TIMEOUT; done = true; break; }
         if (fl & 1) {
             last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
@@ -440,6 +477,7 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
             t[2 * h + 1] = odd ? mine : oth;
         }
         if (it >= 1) chk = chk + 1 == p.check_every ? 0 : chk + 1;
+        OTF_M64ST(it, 2);
         T errv = 0;
         int vbad = vbad_cb, stall = 0;
         if (ncb == 1) {
@@ -456,8 +494,15 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
             const bool act = q < ncb;
             I4 x0 = I4{0, 0, 0, 0}, x1 = I4{0, 0, 0, 0};
             if (act) {
-                if (!poll64<false>(rs, rowx(e, q) + (uint32_t)(w * 16 + rc) * 16, (unsigned)e, deadline, x0)) stall = 1;
-                if (!poll64<false>(rs, rowx(e, q) + (uint32_t)(w * 16 + 8 + rc) * 16, (unsigned)e, deadline, x1)) stall = 1;
+                // both chunks in flight together, reloaded until both carry epoch e
+                const uint32_t o0 = rowx(e, q) + (uint32_t)(w * 16 + rc) * 16, o1 = o0 + 8 * 16;
+                for (;;) {
+                    x0 = gload(rs, o0);
+                    x1 = gload(rs, o1);
+                    if (dchunk_at(x0, (unsigned)e) && dchunk_at(x1, (unsigned)e)) break;
+                    if (__builtin_amdgcn_s_memrealtime() > deadline) { stall = 1; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
             }
             t[0] = act ? dchunk_v0(x0) : 0.0;
             t[1] = act ? dchunk_v1(x0) : 0.0;
@@ -473,6 +518,7 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
             if (check && !err_total(e, errv)) stall = 1;
             stall = __any(stall) ? 1 : 0;
         }
+        OTF_M64ST(it, 3);
         // u of this lane group's four rows; the group's first lane writes them to the
         // history, which the wave then reads back as wave-uniform values
         int badu = 0;
@@ -501,7 +547,9 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
         *reinterpret_cast<D2*>(&vhist[slot][2 * tid]) = *reinterpret_cast<const D2*>(&vcur[2 * tid]);
         if (badu) s_ep[0] = it;
         if (stall) s_ep[4] = it;
+        OTF_M64ST(it, 4);
         __syncthreads();
+        OTF_M64ST(it, 5);
         if (s_ep[4] == it) { status = OTF_SK_TIMEOUT; done = true; break; }
         if (check) {
             if (lead) p.errlog[n_err] = err;
@@ -518,7 +566,9 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
             break;
         }
         publish_cols(e + 1, s_ep[0] == it ? 1 : 0);
+        OTF_M64ST(it, 6);
         if (w == 0 && !reduce(e + 1, chk == 0)) s_ep[1] = e + 1;
+        OTF_M64ST(it, 7);
     }
     if (!done && p.max_iter > 0) {
         const int it = p.max_iter - 1;
@@ -553,6 +603,7 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
     }
 
     // ---- outputs: (u, v) of last_good from the histories, the plan from K
+    OTF_M64PRO(3);
     __syncthreads();
     const int hs = last_good & 1;
     D2 vo[4];
@@ -584,6 +635,7 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
                     *reinterpret_cast<F4*>(prow + g * 256) = F4{(float)o0[0], (float)o0[1], (float)o1[0], (float)o1[1]};
                 }
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
     if (status == OTF_SK_TIMEOUT && tid == 0) mark_stalled(&p.info->stalled, kStallMid);

@@ -1,0 +1,95 @@
+// Diagnostic: the float64 mesh engine's iteration split into phases (wave 0 of every
+// workgroup, iterations 3..13, mean over workgroups).  Builds the library sources with
+// -DOTF_M64_STAMPS and runs the float64 metric shape (N = 4096, eps 0.1, 100 iterations).
+// Build: hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -DOTF_M64_STAMPS -I include \
+//        tools/stamps_mesh64.hip -o tools/stamps_mesh64
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_common.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sinkhorn.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sweep.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_gather.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_mesh.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_mesh2.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_mesh64.hip"
+#include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_comm.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+int main(int argc, char** argv) {
+    const int N = argc > 1 ? atoi(argv[1]) : 4096;
+    const int iters = argc > 2 ? atoi(argv[2]) : 100;
+    double *C, *a, *u, *v, *P;
+    otf_sinkhorn_info* info;
+    (void)hipMalloc(&C, (size_t)N * N * 8);
+    (void)hipMalloc(&a, N * 8);
+    (void)hipMalloc(&u, N * 8);
+    (void)hipMalloc(&v, N * 8);
+    (void)hipMalloc(&P, (size_t)N * N * 8);
+    (void)hipMalloc(&info, sizeof(otf_sinkhorn_info));
+    std::vector<double> h((size_t)N * N);
+    unsigned s = 1;
+    for (auto& x : h) { s = s * 1664525u + 1013904223u; x = (s >> 8) * (1.0 / 16777216.0); }
+    (void)hipMemcpy(C, h.data(), h.size() * 8, hipMemcpyHostToDevice);
+    std::vector<double> ha(N, 1.0 / N);
+    (void)hipMemcpy(a, ha.data(), N * 8, hipMemcpyHostToDevice);
+    const size_t wsb = otf_sinkhorn_workspace_size(N, N, OTF_F64, iters);
+    void* ws;
+    (void)hipMalloc(&ws, wsb);
+    otf_sinkhorn_opts o{};
+    o.reg = 0.1; o.stop_thr = 0; o.max_iter = iters; o.check_every = 10;
+    o.flavor = OTF_FLAVOR_POT; o.engine = OTF_ENGINE_MESH;
+    for (int rep = 0; rep < 4; ++rep) {
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        (void)hipEventRecord(e0, 0);
+        const int rc = otf_sinkhorn(a, a, C, N, N, N, OTF_F64, nullptr, &o, u, v, P, N, OTF_F64, info,
+                                    nullptr, ws, wsb, 0);
+        (void)hipEventRecord(e1, 0);
+        (void)hipDeviceSynchronize();
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        otf_sinkhorn_info hi;
+        (void)hipMemcpy(&hi, info, sizeof(hi), hipMemcpyDeviceToHost);
+        printf("rc=%d status=%d engine=%d solve %.3f ms\n", rc, hi.status, hi.engine, ms);
+    }
+    std::vector<unsigned long long> st(256 * 16 * 8);
+    (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(otf::g_m64st), st.size() * 8);
+    std::vector<unsigned long long> pro(256 * 4);
+    (void)hipMemcpyFromSymbol(pro.data(), HIP_SYMBOL(otf::g_m64pro), pro.size() * 8);
+    double pa[3] = {0};
+    unsigned long long t0 = ~0ull, tend = 0;
+    for (int r = 0; r < 256; ++r) {
+        for (int k = 0; k < 3; ++k) pa[k] += (double)(pro[r * 4 + k + 1] - pro[r * 4 + k]);
+        t0 = std::min(t0, pro[r * 4]);
+        tend = std::max(tend, pro[r * 4 + 3]);
+    }
+    printf("  start -> roles (registration)   %7.3f us (mean)\n", pa[0] / 256 * 0.01);
+    printf("  roles -> K formed (C read, exp) %7.3f us\n", pa[1] / 256 * 0.01);
+    printf("  K formed -> loop end            %7.3f us\n", pa[2] / 256 * 0.01);
+    printf("  first start -> last loop end    %7.3f us\n", (tend - t0) * 0.01);
+    const char* names[7] = {"hop B wait + v + barrier", "row partials (2 x 16 rows)", "row hop (publish + gather)",
+                            "u + col partials", "barrier", "publish cols", "reduce (wave 0)"};
+    double acc[8] = {0};
+    int cnt = 0;
+    for (int r = 0; r < 256; ++r)
+        for (int it = 3; it < 14; ++it) {
+            const unsigned long long* q = &st[((size_t)r * 16 + it) * 8];
+            const unsigned long long* qn = &st[((size_t)r * 16 + it + 1) * 8];
+            if (q[0] == 0 || qn[0] == 0) continue;
+            for (int k = 0; k < 7; ++k) acc[k] += (double)(q[k + 1] - q[k]);
+            acc[7] += (double)(qn[0] - q[7]);
+            ++cnt;
+        }
+    double tot = 0;
+    for (int k = 0; k < 7; ++k) {
+        printf("  %-30s %7.3f us\n", names[k], acc[k] / cnt * 0.01);
+        tot += acc[k];
+    }
+    printf("  %-30s %7.3f us\n", "loop back", acc[7] / cnt * 0.01);
+    tot += acc[7];
+    printf("  = iteration                    %7.3f us  (%d samples)\n", tot / cnt * 0.01, cnt);
+    return 0;
+}
