@@ -448,9 +448,12 @@ def metric_f64_leg(dev, N=4096, d=512, iters=100, eps=0.1, reps=3):
     res = None
     for _ in range(reps):
         e[0].record()
-        C, _ = gw.pairwise_cost_f64(Xd, Yd, scale_max=True)
+        # the max-normalisation (MRI_PET_OT_nojax.py:75) is applied inside the solve through
+        # cost_scale, as in the float32 headline step (no separate C /= max pass)
+        C, cmax = gw.pairwise_cost_f64(Xd, Yd, scale_max=False)
         e[1].record()
-        res = ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, workspace=ws, plan_out=P)
+        res = ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, workspace=ws, plan_out=P,
+                           cost_scale=cmax)
         e[2].record()
         torch.cuda.synchronize()
         tc.append(e[0].elapsed_time(e[1]))

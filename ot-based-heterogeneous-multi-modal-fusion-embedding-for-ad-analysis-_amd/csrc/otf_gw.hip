@@ -1410,10 +1410,10 @@ __global__ __launch_bounds__(256) void dist_scale_kernel(double* C, int64_t ldc,
     for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = fmax(r, red[w]);
     if (cmax && blockIdx.x == 0 && threadIdx.x == 0) *cmax = r;
     if (!scale) return;
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)n * m;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const int i = (int)(e / m), j = (int)(e % m);
-        C[(int64_t)i * ldc + j] = C[(int64_t)i * ldc + j] / r;
+    // rows strided over the grid, columns over the block (no 64-bit division per element)
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        double* row = C + (int64_t)i * ldc;
+        for (int j = threadIdx.x; j < m; j += blockDim.x) row[j] = row[j] / r;
     }
 }
 

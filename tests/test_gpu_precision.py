@@ -189,3 +189,9 @@ def test_metric_shape_float64_leg_vs_oracle(orc, dev, metric_inputs, oracle_plan
         Pr, *_ = oracle_plans(eps) if eps != 0.1 else orc.sinkhorn_knopp(
             np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cr, 0.1, 100, 0.0)
         assert nrel(res.plan.cpu().numpy(), Pr) < 1e-9
+    # the bench form: unscaled float64 cost, the max applied inside the solve (cost_scale)
+    C64u, cmax = gw.pairwise_cost_f64(Xd, Yd, scale_max=False)
+    assert float(cmax) == float(C64u.max())
+    res = ops.sinkhorn(a, a, C64u, 0.1, max_iter=100, stop_thr=0.0, cost_scale=cmax)
+    Pr, *_ = orc.sinkhorn_knopp(np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cr, 0.1, 100, 0.0)
+    assert nrel(res.plan.cpu().numpy(), Pr) < 1e-9
