@@ -459,45 +459,50 @@ __device__ int blk_sinkhorn_knopp(const double* K, int64_t ldk, int n, int m, co
 // loop runs ~1000 inner updates per outer iteration in one serial chain (562 k updates
 // for the 64 x 64, eps = 5e-3 bench problem), so the update latency is the solve time.
 // K (a zero-padded 64 x 65 LDS image, entries outside n x m are 0) is read into
-// registers once per call, in both orientations the two half-updates need:
-//   V half, v = b / K^T u:  wave w owns columns 8w .. 8w + 7; lane (q, s) = (l & 7, l >> 3)
-//                           holds K[8s + r][8w + q], r < 8, and sums them against
-//                           u[8s .. 8s + 7] (LDS, 4 broadcast reads), then xor 8 / 16 / 32;
-//   U half, u = 1 / (Kp v): wave w owns rows 8w .. 8w + 7, lane (q, s) holds
-//                           Kp[8w + q][8s + c] = K / a and sums them against v[8s ..].
-// Every lane of a column (row) group ends with the same sum, so every lane has the new v
-// (u) of its column (row) and keeps the previous one for POT's revert-on-error rule.
-// POT's error check after update ii (every `every` updates: tmp2 = sum_i u_i K_ij v_j,
-// err = ||tmp2 - b||) reuses the V half of update ii + 1 (tmp2_j = (K^T u)_j v_j, the same
-// K^T u), so a check costs one wave sum and one LDS word per wave; on convergence the v
-// that half computed is dropped.  u ends in sh.f, v in sh.g; conv / iters are uniform.
+// registers once per call, in both orientations the two half-updates need; waves 0..3
+// work (one per SIMD), waves 4..7 only meet the barriers:
+//   V half, v = b / K^T u:  wave w owns columns 16w .. 16w + 15; lane (q, s) = (l & 15, l >> 4)
+//                           holds K[16s + r][16w + q], r < 16, and sums them against
+//                           u[16s .. 16s + 15] (LDS, 8 broadcast reads) in four chains,
+//                           then xor 16 / 32 (the permlane swaps);
+//   U half, u = 1 / (Kp v): wave w owns rows 16w .. 16w + 15, lane (q, s) holds
+//                           Kp[16w + q][16s + c] = K / a and sums them against v[16s ..].
+// (tools/ubench_sk64.hip: 620 ns per update in this form against 709 for 8 waves x 8
+// columns with one chain and three exchanges.)  Every lane of a column (row) group ends
+// with the same sum, so every lane has the new v (u) of its column (row) and keeps the
+// previous one for POT's revert-on-error rule.  POT's error check after update ii (every
+// `every` updates: tmp2 = sum_i u_i K_ij v_j, err = ||tmp2 - b||) reuses the V half of
+// update ii + 1 (tmp2_j = (K^T u)_j v_j, the same K^T u), so a check costs one 16-lane sum
+// and one LDS word per wave; on convergence the v that half computed is dropped.  u ends
+// in sh.f, v in sh.g; conv / iters are uniform.
 constexpr int GW_WLD = GW_SMALLN + 1;
 
 template <class Cfg>
 __device__ void small_sinkhorn_knopp(const double* K, int n, int m, const double* a, const double* b,
                                      double thr, int maxit, int every, GwShared<Cfg>& sh,
                                      bool& conv, int& iters) {
-    static_assert(GW_SMALLN == 64, "8 columns / rows per wave");
+    static_assert(GW_SMALLN == 64, "16 columns / rows per wave");
     if constexpr (Cfg::NW != 8) {  // only the GwSmall kernel calls it (n, m <= 64)
         __builtin_trap();
     } else {
     __shared__ __attribute__((aligned(16))) double s_u[GW_SMALLN];
     __shared__ __attribute__((aligned(16))) double s_v[GW_SMALLN];
-    __shared__ double s_e[8];
+    __shared__ double s_e[4];
     __shared__ int s_kf[2];
     const int l = threadIdx.x & (kWave - 1);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int q = l & 7, sg = l >> 3;
-    const int jc = 8 * w + q;  // V half: this lane's column
-    const int ir = 8 * w + q;  // U half: this lane's row
-    const bool cl = jc < m, rl = ir < n;
+    const bool act = w < 4;  // the working waves
+    const int q = l & 15, sg = l >> 4;
+    const int jc = 16 * (w & 3) + q;  // V half: this lane's column
+    const int ir = 16 * (w & 3) + q;  // U half: this lane's row
+    const bool cl = act && jc < m, rl = act && ir < n;
     const double bj = cl ? marg(b, jc, m) : 0.0;
     const double ia = rl ? 1.0 / marg(a, ir, n) : 0.0;
-    double kv[8], ku[8];
+    double kv[16], ku[16];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) kv[r] = K[(8 * sg + r) * GW_WLD + jc];
+    for (int r = 0; r < 16; ++r) kv[r] = act ? K[(16 * sg + r) * GW_WLD + jc] : 0.0;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) ku[c] = ia * K[ir * GW_WLD + 8 * sg + c];  // Kp = K / a (POT)
+    for (int c = 0; c < 16; ++c) ku[c] = act ? ia * K[ir * GW_WLD + 16 * sg + c] : 0.0;  // Kp = K / a (POT)
     if (threadIdx.x < GW_SMALLN) s_u[threadIdx.x] = (int)threadIdx.x < n ? 1.0 / (double)n : 0.0;
     if (threadIdx.x < 2) s_kf[threadIdx.x] = 0;
     double u = rl ? 1.0 / (double)n : 0.0, v = cl ? 1.0 / (double)m : 0.0;  // last good pair
@@ -507,68 +512,61 @@ __device__ void small_sinkhorn_knopp(const double* K, int n, int m, const double
     bool check = false;  // POT's error check of the previous update is pending
     int cnt = 0;         // ii % every
     using D2 = __attribute__((ext_vector_type(2))) double;
+    // sum of 16 products in four chains of four, then over the 4 lane segments
+    auto dot16 = [&](const double (&k)[16], const double* x) -> double {
+        const D2* xp = reinterpret_cast<const D2*>(x);
+        double c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const D2 x0 = xp[2 * h], x1 = xp[2 * h + 1];
+            c0 = fma(k[4 * h], x0[0], c0);
+            c1 = fma(k[4 * h + 1], x0[1], c1);
+            c2 = fma(k[4 * h + 2], x1[0], c2);
+            c3 = fma(k[4 * h + 3], x1[1], c3);
+        }
+        double t = (c0 + c1) + (c2 + c3);
+        t += wave_xor<double, 16>(t);
+        t += wave_xor<double, 32>(t);
+        return t;
+    };
     for (int ii = 0;; ++ii) {
         if (ii == maxit && !check) break;
-        // ---- V half: s = (K^T u)_jc; v = b / s
-        double s;
-        {
-            const D2* up = reinterpret_cast<const D2*>(&s_u[8 * sg]);
-            const D2 u01 = up[0], u23 = up[1], u45 = up[2], u67 = up[3];
-            s = kv[0] * u01[0];
-            s = fma(kv[1], u01[1], s);
-            s = fma(kv[2], u23[0], s);
-            s = fma(kv[3], u23[1], s);
-            s = fma(kv[4], u45[0], s);
-            s = fma(kv[5], u45[1], s);
-            s = fma(kv[6], u67[0], s);
-            s = fma(kv[7], u67[1], s);
-            s += wave_xor<double, 8>(s);
-            s += wave_xor<double, 16>(s);
-            s += wave_xor<double, 32>(s);
+        double s = 0, vn = 0;
+        if (act) {
+            // ---- V half: s = (K^T u)_jc; v = b / s
+            s = dot16(kv, &s_u[16 * sg]);
+            if (check) {
+                // err of the previous update: tmp2_j = (K^T u)_j v_j
+                const double d = cl ? s * v - bj : 0.0;
+                double e = sg == 0 ? d * d : 0.0;
+                e += wave_xor<double, 1>(e);
+                e += wave_xor<double, 2>(e);
+                e += wave_xor<double, 4>(e);
+                e += wave_xor<double, 8>(e);
+                if (l == 0) s_e[w] = e;
+            }
+            vn = cl ? bj / s : 0.0;
+            const bool badv = cl && (s == 0.0 || !finite_val(vn));
+            if (sg == 0) s_v[jc] = vn;
+            if (__ballot(badv) != 0 && l == 0) s_kf[ii & 1] = 1;
         }
-        if (check) {
-            // err of the previous update: tmp2_j = (K^T u)_j v_j
-            const double d = cl ? s * v - bj : 0.0;
-            double e = sg == 0 ? d * d : 0.0;
-            e += wave_xor<double, 1>(e);
-            e += wave_xor<double, 2>(e);
-            e += wave_xor<double, 4>(e);
-            if (l == 0) s_e[w] = e;
-        }
-        const double vn = cl ? bj / s : 0.0;
-        const bool badv = cl && (s == 0.0 || !finite_val(vn));
-        if (sg == 0) s_v[jc] = vn;
-        if (__ballot(badv) != 0 && l == 0) s_kf[ii & 1] = 1;
         __syncthreads();
         if (check) {
-            double e2 = s_e[0];
-#pragma unroll
-            for (int k = 1; k < 8; ++k) e2 += s_e[k];
+            const double e2 = (s_e[0] + s_e[1]) + (s_e[2] + s_e[3]);
             if (sqrt(e2) < thr) { conv = true; iters = ii; break; }  // the checked update's pair
         }
         if (ii == maxit) break;  // the last update's check only
         // every reader of the other parity's flag (update ii - 1) is past this barrier
         if (threadIdx.x == 0) s_kf[(ii + 1) & 1] = 0;
-        // ---- U half: s = (Kp v)_ir; u = 1 / s
-        {
-            const D2* vp = reinterpret_cast<const D2*>(&s_v[8 * sg]);
-            const D2 v01 = vp[0], v23 = vp[1], v45 = vp[2], v67 = vp[3];
-            s = ku[0] * v01[0];
-            s = fma(ku[1], v01[1], s);
-            s = fma(ku[2], v23[0], s);
-            s = fma(ku[3], v23[1], s);
-            s = fma(ku[4], v45[0], s);
-            s = fma(ku[5], v45[1], s);
-            s = fma(ku[6], v67[0], s);
-            s = fma(ku[7], v67[1], s);
-            s += wave_xor<double, 8>(s);
-            s += wave_xor<double, 16>(s);
-            s += wave_xor<double, 32>(s);
+        double un = 0;
+        if (act) {
+            // ---- U half: s = (Kp v)_ir; u = 1 / s
+            s = dot16(ku, &s_v[16 * sg]);
+            un = rl ? 1.0 / s : 0.0;
+            const bool badu = rl && !finite_val(un);
+            if (sg == 0) s_u[ir] = un;
+            if (__ballot(badu) != 0 && l == 0) s_kf[ii & 1] = 1;
         }
-        const double un = rl ? 1.0 / s : 0.0;
-        const bool badu = rl && !finite_val(un);
-        if (sg == 0) s_u[ir] = un;
-        if (__ballot(badu) != 0 && l == 0) s_kf[ii & 1] = 1;
         __syncthreads();
         if (s_kf[ii & 1]) { iters = ii + 1; break; }  // numerical error: keep the previous pair
         u = un;
@@ -576,7 +574,7 @@ __device__ void small_sinkhorn_knopp(const double* K, int n, int m, const double
         check = cnt == 0;  // ii % every == 0, as a counter (no integer division per update)
         cnt = cnt + 1 == every ? 0 : cnt + 1;
     }
-    if (sg == 0) {
+    if (act && sg == 0) {
         sh.f[ir] = u;
         sh.g[jc] = v;
     }

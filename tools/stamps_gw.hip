@@ -30,7 +30,7 @@ int main(int argc, char** argv) {
     (void)hipMalloc(&dws, dwb);
     otf_gw_info* info;
     (void)hipMalloc(&info, 2 * sizeof(otf_gw_info));
-    for (int solver = 0; solver < 2; ++solver) {
+    for (int solver = 0; solver < 3; ++solver) {
         const int metric = solver == OTF_GW_CG ? OTF_EUCLIDEAN : OTF_SQEUCLIDEAN;
         for (int k = 0; k < 2; ++k) {
             otf_cost_pairwise_f64(X, d, X, d, n, n, d, metric, solver == OTF_GW_CG, 1, C[2 * k], n, cm, dws, dwb, 0);
@@ -41,9 +41,9 @@ int main(int argc, char** argv) {
             pr[k] = otf_gw_problem{C[2 * k], n, C[2 * k + 1], n, nullptr, nullptr, nullptr, nullptr, T[k], n, n, n};
         }
         otf_gw_opts o{};
-        o.solver = solver; o.max_iter = solver == OTF_GW_CG ? 10000 : 2000; o.min_iter = 5;
-        o.sk_max_iter = 2000; o.sk_inner = 10; o.warm_start = 1; o.tol_rel = 1e-9; o.tol_abs = 1e-9;
-        o.threshold = 1e-3; o.sk_threshold = 1e-3; o.eps = 5e-3;
+        o.solver = solver; o.max_iter = solver == OTF_GW_CG ? 10000 : solver == OTF_GW_PGD ? 1000 : 2000; o.min_iter = 5;
+        o.sk_max_iter = solver == OTF_GW_PGD ? 1000 : 2000; o.sk_inner = 10; o.warm_start = 1; o.tol_rel = 1e-9; o.tol_abs = 1e-9;
+        o.threshold = 1e-3; o.sk_threshold = solver == OTF_GW_PGD ? 1e-9 : 1e-3; o.eps = 5e-3;
         const size_t wsb = otf_gw_workspace_size(2, pr);
         void* ws;
         (void)hipMalloc(&ws, wsb);
@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
             otf_gw_info hi[2];
             (void)hipMemcpy(hi, info, sizeof(hi), hipMemcpyDeviceToHost);
             printf("%s n=%d rc=%d outer=%d inner=%d | gemm %.1f us  lap %.1f us  sinkhorn %.1f us  total %.1f us\n",
-                   solver == OTF_GW_CG ? "cg" : "entropic", n, rc, hi[0].n_iter, hi[0].inner_iters,
+                   solver == OTF_GW_CG ? "cg" : solver == OTF_GW_PGD ? "pgd" : "entropic", n, rc, hi[0].n_iter, hi[0].inner_iters,
                    st[0] / 100.0, st[1] / 100.0, st[2] / 100.0, st[3] / 100.0);
             if (hi[0].inner_iters) printf("   per update: col %.2f us  row %.2f us; per check: err %.2f us\n", sk[0] / 100.0 / hi[0].inner_iters, sk[1] / 100.0 / hi[0].inner_iters, sk[2] / 100.0 / (hi[0].inner_iters / 10.0));
         }
