@@ -25,6 +25,7 @@
 // The error chunks, written only every check_every epochs, carry ONE value and the full
 // epoch tag instead.  Every sum has one fixed order: bitwise reproducible run to run.
 #include "otf_persist.h"
+#include <type_traits>
 
 namespace otf {
 namespace {
@@ -299,13 +300,12 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
         return p.off_colb + ((uint32_t)((e & 1) * ncb + cb) * (uint32_t)nrb + (uint32_t)j) * p.bstride;
     };
 
-    // column partials of this wave's 32 rows against u (LDS, wave-uniform reads) -> colbuf
-    auto col_partials = [&](const T* ur) {
-        D2 acc[4];
+    // column partials of rows [R0, R0 + NR) of this wave against u (LDS, wave-uniform
+    // reads), accumulated into acc in ascending row order
+    auto col_acc = [&](D2 (&acc)[4], const T* ur, auto r0c) {
+        constexpr int R0 = decltype(r0c)::value;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = D2{0.0, 0.0};
-#pragma unroll
-        for (int r = 0; r < R; r += 2) {
+        for (int r = R0; r < R0 + 16; r += 2) {
             const D2 uu = *reinterpret_cast<const D2*>(ur + r);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -313,9 +313,19 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
                 acc[j] = __builtin_elementwise_fma(kget(r + 1, j), D2{uu[1], uu[1]}, acc[j]);
             }
         }
+    };
+    auto col_store = [&](const D2 (&acc)[4]) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             *reinterpret_cast<D2*>(&colbuf[w][(j >> 1) * 256 + lane * 4 + (j & 1) * 2]) = acc[j];
+    };
+    auto col_partials = [&](const T* ur) {
+        D2 acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = D2{0.0, 0.0};
+        col_acc(acc, ur, std::integral_constant<int, 0>{});
+        col_acc(acc, ur, std::integral_constant<int, 16>{});
+        col_store(acc);
     };
     // hop A: the workgroup's column partials (after the barrier), epoch e; flag = non-finite u
     auto publish_cols = [&](int e, int flag) {
@@ -458,8 +468,13 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
         D2 vn[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) vn[j] = *reinterpret_cast<const D2*>(&vcur[(j >> 1) * 256 + lane * 4 + (j & 1) * 2]);
-        // row partials over this tile's columns, wave totals in two halves of 16 rows:
-        // lane group c = lane >> 3 ends with rows 2c, 2c + 1 of each half
+        // Two halves of the wave's 32 rows, pipelined: each half's row partials are
+        // published as soon as its wave totals are known, so the row hop of rows 0..15 is
+        // in flight while rows 16..31 are summed, and rows 16..31's hop while the column
+        // partials of rows 0..15 run.  Lane group c = lane >> 3 ends a half with its rows
+        // 2c, 2c + 1.
+        if (it >= 1) chk = chk + 1 == p.check_every ? 0 : chk + 1;
+        const bool hop = ncb > 1;
         T t[4];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -475,66 +490,51 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
             const bool odd = (lane & 4) != 0;
             t[2 * h] = odd ? oth : mine;
             t[2 * h + 1] = odd ? mine : oth;
+            if (hop && (lane & 7) == 0)
+                gstore(rs, rowx(e, cb) + (uint32_t)(w * 16 + 8 * h + rc) * 16, dchunk(t[2 * h], t[2 * h + 1], e, vbad_cb));
         }
-        if (it >= 1) chk = chk + 1 == p.check_every ? 0 : chk + 1;
         OTF_M64ST(it, 2);
-        T errv = 0;
-        int vbad = vbad_cb, stall = 0;
-        if (ncb == 1) {
-            errv = s_E;
-        } else {
-            // row hop: publish this wave's 32 row partials (16 chunks: lane 8c, halves h)
-            // and the column tile's error partial; gather the ncb members' chunks
-            if ((lane & 7) == 0) {
-                gstore(rs, rowx(e, cb) + (uint32_t)(w * 16 + rc) * 16, dchunk(t[0], t[1], e, vbad_cb));
-                gstore(rs, rowx(e, cb) + (uint32_t)(w * 16 + 8 + rc) * 16, dchunk(t[2], t[3], e, vbad_cb));
-            }
-            if (check && w == 0 && lane == 1) gstore(rs, rowx(e, cb) + 64 * 16, echunk(s_E, e));
-            const int q = lane & 7;
-            const bool act = q < ncb;
-            I4 x0 = I4{0, 0, 0, 0}, x1 = I4{0, 0, 0, 0};
-            if (act) {
-                // both chunks in flight together, reloaded until both carry epoch e
-                const uint32_t o0 = rowx(e, q) + (uint32_t)(w * 16 + rc) * 16, o1 = o0 + 8 * 16;
-                for (;;) {
-                    x0 = gload(rs, o0);
-                    x1 = gload(rs, o1);
-                    if (dchunk_at(x0, (unsigned)e) && dchunk_at(x1, (unsigned)e)) break;
-                    if (__builtin_amdgcn_s_memrealtime() > deadline) { stall = 1; break; }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            t[0] = act ? dchunk_v0(x0) : 0.0;
-            t[1] = act ? dchunk_v1(x0) : 0.0;
-            t[2] = act ? dchunk_v0(x1) : 0.0;
-            t[3] = act ? dchunk_v1(x1) : 0.0;
-            vbad = __any(act && (dchunk_flag(x0) | dchunk_flag(x1))) ? 1 : 0;
+        if (hop && check && w == 0 && lane == 1) gstore(rs, rowx(e, cb) + 64 * 16, echunk(s_E, e));
+        T errv = hop ? 0.0 : s_E;
+        int vbad = vbad_cb, stall = 0, badu = 0;
+        const int q = lane & 7;
+        const bool act = hop && q < ncb;
+        D2 cacc[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                t[k] += dpp_lane<0xB1>(t[k]);
-                t[k] += dpp_lane<0x4E>(t[k]);
-                t[k] += dpp_lane<0x141>(t[k]);
-            }
-            if (check && !err_total(e, errv)) stall = 1;
-            stall = __any(stall) ? 1 : 0;
-        }
-        OTF_M64ST(it, 3);
-        // u of this lane group's four rows; the group's first lane writes them to the
-        // history, which the wave then reads back as wave-uniform values
-        int badu = 0;
-        {
-            T un[4];
+        for (int j = 0; j < 4; ++j) cacc[j] = D2{0.0, 0.0};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) un[k] = 1.0 / (t[k] * ia[k]);
-            badu = __any(!finite_val(un[0]) || !finite_val(un[1]) || !finite_val(un[2]) || !finite_val(un[3])) ? 1 : 0;
-            if ((lane & 7) == 0) {
-                *reinterpret_cast<D2*>(&uhist[it & 1][w * R + 2 * rc]) = D2{un[0], un[1]};
-                *reinterpret_cast<D2*>(&uhist[it & 1][w * R + 16 + 2 * rc]) = D2{un[2], un[3]};
+        for (int h = 0; h < 2; ++h) {
+            T th0 = t[2 * h], th1 = t[2 * h + 1];
+            if (hop) {
+                // gather the ncb members' chunk of this half (lane (c, q): member q)
+                I4 x = I4{0, 0, 0, 0};
+                if (act && !poll64<false>(rs, rowx(e, q) + (uint32_t)(w * 16 + 8 * h + rc) * 16, (unsigned)e, deadline, x))
+                    stall = 1;
+                th0 = act ? dchunk_v0(x) : 0.0;
+                th1 = act ? dchunk_v1(x) : 0.0;
+                if (__any(act && dchunk_flag(x))) vbad = 1;
+                th0 += dpp_lane<0xB1>(th0);
+                th1 += dpp_lane<0xB1>(th1);
+                th0 += dpp_lane<0x4E>(th0);
+                th1 += dpp_lane<0x4E>(th1);
+                th0 += dpp_lane<0x141>(th0);
+                th1 += dpp_lane<0x141>(th1);
             }
+            // u of this half's two rows of the lane group; the group's first lane writes
+            // them to the history, which the wave then reads back as wave-uniform values
+            const T un0 = 1.0 / (th0 * ia[2 * h]), un1 = 1.0 / (th1 * ia[2 * h + 1]);
+            if (__any(!finite_val(un0) || !finite_val(un1))) badu = 1;
+            if ((lane & 7) == 0) *reinterpret_cast<D2*>(&uhist[it & 1][w * R + 16 * h + 2 * rc]) = D2{un0, un1};
             // the wave's own LDS writes complete before its reads (in-order LDS per wave);
             // the clobber keeps the compiler from hoisting the reads above the writes
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (h == 0) col_acc(cacc, &uhist[it & 1][w * R], std::integral_constant<int, 0>{});
+            else col_acc(cacc, &uhist[it & 1][w * R], std::integral_constant<int, 16>{});
         }
+        col_store(cacc);
+        if (hop && check && !err_total(e, errv)) stall = 1;
+        stall = __any(stall) ? 1 : 0;
+        OTF_M64ST(it, 3);
         double err = 0.0;
         int dec = 0;
         if (check) {
@@ -542,7 +542,6 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
             if (stop_ok(err)) dec = 1;
         }
         if (dec == 0 && vbad) dec = 2;
-        col_partials(&uhist[it & 1][w * R]);
         const int slot = it & 1;
         *reinterpret_cast<D2*>(&vhist[slot][2 * tid]) = *reinterpret_cast<const D2*>(&vcur[2 * tid]);
         if (badu) s_ep[0] = it;
