@@ -1325,10 +1325,13 @@ __global__ __launch_bounds__(256, 2) void dist_tile_f64_kernel(const float* __re
 #pragma unroll 2
         for (int kk = 0; kk < DK; ++kk) {
             double av[8], bv[8];
+            // a thread's 8 columns are the pairs 32 h + 2 tx, + 1 (h < 4): the 16 lanes of a
+            // ds_read_b128 phase read 16 consecutive 16-B slots (tx * 8 + 2 h had them 64 B
+            // apart: four lanes per bank group), and the epilogue stores 256-B row runs
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
                 const D2 a2 = *reinterpret_cast<const D2*>(&As[buf][kk][ty * 8 + 2 * h]);
-                const D2 b2 = *reinterpret_cast<const D2*>(&Bs[buf][kk][tx * 8 + 2 * h]);
+                const D2 b2 = *reinterpret_cast<const D2*>(&Bs[buf][kk][32 * h + 2 * tx]);
                 av[2 * h] = a2[0];
                 av[2 * h + 1] = a2[1];
                 bv[2 * h] = b2[0];
@@ -1351,7 +1354,7 @@ __global__ __launch_bounds__(256, 2) void dist_tile_f64_kernel(const float* __re
         double* crow = C + (int64_t)i * ldc;
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
-            const int j = j0 + tx * 8 + b;
+            const int j = j0 + 32 * (b >> 1) + 2 * tx + (b & 1);
             if (j >= m) continue;
             double v = -2.0 * acc[a][b];
             v += rx;
