@@ -1372,6 +1372,117 @@ __global__ __launch_bounds__(256, 2) void dist_tile_f64_kernel(const float* __re
     if (tid == 0) part[tile] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
 }
 
+// The same 128 x 128 float64 tile on v_mfma_f64_16x16x4_f64 (the matrix cores free the
+// VALU for nothing else here, but one MFMA replaces 16 vector FMAs and their operand
+// reads): 4 waves, each a 64 x 64 quarter as 4 x 4 blocks of 16 x 16; per 4-deep k-step a
+// lane reads one double of each of its 4 row blocks and 4 column blocks from the LDS
+// stage (16 consecutive doubles per lane group: conflict-free).  Operand staging, the
+// epilogue (POT euclidean_distances order, clamp, sqrt, zero diagonal) and the per-tile
+// max are dist_tile_f64_kernel's.  Result lanes: column l & 15, rows (l >> 4) + 4 r.
+__global__ __launch_bounds__(256, 2) void dist_mfma_f64_kernel(const float* __restrict__ X, int64_t ldx,
+                                                               const float* __restrict__ Y, int64_t ldy,
+                                                               int n, int m, int d, const double* nx,
+                                                               const double* ny, int euclid, int zero_diag,
+                                                               double* C, int64_t ldc, double* part, int tiles_m,
+                                                               int vec) {
+    __shared__ __attribute__((aligned(16))) double As[2][DK][DT];
+    __shared__ __attribute__((aligned(16))) double Bs[2][DK][DT];
+    __shared__ double red[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1, li = lane & 15, lk = lane >> 4;
+    const int tile = blockIdx.x;
+    const int i0 = (tile % tiles_m) * DT, j0 = (tile / tiles_m) * DT;
+    const int lr = tid >> 1, lkk = (tid & 1) * 8;
+    const int gi = i0 + lr < n ? i0 + lr : n - 1, gj = j0 + lr < m ? j0 + lr : m - 1;
+    const float* xr = X + (int64_t)gi * ldx;
+    const float* yr = Y + (int64_t)gj * ldy;
+    float xa[8], yb[8];
+    auto gload = [&](int k0) {
+        const int kb = k0 + lkk;
+        if (vec && kb + 8 <= d) {
+            using F4 = __attribute__((ext_vector_type(4))) float;
+            const F4 x0 = *reinterpret_cast<const F4*>(xr + kb), x1 = *reinterpret_cast<const F4*>(xr + kb + 4);
+            const F4 y0 = *reinterpret_cast<const F4*>(yr + kb), y1 = *reinterpret_cast<const F4*>(yr + kb + 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                xa[q] = x0[q];
+                xa[q + 4] = x1[q];
+                yb[q] = y0[q];
+                yb[q + 4] = y1[q];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int k = kb + q;
+                xa[q] = k < d ? xr[k] : 0.f;
+                yb[q] = k < d ? yr[k] : 0.f;
+            }
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            As[buf][lkk + q][lr] = (double)xa[q];
+            Bs[buf][lkk + q][lr] = (double)yb[q];
+        }
+    };
+    gw_f64x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = gw_f64x4{0.0, 0.0, 0.0, 0.0};
+    const int nk = (d + DK - 1) / DK;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) gload((kt + 1) * DK);
+#pragma unroll
+        for (int ks = 0; ks < DK / 4; ++ks) {
+            const int k = 4 * ks + lk;
+            double av[4], bv[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                av[t] = As[buf][k][wm * 64 + t * 16 + li];
+                bv[t] = Bs[buf][k][wn * 64 + t * 16 + li];
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+        }
+        if (kt + 1 < nk) lstore(buf ^ 1);
+        __syncthreads();
+    }
+    double mx = 0.0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int j = j0 + wn * 64 + b * 16 + li;
+        const bool jok = j < m;
+        const double ry = jok ? ny[j] : 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + wm * 64 + a * 16 + lk + 4 * r;
+                if (i >= n || !jok) continue;
+                double v = -2.0 * acc[a][b][r];
+                v += nx[i];
+                v += ry;
+                v = v > 0 ? v : 0.0;
+                if (euclid) v = sqrt(v);
+                if (zero_diag && i == j) v = 0.0;
+                C[(int64_t)i * ldc + j] = v;
+                mx = fmax(mx, v);
+            }
+    }
+    mx = wave_max(mx);
+    if (lane == 0) red[w] = mx;
+    __syncthreads();
+    if (tid == 0) part[tile] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+}
+
 // clamp >= 0, sqrt (euclidean), zero diagonal; per-block max to part[blockIdx.x]
 __global__ __launch_bounds__(256) void dist_finalize_kernel(double* C, int64_t ldc, int n, int m,
                                                             int euclid, int zero_diag, double* part) {
@@ -1470,9 +1581,16 @@ int otf_cost_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64_t l
         const int tiles_m = (int)((n + otf::DT - 1) / otf::DT), tiles_n = (int)((m + otf::DT - 1) / otf::DT);
         const int ntiles = tiles_m * tiles_n;
         const int vec = (ldx % 4 == 0) && (ldy % 4 == 0) && ((uintptr_t)X % 16 == 0) && ((uintptr_t)Y % 16 == 0);
-        otf::dist_tile_f64_kernel<<<ntiles, 256, 0, s>>>(X, ldx, Y, ldy, (int)n, (int)m, (int)d, nx, ny,
-                                                         metric == OTF_EUCLIDEAN, zero_diag, C, ldc, part,
-                                                         tiles_m, vec);
+        // OTF_DIST_MFMA=0: the VALU tile kernel (A/B; the same sums in another order)
+        const char* ev = getenv("OTF_DIST_MFMA");
+        if (ev && atoi(ev) == 0)
+            otf::dist_tile_f64_kernel<<<ntiles, 256, 0, s>>>(X, ldx, Y, ldy, (int)n, (int)m, (int)d, nx, ny,
+                                                             metric == OTF_EUCLIDEAN, zero_diag, C, ldc, part,
+                                                             tiles_m, vec);
+        else
+            otf::dist_mfma_f64_kernel<<<ntiles, 256, 0, s>>>(X, ldx, Y, ldy, (int)n, (int)m, (int)d, nx, ny,
+                                                             metric == OTF_EUCLIDEAN, zero_diag, C, ldc, part,
+                                                             tiles_m, vec);
         OTF_HIP(hipGetLastError());
         const int64_t tot = n * m;
         int grid = (int)((tot + 255) / 256);
