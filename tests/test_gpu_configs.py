@@ -287,7 +287,7 @@ def test_eot_and_leot_dropins_vs_oracle(orc, dev):
 
 
 @pytest.mark.parametrize("engine,n,dt", [("tiled", 4096, torch.float32), ("mesh", 4096, torch.float32),
-                                         ("gather", 512, torch.float64)])
+                                         ("gather", 512, torch.float64), ("mesh", 1024, torch.float64)])
 def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch, engine, n, dt):
     """A persistent solve launched together with a full-grid persistent solve on another
     stream (the r02 stall scenario: e.g. RCCL kernels holding CUs) cannot always become
@@ -326,7 +326,8 @@ def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch,
     assert (r.plan - ref).abs().max() / ref.abs().max() < 1e-5
 
 
-def test_solo_fallback_when_registration_cannot_complete(dev, monkeypatch):
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+def test_solo_fallback_when_registration_cannot_complete(dev, monkeypatch, dt):
     """Force the fallback: a long gather solve (its XCC team holds 8 CUs for ~0.1 s) on
     one stream, then a mesh solve (a whole grid, one workgroup per CU) on another with a
     1-ms registration window: 8 of its workgroups cannot start, its registration gives
@@ -335,8 +336,8 @@ def test_solo_fallback_when_registration_cannot_complete(dev, monkeypatch):
     from otfuse import ops
     monkeypatch.setenv("OTF_REG_MS", "1")
     g = torch.Generator(device=dev).manual_seed(3)
-    C = torch.rand(4096, 4096, device=dev, generator=g)
-    a = torch.full((4096,), 1.0 / 4096, device=dev)
+    C = torch.rand(4096, 4096, device=dev, generator=g).to(dt)
+    a = torch.full((4096,), 1.0 / 4096, device=dev, dtype=dt)
     Cg = torch.rand(512, 512, device=dev, generator=g, dtype=torch.float64)
     ag = torch.full((512,), 1.0 / 512, device=dev, dtype=torch.float64)
     ref = ops.sinkhorn(a, a, C, 0.1, max_iter=20, stop_thr=0.0, engine="stream").plan
@@ -358,6 +359,7 @@ def test_solo_fallback_when_registration_cannot_complete(dev, monkeypatch):
 
 @pytest.mark.parametrize("engine,n,m,dt,iters", [("tiled", 4096, 4096, torch.float32, 20000),
                                                  ("mesh", 4096, 4096, torch.float32, 40000),
+                                                 ("mesh", 4096, 4096, torch.float64, 12000),
                                                  ("resident", 512, 512, torch.float64, 30000),
                                                  ("gather", 512, 512, torch.float64, 60000),
                                                  ("sweep", 1024, 8192, torch.float32, 20000)])
