@@ -478,7 +478,7 @@ __device__ int blk_sinkhorn_knopp(const double* K, int64_t ldk, int n, int m, co
 constexpr int GW_WLD = GW_SMALLN + 1;
 
 template <class Cfg>
-__device__ void small_sinkhorn_knopp(const double* K, int n, int m, const double* a, const double* b,
+__device__ __attribute__((noinline)) void small_sinkhorn_knopp(const double* K, int n, int m, const double* a, const double* b,
                                      double thr, int maxit, int every, GwShared<Cfg>& sh,
                                      bool& conv, int& iters) {
     static_assert(GW_SMALLN == 64, "16 columns / rows per wave");
