@@ -86,6 +86,8 @@ def parse():
                    help="run warmup + steps only (for rocprofv3 runs); no probes, no JSON")
     p.add_argument("--profile-config5", action="store_true",
                    help="with --profile-only: run the config-5 sweep workload instead")
+    p.add_argument("--profile-f64", action="store_true",
+                   help="with --profile-only: run the float64 metric leg instead")
     p.add_argument("--no-gw", action="store_true", help="skip the per-epoch GW latency leg")
     p.add_argument("--no-f64", action="store_true", help="skip the float64 metric leg")
     p.add_argument("--no-config5", action="store_true",
@@ -118,6 +120,9 @@ def main():
 
     if args.profile_only and args.profile_config5:
         config5_leg(dev, reps=args.steps)
+        return
+    if args.profile_only and args.profile_f64:
+        metric_f64_leg(dev, args.n, args.d, args.iters, args.eps, reps=args.steps)
         return
 
     N, d, iters, eps = args.n, args.d, args.iters, args.eps

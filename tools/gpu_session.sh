@@ -24,6 +24,10 @@ if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run --output-format csv -- python3 bench.py --profile-only --profile-config5 --steps 3 > gpurun_out/rocprof_c5.log 2>&1
   rc=$?; echo "rocprof c5 rc=$rc"; stop_if_fatal $rc rocprof_c5
 fi
+if [ "${PROFILE:-1}" = "1" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_f64 -o run --output-format csv -- python3 bench.py --profile-only --profile-f64 --steps 5 > gpurun_out/rocprof_f64.log 2>&1
+  rc=$?; echo "rocprof f64 rc=$rc"; stop_if_fatal $rc rocprof_f64
+fi
 if [ "${PMC:-0}" = "1" ]; then
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --stats -d gpurun_out/pmc_${ctr}_c5 -o run --output-format csv -- python3 bench.py --profile-only --profile-config5 --steps 2 > gpurun_out/pmc_${ctr}_c5.log 2>&1

@@ -76,6 +76,14 @@ def main():
     if os.path.exists(c5trace):
         d5, n5 = medians(c5trace)
         summary["config5_kernels"] = {k: {"median_us": d5[k] / 1e3, "launches": n5[k]} for k in d5}
+    # float64 metric leg (bench.py --profile-only --profile-f64): cost + float64 mesh
+    summary["f64_kernels"] = {}
+    f64trace = os.path.join(OUT, "prof_f64", "run_kernel_trace.csv")
+    if os.path.exists(f64trace):
+        d6, n6 = medians(f64trace)
+        summary["f64_kernels"] = {k: {"median_us": d6[k] / 1e3, "launches": n6[k]} for k in d6}
+        shutil.copy(os.path.join(OUT, "prof_f64", "run_kernel_stats.csv"),
+                    os.path.join(PROF, f"{tag}_f64_kernel_stats.csv"))
     for ctr, factor in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
         for p in glob.glob(os.path.join(OUT, f"pmc_{ctr}*", "run_counter_collection.csv")):
             med, _ = medians(p, "Counter_Value")
