@@ -829,7 +829,15 @@ __device__ __forceinline__ float epilogue_tile256_16t(const f32x4 (&acc)[4][8], 
 // the row's power-of-two scale 1 / xs (the prep kernel then writes only the norms and
 // scales): the same images as split16_prep2_kernel's, so the same bits, without their
 // 33.7 MB HBM round trip (fp32 operand bytes = hi + lo image bytes).
-template <int NS, typename TC, bool F32IN = false>
+// first column block after which a split piece runs (build switch; 4 pieces)
+#ifndef OTF_COST_ILV_AT
+#define OTF_COST_ILV_AT 3
+#endif
+// ILV (F32IN only, OTF_COST_ILV=1): the next stage's split + LDS writes run in four pieces
+// between the MFMA groups of the current stage (after column blocks 3..6) instead of after
+// all of them, and every stage issues its loads (the last one reloads itself into the idle
+// buffer), so the loop body is one basic block the scheduler can interleave.
+template <int NS, typename TC, bool F32IN = false, bool ILV = false>
 __global__ __launch_bounds__(512) void cost_big16_kernel(
     const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
     const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
@@ -911,6 +919,23 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
         h = __builtin_bit_cast(u4, hv);
         l = __builtin_bit_cast(u4, lv);
     };
+    // one quarter of lstore (F32IN): chunk part >> 1, operand X (part even) or Y
+    auto lstore_part = [&](int buf, int part) {
+        if constexpr (!F32IN) return;
+        const int c = part >> 1;
+        const int chunk = tid + 512 * c;
+        const int row = chunk / GCPR, kc = chunk % GCPR;
+        u4 h, l;
+        if ((part & 1) == 0) {
+            split8(st[c][0], st[c][1], scx[c], h, l);
+            *reinterpret_cast<u4*>(&As[buf][0][g16swz(row, kc)]) = h;
+            *reinterpret_cast<u4*>(&As[buf][1][g16swz(row, kc)]) = l;
+        } else {
+            split8(st[c][NI], st[c][NI + 1], scy[c], h, l);
+            *reinterpret_cast<u4*>(&Bs[buf][0][g16swz(row, kc)]) = h;
+            *reinterpret_cast<u4*>(&Bs[buf][1][g16swz(row, kc)]) = l;
+        }
+    };
     auto lstore = [&](int buf) {
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
@@ -954,12 +979,17 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
     for (int kt = 0; kt < nk; ++kt) {
         if (kt == nk / 2) OTF_CST(4);
         const int buf = kt & 1;
+        if constexpr (ILV) {
+            gload((kt + 1 < nk ? kt + 1 : kt) * GBK);
+            __builtin_amdgcn_sched_barrier(0);  // the next stage's loads go out first
+        } else {
 #if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 4)
         if (false)
 #else
         if (kt + 1 < nk)
 #endif
             gload((kt + 1) * GBK);
+        }
         f16x8 ah[4], al[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -987,13 +1017,18 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
                 acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, ah[mi], acc[mi][nj], 0, 0, 0);
 #endif
             }
+            if constexpr (ILV) {
+                if (nj >= OTF_COST_ILV_AT && nj < OTF_COST_ILV_AT + 4) lstore_part(buf ^ 1, nj - OTF_COST_ILV_AT);
+            }
         }
+        if constexpr (!ILV) {
 #if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 4)
         if (false)
 #else
         if (kt + 1 < nk)
 #endif
             lstore(buf ^ 1);
+        }
         __syncthreads();
     }
 
@@ -1504,6 +1539,12 @@ static bool cost_mfma16_enabled(bool f16out) {
 }
 // OTF_COST_F32IN=0 keeps the fp16 images in the workspace for the 16x16x32 kernel instead of
 // splitting the float32 operands in it (A/B and the bit-identity test; read per call)
+// the F32IN kernel with the next stage's split interleaved into the MFMAs (default; r04:
+// kernel 59.0 -> 56.2 us at the metric shape); OTF_COST_ILV=0 keeps the split after them
+static bool cost_ilv_enabled() {
+    const char* e = getenv("OTF_COST_ILV");
+    return !(e && atoi(e) == 0);
+}
 static bool cost_f32in_enabled() {
     const char* e = getenv("OTF_COST_F32IN");
     return e ? atoi(e) != 0 : true;
@@ -1691,6 +1732,11 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
             otf::cost_ring_kernel<NS, TC><<<(int)nwg, 512, otf::kRingLds, s>>>(                  \
                 Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
                 zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
+        else if (big && mfma16 && f32in && cost_ilv_enabled())                                    \
+            otf::cost_big16_kernel<NS, TC, NS == 3, NS == 3><<<(int)nwg, 512, 0, s>>>(           \
+                (const _Float16*)X, nullptr, xs, xx, (const _Float16*)Y, nullptr, ys, yy, ldx,   \
+                ldy, (int)n, (int)m, (int)d, metric, zero_diag, (TC*)C, ldc, (unsigned int*)cmax, \
+                tiles_n, store_scale);                                                            \
         else if (big && mfma16 && f32in)                                                          \
             otf::cost_big16_kernel<NS, TC, NS == 3><<<(int)nwg, 512, 0, s>>>(                    \
                 (const _Float16*)X, nullptr, xs, xx, (const _Float16*)Y, nullptr, ys, yy, ldx,   \
