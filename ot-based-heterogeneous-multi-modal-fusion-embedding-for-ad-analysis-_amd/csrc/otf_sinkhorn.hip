@@ -2196,14 +2196,20 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     // the mesh engine's region is zeroed by the init kernel (no memset launch)
     // float64: the mesh engine's float64 form on a float64 cost of whole 128 x 512 tiles
     constexpr bool kMesh64 = sizeof(T) == 8 && std::is_same<CT, double>::value;
-    bool mesh_shape_ok = false;
+    bool mesh_shape_ok = false, mesh_auto_ok = true;
     if constexpr (sizeof(T) == 4) mesh_shape_ok = mesh_supported(n, m);
-    else if constexpr (kMesh64) mesh_shape_ok = !sh && mesh64_supported(n, m);
+    else if constexpr (kMesh64) {
+        mesh_shape_ok = !sh && mesh64_supported(n, m);
+        // AUTO keeps the tiled engine while every float64 tile has its own CU (N <= 2048:
+        // 7.36 vs 7.47 us per iteration at 2048^2, a shorter prologue); the float64 mesh
+        // takes the shapes past it (N = 4096: the sweep engine otherwise)
+        mesh_auto_ok = su.w.t_nrb * su.w.t_ncb > device_cu_count();
+    }
     bool mesh_pick = false;
     if constexpr (sizeof(T) == 4 || kMesh64)
         mesh_pick = !LOG && !avg_pass_ms && whole && o.max_iter >= 1 && su.w.mesh_bytes > 0 &&
                     mesh_shape_ok &&
-                    (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled() &&
+                    (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled() && mesh_auto_ok &&
                                                      !(gather_supported<T>(n, m) && su.w.gather_bytes > 0)));
     // gather engine: small problems, one granule hop per iteration, no barrier (and
     // deterministic by construction); its region is zeroed by the init kernel too
@@ -2241,7 +2247,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
                 su.w.mesh_bytes > 0;
     if (o.engine == OTF_ENGINE_MESH && !mfits) return OTF_EUNSUPPORTED;
     if constexpr (kMesh64) {
-        if (mfits && (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled()))) {
+        if (mfits && (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled() && mesh_auto_ok))) {
             const hipError_t e = run_mesh64((const double*)C, ldc, (int)n, (int)m, (const double*)su.w.a_pad,
                                             (const double*)su.w.b_pad, (const double*)cost_scale, o, su.w.mesh,
                                             (double*)u_out, (double*)v_out, P_out, ldp, P_dtype, info, errlog,
