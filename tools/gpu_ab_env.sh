@@ -16,7 +16,7 @@ for rep in $(seq 1 "${REPS:-2}"); do
     if [ "$cfg" != "-" ]; then IFS=',' read -r -a envs <<< "$cfg"; fi
     log=gpurun_out/abenv/run_$k.log
     env "${envs[@]}" timeout -k 10 300 python bench.py $ARGS > "$log" 2>&1 || { echo "rc=$? in $cfg"; exit 1; }
-    echo "$cfg: $(python -c "import json; d=json.loads(open('$log').read().strip().splitlines()[-1]); print(round(d['value']), round(d['ms_per_step'] * 1000, 2), 'us/step', d['breakdown_ms'])")"
+    echo "$cfg: $(python -c "import json; d=json.loads(open('$log').read().strip().splitlines()[-1]); print(round(d['value']), round(d['ms_per_step'] * 1000, 2), 'us/step', d['breakdown_ms'], 'prep', d.get('cost_roofline', {}).get('prep_us'), 'kernel', d.get('cost_roofline', {}).get('kernel_us'))")"
   done
 done
 exit 0
