@@ -1,40 +1,40 @@
 """Benchmark of the Sinkhorn OT fusion hot path (BASELINE.json metric).
 
 Workload (one "step" = one solve): seeded paired MRI/PET embeddings
-X, Y in HBM (N = 4096, d = 512, float32) -> pairwise squared-Euclidean cost on MFMA
-(max-normalised) -> 100 POT-semantics Sinkhorn iterations (eps = 0.1, stopThr = 0,
-so every iteration runs) -> N x N transport plan written to HBM.
+X, Y in HBM (N = 4096, d = 512, float32) -> pairwise squared-Euclidean cost in float64
+(POT euclidean_distances order, the max-normalisation applied inside the solve) -> 100
+POT-semantics Sinkhorn iterations in float64 (eps = 0.1, stopThr = 0, so every iteration
+runs) -> N x N float64 transport plan written to HBM.  float64 is the reference's own
+precision (POT on NumPy float64, MRI_PET_OT_nojax.py:121-143), so the headline is
+like-for-like with the CPU path; parity: tests/test_gpu_precision.py (1e-9 of the oracle).
 
   value            = MRI+PET pairs aligned per second, whole job (N x ranks / step time)
   sinkhorn_iters_per_sec = iterations / time of the Sinkhorn call (incl. plan write)
-  roofline         = the dominant kernel, sk_mesh_kernel (one launch runs all 100
-                     iterations with K = exp(-C/eps) held in registers, so C crosses HBM
-                     once per solve): its bound is LATENCY (per iteration three in-launch
-                     granule hops: row partials within the row block, column partials to
-                     the reducers, sums back), reported as us per iteration against the
-                     VALU floor of the iteration's 2 N^2 FMAs; the algorithmic-byte rate and
-                     the PMC HBM traffic (profiles/kernel_traffic.json, only when it was
-                     measured on this exact library build) are reported beside it
-  cost_roofline    = the split-fp16 MFMA cost kernel vs the dense fp16 MFMA peak (its
-                     three fp16 products per fp32-accurate product are counted)
+  roofline         = the dominant kernel, sk_mesh64_kernel (one launch runs all 100
+                     iterations with the float64 K = exp(-C/eps) held in the register files
+                     and LDS): its bound is LATENCY (per iteration three in-launch granule
+                     hops), reported as us per iteration against the VALU floor of the
+                     iteration's 2 N^2 float64 FMAs; the PMC traffic
+                     (profiles/kernel_traffic.json, only when measured on this exact library
+                     build) beside it
+  cost_roofline    = the float64 cost on v_mfma_f64_16x16x4_f64 vs the float64 matrix peak
+  metric_f32       = the same workload at float32 compute (split-fp16 cost, float32 mesh):
+                     faster, within 1e-4 of the float64 oracle, NOT the reference's precision
   sweep_config5    = BASELINE config 5 on one GPU (N = 8192, d = 1024, fp16 cost, 200
                      iterations): the sweep engine streams the 128 MiB cost from the
                      Infinity Cache once per iteration -> an HBM-class roofline
   hbm_probe        = the sweep engine on an N = 16384 fp32 cost (1 GiB, 4x the Infinity
                      Cache): true-HBM rate per iteration
-  cpu_baseline     = the float64 C/OpenMP restatement (oracle/, POT semantics) on ALL
-                     host cores (nproc), same workload, rank 0 at N = 1 only; also the
-                     1-core run, the cgroup-share run and the NumPy restatement
-                     (reference-equivalent: POT's NumPy loop, BLAS threads = cores)
+  cpu_baseline     = the float64 C/OpenMP restatement (oracle/, POT semantics) on this
+                     process's host CPU share, same workload, rank 0 at N = 1 only; also the
+                     1-core run and the NumPy restatement (reference-equivalent: POT's NumPy
+                     loop); vs_cpu = float64 GPU / float64 CPU
 
 Multi-GPU: one process per GPU (torchrun); every rank solves its own independent
 N = 4096 problem (per-rank minibatch) — "weak" scaling, no collective on the headline
 path; barrier + max-over-ranks timing as the driver requires.  At world > 1 two more
-legs time the north star's sharded path over RCCL (otf_comm_*): config 5 as ONE
-row-sharded solve (all-gather of the PET shards, one all-reduce of m + 1 column sums
-per iteration, whole loop in one C call), and config 3's per-epoch chain (all-gather
-of 32 x d = 2048 embeddings per rank, per-label entropic GW, get_coupling_fot on the
-2048^2 float64 feature cost).
+legs time the north star's sharded path (config 5 as ONE row-sharded solve with the
+column sums exchanged in-kernel over xGMI or by RCCL, and config 3's per-epoch chain).
 """
 import argparse
 import json
@@ -86,10 +86,11 @@ def parse():
                    help="run warmup + steps only (for rocprofv3 runs); no probes, no JSON")
     p.add_argument("--profile-config5", action="store_true",
                    help="with --profile-only: run the config-5 sweep workload instead")
-    p.add_argument("--profile-f64", action="store_true",
-                   help="with --profile-only: run the float64 metric leg instead")
+    p.add_argument("--profile-f32", action="store_true",
+                   help="with --profile-only: run the float32 metric leg instead")
     p.add_argument("--no-gw", action="store_true", help="skip the per-epoch GW latency leg")
-    p.add_argument("--no-f64", action="store_true", help="skip the float64 metric leg")
+    p.add_argument("--no-f32", action="store_true",
+                   help="skip the float32 (split-fp16 cost, float32 solve) leg of the metric config")
     p.add_argument("--no-config5", action="store_true",
                    help="skip the N=8192 d=1024 fp16 200-iteration single-GPU leg")
     p.add_argument("--no-batch-ot", action="store_true",
@@ -115,36 +116,44 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from otfuse import ops
+    from otfuse import gw, ops
     from otfuse.synthetic import paired_embeddings
 
     if args.profile_only and args.profile_config5:
         config5_leg(dev, reps=args.steps)
         return
-    if args.profile_only and args.profile_f64:
-        metric_f64_leg(dev, args.n, args.d, args.iters, args.eps, reps=args.steps)
+    if args.profile_only and args.profile_f32:
+        Xp, Yp, _ = paired_embeddings(args.n, args.d, seed=1234)
+        metric_f32_leg(dev, torch.from_numpy(Xp).to(dev), torch.from_numpy(Yp).to(dev), args.n, args.d,
+                       args.iters, args.eps, args.engine, None, steps=args.steps, warmup=args.warmup,
+                       profile_only=True)
         return
 
     N, d, iters, eps = args.n, args.d, args.iters, args.eps
     X_np, Y_np, _ = paired_embeddings(N, d, seed=1234 + rank)
     X = torch.from_numpy(X_np).to(dev)
     Y = torch.from_numpy(Y_np).to(dev)
-    a = torch.full((N,), 1.0 / N, device=dev)
-    ws = ops.sinkhorn_workspace(N, N, torch.float32, iters, dev)
-    P = torch.empty((N, N), dtype=torch.float32, device=dev)
+    # the headline step in the reference's own precision (POT runs NumPy float64,
+    # MRI_PET_OT_nojax.py:121-143): float64 cost from the float32 embeddings, float64 POT
+    # Sinkhorn, float64 plan
+    a64 = torch.full((N,), 1.0 / N, device=dev, dtype=torch.float64)
+    ws64 = ops.sinkhorn_workspace(N, N, torch.float64, iters, dev)
+    P64 = torch.empty((N, N), dtype=torch.float64, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 
     def step(record):
         if record:
             ev[0].record()
-        C, cmax = ops.pairwise_cost(X, Y)
+        # the max-normalisation (MRI_PET_OT_nojax.py:75) is applied inside the solve through
+        # cost_scale (no separate C /= max pass)
+        C, cmax = gw.pairwise_cost_f64(X, Y, scale_max=False)
         if record:
             ev[1].record()
-        ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, cost_scale=cmax, workspace=ws,
-                     plan_out=P, engine=args.engine)
+        res = ops.sinkhorn(a64, a64, C, eps, max_iter=iters, stop_thr=0.0, cost_scale=cmax,
+                           workspace=ws64, plan_out=P64, engine=args.engine)
         if record:
             ev[2].record()
-        return C, cmax
+        return res
 
     for _ in range(args.warmup):
         step(False)
@@ -174,31 +183,17 @@ def main():
     # step would leave the GPU idle while the host enqueues the next call, and the events
     # would time the host's Python overhead instead of the device
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(6)]
+    res = None
     for k in range(6):
         ev[:] = evs[k]
-        step(True)
+        res = step(True)
     torch.cuda.synchronize()
-    cost_l = [e[0].elapsed_time(e[1]) for e in evs[1:]]
-    sk_l = [e[1].elapsed_time(e[2]) for e in evs[1:]]
-    cost_ms = sorted(cost_l)[2]
-    sk_ms = sorted(sk_l)[2]
-    # the cost op split into its prep (split / norms) and the MFMA kernel (device events
-    # recorded by the library around each, OTF_COST_PHASES)
-    os.environ["OTF_COST_PHASES"] = "1"
-    ph = []
-    for _ in range(5):
-        ops.pairwise_cost(X, Y)
-        ph.append(ops.cost_last_phases())
-    os.environ.pop("OTF_COST_PHASES", None)
-    prep_ms = sorted(p for p, _ in ph)[2]
-    kern_ms = sorted(k for _, k in ph)[2]
-    C, cmax = ops.pairwise_cost(X, Y)
-    res = ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, cost_scale=cmax, workspace=ws,
-                       plan_out=P, engine=args.engine)
-    engine = res.info()["engine_name"]
-    kernel_name = {"resident": "sk_resident_kernel", "tiled": "sk_tiled_kernel",
-                   "sweep": "sk_sweep_kernel", "mesh": "sk_mesh_kernel",
-                   "gather": "sk_gather_kernel"}.get(engine, "sk_pass_kernel")
+    cost_ms = sorted(e[0].elapsed_time(e[1]) for e in evs[1:])[2]
+    sk_ms = sorted(e[1].elapsed_time(e[2]) for e in evs[1:])[2]
+    info = res.info()
+    engine = info["engine_name"]
+    kernel_name = {"mesh": "sk_mesh64_kernel", "sweep": "sk_sweep_kernel", "tiled": "sk_tiled_kernel",
+                   "resident": "sk_resident_kernel"}.get(engine, "sk_pass_kernel")
 
     # PMC traffic: only when profiles/kernel_traffic.json was measured on THIS library
     # build and shape (a stale profile is reported as null, not reused)
@@ -214,39 +209,33 @@ def main():
             return None
         return tj.get("kernels", {}).get(kname, {}).get("hbm_bytes_per_launch")
 
-    iter_bytes = N * N * 4
+    iter_bytes = N * N * 8
     traffic = pmc_traffic(kernel_name)
     sk_s = sk_ms * 1e-3
     us_per_iter = sk_ms * 1e3 / iters
-    # VALU floor of one resident iteration: 2 N^2 FMAs (row sums K v, column sums K^T u)
-    floor_us = 2.0 * N * N / (VALU_F32_PEAK_TFMA * 1e12) * 1e6
+    # VALU floor of one iteration: 2 N^2 float64 FMAs (row sums K v, column sums K^T u) at
+    # the float64 vector peak (78.6 TFLOP/s = 39.3 T FMA/s)
+    floor_us = 2.0 * N * N / (F64_VALU_TFLOPS / 2 * 1e12) * 1e6
     algo_gbs = iter_bytes * iters / sk_s / 1e9
-    if engine in ("resident", "tiled", "mesh", "gather"):
+    if engine in ("mesh", "tiled", "resident"):
         roofline = {"bound": "latency", "kernel": kernel_name, "achieved": us_per_iter,
                     "peak": floor_us, "unit": "us per iteration", "frac": floor_us / us_per_iter,
                     "traffic": traffic,
                     "traffic_GBs": (traffic / sk_s / 1e9) if traffic else None,
-                    "traffic_frac_of_hbm": (traffic / sk_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
                     "algorithmic_bytes_per_launch": iter_bytes * iters,
                     "algorithmic_GBs": algo_gbs,
-                    "note": ("the whole solve is one launch holding K = exp(-C/eps) in registers: C "
-                             "crosses HBM once, so the HBM-equivalent rate (algorithmic_GBs, iters x "
-                             "N*N*4 B / launch time) is not an HBM measurement; per iteration the "
-                             "mesh kernel pays three in-launch granule hops (row partials within the "
-                             "row block, column partials to the reducers, sums back; "
-                             "tools/stamps_resident.hip, DESIGN.md 4) against a VALU floor (peak) of "
-                             "2 N^2 FMAs at 78.6 TFMA/s; the HBM-bound engine is measured in "
-                             "sweep_config5 / hbm_probe")}
+                    "note": ("float64 K = exp(-C/eps) held on chip (register files + LDS) for the "
+                             "whole solve, C read once: per iteration three in-launch granule hops "
+                             "(row partials within the row block, column partials to the reducers, "
+                             "sums back; csrc/otf_mesh64.hip) against a VALU floor (peak) of 2 N^2 "
+                             "float64 FMAs at 39.3 T FMA/s; achieved = the Sinkhorn call's device "
+                             "time / iterations (incl. prologue and the N x N float64 plan write); "
+                             "the HBM-bound engine is measured in sweep_config5 / hbm_probe")}
     else:
         roofline = {"bound": "hbm", "kernel": kernel_name, "achieved": algo_gbs,
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": algo_gbs / HBM_PEAK_GBS,
-                    "traffic": traffic, "algorithmic_bytes_per_launch": iter_bytes * iters}
-    # the C side takes 256 x 256 tiles when they need fewer rounds of resident workgroups
-    # (otf_cost.hip: N = 4096 -> the 16x16x32 form cost_big16_kernel for fp32 storage,
-    # cost_big_kernel with OTF_COST_MFMA16=0)
-    mf16 = os.environ.get("OTF_COST_MFMA16", "1") != "0"
-    cost_kernel = (("cost_big16_kernel" if mf16 else "cost_big_kernel") if N >= 4096
-                   else "cost_split16_kernel")
+                    "traffic": traffic, "algorithmic_bytes_per_launch": iter_bytes * iters,
+                    "note": "N*N*8 B per sweep"}
     cost_flops = 2.0 * N * N * d
     cost_tflops = cost_flops / (cost_ms * 1e-3) / 1e12
 
@@ -263,41 +252,38 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f64",
         "data": "synthetic: seeded paired structured embeddings (SURVEY.md 8d), resident in HBM",
         "config": {"workload": f"sinkhorn_pairwise_N{N}_d{d}_it{iters}", "N": N, "d": d,
-                   "iters": iters, "eps": eps, "cost": "sqeuclidean / max (split-fp16 MFMA, fp32-accurate)",
-                   "sinkhorn": "POT sinkhorn_knopp semantics, stopThr=0",
-                   "plan": "N x N float32 written per step", "global_batch": N * world,
+                   "iters": iters, "eps": eps,
+                   "cost": "sqeuclidean float64 from the float32 embeddings (POT euclidean_distances "
+                           "order), max applied in the solve",
+                   "sinkhorn": "POT sinkhorn_knopp semantics in float64, stopThr=0",
+                   "plan": "N x N float64 written per step", "global_batch": N * world,
                    "parallelism": f"replicas x{world} (independent problems)"},
         "sinkhorn_iters_per_sec": iters / sk_s,
         "engine": engine,
+        "status": info["status_name"],
         "breakdown_ms": {"cost": cost_ms, "sinkhorn_incl_plan": sk_ms},
         "roofline": roofline,
-        "cost_roofline": {"bound": "mfma", "kernel": cost_kernel,
-                          "achieved": 3.0 * cost_flops / (kern_ms * 1e-3) / 1e12,
-                          "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                          "frac": 3.0 * cost_flops / (kern_ms * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS,
-                          "kernel_us": kern_ms * 1e3, "prep_us": prep_ms * 1e3,
-                          "op_us": cost_ms * 1e3,
-                          "op_achieved": 3.0 * cost_tflops,
-                          "fp32_equivalent_TFLOPs": cost_flops / (kern_ms * 1e-3) / 1e12,
-                          "traffic": pmc_traffic(cost_kernel),
-                          "note": "the fp32-accurate product x.y = hi.hi + hi.lo + lo.hi runs as "
-                                  "three fp16 MFMA contractions: achieved = 3 x 2*N*N*d / the MFMA "
-                                  "kernel's device time (kernel_us; prep_us = the split / norms "
-                                  "kernel before it; op_us / op_achieved = the whole host call "
-                                  "incl. launch gaps) vs the dense fp16 MFMA peak"},
+        "cost_roofline": {"bound": "mfma", "kernel": "dist_mfma_f64_kernel",
+                          "achieved": cost_tflops, "peak": F64_VALU_TFLOPS, "unit": "TFLOP/s",
+                          "frac": cost_tflops / F64_VALU_TFLOPS, "op_us": cost_ms * 1e3,
+                          "traffic": pmc_traffic("dist_mfma_f64_kernel"),
+                          "note": "2 N^2 d float64 FLOP on v_mfma_f64_16x16x4_f64 over the whole "
+                                  "host call (norm kernels, tile kernel, max) against the float64 "
+                                  "matrix peak (78.6 TFLOP/s)"},
         "traffic_profile": {"fresh": fresh, "round": tj.get("round"), "lib_md5": lib_md5()},
     }
+    del ws64, P64
+    if rank == 0 and not args.no_f32:
+        out["metric_f32"] = metric_f32_leg(dev, X, Y, N, d, iters, eps, args.engine, pmc_traffic)
     if not args.no_hbm_probe:
         out["hbm_probe"] = hbm_probe(ops, paired_embeddings, args.hbm_probe_n, d, eps, dev)
     if rank == 0 and not args.no_gw:
         out["gw_per_epoch"] = gw_leg(dev, world == 1 and not args.no_cpu_baseline)
     if rank == 0 and not args.no_config5:
         out["sweep_config5"] = config5_leg(dev)
-    if rank == 0 and not args.no_f64:
-        out["metric_f64"] = metric_f64_leg(dev, N, d, iters, eps)
     if rank == 0 and not args.no_batch_ot:
         out["batch_ot_per_step"] = batch_ot_leg(dev, world == 1 and not args.no_cpu_baseline)
     if world > 1 or args.multi_legs:
@@ -430,66 +416,87 @@ def config5_leg(dev, N=8192, d=1024, iters=200, eps=0.1, reps=4):
                                  "plan / (iters + 1); the plan write is timed separately"}}
 
 
-def metric_f64_leg(dev, N=4096, d=512, iters=100, eps=0.1, reps=3):
-    """The metric config in the reference's own precision (POT runs NumPy float64,
-    MRI_PET_OT_nojax.py:143): float64 pairwise cost from the float32 embeddings
-    (otf_cost_pairwise_f64, POT euclidean_distances order, divided by its max) and a
-    float64 POT Sinkhorn, 100 iterations, float64 plan.  AUTO runs the float64 mesh
-    (csrc/otf_mesh64.hip: the 128 MiB K split between the register files and LDS for the
-    whole solve, latency-bound); with the mesh off (OTF_MESH=0) the sweep engine streams K
-    once per iteration, roofline N*N*8 bytes per sweep against HBM.  Parity:
-    tests/test_gpu_precision.py, tests/test_gpu_mesh64.py (1e-9 of the oracle)."""
-    import numpy as np
-    from otfuse import gw, ops
-    from otfuse.synthetic import paired_embeddings
-    X, Y, _ = paired_embeddings(N, d, seed=1234)
-    Xd = torch.from_numpy(X).to(dev)
-    Yd = torch.from_numpy(Y).to(dev)
-    a = torch.full((N,), 1.0 / N, device=dev, dtype=torch.float64)
-    ws = ops.sinkhorn_workspace(N, N, torch.float64, iters, dev)
-    P = torch.empty((N, N), dtype=torch.float64, device=dev)
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    tc, ts = [], []
+def metric_f32_leg(dev, X, Y, N, d, iters, eps, engine, pmc_traffic, steps=20, warmup=3,
+                   profile_only=False):
+    """The metric config at float32 compute (not the reference's precision; reported beside
+    the float64 headline): split-fp16 cost on fp16 MFMA (fp32-accurate: x.y = hi.hi + hi.lo
+    + lo.hi), float32 POT Sinkhorn on the float32 mesh (csrc/otf_mesh.hip), float32 plan.
+    Parity: within 1e-4 of the float64 oracle at eps 0.1 ... 5e-3
+    (tests/test_gpu_precision.py)."""
+    from otfuse import ops
+    a = torch.full((N,), 1.0 / N, device=dev)
+    ws = ops.sinkhorn_workspace(N, N, torch.float32, iters, dev)
+    P = torch.empty((N, N), dtype=torch.float32, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+    def step(record):
+        if record:
+            ev[0].record()
+        C, cmax = ops.pairwise_cost(X, Y)
+        if record:
+            ev[1].record()
+        r = ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, cost_scale=cmax, workspace=ws,
+                         plan_out=P, engine=engine)
+        if record:
+            ev[2].record()
+        return r
+
+    for _ in range(warmup):
+        step(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(False)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if profile_only:
+        return None
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(6)]
     res = None
-    for _ in range(reps):
-        e[0].record()
-        # the max-normalisation (MRI_PET_OT_nojax.py:75) is applied inside the solve through
-        # cost_scale, as in the float32 headline step (no separate C /= max pass)
-        C, cmax = gw.pairwise_cost_f64(Xd, Yd, scale_max=False)
-        e[1].record()
-        res = ops.sinkhorn(a, a, C, eps, max_iter=iters, stop_thr=0.0, workspace=ws, plan_out=P,
-                           cost_scale=cmax)
-        e[2].record()
-        torch.cuda.synchronize()
-        tc.append(e[0].elapsed_time(e[1]))
-        ts.append(e[1].elapsed_time(e[2]))
-        del C
-    k = len(tc) // 2
-    tc, ts = sorted(tc)[k], sorted(ts)[k]
+    for k in range(6):
+        ev[:] = evs[k]
+        res = step(True)
+    torch.cuda.synchronize()
+    cost_ms = sorted(e[0].elapsed_time(e[1]) for e in evs[1:])[2]
+    sk_ms = sorted(e[1].elapsed_time(e[2]) for e in evs[1:])[2]
+    # the cost op split into its prep (norms / scales) and the MFMA kernel (device events
+    # recorded by the library around each, OTF_COST_PHASES)
+    os.environ["OTF_COST_PHASES"] = "1"
+    ph = []
+    for _ in range(5):
+        ops.pairwise_cost(X, Y)
+        ph.append(ops.cost_last_phases())
+    os.environ.pop("OTF_COST_PHASES", None)
+    prep_ms = sorted(p for p, _ in ph)[2]
+    kern_ms = sorted(k for _, k in ph)[2]
     info = res.info()
-    sweep_us = ts * 1e3 / (iters + 1)
-    gbs = N * N * 8 / (sweep_us * 1e-6) / 1e9
-    if info["engine_name"] == "mesh":
-        # K on chip for the whole solve (csrc/otf_mesh64.hip): latency-bound like the
-        # headline mesh; floor = the two N^2 float64 FMA passes per iteration at the
-        # 78.6 TFLOP/s float64 vector peak
-        it_us = ts * 1e3 / iters
-        floor_us = 2.0 * N * N / (F64_VALU_TFLOPS / 2 * 1e12) * 1e6
-        roof = {"bound": "latency", "kernel": "sk_mesh64_kernel", "achieved": it_us, "peak": floor_us,
-                "unit": "us per iteration", "frac": floor_us / it_us, "hbm_equivalent_GBs": gbs,
-                "note": "float64 K = exp(-C/eps) held in the register files (24 of every 32 rows) "
-                        "and LDS (8) for the whole solve, C read once; per iteration three granule "
-                        "hops (row hop, column partials to reducers, sums back) against a VALU floor "
-                        "(peak) of 2 N^2 float64 FMAs"}
-    else:
-        roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": gbs / HBM_PEAK_GBS,
-                "note": "N*N*8 B per sweep (iters + 1 sweeps incl. the plan pass)"}
-    return {"N": N, "d": d, "iters": iters, "eps": eps, "dtype": "f64",
-            "engine": info["engine_name"], "status": info["status_name"],
-            "cost_ms": tc, "sinkhorn_incl_plan_ms": ts, "ms_per_step": tc + ts,
-            "pairs_per_s": N / ((tc + ts) * 1e-3), "sinkhorn_iters_per_s": iters / (ts * 1e-3),
-            "roofline": roof}
+    eng = info["engine_name"]
+    kname = {"mesh": "sk_mesh_kernel", "tiled": "sk_tiled_kernel", "sweep": "sk_sweep_kernel",
+             "resident": "sk_resident_kernel", "gather": "sk_gather_kernel"}.get(eng, "sk_pass_kernel")
+    floor_us = 2.0 * N * N / (VALU_F32_PEAK_TFMA * 1e12) * 1e6
+    it_us = sk_ms * 1e3 / iters
+    traffic = pmc_traffic(kname) if pmc_traffic else None
+    cost_flops = 2.0 * N * N * d
+    ms_per_step = elapsed * 1e3 / steps
+    return {"dtype": "f32", "N": N, "d": d, "iters": iters, "eps": eps, "engine": eng,
+            "status": info["status_name"], "ms_per_step": ms_per_step,
+            "pairs_per_s": N / (ms_per_step * 1e-3), "sinkhorn_iters_per_s": iters / (sk_ms * 1e-3),
+            "breakdown_ms": {"cost": cost_ms, "sinkhorn_incl_plan": sk_ms},
+            "roofline": {"bound": "latency", "kernel": kname, "achieved": it_us, "peak": floor_us,
+                         "unit": "us per iteration", "frac": floor_us / it_us, "traffic": traffic,
+                         "note": "K in registers for the whole solve; VALU floor of 2 N^2 float32 "
+                                 "FMAs at 78.6 T FMA/s"},
+            "cost_roofline": {"bound": "mfma", "kernel": "cost_big16_kernel",
+                              "achieved": 3.0 * cost_flops / (kern_ms * 1e-3) / 1e12,
+                              "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": 3.0 * cost_flops / (kern_ms * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS,
+                              "kernel_us": kern_ms * 1e3, "prep_us": prep_ms * 1e3,
+                              "op_us": cost_ms * 1e3, "traffic": pmc_traffic("cost_big16_kernel") if pmc_traffic else None,
+                              "note": "the fp32-accurate product x.y = hi.hi + hi.lo + lo.hi runs as "
+                                      "three fp16 MFMA contractions: achieved = 3 x 2*N*N*d / the MFMA "
+                                      "kernel's device time vs the dense fp16 MFMA peak"},
+            "note": "float32 compute: within 1e-4 of the float64 oracle (tests/test_gpu_precision.py), "
+                    "not the reference's precision -- the headline is the float64 step"}
 
 
 def gw_leg(dev, with_cpu, labels=2, per_label=64, d=512, eps=5e-3):

@@ -1059,430 +1059,6 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
     }
 }
 
-// 256 x 256 output tile per 512-thread workgroup with the operands staged by LDS-DMA
-// (global_load_lds_dwordx4) into a RING of 4 stages of 16-deep K -- the hi and lo fp16
-// images of both operands, 32 KB a stage, 128 KB the ring: three stages are in flight
-// while one is computed; the waits are counted (vmcnt of the stages issued later) and
-// the barrier is the raw s_barrier, so nothing drains the ring.  cost_big_kernel stages
-// one 32-deep stage through registers (one stage in flight, an LDS write pass and a
-// full drain per barrier): 0.30 of the fp16 MFMA peak at the metric shape.
-// LDS image of an operand for one stage: 256 rows x 32 B with the two 16-B chunks of a
-// row swapped when row bit 3 is set, so the 16 lanes of every ds_read_b128 phase (rows
-// r and r + 8 alike) hit 16 distinct bank groups.  The DMA writes lane-linear (lane L:
-// row L / 2, slot L % 2 of its wave's 32 rows), so the swap is applied to each lane's
-// SOURCE chunk (cdna_hip_programming.md §5.4 rule 21).  Wave w issues the DMA of rows
-// [32 w, 32 w + 32) of each image; the fragments are read with the same swap.
-constexpr int RBK = 16, RSLOTS = 4;
-__device__ __forceinline__ int rswz(int row, int chunk) { return row * 32 + ((chunk ^ ((row >> 3) & 1)) << 4); }
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
-
-template <int N> __device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int NS, typename TC>
-__global__ __launch_bounds__(512) void cost_ring_kernel(
-    const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
-    const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
-    const float* __restrict__ ys, const float* __restrict__ yy, int64_t ldxh, int64_t ldyh, int n, int m, int kpad,
-    int metric, int zero_diag, TC* __restrict__ C, int64_t ldc, unsigned int* cmax, int tiles_n,
-    const float* __restrict__ store_scale) {
-    constexpr int NI = NS == 3 ? 2 : 1;           // fp16 images per operand
-    constexpr int IMG = GBM * RBK * 2;            // 8 KB: one image of one stage
-    constexpr int STAGE = 2 * NI * IMG;
-    constexpr int PER = 2 * NI;                   // DMA instructions per wave per stage
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* sxs = reinterpret_cast<float*>(smem + RSLOTS * STAGE);
-    float* sxx = sxs + GBM;
-    float* wmx = sxx + GBM;
-
-    OTF_CST(0);
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-    int tm, tn;
-    grouped_tile(wg, nwg, tiles_n, tm, tn);
-    const int i0 = tm * GBM, j0 = tn * GBN;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
-
-    // this lane's DMA sources: row 32 wid + lane / 2 of each image, the chunk stored at
-    // slot lane % 2 (swapped on row bit 3); clamped rows past n / m are never stored
-    const int drow = 32 * wid + (lane >> 1);
-    const int dchk = (lane & 1) ^ ((drow >> 3) & 1);
-    const int gi = i0 + drow < n ? i0 + drow : n - 1;
-    const int gj = j0 + drow < m ? j0 + drow : m - 1;
-    const _Float16* pa[NI];
-    const _Float16* pb[NI];
-    pa[0] = Xh + (int64_t)gi * ldxh + dchk * 8;
-    pb[0] = Yh + (int64_t)gj * ldyh + dchk * 8;
-    if constexpr (NI == 2) {
-        pa[NI - 1] = Xl + (int64_t)gi * ldxh + dchk * 8;
-        pb[NI - 1] = Yl + (int64_t)gj * ldyh + dchk * 8;
-    }
-    auto issue = [&](int st) {
-        char* slot = smem + (st % RSLOTS) * STAGE + wid * 1024;
-        const int k0 = st * RBK;
-#pragma unroll
-        for (int h = 0; h < NI; ++h) {
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)(pa[h] + k0), (lds_void_t*)(slot + h * IMG), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)(pb[h] + k0), (lds_void_t*)(slot + (NI + h) * IMG), 16, 0, 0);
-        }
-    };
-
-    // norms first: ordinary loads, none inside the ring loop (hipcc waits vmcnt(0) at the
-    // use of an ordinary load while a DMA is in flight)
-    if (tid < GBM) {
-        const int g = i0 + tid < n ? i0 + tid : n - 1;
-        sxs[tid] = xs[g];
-        sxx[tid] = xx[g];
-    }
-    float cys[4], cyy[4];
-#pragma unroll
-    for (int nj = 0; nj < 4; ++nj) {
-        const int gj0 = j0 + wn * 128 + nj * 32 + (lane & 31);
-        const int g = gj0 < m ? gj0 : m - 1;
-        cys[nj] = ys[g];
-        cyy[nj] = yy[g];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    OTF_CST(1);
-
-    f32x16 acc[2][4];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-
-    const int nk = kpad / RBK;
-#pragma unroll
-    for (int st = 0; st < RSLOTS - 1; ++st)
-        if (st < nk) issue(st);
-    const int fch = lane >> 5;
-    for (int kt = 0; kt < nk; ++kt) {
-        // stage kt has landed once only the stages issued after it are outstanding
-        const int later = nk - 1 - kt < RSLOTS - 2 ? nk - 1 - kt : RSLOTS - 2;
-        if (later >= 2) wait_vm<2 * PER>();
-        else if (later == 1) wait_vm<PER>();
-        else wait_vm<0>();
-        // every wave's DMA of stage kt has landed; every wave is done reading stage kt - 1,
-        // whose slot the next issue refills
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 4)
-        // diagnostic: no DMA after the prologue (the loop re-reads stale slots)
-#else
-        if (kt + RSLOTS - 1 < nk) issue(kt + RSLOTS - 1);
-#endif
-        if (kt == nk / 2) OTF_CST(4);
-        const char* sl = smem + (kt % RSLOTS) * STAGE;
-        f16x8 ah[2], al[2], bh[4], bl[4];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int ar = wm * 64 + t * 32 + (lane & 31);
-            ah[t] = *reinterpret_cast<const f16x8*>(sl + rswz(ar, fch));
-            if (NI == 2) al[t] = *reinterpret_cast<const f16x8*>(sl + IMG + rswz(ar, fch));
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int br = wn * 128 + t * 32 + (lane & 31);
-            bh[t] = *reinterpret_cast<const f16x8*>(sl + NI * IMG + rswz(br, fch));
-            if (NI == 2) bl[t] = *reinterpret_cast<const f16x8*>(sl + (NI + 1) * IMG + rswz(br, fch));
-        }
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int nj = 0; nj < 4; ++nj) {
-#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 2)
-                // diagnostic: no MFMAs (the fragments still feed one add each)
-                acc[mi][nj][0] += (float)ah[mi][0] + (float)bh[nj][0] + (NI == 2 ? (float)al[mi][0] + (float)bl[nj][0] : 0.f);
-#else
-                if (NS == 3) {
-                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mi], bh[nj], acc[mi][nj], 0, 0, 0);
-                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bl[nj], acc[mi][nj], 0, 0, 0);
-                }
-                acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mi], bh[nj], acc[mi][nj], 0, 0, 0);
-#endif
-            }
-    }
-
-    OTF_CST(2);
-    const float os = store_scale ? store_scale[0] : 1.0f;
-    float lmax = epilogue_tile256<TC>(acc, sxs, sxx, cys, cyy, wm, wn, lane, i0, j0, n, m, metric, zero_diag, C,
-                                      ldc, os);
-    OTF_CST(3);
-    if (cmax) {
-        lmax = wave_max(lmax);
-        if (lane == 0) wmx[wid] = lmax;
-        __syncthreads();
-        if (tid == 0) {
-            float v = wmx[0];
-#pragma unroll
-            for (int w = 1; w < 8; ++w) v = fmaxf(v, wmx[w]);
-            const unsigned int u = __float_as_uint(v);
-            if (u > __hip_atomic_load(cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(cmax, u);
-        }
-    }
-}
-constexpr size_t kRingLds = (size_t)RSLOTS * 2 * 2 * (GBM * RBK * 2) + (2 * GBM + 8) * sizeof(float);
-
-// Warp-specialised persistent kernel (OTF_COST_WS): 768 threads = 8 MATH waves (a
-// 64 x 64 output block each: 2 x 2 v_mfma_f32_32x32x16_f16 accumulators) + 4 LOADER
-// waves that only move operands, HBM/L2 -> LDS by global_load_lds_dwordx4, into a
-// 4-slot ring of 16-deep K stages (hi and lo fp16 images of a 256-row X panel and a
-// 128-row Y panel: 24 KB a stage).  Each workgroup walks a contiguous run of 256 x 128
-// output tiles (the same X panel, neighbouring Y panels: the panel stays in L2) as one
-// stream of stages g = tile * nk + k: the loaders run three stages ahead across tile
-// boundaries, so the next tile's operands are in flight while the math waves store the
-// finished tile -- stores only count in the math waves' vmcnt, which nothing waits on,
-// so a tile's epilogue overlaps the next tile's MFMAs.  Per stage both roles meet at one
-// s_barrier: the loaders have waited for stage g + 1 (their own vmcnt) and refill the
-// slot of stage g - 1 after it; the math waves read stage g + 1's fragments into the
-// second register set while the MFMAs of stage g run (software pipeline, unrolled by
-// two in effect through the set index).  Norms of all of the workgroup's tiles are
-// staged in LDS before the ring starts (no ordinary load inside the loop).
-constexpr int WS_BM = 256, WS_BN = 128, WS_MAXT = 16;
-constexpr int WS_NT = 768;
-
-template <int NS, typename TC>
-__global__ __launch_bounds__(768) void cost_ws_kernel(
-    const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
-    const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
-    const float* __restrict__ ys, const float* __restrict__ yy, int64_t ldxh, int64_t ldyh, int n, int m, int kpad,
-    int metric, int zero_diag, TC* __restrict__ C, int64_t ldc, unsigned int* cmax, int tiles_n, int ntiles,
-    int tpw, const float* __restrict__ store_scale) {
-    constexpr int NI = NS == 3 ? 2 : 1;
-    constexpr int AIMG = WS_BM * RBK * 2;             // 8 KB
-    constexpr int BIMG = WS_BN * RBK * 2;             // 4 KB
-    constexpr int STAGE = NI * (AIMG + BIMG);
-    constexpr int PER = 3 * NI;                       // DMA instructions per loader wave per stage
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* nrm = reinterpret_cast<float*>(smem + RSLOTS * STAGE);  // per tile: xs, xx | ys, yy
-    float* wmx = nrm + WS_MAXT * (2 * WS_BM + 2 * WS_BN);
-
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-    const int lw = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-    const int t0 = lw * tpw;
-    const int nt = ntiles - t0 < tpw ? (ntiles - t0 > 0 ? ntiles - t0 : 0) : tpw;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int nk = kpad / RBK;
-    const int NG = nt * nk;
-
-    // ---- norms of every tile of this workgroup (ordinary loads, before the ring)
-    for (int q = tid; q < nt * (WS_BM + WS_BN); q += WS_NT) {
-        const int j = q / (WS_BM + WS_BN), r = q % (WS_BM + WS_BN);
-        const int tile = t0 + j, tm = tile / tiles_n, tn = tile % tiles_n;
-        float* nb = nrm + j * (2 * WS_BM + 2 * WS_BN);
-        if (r < WS_BM) {
-            const int g = tm * WS_BM + r < n ? tm * WS_BM + r : n - 1;
-            nb[r] = xs[g];
-            nb[WS_BM + r] = xx[g];
-        } else {
-            const int c = r - WS_BM;
-            const int g = tn * WS_BN + c < m ? tn * WS_BN + c : m - 1;
-            nb[2 * WS_BM + c] = ys[g];
-            nb[2 * WS_BM + WS_BN + c] = yy[g];
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    float lmax = 0.f;
-    if (wid >= 8) {
-        // ================= loader waves
-        const int lv = wid - 8;
-        auto issue = [&](int g) {
-            const int j = g / nk, kt = g - j * nk;
-            const int tile = t0 + j, tm = tile / tiles_n, tn = tile % tiles_n;
-            char* slot = smem + (g % RSLOTS) * STAGE;
-            const int k0 = kt * RBK;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int r = 64 * lv + 32 * h + (lane >> 1);
-                const int ch = (lane & 1) ^ ((r >> 3) & 1);
-                const int gi = tm * WS_BM + r < n ? tm * WS_BM + r : n - 1;
-                const int64_t o = (int64_t)gi * ldxh + ch * 8 + k0;
-                char* dst = slot + (2 * lv + h) * 1024;
-                __builtin_amdgcn_global_load_lds((gbl_void_t*)(Xh + o), (lds_void_t*)dst, 16, 0, 0);
-                if constexpr (NI == 2)
-                    __builtin_amdgcn_global_load_lds((gbl_void_t*)(Xl + o), (lds_void_t*)(dst + AIMG), 16, 0, 0);
-            }
-            {
-                const int r = 32 * lv + (lane >> 1);
-                const int ch = (lane & 1) ^ ((r >> 3) & 1);
-                const int gj = tn * WS_BN + r < m ? tn * WS_BN + r : m - 1;
-                const int64_t o = (int64_t)gj * ldyh + ch * 8 + k0;
-                char* dst = slot + NI * AIMG + lv * 1024;
-                __builtin_amdgcn_global_load_lds((gbl_void_t*)(Yh + o), (lds_void_t*)dst, 16, 0, 0);
-                if constexpr (NI == 2)
-                    __builtin_amdgcn_global_load_lds((gbl_void_t*)(Yl + o), (lds_void_t*)(dst + BIMG), 16, 0, 0);
-            }
-        };
-#pragma unroll
-        for (int g = 0; g < RSLOTS; ++g)
-            if (g < NG) issue(g);
-        for (int g = -1; g < NG; ++g) {
-            // stage g + 1 complete: only the stages issued after it may be outstanding
-            const int last = NG - 1 < g + 3 ? NG - 1 : g + 3;  // highest stage issued so far
-            const int after = last - (g + 1);
-            if (g + 1 < NG) {
-                if (after >= 2) wait_vm<2 * PER>();
-                else if (after == 1) wait_vm<PER>();
-                else wait_vm<0>();
-            }
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            // every math wave consumed stage g (its fragments are in registers): refill
-            if (g >= 0 && g + RSLOTS < NG) issue(g + RSLOTS);
-        }
-    } else {
-        // ================= math waves
-        const int wm = wid >> 1, wn = wid & 1;   // 4 x 2 waves of 64 x 64
-        const int fch = lane >> 5;
-        const float os = store_scale ? store_scale[0] : 1.0f;
-#if defined(OTF_COST_WS_PIPE)
-        f16x8 fa[2][2][2], fb[2][2][2];          // [set][t][hi / lo]
-#else
-        f16x8 fa[1][2][2], fb[1][2][2];
-#endif
-        f32x16 acc[2][2];
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-        auto read_frags = [&](int g, int set) {
-            const char* sl = smem + (g % RSLOTS) * STAGE;
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int ar = wm * 64 + t * 32 + (lane & 31);
-                const int br = wn * 64 + t * 32 + (lane & 31);
-                fa[set][t][0] = *reinterpret_cast<const f16x8*>(sl + rswz(ar, fch));
-                fb[set][t][0] = *reinterpret_cast<const f16x8*>(sl + NI * AIMG + rswz(br, fch));
-                if constexpr (NI == 2) {
-                    fa[set][t][1] = *reinterpret_cast<const f16x8*>(sl + AIMG + rswz(ar, fch));
-                    fb[set][t][1] = *reinterpret_cast<const f16x8*>(sl + NI * AIMG + BIMG + rswz(br, fch));
-                }
-            }
-        };
-        auto mfmas = [&](int set) {
-#pragma unroll
-            for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-                for (int nj = 0; nj < 2; ++nj) {
-                    if constexpr (NS == 3) {
-                        acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[set][mi][1], fb[set][nj][0], acc[mi][nj], 0, 0, 0);
-                        acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[set][mi][0], fb[set][nj][1], acc[mi][nj], 0, 0, 0);
-                    }
-                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[set][mi][0], fb[set][nj][0], acc[mi][nj], 0, 0, 0);
-                }
-        };
-        // one tile's cost values: 32-bit offsets from the tile's corner, a bounds-free
-        // path for whole tiles; the accumulators are cleared for the next tile
-        auto epilogue = [&](int j) {
-            const int tile = t0 + j, tm = tile / tiles_n, tn = tile % tiles_n;
-            const int i0 = tm * WS_BM, j0 = tn * WS_BN;
-            const float* nb = nrm + j * (2 * WS_BM + 2 * WS_BN);
-            // stores through one buffer descriptor at the tile's corner: 32-bit offsets, no
-            // 64-bit address per element
-            const __amdgpu_buffer_rsrc_t ct = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(C + (int64_t)i0 * ldc + j0), 0, 0x7fffffff, 0x00020000);
-            const bool whole = i0 + WS_BM <= n && j0 + WS_BN <= m && !zero_diag;
-            const int r0 = wm * 64 + 4 * (lane >> 5);
-#pragma unroll
-            for (int nj = 0; nj < 2; ++nj) {
-                const int cl = wn * 64 + nj * 32 + (lane & 31);
-                const float cy = nb[2 * WS_BM + cl], cyy = nb[2 * WS_BM + WS_BN + cl];
-#pragma unroll
-                for (int mi = 0; mi < 2; ++mi) {
-                    // one 32 x 32 block at a time (keeps the scheduler from hoisting all
-                    // 64 results' loads and addresses at once); the lane's offset is one
-                    // VGPR (opaque, so it is not hoisted out of the stage loop), the row
-                    // step of element e a scalar offset
-                    __builtin_amdgcn_sched_barrier(0);
-                    uint32_t vb = (uint32_t)((r0 + mi * 32) * (int)ldc + cl) * (uint32_t)sizeof(TC);
-                    asm volatile("" : "+v"(vb));
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) {
-                        const int rl = r0 + mi * 32 + (e & 3) + 8 * (e >> 2);
-                        const float dot = acc[mi][nj][e] * nb[rl] * cy;
-                        float c = nb[WS_BM + rl] + cyy - 2.f * dot;
-                        c = c > 0.f ? c : 0.f;
-                        if (metric == OTF_EUCLIDEAN) c = sqrtf(c);
-                        acc[mi][nj][e] = 0.f;
-                        if (!whole) {
-                            if (i0 + rl >= n || j0 + cl >= m) continue;
-                            if (zero_diag && i0 + rl == j0 + cl) c = 0.f;
-                        }
-                        const TC cs = (TC)(c * os);
-                        const uint32_t so = (uint32_t)(((e & 3) + 8 * (e >> 2)) * (int)ldc) * (uint32_t)sizeof(TC);
-#if defined(OTF_COST_ABLATE) && (OTF_COST_ABLATE & 1)
-                        if (c == -12345.f)  // diagnostic (tools/ubench_cost.hip): no cost stores
-#endif
-                        {
-                            if constexpr (sizeof(TC) == 4)
-                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, (float)cs), ct, vb, so, 0);
-                            else
-                                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, cs), ct, vb, so, 0);
-                        }
-                        lmax = fmaxf(lmax, (float)cs);
-                    }
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        // one fragment set (two math waves per SIMD hide each other's LDS reads): after
-        // the barrier of stage g, read stage g's fragments, run its MFMAs
-#if defined(OTF_COST_WS_PIPE)
-        // (diagnostic) software-pipelined form: stage g + 1's reads fly under stage g's MFMAs
-        __builtin_amdgcn_s_barrier();                  // g = -1
-        asm volatile("" ::: "memory");
-        if (0 < NG) read_frags(0, 0);
-        for (int g = 0; g < NG; g += 2) {
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            if (g + 1 < NG) read_frags(g + 1, 1);
-            mfmas(0);
-            if ((g + 1) % nk == 0) epilogue(g / nk);
-            if (g + 1 >= NG) break;
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            if (g + 2 < NG) read_frags(g + 2, 0);
-            mfmas(1);
-            if ((g + 2) % nk == 0) epilogue((g + 1) / nk);
-        }
-#else
-        __builtin_amdgcn_s_barrier();                  // g = -1: stage 0 is visible
-        asm volatile("" ::: "memory");
-        for (int g = 0; g < NG; ++g) {
-            read_frags(g, 0);
-            mfmas(0);
-            __builtin_amdgcn_s_barrier();              // stage g + 1 visible, stage g consumed
-            asm volatile("" ::: "memory");
-            if ((g + 1) % nk == 0) epilogue(g / nk);
-        }
-#endif
-    }
-    if (cmax) {
-        lmax = wave_max(lmax);
-        if (lane == 0) wmx[wid] = lmax;
-        __syncthreads();
-        if (tid == 0) {
-            float v = wmx[0];
-#pragma unroll
-            for (int w = 1; w < 8; ++w) v = fmaxf(v, wmx[w]);
-            const unsigned int u = __float_as_uint(v);
-            if (u > __hip_atomic_load(cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(cmax, u);
-        }
-    }
-}
-constexpr size_t kWsLds = (size_t)RSLOTS * 2 * (WS_BM + WS_BN) * RBK * 2 +
-                          ((size_t)WS_MAXT * (2 * WS_BM + 2 * WS_BN) + 16) * sizeof(float);
 
 }  // namespace
 }  // namespace otf
@@ -1513,74 +1089,15 @@ int otf_cost_pairwise(const float* X, int64_t ldx, const float* Y, int64_t ldy, 
 
 static size_t otf_al(size_t x) { return (x + 255) / 256 * 256; }
 
-// OTF_COST_BIG=0 keeps the 128 x 128 tile for every shape (A/B measurements)
-static bool cost_big_enabled() {
-    static int env = -1;
-    if (env < 0) {
-        const char* e = getenv("OTF_COST_BIG");
-        env = e ? atoi(e) : 1;
-    }
-    return env != 0;
-}
-
-// OTF_COST_RING=1 selects the LDS-DMA ring kernel (A/B against the register-staged one)
-// (read per call: a test switches it in-process)
-static bool cost_ring_enabled() {
-    const char* e = getenv("OTF_COST_RING");
-    return e ? atoi(e) != 0 : false;
-}
 // The 16x16x32 form of the 256 x 256 kernel for float32 cost storage (metric shape: 52
 // vs 56 us, r03 stamps); the fp16-storage config-5 cost keeps the 32x32x16 form (its
-// 8-B transposed stores measured no faster).  OTF_COST_MFMA16=0 / 1 forces either form
-// (read per call).
-static bool cost_mfma16_enabled(bool f16out) {
-    const char* e = getenv("OTF_COST_MFMA16");
-    return e ? atoi(e) != 0 : !f16out;
-}
-// OTF_COST_F32IN=0 keeps the fp16 images in the workspace for the 16x16x32 kernel instead of
-// splitting the float32 operands in it (A/B and the bit-identity test; read per call)
-// the F32IN kernel with the next stage's split interleaved into the MFMAs (default; r04:
-// kernel 59.0 -> 56.2 us at the metric shape); OTF_COST_ILV=0 keeps the split after them
-static bool cost_ilv_enabled() {
-    const char* e = getenv("OTF_COST_ILV");
-    return !(e && atoi(e) == 0);
-}
-static bool cost_f32in_enabled() {
-    const char* e = getenv("OTF_COST_F32IN");
-    return e ? atoi(e) != 0 : true;
-}
-// OTF_COST_WS=1 selects the warp-specialised persistent kernel (read per call)
-static bool cost_ws_enabled() {
-    const char* e = getenv("OTF_COST_WS");
-    return e ? atoi(e) != 0 : false;
-}
-static bool ws_lds_ok() {
-    static int ok = -1;
-    if (ok < 0) {
-        ok = 1;
-        if (hipFuncSetAttribute((const void*)otf::cost_ws_kernel<3, float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kWsLds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)otf::cost_ws_kernel<3, _Float16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kWsLds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)otf::cost_ws_kernel<1, float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kWsLds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)otf::cost_ws_kernel<1, _Float16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kWsLds) != hipSuccess)
-            ok = 0;
-        (void)hipGetLastError();
-    }
-    return ok != 0;
-}
-// the ring kernel asks for 130 KB of dynamic LDS: raise the launch limit once
-static bool ring_lds_ok() {
-    static int ok = -1;
-    if (ok < 0) {
-        ok = 1;
-        if (hipFuncSetAttribute((const void*)otf::cost_ring_kernel<3, float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kRingLds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)otf::cost_ring_kernel<3, _Float16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kRingLds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)otf::cost_ring_kernel<1, float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kRingLds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)otf::cost_ring_kernel<1, _Float16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)otf::kRingLds) != hipSuccess)
-            ok = 0;
-        (void)hipGetLastError();
-    }
-    return ok != 0;
-}
+// 8-B transposed stores measured no faster).  Float32 operands are split into hi / lo fp16
+// inside the 16x16x32 kernel (F32IN, the next stage's split interleaved between the MFMA
+// groups: r04 kernel 59.0 -> 56.2 us) where the rows are whole 16-B aligned stages; other
+// float32 rows go through the prep's fp16 images (the same bits, tests/test_gpu_parity.py).
+// Measured and removed in r05 (numbers in DESIGN.md 4.2): the LDS-DMA ring and the
+// warp-specialised persistent kernels, the 128 x 128 tile at every shape, the split after
+// the MFMA groups.
 
 size_t otf_cost_ex_workspace_size(int64_t n, int64_t m, int64_t d, int32_t in_dtype) {
     const size_t ldh = (size_t)((d + otf::SBK - 1) / otf::SBK * otf::SBK);
@@ -1660,9 +1177,9 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     const int64_t cus0 = otf::device_cu_count();
     const int64_t big_rounds = (((n + otf::GBM - 1) / otf::GBM) * ((m + otf::GBN - 1) / otf::GBN) + cus0 - 1) / cus0;
     const int64_t small_rounds = (((n + otf::BM - 1) / otf::BM) * ((m + otf::BN - 1) / otf::BN) + 2 * cus0 - 1) / (2 * cus0);
-    const bool big0 = 18 * big_rounds < 10 * small_rounds && cost_big_enabled();
-    const bool f32in = split && big0 && cost_mfma16_enabled(c_dtype == OTF_F16) && cost_f32in_enabled() &&
-                       !cost_ring_enabled() && !cost_ws_enabled() && d % otf::SBK == 0 && ldx % 4 == 0 &&
+    const bool big0 = 18 * big_rounds < 10 * small_rounds;
+    const bool mfma16 = !f16out;
+    const bool f32in = split && big0 && mfma16 && d % otf::SBK == 0 && ldx % 4 == 0 &&
                        ldy % 4 == 0 && (uintptr_t)X % 16 == 0 && (uintptr_t)Y % 16 == 0;
     {
         const int rows = (int)n + (same ? 0 : (int)m);
@@ -1706,39 +1223,16 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
         store_scale = small + 2;
     }
     // cmax = 0 and c_unit = 1 (fp32 storage) were written by the prep kernel
-    const int64_t cus = cus0;
     const bool big = big0;
-    const bool ring = cost_ring_enabled() && ring_lds_ok();
-    const bool mfma16 = cost_mfma16_enabled(f16out);
     const int BMx = big ? otf::GBM : otf::BM, BNx = big ? otf::GBN : otf::BN;
     const int tiles_m = (int)((n + BMx - 1) / BMx);
     const int tiles_n = (int)((m + BNx - 1) / BNx);
     const int64_t nwg = (int64_t)tiles_m * tiles_n;
     if (nwg > INT32_MAX) return OTF_EUNSUPPORTED;
-    // warp-specialised persistent kernel: 256 x 128 tiles, a contiguous run per workgroup
-    const int64_t ws_tiles = ((n + otf::WS_BM - 1) / otf::WS_BM) * ((m + otf::WS_BN - 1) / otf::WS_BN);
-    const int ws_tn = (int)((m + otf::WS_BN - 1) / otf::WS_BN);
-    const int64_t ws_tpw = (ws_tiles + cus - 1) / cus;
-    const bool wsk = cost_ws_enabled() && ws_tpw <= otf::WS_MAXT && ws_lds_ok();
-    const int ws_grid = (int)((ws_tiles + ws_tpw - 1) / (ws_tpw > 0 ? ws_tpw : 1));
 #define OTF_COST_LAUNCH(NS, TC)                                                                   \
     do {                                                                                          \
-        if (wsk)                                                                                  \
-            otf::cost_ws_kernel<NS, TC><<<ws_grid, otf::WS_NT, otf::kWsLds, s>>>(                \
-                Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
-                zero_diag, (TC*)C, ldc, (unsigned int*)cmax, ws_tn, (int)ws_tiles, (int)ws_tpw,  \
-                store_scale);                                                                     \
-        else if (big && ring)                                                                     \
-            otf::cost_ring_kernel<NS, TC><<<(int)nwg, 512, otf::kRingLds, s>>>(                  \
-                Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
-                zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
-        else if (big && mfma16 && f32in && cost_ilv_enabled())                                    \
+        if (big && mfma16 && f32in)                                                               \
             otf::cost_big16_kernel<NS, TC, NS == 3, NS == 3><<<(int)nwg, 512, 0, s>>>(           \
-                (const _Float16*)X, nullptr, xs, xx, (const _Float16*)Y, nullptr, ys, yy, ldx,   \
-                ldy, (int)n, (int)m, (int)d, metric, zero_diag, (TC*)C, ldc, (unsigned int*)cmax, \
-                tiles_n, store_scale);                                                            \
-        else if (big && mfma16 && f32in)                                                          \
-            otf::cost_big16_kernel<NS, TC, NS == 3><<<(int)nwg, 512, 0, s>>>(                    \
                 (const _Float16*)X, nullptr, xs, xx, (const _Float16*)Y, nullptr, ys, yy, ldx,   \
                 ldy, (int)n, (int)m, (int)d, metric, zero_diag, (TC*)C, ldc, (unsigned int*)cmax, \
                 tiles_n, store_scale);                                                            \

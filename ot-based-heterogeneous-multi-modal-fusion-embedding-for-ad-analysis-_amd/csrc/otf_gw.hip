@@ -1254,131 +1254,17 @@ __global__ __launch_bounds__(512) void dot_cost_f64_kernel(const float* X, int64
 }
 
 // Larger outputs (the float64 metric leg: 4096 x 4096 x 512): 128 x 128 tiles of C per
-// 256-thread workgroup, 8 x 8 outputs per thread in float64 registers, the float32 rows
-// widened to float64 on the way into LDS (k-major, 16 deep, double-buffered through
-// registers), and the epilogue of dist_finalize_kernel fused: v = -2 acc + |x|^2 + |y|^2
-// (POT euclidean_distances order), clamp >= 0, sqrt (euclidean), zero diagonal, stored
-// once; the tile's max goes to part[tile].  (The generic 64 x 64 GEMM + a finalize pass
-// over C took ~0.7 ms at the metric shape.)
+// 256-thread workgroup on v_mfma_f64_16x16x4_f64 (one MFMA replaces 16 vector FMAs and
+// their operand reads): 4 waves, each a 64 x 64 quarter as 4 x 4 blocks of 16 x 16; the
+// float32 rows widened to float64 on the way into LDS (k-major, 16 deep, double-buffered
+// through registers); per 4-deep k-step a lane reads one double of each of its 4 row
+// blocks and 4 column blocks from the LDS stage (16 consecutive doubles per lane group:
+// conflict-free).  The epilogue of dist_finalize_kernel is fused: v = -2 acc + |x|^2 +
+// |y|^2 (POT euclidean_distances order), clamp >= 0, sqrt (euclidean), zero diagonal,
+// stored once; the tile's max goes to part[tile].  Result lanes: column l & 15, rows
+// (l >> 4) + 4 r.  (The generic 64 x 64 GEMM + a finalize pass over C took ~0.7 ms at the
+// metric shape, the VALU form of this tile 0.45 ms -- removed in r05 -- this one 0.32 ms.)
 constexpr int DT = 128, DK = 16;
-__global__ __launch_bounds__(256, 2) void dist_tile_f64_kernel(const float* __restrict__ X, int64_t ldx,
-                                                               const float* __restrict__ Y, int64_t ldy,
-                                                               int n, int m, int d, const double* nx,
-                                                               const double* ny, int euclid, int zero_diag,
-                                                               double* C, int64_t ldc, double* part, int tiles_m,
-                                                               int vec) {
-    __shared__ __attribute__((aligned(16))) double As[2][DK][DT];
-    __shared__ __attribute__((aligned(16))) double Bs[2][DK][DT];
-    __shared__ double red[4];
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    const int tile = blockIdx.x;
-    const int i0 = (tile % tiles_m) * DT, j0 = (tile / tiles_m) * DT;
-    // staging: thread t loads row (t >> 1) of the tile, k half (t & 1) * 8 .. + 8 of the stage
-    const int lr = tid >> 1, lk = (tid & 1) * 8;
-    const int gi = i0 + lr < n ? i0 + lr : n - 1, gj = j0 + lr < m ? j0 + lr : m - 1;
-    const float* xr = X + (int64_t)gi * ldx;
-    const float* yr = Y + (int64_t)gj * ldy;
-    float xa[8], yb[8];
-    auto gload = [&](int k0) {
-        const int kb = k0 + lk;
-        if (vec && kb + 8 <= d) {  // 16-B aligned rows: two float4 per operand
-            using F4 = __attribute__((ext_vector_type(4))) float;
-            const F4 x0 = *reinterpret_cast<const F4*>(xr + kb), x1 = *reinterpret_cast<const F4*>(xr + kb + 4);
-            const F4 y0 = *reinterpret_cast<const F4*>(yr + kb), y1 = *reinterpret_cast<const F4*>(yr + kb + 4);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                xa[q] = x0[q];
-                xa[q + 4] = x1[q];
-                yb[q] = y0[q];
-                yb[q + 4] = y1[q];
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int k = kb + q;
-                xa[q] = k < d ? xr[k] : 0.f;
-                yb[q] = k < d ? yr[k] : 0.f;
-            }
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            As[buf][lk + q][lr] = (double)xa[q];
-            Bs[buf][lk + q][lr] = (double)yb[q];
-        }
-    };
-    double acc[8][8];
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 8; ++b) acc[a][b] = 0.0;
-    const int nk = (d + DK - 1) / DK;
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    using D2 = __attribute__((ext_vector_type(2))) double;
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) gload((kt + 1) * DK);
-        // (fully unrolled, the LDS reads of every kk were hoisted and spilled)
-#pragma unroll 2
-        for (int kk = 0; kk < DK; ++kk) {
-            double av[8], bv[8];
-            // a thread's 8 columns are the pairs 32 h + 2 tx, + 1 (h < 4): the 16 lanes of a
-            // ds_read_b128 phase read 16 consecutive 16-B slots (tx * 8 + 2 h had them 64 B
-            // apart: four lanes per bank group), and the epilogue stores 256-B row runs
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const D2 a2 = *reinterpret_cast<const D2*>(&As[buf][kk][ty * 8 + 2 * h]);
-                const D2 b2 = *reinterpret_cast<const D2*>(&Bs[buf][kk][32 * h + 2 * tx]);
-                av[2 * h] = a2[0];
-                av[2 * h + 1] = a2[1];
-                bv[2 * h] = b2[0];
-                bv[2 * h + 1] = b2[1];
-            }
-#pragma unroll
-            for (int a = 0; a < 8; ++a)
-#pragma unroll
-                for (int b = 0; b < 8; ++b) acc[a][b] = fma(av[a], bv[b], acc[a][b]);
-        }
-        if (kt + 1 < nk) lstore(buf ^ 1);
-        __syncthreads();
-    }
-    double mx = 0.0;
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-        const int i = i0 + ty * 8 + a;
-        if (i >= n) continue;
-        const double rx = nx[i];
-        double* crow = C + (int64_t)i * ldc;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const int j = j0 + 32 * (b >> 1) + 2 * tx + (b & 1);
-            if (j >= m) continue;
-            double v = -2.0 * acc[a][b];
-            v += rx;
-            v += ny[j];
-            v = v > 0 ? v : 0.0;
-            if (euclid) v = sqrt(v);
-            if (zero_diag && i == j) v = 0.0;
-            crow[j] = v;
-            mx = fmax(mx, v);
-        }
-    }
-    mx = wave_max(mx);
-    if ((tid & 63) == 0) red[tid >> 6] = mx;
-    __syncthreads();
-    if (tid == 0) part[tile] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-}
-
-// The same 128 x 128 float64 tile on v_mfma_f64_16x16x4_f64 (the matrix cores free the
-// VALU for nothing else here, but one MFMA replaces 16 vector FMAs and their operand
-// reads): 4 waves, each a 64 x 64 quarter as 4 x 4 blocks of 16 x 16; per 4-deep k-step a
-// lane reads one double of each of its 4 row blocks and 4 column blocks from the LDS
-// stage (16 consecutive doubles per lane group: conflict-free).  Operand staging, the
-// epilogue (POT euclidean_distances order, clamp, sqrt, zero diagonal) and the per-tile
-// max are dist_tile_f64_kernel's.  Result lanes: column l & 15, rows (l >> 4) + 4 r.
 __global__ __launch_bounds__(256, 2) void dist_mfma_f64_kernel(const float* __restrict__ X, int64_t ldx,
                                                                const float* __restrict__ Y, int64_t ldy,
                                                                int n, int m, int d, const double* nx,
@@ -1577,20 +1463,13 @@ int otf_cost_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64_t l
                                                                              (int)d, vec, nx, ny, C, ldc);
         OTF_HIP(hipGetLastError());
     } else {
-        // 128 x 128 float64 tiles with the finalize epilogue fused (dist_tile_f64_kernel)
+        // 128 x 128 float64 tiles with the finalize epilogue fused (dist_mfma_f64_kernel)
         const int tiles_m = (int)((n + otf::DT - 1) / otf::DT), tiles_n = (int)((m + otf::DT - 1) / otf::DT);
         const int ntiles = tiles_m * tiles_n;
         const int vec = (ldx % 4 == 0) && (ldy % 4 == 0) && ((uintptr_t)X % 16 == 0) && ((uintptr_t)Y % 16 == 0);
-        // OTF_DIST_MFMA=0: the VALU tile kernel (A/B; the same sums in another order)
-        const char* ev = getenv("OTF_DIST_MFMA");
-        if (ev && atoi(ev) == 0)
-            otf::dist_tile_f64_kernel<<<ntiles, 256, 0, s>>>(X, ldx, Y, ldy, (int)n, (int)m, (int)d, nx, ny,
-                                                             metric == OTF_EUCLIDEAN, zero_diag, C, ldc, part,
-                                                             tiles_m, vec);
-        else
-            otf::dist_mfma_f64_kernel<<<ntiles, 256, 0, s>>>(X, ldx, Y, ldy, (int)n, (int)m, (int)d, nx, ny,
-                                                             metric == OTF_EUCLIDEAN, zero_diag, C, ldc, part,
-                                                             tiles_m, vec);
+        otf::dist_mfma_f64_kernel<<<ntiles, 256, 0, s>>>(X, ldx, Y, ldy, (int)n, (int)m, (int)d, nx, ny,
+                                                         metric == OTF_EUCLIDEAN, zero_diag, C, ldc, part,
+                                                         tiles_m, vec);
         OTF_HIP(hipGetLastError());
         const int64_t tot = n * m;
         int grid = (int)((tot + 255) / 256);

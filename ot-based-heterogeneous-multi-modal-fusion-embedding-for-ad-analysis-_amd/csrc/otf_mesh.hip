@@ -74,7 +74,7 @@ struct SkMeshArgs {
     double stop_thr;
     void* gran;  // granule region, zeroed per solve
     uint32_t off_row, off_cola, off_colb, bstride;
-    int nrb, ncb, cpr, xcd_rows, xcc_local;
+    int nrb, ncb, cpr, xcc_local;
     int* xreg;  // [8 x 64] workgroups per XCC (registration), then the flat barrier word
     otf_sinkhorn_info* info;
     double* errlog;
@@ -177,8 +177,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     // chunks) need write-through stores.  Measured 7.2 -> 5.7 us per iteration; with the
     // column tiles spread over XCCs the same plain stores are never seen (the solve ends
     // in OTF_SK_TIMEOUT), which is why roles follow the registration, never blockIdx.
-    // Otherwise: blockIdx roles, every hop write-through (xcd_rows: a row block's members
-    // on one XCD under round-robin placement, speed only).
+    // Otherwise: blockIdx roles, every hop write-through.
     int rb = 0, cb = 0, xl = 0;
     if (p.xcc_local) {
         __shared__ int s_reg[4];
@@ -221,14 +220,8 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     if (!xl) {
         const int bi = blockIdx.x;
         if (bi >= nrb * ncb) return;  // the launch's surplus (XCC mode launches 8 x nrb)
-        if (p.xcd_rows && (nrb & 7) == 0) {
-            const int x = bi & 7, q = bi >> 3;
-            cb = q % ncb;
-            rb = (q / ncb) * 8 + x;
-        } else {
-            rb = bi / ncb;
-            cb = bi % ncb;
-        }
+        rb = bi / ncb;
+        cb = bi % ncb;
     }
     const bool lead = (rb == 0 && cb == 0 && tid == 0);  // writes info and the error log
 #ifdef OTF_MESH_STAMPS
@@ -843,16 +836,6 @@ MeshShape mesh_shape(int64_t n, int64_t m) {
     return s;
 }
 
-// OTF_MESH_XCD_ROWS=1: a row block's members on one XCD instead of a column tile's
-inline int mesh_xcd_rows() {
-    static int env = -1;
-    if (env < 0) {
-        const char* e = getenv("OTF_MESH_XCD_ROWS");
-        env = e ? atoi(e) : 0;
-    }
-    return env;
-}
-
 }  // namespace
 
 bool mesh_supported(int64_t n, int64_t m) {
@@ -865,9 +848,7 @@ bool mesh_supported(int64_t n, int64_t m) {
 size_t mesh_region_bytes(int64_t n, int64_t m) {
     if (!mesh_supported(n, m)) return 0;
     const MeshShape s = mesh_shape(n, m);
-    const size_t b = kMeshRegBytes + s.row_bytes + s.cola_bytes + s.colb_bytes;
-    const size_t b2 = mesh2_region_bytes(n, m);  // the two-hop form shares the region
-    return b > b2 ? b : b2;
+    return kMeshRegBytes + s.row_bytes + s.cola_bytes + s.colb_bytes;
 }
 
 template <typename CT>
@@ -876,9 +857,6 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                     double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* shift) {
     if (!mesh_supported(n, m) || !region) return hipErrorInvalidValue;
-    if (mesh2_enabled() && mesh2_supported(n, m))
-        return run_mesh2<CT>(C, ldc, n, m, a_pad, b_pad, cost_scale, o, region, u_out, v_out, P_out, ldp,
-                             P_dtype, info, errlog, zeroed, s, shift);
     const MeshShape sh = mesh_shape(n, m);
     if (sh.nrb * sh.ncb > device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
     SkMeshArgs p{};
@@ -903,7 +881,6 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
     p.nrb = sh.nrb;
     p.ncb = sh.ncb;
     p.cpr = sh.cpr;
-    p.xcd_rows = mesh_xcd_rows();
     {
         const char* e = getenv("OTF_MESH_XCC");  // 0: blockIdx roles, write-through everywhere
         p.xcc_local = e ? atoi(e) : 1;

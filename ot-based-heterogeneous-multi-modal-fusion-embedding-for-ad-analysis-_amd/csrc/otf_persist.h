@@ -342,16 +342,6 @@ hipError_t run_gather(const CT* C, int64_t ldc, int n, int m, const T* a_pad, co
 // it does not take.
 bool mesh_supported(int64_t n, int64_t m);
 size_t mesh_region_bytes(int64_t n, int64_t m);
-// Two-hop form of the mesh engine (otf_mesh2.hip): whole 256 x 256 tiles, 8 / 16 row blocks x
-// 8 / 16 column tiles; run by run_mesh when mesh2_enabled() (OTF_MESH2) and the shape fits
-bool mesh2_supported(int64_t n, int64_t m);
-size_t mesh2_region_bytes(int64_t n, int64_t m);
-bool mesh2_enabled();
-template <typename CT>
-hipError_t run_mesh2(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
-                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
-                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                     double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* shift);
 // float64 form (otf_mesh64.hip): whole 128 x 512 tiles, 4..32 (a power of two) x 1..8, K
 // split between the register files and LDS
 bool mesh64_supported(int64_t n, int64_t m);

@@ -1720,17 +1720,6 @@ hipError_t launch_pass(const PassCfg& c, int grid, const SkArgs<T>& p, hipStream
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// OTF_FALLBACK=0 launches no solo fallback behind the persistent engines (A/B timing);
-// a persistent solve that cannot become co-resident then ends in OTF_SK_TIMEOUT
-inline bool fallback_enabled() {
-    static int env = -1;
-    if (env < 0) {
-        const char* e = getenv("OTF_FALLBACK");
-        env = e ? atoi(e) : 1;
-    }
-    return env != 0;
-}
-
 struct Workspace {
     void* a_pad;
     void* b_pad;
@@ -1915,23 +1904,13 @@ hipError_t launch_tiled_g(int grid, SkTileArgs<T>& p, hipStream_t s) {
     return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
 }
 
-inline int tiled_nrep(const Workspace& w) {
-    static int env = -1;
-    if (env < 0) {
-        const char* e = getenv("OTF_TILED_NREP");
-        env = e ? atoi(e) : 1;
-    }
-    int r = env == 2 || env == 4 ? env : 1;
-    return r <= w.nrep ? r : 1;
-}
-
 template <typename T, typename CT>
 hipError_t run_tiled(const CT* C, int64_t ldc, int n, int m, const T* cost_scale,
                      const otf_sinkhorn_opts& o, Workspace& w, T* u_out, T* v_out,
                      void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                      double* errlog, hipStream_t s) {
     SkTileArgs<T> p{};
-    const int nrep = tiled_nrep(w);
+    const int nrep = 1;
     p.C = C;
     p.ldc = ldc;
     p.n = n;
@@ -2099,7 +2078,6 @@ hipError_t launch_solo(const SkSetup<T>& su, const CT* C, int64_t ldc, int64_t n
                        const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out,
                        void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                        double* errlog, hipStream_t s) {
-    if (!fallback_enabled()) return hipSuccess;
     SkArgs<T> p = sk_args<T, CT, false>(su, C, ldc, n, m, cost_scale, o, info, errlog, false);
     SoloArgs<T> x{(T*)su.w.cs, (T*)su.w.u2, (T*)su.w.v2, su.w.cs_stride, o.max_iter, u_out, v_out,
                   P_out, ldp, P_dtype == OTF_F64 ? 1 : 0, p.v0v};
@@ -2286,12 +2264,15 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     // tiled engine: every (128 x 512 float / 64 x 512 double) tile on its own CU
     const bool tfits = whole && su.w.t_nrb * su.w.t_ncb <= device_cu_count() &&
                        su.w.t_nrb * su.w.t_ncb <= kMaxResidentWG;
-    // AUTO takes it for float only: for float64 (64-row tiles) it measured no faster
-    // than the row-block resident engine (config 2, d = 512: 12.8 vs 12.3 ms per step --
-    // both sit on the ~5 us grid-sync round trip per iteration); TILED forces it
+    // AUTO takes it for float, and for the float64 whole-tile shapes the float64 mesh
+    // leaves to it (every tile on its own CU, mesh_auto_ok false: 7.36 vs 7.47 us per
+    // iteration at 2048^2).  Other float64 shapes (64-row tiles) measured no faster than
+    // the row-block resident engine (config 2, d = 512: 12.8 vs 12.3 ms per step -- both
+    // sit on the ~5 us grid-sync round trip per iteration); TILED forces it
     const bool want_tiled = !LOG && !sh && !avg_pass_ms && tfits && o.max_iter >= 1 &&
                             (o.engine == OTF_ENGINE_TILED ||
-                             (o.engine == OTF_ENGINE_AUTO && sizeof(T) == 4));
+                             (o.engine == OTF_ENGINE_AUTO &&
+                              (sizeof(T) == 4 || (kMesh64 && mesh_shape_ok && !mesh_auto_ok))));
     if (o.engine == OTF_ENGINE_TILED && (LOG || sh || !tfits)) return OTF_EUNSUPPORTED;
     if (want_tiled) {
         Workspace w = su.w;

@@ -1193,7 +1193,6 @@ hipError_t launch_sweep_gs(int grid, SkSweepArgs<T>& p, hipStream_t s) {
     int nres = base < kSwLdsMax ? (int)((kSwLdsMax - base) / sweep_block_lds(R, G)) : 0;
     if (nres > OTF_SWEEP_MAXRES) nres = OTF_SWEEP_MAXRES;
     if (nres > min_nb - 1) nres = min_nb - 1 > 0 ? min_nb - 1 : 0;
-    if (const char* e = getenv("OTF_SWEEP_NRES")) nres = atoi(e) < nres ? atoi(e) : nres;
     p.nres = nres;
     void* args[] = {&p};
     const void* k = (const void*)sk_sweep_kernel<T, CT, TP, G, R, OTF_SWEEP_NREP, SH, KS>;
@@ -1310,9 +1309,9 @@ hipError_t run_sweep(const CT* C, int64_t ldc, int n, int m, int m_pad, const T*
     p.reg_ticks = reg_stall_ticks();
     p.nt_loads = (double)n * ldc * sizeof(CT) > 192.0 * (1 << 20) ? 1 : 0;
     p.det = o.deterministic ? 1 : 0;
-    // OTF_SWEEP_GRAN=0: the r02 flush (slab + group counter + atomics + grid barrier)
-    const char* ge = getenv("OTF_SWEEP_GRAN");
-    p.gran = (sizeof(T) == 4 && !p.det && !(ge && atoi(ge) == 0)) ? 1 : 0;
+    // float outside the deterministic mode: the granule flush; float64 and the
+    // deterministic mode: the r02 flush (slab + group counter + atomics + grid barrier)
+    p.gran = (sizeof(T) == 4 && !p.det) ? 1 : 0;
     p.world = 1;
     p.n_total = n;
     // float64: stream K (written by the prologue) when the caller's workspace holds it

@@ -96,8 +96,13 @@ def split_label_plans(pets, mris, comm, solve):
     mris) -> (plans, result)`` on its share) and ONE all-reduce(SUM) of an L x P x P
     float64 buffer (P = the largest group, zeros where a rank does not own the label)
     gives every rank every plan.  Each plan has exactly one nonzero contribution, so the
-    sum reproduces it bit for bit: the result equals the unsplit solve.  Returns
-    ``(plans, result of this rank's solve or None)``."""
+    sum reproduces this rank's solve of it bit for bit.  That solve equals the unsplit
+    one bit for bit when the share takes the same GW kernel form as the whole batch
+    (otf_gw.hip gw_launch picks the small-problem kernel only when EVERY group of a
+    launch has <= 64 samples, as with the reference's --max-jax-samples 64); when the
+    groups straddle 64 a rank's share can take the other form and its plans agree with
+    the unsplit solve to rounding (same algorithm and iterates, different reduction
+    order).  Returns ``(plans, result of this rank's solve or None)``."""
     L = len(pets)
     world, rank = comm.nranks, comm.rank
     own = list(range(rank, L, world))
@@ -252,6 +257,7 @@ class XPeer:
     def __init__(self, m: int, group=None):
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self._group = group
         self.m = int(m)
         lib = L.lib()
         hs = int(lib.otf_xpeer_handle_size())
@@ -279,15 +285,16 @@ class XPeer:
             raise RuntimeError("XPeer is closed")
         return self._h
 
-    def close(self, group=None):
-        """Collective: every rank must call it after its last solve on this exchange.
-        The device is synchronised (this rank's grids are done) and the ranks meet at a
-        barrier (every peer's grids are done storing into this rank's buffer) before the
-        buffer is freed."""
+    def close(self):
+        """Collective over the exchange's group (the one it was built on): every member
+        must call it after its last solve on this exchange.  The device is synchronised
+        (this rank's grids are done) and the members meet at a barrier of that group
+        (every peer's grids are done storing into this rank's buffer) before the buffer is
+        freed; a one-member exchange has no peer and skips the barrier."""
         if self._h is not None:
             torch.cuda.synchronize()
-            if dist.is_available() and dist.is_initialized():
-                dist.barrier(group=group)
+            if self.world > 1 and dist.is_available() and dist.is_initialized():
+                dist.barrier(group=self._group)
             L.lib().otf_xpeer_destroy(self._h)
             self._h = None
 

@@ -83,7 +83,19 @@ def pairwise_cost(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str = 
             C.data_ptr(), C.stride(0), L.ptr(cmax), L.stream_handle(X.device)), "otf_cost_pairwise")
     else:
         raise ValueError(f"algo {algo!r}")
-    return C, cmax
+    return C, (mark_cost_max(cmax) if cmax is not None else None)
+
+
+def mark_cost_max(t: torch.Tensor) -> torch.Tensor:
+    """Tags a device scalar as max(C) of the cost it scales (scale_cost = "max_cost"), so
+    ``sinkhorn`` may take max(C / cost_scale) = 1 without reading C.  The library's cost
+    builders tag the maxima they return; an untagged ``cost_scale`` is measured."""
+    t._otf_cost_max = True
+    return t
+
+
+def is_cost_max(t) -> bool:
+    return bool(getattr(t, "_otf_cost_max", False))
 
 
 def cost_last_phases() -> tuple[float, float]:
@@ -134,7 +146,7 @@ def pairwise_cost_ex(X: torch.Tensor, Y: torch.Tensor | None = None, metric: str
         X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), _DT[in_dtype], n, m, d, met,
         int(zero_diag), C.data_ptr(), C.stride(0), _DT[out_dtype], cmax.data_ptr(), unit.data_ptr(),
         workspace.data_ptr(), workspace.numel(), L.stream_handle(X.device)), "otf_cost_pairwise_ex")
-    return C, cmax, unit
+    return C, mark_cost_max(cmax), unit
 
 
 def scale_inplace(C: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
@@ -332,13 +344,24 @@ SHIFT_RANGE_F64 = 700.0
 _SHIFT_ENGINES = ("auto", "mesh", "sweep", "stream")
 
 
-def _want_shift(C: torch.Tensor, reg: float, cost_scale, flavor: str, dt, engine: str) -> bool:
+def _cost_ratio(C: torch.Tensor, reg: float, cost_scale) -> float:
+    """max(C / cost_scale) / reg.  A ``cost_scale`` tagged as max(C) (mark_cost_max: the
+    library's cost builders) gives 1 / reg without touching C; otherwise one device
+    reduction and a host read."""
+    if cost_scale is not None and is_cost_max(cost_scale):
+        return 1.0 / float(reg)
+    cmax = float(C.amax()) if C.numel() else 0.0
+    if cost_scale is not None:
+        cs = float(cost_scale.reshape(-1)[0])
+        cmax = cmax / cs if cs != 0.0 else (0.0 if cmax == 0.0 else float("inf"))
+    return cmax / float(reg)
+
+
+def _want_shift(C: torch.Tensor, reg: float, cost_scale, flavor: str, dt, engine: str,
+                ratio: float | None = None) -> bool:
     if flavor != "pot" or dt != torch.float32 or engine not in _SHIFT_ENGINES:
         return False
-    if cost_scale is not None:       # scale_cost = "max_cost": C / cost_scale <= 1
-        r = 1.0 / float(reg)
-    else:
-        r = (float(C.amax()) if C.numel() else 0.0) / float(reg)  # one reduction + host read
+    r = _cost_ratio(C, reg, cost_scale) if ratio is None else ratio
     return SHIFT_RANGE < r <= SHIFT_RANGE_F64
 
 
@@ -359,8 +382,12 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
     by construction, else the sweep engine's fixed-order mode; POT flavour):
     bitwise-identical results run to run.
 
-    ``precision``: "as_given" (and its alias "auto") computes in C's dtype; "fp64" in
-    float64 (the reference's POT path is float64 NumPy).
+    ``precision``: "as_given" computes in C's dtype; "fp64" in float64 (the reference's
+    POT path is float64 NumPy); "auto" computes a float32 / float16 POT solve in float32
+    where that holds POT's result -- max(C / cost_scale) / reg <= SHIFT_RANGE, or the
+    shifted kernel applies (below) -- and promotes it to float64 otherwise (past
+    SHIFT_RANGE_F64, on an engine without the shifted kernel, or with ``shift=False``),
+    where float32 kernel-domain POT would break at iteration 0 or lose the plan.
 
     ``shift`` (float32 POT only): run POT's iteration on the shifted kernel
     K~ = 2^(C ks + A_i + B_j) (include/otfuse.h opts.shift) -- the same iterates, with
@@ -378,6 +405,15 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
     _dev(C, "C")
     if precision not in ("as_given", "fp64", "auto"):
         raise ValueError(f"precision must be 'as_given', 'fp64' or 'auto', not {precision!r}")
+    if precision == "auto" and flavor == "pot" and C.dtype != torch.float64:
+        ratio = _cost_ratio(C, reg, cost_scale)
+        if ratio > SHIFT_RANGE:
+            shifts = shift is not False and _want_shift(C, reg, cost_scale, flavor, torch.float32,
+                                                        engine, ratio)
+            if shifts:
+                shift = True
+            else:
+                precision = "fp64"
     if precision == "fp64" and C.dtype != torch.float64:
         C = C.double()
         if cost_scale is not None:

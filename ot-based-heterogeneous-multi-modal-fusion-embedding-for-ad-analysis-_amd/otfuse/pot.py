@@ -106,8 +106,12 @@ def sinkhorn(a, b, M, reg: float, method: str = "sinkhorn", numItermax: int = 10
     P = res.plan if is_torch else ops.to_host(res.plan)
     if not log:
         return P
-    u = res.u if is_torch else res.u.cpu().numpy()
-    v = res.v if is_torch else res.v.cpu().numpy()
+    # a shifted float32 solve (ops.sinkhorn's default at 64 < max(M)/reg <= 700) holds
+    # u~, v~; POT's log reports its own scalings u = 2^A u~, v = 2^B v~ (float64: at small
+    # reg they can leave float32's range)
+    u, v = res.pot_scalings() if res.shifted else (res.u, res.v)
+    if not is_torch:
+        u, v = u.cpu().numpy(), v.cpu().numpy()
     return P, {"err": info["err"], "niter": info["niter"], "u": u, "v": v,
                "status": info["status_name"]}
 

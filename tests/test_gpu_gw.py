@@ -29,12 +29,10 @@ def _emb(n, d, seed):
                                                     ("euclidean", True, 1000, 1000, 64),
                                                     ("sqeuclidean", False, 1030, 777, 300),
                                                     ("sqeuclidean", False, 2048, 300, 1027)])
-@pytest.mark.parametrize("mfma", ["1", "0"])
-def test_pairwise_cost_f64_vs_oracle(orc, dev, monkeypatch, metric, zero_diag, n, m, d, mfma):
-    """Past 16384 outputs the 128 x 128 tile kernels: on float64 MFMA (default) and in the
-    VALU form (OTF_DIST_MFMA=0), both to 1e-12 of the oracle."""
+def test_pairwise_cost_f64_vs_oracle(orc, dev, metric, zero_diag, n, m, d):
+    """Past 16384 outputs the 128 x 128 tile kernel on float64 MFMA, to 1e-12 of the
+    oracle."""
     from otfuse import gw
-    monkeypatch.setenv("OTF_DIST_MFMA", mfma)
     X, _, _ = _emb(n, d, 1)
     _, Y, _ = _emb(m, d, 2)
     same = n == m and zero_diag

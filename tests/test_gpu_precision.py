@@ -71,6 +71,87 @@ def test_metric_shape_float32_vs_float64_oracle(dev, metric_inputs, oracle_plans
     np.testing.assert_allclose(info["err"], info_r["err"], rtol=2e-3, atol=1e-9)
 
 
+@pytest.mark.parametrize("eps", [0.04, 0.03, 0.02, 0.016, 0.0155])
+def test_shift_threshold_metric_shape_vs_oracle(dev, metric_inputs, oracle_plans, eps):
+    """Around the shift threshold (ops.SHIFT_RANGE = 64: max(C / cmax) / reg, i.e.
+    reg = 1/64 = 0.015625 on a max-normalised cost): the plain float32 kernel at reg = 0.04,
+    0.03, 0.02 and 0.016 (ratios 25 ... 62.5) and the shifted one just below 1/64
+    (0.0155, ratio 64.5) -- all within the north star's 1e-4 of the float64 oracle with
+    the oracle's error log."""
+    from otfuse import ops
+    X, Y, C, cmax, Cr = metric_inputs
+    a = torch.full((N,), 1.0 / N, device=dev)
+    res = ops.sinkhorn(a, a, C, eps, max_iter=100, stop_thr=0.0, cost_scale=cmax)
+    info = res.info()
+    assert info["engine_name"] == "mesh" and info["niter"] == 99
+    assert res.shifted == (1.0 / eps > ops.SHIFT_RANGE)
+    Pr, _, _, info_r = oracle_plans(eps)
+    assert info_r["break_iter"] == -1
+    assert nrel(res.plan.cpu().numpy(), Pr) < TOL32
+    assert info["n_err"] == len(info_r["err"])
+    np.testing.assert_allclose(info["err"], info_r["err"], rtol=2e-3, atol=1e-9)
+
+
+def test_cost_scale_not_the_max_is_measured(dev, metric_inputs, oracle_plans):
+    """A cost_scale that is not max(C) (here max / 2, an untagged tensor): the shift
+    decision measures max(C / cost_scale) / reg (= 2 / 0.02 = 100 > 64, shifted) instead of
+    assuming 1 / reg (= 50, plain), and the plan matches the oracle on C / (max / 2) =
+    2 * Cr at reg 0.02, i.e. Cr at reg 0.01."""
+    from otfuse import ops
+    X, Y, C, cmax, Cr = metric_inputs
+    half = cmax.clone() * 0.5
+    assert ops.is_cost_max(cmax) and not ops.is_cost_max(half)
+    a = torch.full((N,), 1.0 / N, device=dev)
+    res = ops.sinkhorn(a, a, C, 0.02, max_iter=100, stop_thr=0.0, cost_scale=half)
+    assert res.shifted and res.info()["niter"] == 99
+    Pr, *_ = oracle_plans(0.01)
+    assert nrel(res.plan.cpu().numpy(), Pr) < TOL32
+
+
+def test_precision_auto_promotes_when_the_shift_cannot_apply(orc, dev, metric_inputs, oracle_plans):
+    """precision='auto' on a float32 cost: float32 with the shifted kernel where it applies
+    (reg = 0.01), float64 where float32 kernel-domain POT would lose the plan and the shift
+    cannot run -- with shift=False at reg = 0.01, and past SHIFT_RANGE_F64 (reg = 1e-3,
+    ratio 1000), where POT's own float64 K has exact zeros: there the float64 solve takes
+    POT's decision (the oracle's status and iteration count)."""
+    from otfuse import ops
+    X, Y, C, cmax, Cr = metric_inputs
+    a = torch.full((N,), 1.0 / N, device=dev)
+    Pr, *_ = oracle_plans(0.01)
+    r = ops.sinkhorn(a, a, C, 0.01, max_iter=100, stop_thr=0.0, cost_scale=cmax, precision="auto")
+    assert r.shifted and r.u.dtype == torch.float32
+    assert nrel(r.plan.cpu().numpy(), Pr) < TOL32
+    r = ops.sinkhorn(a, a, C, 0.01, max_iter=100, stop_thr=0.0, cost_scale=cmax, precision="auto",
+                     shift=False)
+    assert r.u.dtype == torch.float64 and not r.shifted and r.info()["niter"] == 99
+    assert nrel(r.plan.cpu().numpy(), Pr) < TOL32
+    r = ops.sinkhorn(a, a, C, 1e-3, max_iter=100, stop_thr=0.0, cost_scale=cmax, precision="auto")
+    assert r.u.dtype == torch.float64 and not r.shifted
+    Cs = (C / cmax).double().cpu().numpy()
+    Pr3, _, _, ir = orc.sinkhorn_knopp(np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cs, 1e-3, 100, 0.0)
+    i = r.info()
+    assert (i["niter"], i["break_iter"]) == (ir["niter"], ir["break_iter"])
+    assert nrel(r.plan.cpu().numpy(), Pr3) < 1e-9
+
+
+def test_pot_sinkhorn_log_returns_pot_scalings_when_shifted(dev, metric_inputs, oracle_plans):
+    """ot.sinkhorn drop-in (otfuse.pot.sinkhorn) with log=True on a max-normalised float32
+    cost at reg = 0.01, where ops.sinkhorn takes the shifted kernel: log['u'], log['v'] are
+    POT's scalings (2^A u~, 2^B v~, float64), equal to the oracle's up to POT's scale mode."""
+    from otfuse import pot
+    X, Y, C, cmax, Cr = metric_inputs
+    M = C / cmax
+    a = torch.full((N,), 1.0 / N, device=dev)
+    P, log = pot.sinkhorn(a, a, M, 0.01, numItermax=100, stopThr=0.0, log=True)
+    Pr, ur, vr, _ = oracle_plans(0.01)
+    assert nrel(P.cpu().numpy(), Pr) < TOL32
+    u, v = log["u"].cpu().numpy(), log["v"].cpu().numpy()
+    assert log["u"].dtype == torch.float64
+    c = np.median(u / ur)
+    np.testing.assert_allclose(u / c, ur, rtol=5e-4)
+    np.testing.assert_allclose(v * c, vr, rtol=5e-4)
+
+
 @pytest.mark.parametrize("engine", ["mesh", "sweep", "stream"])
 def test_shifted_kernel_every_engine_vs_oracle(dev, metric_inputs, oracle_plans, engine):
     """The shifted kernel on each engine that runs it (register-resident mesh, persistent
