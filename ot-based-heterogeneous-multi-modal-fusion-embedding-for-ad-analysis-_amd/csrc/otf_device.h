@@ -58,12 +58,12 @@ template <typename T> __device__ __forceinline__ bool finite_val(T x) {
 // tools/ubench_xor.hip checks every offset on the device.
 template <int O> __device__ __forceinline__ unsigned wave_xor_u32(unsigned x) {
     if constexpr (O == 1) {
-        return __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
     } else if constexpr (O == 2) {
-        return __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+        return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
     } else if constexpr (O == 4 || O == 8) {
-        const unsigned from_up = __builtin_amdgcn_update_dpp(0u, x, 0x100 + O, 0xF, 0xF, false);  // row_shl
-        const unsigned from_dn = __builtin_amdgcn_update_dpp(0u, x, 0x110 + O, 0xF, 0xF, false);  // row_shr
+        const unsigned from_up = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x100 + O, 0xF, 0xF, true);  // row_shl
+        const unsigned from_dn = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x110 + O, 0xF, 0xF, true);  // row_shr
         return (__lane_id() & O) ? from_dn : from_up;
     } else if constexpr (O == 16) {
         const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
@@ -172,9 +172,13 @@ template <typename T, typename F> __device__ __forceinline__ T map_words(T x, F 
     }
 }
 // x of another lane by a DPP control: quad_perm 0xB1 (^1), 0x4E (^2), row_half_mirror
-// 0x141 (lane i <-> 7 - i within its 8), row_mirror 0x140 (i <-> 15 - i within its 16)
+// 0x141 (lane i <-> 7 - i within its 8), row_mirror 0x140 (i <-> 15 - i within its 16).
+// A plain DPP move with bound_ctrl (every lane of these patterns has a source, so no
+// "old" value is read): update_dpp with old = 0 made the compiler zero the destination
+// before every move, one extra v_mov per 32-bit word (r05: ~100 per float64 mesh
+// iteration).
 template <int CTRL, typename T> __device__ __forceinline__ T dpp_lane(T x) {
-    return map_words(x, [](unsigned w) { return (unsigned)__builtin_amdgcn_update_dpp(0u, w, CTRL, 0xF, 0xF, false); });
+    return map_words(x, [](unsigned w) { return (unsigned)__builtin_amdgcn_mov_dpp((int)w, CTRL, 0xF, 0xF, true); });
 }
 // v_permlane32_swap / v_permlane16_swap of (a, b), then the sum of the two results:
 // lanes of the lower half (row of 16) end with their a plus the partner half's a, lanes

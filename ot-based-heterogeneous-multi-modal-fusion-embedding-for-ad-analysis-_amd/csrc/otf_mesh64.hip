@@ -4,38 +4,53 @@
 // Replaces ot.sinkhorn (POT 0.9.6 sinkhorn_knopp, MRI_PET_OT_nojax.py:143 /
 // perturbot/perturbot/match/utils.py:6-115) in the reference's own precision for the
 // whole-tile shapes whose float64 K fits the chip: up to 32 x 8 tiles of 128 x 512, i.e.
-// the N = 4096 metric shape (bench.py metric_f64), where the sweep engine streams the
+// the N = 4096 metric shape (bench.py headline), where the sweep engine streams the
 // 134 MB K from the Infinity Cache every iteration (27 us per iteration).
 //
 // Storage.  A float64 K at N = 4096 is 128 MiB -- the size of all 256 CUs' register files
-// together.  Each workgroup runs ONE wave per SIMD (4 waves, 256 threads), so a lane may
-// address 512 registers (256 arch + 256 acc); its 32 rows x 8 columns of K are 256
-// doubles: rows 0..23 of a wave's 32 live in registers (384 words; the compiler parks
-// what exceeds the arch file in the acc file), rows 24..31 in LDS (128 KiB per
-// workgroup, 16-B slots laid out lane-fastest so every ds_read_b128 is conflict-free).
+// together.  Each workgroup runs EIGHT waves (two per SIMD, 256 registers a lane, all of
+// them architectural: no accumulation-file reads in the loop) and holds its 128 x 512 tile
+// as 8 stripes of 64 columns, one per wave.  Lane l of wave w (rr = l & 15, g = l >> 4)
+// owns rows rr + 16 a (a < 8) and columns 64 w + 16 b + 4 g + i (b, i < 4) -- the
+// accumulator layout of v_mfma_f64_16x16x4_f64 with the column block as the M index --
+// column blocks b = 0..2 in registers (192 words), b = 3 in LDS (128 KiB per workgroup,
+// lane-fastest 16-B slots: every ds_read_b128 is conflict-free).  (r04's form: four waves,
+// one per SIMD, 32 rows x 8 columns a lane, ~220 of its 384 K words in the accumulation
+// file: ~480 v_accvgpr_read and ~2 080 VALU per iteration against ~1 000 here.)
 //
-// Protocol: the float mesh's three epoch-tagged granule hops per iteration (row hop
-// across the row block's ncb members, hop A column partials to the column tile's
-// reducers, hop B sums back), same roles (XCC-local column tiles after registration),
-// same POT decisions carried in the tags.  A 16-B chunk carries two float64 values whose
-// three low mantissa bits hold the tag -- epoch mod 4 and one flag bit (the gather
-// engine's encoding, otf_gather.hip make_chunk): a slot written every epoch holds epoch
-// e - 2 or e when a consumer waits for e, so two bits tell them apart; the value keeps a
-// 49-bit mantissa (relative 2^-50, below the float64 rounding of the sums it enters).
-// The error chunks, written only every check_every epochs, carry ONE value and the full
-// epoch tag instead.  Every sum has one fixed order: bitwise reproducible run to run.
+// Per iteration (epoch e = it + 1):
+//   hop B    each wave polls the 32 column-sum chunks of its stripe from the reducers ->
+//            v (wave-local LDS, no workgroup barrier);
+//   rows     K v over the lane's 16 columns, the 4 lanes of a row (lane bits 5, 4) by two
+//            permlane swaps, the 8 waves' partials through LDS -- barrier B1 -- and wave 0
+//            publishes the tile's 128 row partials (64 chunks) for the row hop;
+//   row hop  every thread polls one (chunk, member) of the row block's ncb column tiles,
+//            8-lane DPP sums -> u of 2 rows -> LDS -- barrier B2;
+//   columns  K^T u over the lane's 8 rows, the 16 lanes of a column (lane bits 3..0) by a
+//            DPP halving butterfly, published per wave straight to the column tile's
+//            reducers (no workgroup reduction);
+//   reduce   wave 0 of workgroup rb sums chunks [rb CPR, +CPR) over the nrb producers in a
+//            fixed order and publishes S (and POT's marginal-error terms).
+// POT's decisions (zero / non-finite v, non-finite u, the error check and stop) ride in the
+// tags and in LDS flags keyed by epoch, read after the barriers, so every wave of every
+// workgroup takes the same decision at the same iteration.  A 16-B chunk carries two
+// float64 values whose three low mantissa bits hold the tag -- epoch mod 4 and one flag
+// bit (otf_gather.hip make_chunk); the error chunks, written only every check_every epochs,
+// carry ONE value and the full epoch tag.  Every sum has one fixed order: bitwise
+// reproducible run to run.
 #include "otf_persist.h"
 #include <type_traits>
 
 namespace otf {
 namespace {
 
-constexpr int kM64NW = 4;                   // waves per workgroup (one per SIMD)
-constexpr int kM64RW = 32;                  // rows per wave
-constexpr int kM64RR = 24;                  // of them in registers
-constexpr int kM64RL = kM64RW - kM64RR;     // in LDS
-constexpr int kM64TR = kM64NW * kM64RW;     // 128 rows per tile
+constexpr int kM64NW = 8;                   // waves per workgroup (two per SIMD)
+constexpr int kM64TR = 128;                 // rows per tile
 constexpr int kM64TC = 512;                 // columns per tile
+constexpr int kM64WC = kM64TC / kM64NW;     // 64 columns per wave
+constexpr int kM64NA = 8;                   // lane rows rr + 16 a
+constexpr int kM64NB = 4;                   // lane columns 16 b + 4 g + i
+constexpr int kM64RB = 3;                   // column blocks in registers (b = 3 in LDS)
 constexpr int kM64NCH = kM64TC / 2;         // 16-B chunks (two columns) per tile row
 constexpr uint32_t kM64RowStride = 1280;    // per producer: 64 row chunks + the error chunk
 constexpr uint32_t kM64ColStride = 4096;    // per producer: 256 column chunks
@@ -120,13 +135,6 @@ __device__ __forceinline__ bool poll64(__amdgpu_buffer_rsrc_t rs, uint32_t off, 
     }
 }
 
-__device__ __forceinline__ double lane0_f64(double x) {
-    const ull b = __builtin_bit_cast(ull, x);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
-    return __builtin_bit_cast(double, ((ull)hi << 32) | lo);
-}
-
 // Diagnostic build only (-DOTF_M64_STAMPS, tools/stamps_mesh64.hip): wave 0's wall clock
 // at the phases of iterations 0..15, keyed by the workgroup's role rb * ncb + cb
 #ifdef OTF_M64_STAMPS
@@ -152,24 +160,31 @@ __device__ unsigned long long g_m64pro[256 * 4];  // kernel start, roles known, 
 #endif
 
 constexpr int pow2_ceil(int x) { return x <= 1 ? 1 : 2 * pow2_ceil((x + 1) / 2); }
+// u history slot of tile row r: lane rr = r & 15 reads its 8 rows rr + 16 a as one run
+__device__ __forceinline__ int upos(int r) { return (r & 15) * 8 + (r >> 4); }
 
 // SNRB, SNCB: the shape compiled in (0 = from the arguments).  Every shape is a mesh of
 // whole tiles (n = nrb * 128, m = ncb * 512), so there are no bound tests.
 template <typename TP, int SNRB, int SNCB>
-__global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
+__global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     using T = double;
-    constexpr int NW = kM64NW, R = kM64RW, RR = kM64RR, RL = kM64RL, TR = kM64TR, TC = kM64TC;
+    constexpr int NW = kM64NW, TR = kM64TR, TC = kM64TC, WC = kM64WC, NA = kM64NA, NB = kM64NB,
+                  RB = kM64RB;
     constexpr bool FULL = SNRB != 0 && SNCB != 0;
     constexpr int KQ = 4;  // reducer loads per lane: nrb x CPR = 256 chunks over 64 lanes
-    __shared__ __attribute__((aligned(16))) D2 sK[NW][RL][4][kWave];  // K rows 24..31 of each wave
-    __shared__ __attribute__((aligned(16))) T colbuf[NW][TC];
-    __shared__ __attribute__((aligned(16))) T vcur[TC];
+    __shared__ __attribute__((aligned(16))) D2 sK[NW][NA][2][kWave];  // column block b = 3
+    __shared__ __attribute__((aligned(16))) T rowbuf[NW][TR];         // per-wave row partials
+    __shared__ __attribute__((aligned(16))) T vcur[NW][WC];           // v of this iteration
     __shared__ __attribute__((aligned(16))) T vhist[2][TC];
-    __shared__ __attribute__((aligned(16))) T uhist[2][TR];
-    __shared__ T s_E;
-    // flags keyed by epoch / iteration (keys only grow): [0] non-finite u here, [1] hop-B
-    // stall, [2] hop-B producer flag, [3] zero / non-finite v, [4] row-hop stall
-    __shared__ int s_ep[5];
+    __shared__ __attribute__((aligned(16))) T uhist[2][TR];           // slot upos(r)
+    __shared__ __attribute__((aligned(16))) T bsh[TC];                // b of the tile's columns
+    __shared__ __attribute__((aligned(16))) T iash[TR];               // 1 / a of its rows
+    __shared__ __attribute__((aligned(16))) T spsh[2][kWave];         // the reducer's S[k - 1]
+    __shared__ T s_err;
+    // flags keyed by epoch / iteration (keys only grow): [0] non-finite u, [1] hop-B stall,
+    // [2] hop-B producer flag, [3] zero / non-finite v, [4] row-hop stall, [5] a member's
+    // bad-v flag in the row hop
+    __shared__ int s_ep[6];
     __shared__ int s_reg[4];
     int tid = threadIdx.x, lane = tid & 63;
     const int w = (int)threadIdx.x >> 6;
@@ -226,8 +241,10 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
     if (threadIdx.x == 0 && rb * ncb + cb < 256) g_m64pro[(rb * ncb + cb) * 4] = t_start;
 #endif
     OTF_M64PRO(1);
-    const int row0 = rb * TR + w * R;
+    const int rr = lane & 15, g = lane >> 4;
+    const int row0 = rb * TR;
     const int col0 = cb * TC;
+    const int cw = w * WC;
     const int nch = kM64NCH;
     const int nred = (nch + CPR - 1) / CPR;
 
@@ -235,58 +252,54 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
     if (p.cost_scale) cinv = 1.0 / p.cost_scale[0];
     const T ks = -1.0 / p.reg * cinv;
 
-    // ---- K: this wave's 32 rows x this lane's 8 columns (pairs j = 2 g + k2 of columns
-    // (lane + 64 g) * 4 + 2 k2, + 1); rows < 24 in registers, the rest in LDS
-    D2 kv[RR][4];
+    // ---- K: rows rr + 16 a, columns cw + 16 b + 4 g + (0..3) as two pairs h; blocks
+    // b < 3 in registers, b = 3 in LDS
+    D2 kr[NA][RB][2];
     {
-        const T* crow = p.C + (int64_t)row0 * p.ldc + col0 + lane * 4;
+        const T* cbase = p.C + (int64_t)(row0 + rr) * p.ldc + col0 + cw + 4 * g;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
+        for (int a = 0; a < NA; ++a) {
+            const T* crow = cbase + (int64_t)(16 * a) * p.ldc;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const D2 c = *reinterpret_cast<const D2*>(crow + (j >> 1) * 256 + (j & 1) * 2);
-                const D2 e = D2{exp(c[0] * ks), exp(c[1] * ks)};
-                if (r < RR) kv[r][j] = e;
-                else sK[w][r - RR][j][lane] = e;
+            for (int b = 0; b < NB; ++b) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const D2 c = *reinterpret_cast<const D2*>(crow + 16 * b + 2 * h);
+                    const D2 e = D2{exp(c[0] * ks), exp(c[1] * ks)};
+                    if (b < RB) kr[a][b][h] = e;
+                    else sK[w][a][h][lane] = e;
+                }
             }
-            crow += p.ldc;
-            // one row's loads in flight at a time: hoisting all 32 rows' loads needs 512
-            // registers on top of K and spills the prologue to scratch
+            // one row group's loads in flight at a time: hoisting them all needs 256
+            // registers on top of K
             __builtin_amdgcn_sched_barrier(0);
         }
     }
     OTF_M64PRO(2);
-    auto kget = [&](int r, int j) -> D2 { return r < RR ? kv[r][j] : sK[w][r - RR][j][lane]; };
-    // 1 / a of the rows this lane group finishes after the row hop: chunk c = lane >> 3
-    // of each half (rows 2c, 2c + 1 and 16 + 2c, 16 + 2c + 1 of the wave's 32)
-    const int rc = lane >> 3;
-    T ia[4];
-    ia[0] = 1.0 / p.a[row0 + 2 * rc];
-    ia[1] = 1.0 / p.a[row0 + 2 * rc + 1];
-    ia[2] = 1.0 / p.a[row0 + 16 + 2 * rc];
-    ia[3] = 1.0 / p.a[row0 + 16 + 2 * rc + 1];
-    // hop-B consumer: chunk tid -> columns col0 + 2 tid, + 1
-    const T bch0 = p.b[col0 + 2 * tid], bch1 = p.b[col0 + 2 * tid + 1];
+    auto kget = [&](int a, int b, int h) -> D2 { return b < RB ? kr[a][b][h] : sK[w][a][h][lane]; };
+    // row hop: thread -> chunk gc (rows 2 gc, 2 gc + 1 of the tile), member gq
+    const int gc = 8 * w + (lane >> 3), gq = lane & 7;
+    // hop B: lane < 32 polls chunk 32 w + lane of the tile (columns cw + 2 lane, + 1)
+    const int hch = 32 * w + (lane & 31);
     // reducer (wave 0): chunk r_cc = lane % CPR of this workgroup's range, producers
     // q = lane / CPR + LPC k
     const int LPC = kWave / CPR;
     const int r_cc = lane & (CPR - 1), r_qlo = lane / CPR;
     const int r_ch = rb * CPR + r_cc;
     const bool r_ok = r_ch < nch;
-    T rb0 = 0, rb1 = 0;
-    if (w == 0 && r_ok) {
-        rb0 = p.b[col0 + 2 * r_ch];
-        rb1 = p.b[col0 + 2 * r_ch + 1];
-    }
-    T sp0 = 1, sp1 = 1;  // the reducer's previous sums S[k - 1]
 
+    // the marginals and the reducer's previous sums live in LDS (registers hold K)
     const T u0 = 1.0 / (T)n_, v0 = 1.0 / (T)m_;
-    if (tid < 5) s_ep[tid] = -1;
+    if (tid < 6) s_ep[tid] = -1;
     for (int q = tid; q < TC; q += blockDim.x) {
         vhist[0][q] = vhist[1][q] = v0;
-        vcur[q] = 0;
+        bsh[q] = p.b[col0 + q];
     }
-    if (tid < TR) uhist[0][tid] = uhist[1][tid] = u0;
+    if (tid < TR) {
+        uhist[0][tid] = uhist[1][tid] = u0;
+        iash[tid] = 1.0 / p.a[row0 + tid];
+    }
+    if (tid < kWave) spsh[0][tid] = spsh[1][tid] = 1.0;
     __syncthreads();
 
     const __amdgpu_buffer_rsrc_t rs = sums_rsrc(p.gran);
@@ -300,39 +313,46 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
         return p.off_colb + ((uint32_t)((e & 1) * ncb + cb) * (uint32_t)nrb + (uint32_t)j) * p.bstride;
     };
 
-    // column partials of rows [R0, R0 + NR) of this wave against u (LDS, wave-uniform
-    // reads), accumulated into acc in ascending row order
-    auto col_acc = [&](D2 (&acc)[4], const T* ur, auto r0c) {
-        constexpr int R0 = decltype(r0c)::value;
+    // K^T u over the lane's 8 rows for each column block b, summed over the 16 lanes of a
+    // column (lane bits 3..0: row mirror and half mirror with keep / send, then quad ^2,
+    // ^1 -- every step adds two disjoint lane sets), then published per wave as chunks
+    // (columns i = 0, 1 and 2, 3 of the lane group) by lanes rr = 0 and 8
+    auto col_publish = [&](const T (&u)[NA], int e, int flag) {
 #pragma unroll
-        for (int r = R0; r < R0 + 16; r += 2) {
-            const D2 uu = *reinterpret_cast<const D2*>(ur + r);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                acc[j] = __builtin_elementwise_fma(kget(r, j), D2{uu[0], uu[0]}, acc[j]);
-                acc[j] = __builtin_elementwise_fma(kget(r + 1, j), D2{uu[1], uu[1]}, acc[j]);
+        for (int b = 0; b < NB; ++b) {
+            T c0, c1, c2, c3;
+            {
+                const D2 k0 = kget(0, b, 0), k1 = kget(0, b, 1);
+                c0 = k0[0] * u[0];
+                c1 = k0[1] * u[0];
+                c2 = k1[0] * u[0];
+                c3 = k1[1] * u[0];
             }
+#pragma unroll
+            for (int a = 1; a < NA; ++a) {
+                const D2 k0 = kget(a, b, 0), k1 = kget(a, b, 1);
+                c0 = fma(k0[0], u[a], c0);
+                c1 = fma(k0[1], u[a], c1);
+                c2 = fma(k1[0], u[a], c2);
+                c3 = fma(k1[1], u[a], c3);
+            }
+            const D2 q01 = D2{c0, c1}, q23 = D2{c2, c3};
+            const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0;
+            // bit 3: keep i in {2, 3} (upper) or {0, 1}
+            const T k0 = b3 ? q23[0] : q01[0], k1 = b3 ? q23[1] : q01[1];
+            const T s0 = b3 ? q01[0] : q23[0], s1 = b3 ? q01[1] : q23[1];
+            const T r0 = k0 + dpp_lane<0x140>(s0), r1 = k1 + dpp_lane<0x140>(s1);
+            // bit 2: keep i = 2 b3 + b2
+            const T kk = b2 ? r1 : r0, ss = b2 ? r0 : r1;
+            T t = kk + dpp_lane<0x141>(ss);
+            t += dpp_lane<0x4E>(t);
+            t += dpp_lane<0xB1>(t);
+            // the chunk's second column (i + 1) sits in the lanes with bit 2 flipped
+            const T o = dpp_lane<0x141>(t);
+            if ((lane & 7) == 0)
+                gstore_col(rs, cola(e, rb) + (uint32_t)(32 * w + 8 * b + 2 * g + (b3 ? 1 : 0)) * 16,
+                           dchunk(t, o, e, flag), xl);
         }
-    };
-    auto col_store = [&](const D2 (&acc)[4]) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            *reinterpret_cast<D2*>(&colbuf[w][(j >> 1) * 256 + lane * 4 + (j & 1) * 2]) = acc[j];
-    };
-    auto col_partials = [&](const T* ur) {
-        D2 acc[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = D2{0.0, 0.0};
-        col_acc(acc, ur, std::integral_constant<int, 0>{});
-        col_acc(acc, ur, std::integral_constant<int, 16>{});
-        col_store(acc);
-    };
-    // hop A: the workgroup's column partials (after the barrier), epoch e; flag = non-finite u
-    auto publish_cols = [&](int e, int flag) {
-        D2 s = *reinterpret_cast<const D2*>(&colbuf[0][2 * tid]);
-#pragma unroll
-        for (int ww = 1; ww < NW; ++ww) s += *reinterpret_cast<const D2*>(&colbuf[ww][2 * tid]);
-        gstore_col(rs, cola(e, rb) + (uint32_t)tid * 16, dchunk(s[0], s[1], e, flag), xl);
     };
     // reducer (wave 0): S[e - 1] of this workgroup's chunk range from the nrb producers of
     // epoch e in a fixed order; hop B carries the OR of their flags and (need) the error
@@ -374,8 +394,10 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
         if (CPR <= 32) { s0 += wave_xor<T, 32>(s0); s1 += wave_xor<T, 32>(s1); }
         const int bad = __any(fl) ? 1 : 0;
         T term = 0;
+        const T sp0 = spsh[0][lane], sp1 = spsh[1][lane];
         if (need) {
             if (r_ok) {
+                const T rb0 = bsh[2 * r_ch], rb1 = bsh[2 * r_ch + 1];
                 const T r0 = (rb0 / sp0) * s0 - rb0, r1 = (rb1 / sp1) * s1 - rb1;
                 term = r0 * r0 + r1 * r1;
             }
@@ -386,43 +408,43 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
             if (CPR > 16) term += wave_xor<T, 16>(term);
             if (CPR > 32) term += wave_xor<T, 32>(term);
         }
-        sp0 = s0;
-        sp1 = s1;
+        spsh[0][lane] = s0;
+        spsh[1][lane] = s1;
         if (lane < CPR && r_ok) gstore_col(rs, colb(e, rb) + (uint32_t)r_cc * 16, dchunk(s0, s1, e, bad), xl);
         if (need && lane == 0 && rb < nred) gstore_col(rs, colb(e, rb) + (uint32_t)CPR * 16, echunk(term, e), xl);
         deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
         return ok;
     };
-    // hop B: S[e - 1] of this tile's columns -> v into vcur; the tile's error partial into
-    // s_E.  Returns bit 0 = producer flag, 1 = stall, 2 = bad v.
-    auto gather_b = [&](int e, bool need) -> int {
+    // hop B (per wave): S[e - 1] of this wave's 32 chunks -> v into vcur[w]; wave 0 also
+    // (need) the error terms of the nred reducers -> its tile's error partial.  Returns
+    // bit 0 = producer flag, 1 = stall, 2 = bad v (this wave's columns only).
+    auto gather_b = [&](int e, bool need, T& sE) -> int {
         int fl = 0;
-        {
-            const uint32_t off = colb(e, tid / CPR) + (uint32_t)(tid & (CPR - 1)) * 16;
+        if (lane < 32) {
+            const uint32_t off = colb(e, hch / CPR) + (uint32_t)(hch & (CPR - 1)) * 16;
             I4 x;
             if (!poll64<false>(rs, off, (unsigned)e, deadline, x)) fl |= 2;
             fl |= dchunk_flag(x);
             const T s0 = dchunk_v0(x), s1 = dchunk_v1(x);
-            const T v0n = bch0 / s0, v1n = bch1 / s1;
+            const D2 bb = *reinterpret_cast<const D2*>(&bsh[2 * hch]);
+            const T v0n = bb[0] / s0, v1n = bb[1] / s1;
             if (s0 == 0.0 || !finite_val(v0n) || s1 == 0.0 || !finite_val(v1n)) fl |= 4;
-            *reinterpret_cast<D2*>(&vcur[2 * tid]) = D2{v0n, v1n};
+            *reinterpret_cast<D2*>(&vcur[w][2 * lane]) = D2{v0n, v1n};
         }
-        if (w == 3 && need) {
+        if (w == 0 && need) {
             T ep = 0;
-            if (lane < nred) {
+            if (lane >= 32 && lane - 32 < nred) {
                 I4 x;
-                if (!poll64<true>(rs, colb(e, lane) + (uint32_t)CPR * 16, (unsigned)e, deadline, x)) fl |= 2;
+                if (!poll64<true>(rs, colb(e, lane - 32) + (uint32_t)CPR * 16, (unsigned)e, deadline, x)) fl |= 2;
                 ep = echunk_v(x);
             }
-            ep = wave_sum<T>(ep);
-            if (lane == 0) s_E = ep;
+            sE = wave_sum<T>(ep);
         }
-        if (fl & 1) s_ep[2] = e;
-        if (fl & 2) s_ep[1] = e;
-        if (fl & 4) s_ep[3] = e;
-        __syncthreads();
-        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
-        return (s_ep[2] == e ? 1 : 0) | (s_ep[1] == e ? 2 : 0) | (s_ep[3] == e ? 4 : 0);
+        // the wave's own LDS writes complete before its reads (in-order LDS per wave); the
+        // clobber keeps the compiler from moving the reads of vcur above the writes
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int wf = __any(fl & 1) ? 1 : 0, ws = __any(fl & 2) ? 2 : 0, wb = __any(fl & 4) ? 4 : 0;
+        return wf | ws | wb;
     };
     // total error from the ncb column tiles' partials (row-hop error chunks of epoch er)
     auto err_total = [&](int er, T& tot) -> bool {
@@ -436,124 +458,134 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
         ev += wave_xor<T, 1>(ev);
         ev += wave_xor<T, 2>(ev);
         ev += wave_xor<T, 4>(ev);
-        tot = lane0_f64(ev);
+        tot = ev;
         return __all(ok);
     };
     auto to_err = [&](T e) -> double { return p.err_squared ? e : sqrt(e); };
     auto stop_ok = [&](double err) -> bool { return p.err_squared ? !(err > p.stop_thr) : (err < p.stop_thr); };
 
     // ---- prologue: S[0] = K^T u0 (epoch 1)
-    col_partials(&uhist[0][w * R]);
-    __syncthreads();
-    publish_cols(1, 0);
+    {
+        T uu[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) uu[a] = u0;
+        col_publish(uu, 1, 0);
+    }
     int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
     bool done = false;
     if (w == 0 && !reduce(1, false)) s_ep[1] = 1;
     int chk = 0;
+    T sE = 0;
 
     for (int it = 0; it < p.max_iter; ++it) {
         asm volatile("" : "+v"(tid), "+v"(lane));
         const int e = it + 1;
         const bool check = it >= 1 && chk == 0;
         OTF_M64ST(it, 0);
-        const int fl = gather_b(e, check);
+        {
+            const int fl = gather_b(e, check, sE);
+            if (lane == 0) {
+                if (fl & 2) s_ep[1] = e;
+                if (fl & 1) s_ep[2] = e;
+                if (fl & 4) s_ep[3] = e;
+            }
+        }
         OTF_M64ST(it, 1);
-        if (fl & 2) { status = OTF_SK_TIMEOUT; done = true; break; }
-        if (fl & 1) {
+        if (it >= 1) chk = chk + 1 == p.check_every ? 0 : chk + 1;
+        // row partials K v of the lane's 8 rows over its 16 columns, then the 4 lanes of a
+        // row (bits 5, 4: lane (b5, b4) ends with rows a = 4 b5 + 2 b4 + 0, 1)
+        {
+            T pr[NA];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const D2 va = *reinterpret_cast<const D2*>(&vcur[w][16 * b + 4 * g]);
+                const D2 vb = *reinterpret_cast<const D2*>(&vcur[w][16 * b + 4 * g + 2]);
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    const D2 k0 = kget(a, b, 0), k1 = kget(a, b, 1);
+                    T s = b == 0 ? k0[0] * va[0] : fma(k0[0], va[0], pr[a]);
+                    s = fma(k0[1], va[1], s);
+                    s = fma(k1[0], vb[0], s);
+                    pr[a] = fma(k1[1], vb[1], s);
+                }
+            }
+            T y[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) y[k] = swap_sum<32>(pr[k], pr[k + 4]);
+            const T z0 = swap_sum<16>(y[0], y[2]), z1 = swap_sum<16>(y[1], y[3]);
+            const int a0 = 4 * (lane >> 5) + 2 * ((lane >> 4) & 1);
+            rowbuf[w][rr + 16 * a0] = z0;
+            rowbuf[w][rr + 16 * a0 + 16] = z1;
+        }
+        OTF_M64ST(it, 2);
+        __syncthreads();  // B1
+        // every completed barrier re-arms the stall deadline (a stall, not a long solve,
+        // times out)
+        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+        if (s_ep[1] == e) { status = OTF_SK_TIMEOUT; done = true; break; }
+        if (s_ep[2] == e) {
             last_good = it - 2; niter = it - 1; status = OTF_SK_NUMERICAL_BREAK; brk = it - 1;
             done = true;
             break;
         }
-        const int vbad_cb = (fl & 4) ? 1 : 0;
-        D2 vn[4];
+        const int vbad_cb = s_ep[3] == e ? 1 : 0;
+        if (w == 0) {
+            // the tile's 128 row partials over its 512 columns: the 8 stripes in wave order
+            D2 s = *reinterpret_cast<const D2*>(&rowbuf[0][2 * lane]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) vn[j] = *reinterpret_cast<const D2*>(&vcur[(j >> 1) * 256 + lane * 4 + (j & 1) * 2]);
-        // Two halves of the wave's 32 rows, pipelined: each half's row partials are
-        // published as soon as its wave totals are known, so the row hop of rows 0..15 is
-        // in flight while rows 16..31 are summed, and rows 16..31's hop while the column
-        // partials of rows 0..15 run.  Lane group c = lane >> 3 ends a half with its rows
-        // 2c, 2c + 1.
-        if (it >= 1) chk = chk + 1 == p.check_every ? 0 : chk + 1;
-        const bool hop = ncb > 1;
-        T t[4];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            T rp[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                D2 acc = kget(16 * h + r, 0) * vn[0];
-#pragma unroll
-                for (int j = 1; j < 4; ++j) acc = __builtin_elementwise_fma(kget(16 * h + r, j), vn[j], acc);
-                rp[r] = acc[0] + acc[1];
-            }
-            const T mine = wave_row_totals<T, 16>(rp, lane), oth = dpp_lane<0x141>(mine);
-            const bool odd = (lane & 4) != 0;
-            t[2 * h] = odd ? oth : mine;
-            t[2 * h + 1] = odd ? mine : oth;
-            if (hop && (lane & 7) == 0)
-                gstore(rs, rowx(e, cb) + (uint32_t)(w * 16 + 8 * h + rc) * 16, dchunk(t[2 * h], t[2 * h + 1], e, vbad_cb));
+            for (int ww = 1; ww < NW; ++ww) s += *reinterpret_cast<const D2*>(&rowbuf[ww][2 * lane]);
+            gstore(rs, rowx(e, cb) + (uint32_t)lane * 16, dchunk(s[0], s[1], e, vbad_cb));
+            if (check && lane == 0) gstore(rs, rowx(e, cb) + 64 * 16, echunk(sE, e));
         }
-        OTF_M64ST(it, 2);
-        if (hop && check && w == 0 && lane == 1) gstore(rs, rowx(e, cb) + 64 * 16, echunk(s_E, e));
-        T errv = hop ? 0.0 : s_E;
-        int vbad = vbad_cb, stall = 0, badu = 0;
-        const int q = lane & 7;
-        const bool act = hop && q < ncb;
-        D2 cacc[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cacc[j] = D2{0.0, 0.0};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            T th0 = t[2 * h], th1 = t[2 * h + 1];
-            if (hop) {
-                // gather the ncb members' chunk of this half (lane (c, q): member q)
-                I4 x = I4{0, 0, 0, 0};
-                if (act && !poll64<false>(rs, rowx(e, q) + (uint32_t)(w * 16 + 8 * h + rc) * 16, (unsigned)e, deadline, x))
-                    stall = 1;
-                th0 = act ? dchunk_v0(x) : 0.0;
-                th1 = act ? dchunk_v1(x) : 0.0;
-                if (__any(act && dchunk_flag(x))) vbad = 1;
-                th0 += dpp_lane<0xB1>(th0);
-                th1 += dpp_lane<0xB1>(th1);
-                th0 += dpp_lane<0x4E>(th0);
-                th1 += dpp_lane<0x4E>(th1);
-                th0 += dpp_lane<0x141>(th0);
-                th1 += dpp_lane<0x141>(th1);
-            }
-            // u of this half's two rows of the lane group; the group's first lane writes
-            // them to the history, which the wave then reads back as wave-uniform values
-            const T un0 = 1.0 / (th0 * ia[2 * h]), un1 = 1.0 / (th1 * ia[2 * h + 1]);
-            if (__any(!finite_val(un0) || !finite_val(un1))) badu = 1;
-            if ((lane & 7) == 0) *reinterpret_cast<D2*>(&uhist[it & 1][w * R + 16 * h + 2 * rc]) = D2{un0, un1};
-            // the wave's own LDS writes complete before its reads (in-order LDS per wave);
-            // the clobber keeps the compiler from hoisting the reads above the writes
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (h == 0) col_acc(cacc, &uhist[it & 1][w * R], std::integral_constant<int, 0>{});
-            else col_acc(cacc, &uhist[it & 1][w * R], std::integral_constant<int, 16>{});
-        }
-        col_store(cacc);
-        if (hop && check && !err_total(e, errv)) stall = 1;
-        stall = __any(stall) ? 1 : 0;
         OTF_M64ST(it, 3);
+        // row hop: the ncb members' chunk gc (lane (gc, gq): member gq), summed over the
+        // 8 lanes in a fixed order -> u of rows 2 gc, 2 gc + 1
+        {
+            I4 x = I4{0, 0, 0, 0};
+            int stall = 0;
+            const bool act = gq < ncb;
+            if (act && !poll64<false>(rs, rowx(e, gq) + (uint32_t)gc * 16, (unsigned)e, deadline, x)) stall = 1;
+            T th0 = act ? dchunk_v0(x) : 0.0, th1 = act ? dchunk_v1(x) : 0.0;
+            const int vb = act && dchunk_flag(x);
+            th0 += dpp_lane<0xB1>(th0);
+            th1 += dpp_lane<0xB1>(th1);
+            th0 += dpp_lane<0x4E>(th0);
+            th1 += dpp_lane<0x4E>(th1);
+            th0 += dpp_lane<0x141>(th0);
+            th1 += dpp_lane<0x141>(th1);
+            const D2 ia = *reinterpret_cast<const D2*>(&iash[2 * gc]);
+            const T un0 = 1.0 / (th0 * ia[0]), un1 = 1.0 / (th1 * ia[1]);
+            const bool bu = gq == 0 && (!finite_val(un0) || !finite_val(un1));
+            if (gq == 0) {
+                uhist[it & 1][upos(2 * gc)] = un0;
+                uhist[it & 1][upos(2 * gc + 1)] = un1;
+            }
+            if (w == 0 && check) {
+                T ev;
+                if (!err_total(e, ev)) stall = 1;
+                if (lane == 0) s_err = ev;
+            }
+            const bool any_st = __any(stall), any_vb = __any(vb), any_bu = __any(bu);
+            if (lane == 0) {
+                if (any_st) s_ep[4] = it;
+                if (any_vb) s_ep[5] = it;
+                if (any_bu) s_ep[0] = it;
+            }
+        }
+        OTF_M64ST(it, 4);
+        __syncthreads();  // B2
+        deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
+        OTF_M64ST(it, 5);
+        if (s_ep[4] == it) { status = OTF_SK_TIMEOUT; done = true; break; }
         double err = 0.0;
         int dec = 0;
         if (check) {
-            err = to_err(errv);
+            err = to_err(s_err);
             if (stop_ok(err)) dec = 1;
-        }
-        if (dec == 0 && vbad) dec = 2;
-        const int slot = it & 1;
-        *reinterpret_cast<D2*>(&vhist[slot][2 * tid]) = *reinterpret_cast<const D2*>(&vcur[2 * tid]);
-        if (badu) s_ep[0] = it;
-        if (stall) s_ep[4] = it;
-        OTF_M64ST(it, 4);
-        __syncthreads();
-        OTF_M64ST(it, 5);
-        if (s_ep[4] == it) { status = OTF_SK_TIMEOUT; done = true; break; }
-        if (check) {
             if (lead) p.errlog[n_err] = err;
             ++n_err;
         }
+        if (dec == 0 && s_ep[5] == it) dec = 2;
         if (dec == 1) {
             last_good = it - 1; niter = it - 1; status = OTF_SK_CONVERGED;
             done = true;
@@ -564,7 +596,19 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
             done = true;
             break;
         }
-        publish_cols(e + 1, s_ep[0] == it ? 1 : 0);
+        // v of this iteration into the history (this wave's stripe)
+        if (lane < 32)
+            *reinterpret_cast<D2*>(&vhist[it & 1][cw + 2 * lane]) = *reinterpret_cast<const D2*>(&vcur[w][2 * lane]);
+        {
+            T uu[NA];
+#pragma unroll
+            for (int q = 0; q < NA; q += 2) {
+                const D2 t2 = *reinterpret_cast<const D2*>(&uhist[it & 1][rr * 8 + q]);
+                uu[q] = t2[0];
+                uu[q + 1] = t2[1];
+            }
+            col_publish(uu, e + 1, s_ep[0] == it ? 1 : 0);
+        }
         OTF_M64ST(it, 6);
         if (w == 0 && !reduce(e + 1, chk == 0)) s_ep[1] = e + 1;
         OTF_M64ST(it, 7);
@@ -572,24 +616,26 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
     if (!done && p.max_iter > 0) {
         const int it = p.max_iter - 1;
         const int e = p.max_iter + 1;
-        const int fl = gather_b(e, (it % p.check_every) == 0);
-        if (fl & 2) {
+        const bool need = (it % p.check_every) == 0;
+        {
+            const int fl = gather_b(e, need, sE);
+            if (lane == 0) {
+                if (fl & 2) s_ep[1] = e;
+                if (fl & 1) s_ep[2] = e;
+            }
+        }
+        __syncthreads();
+        if (s_ep[1] == e) {
             status = OTF_SK_TIMEOUT;
-        } else if (fl & 1) {
+        } else if (s_ep[2] == e) {
             last_good = it - 1; niter = it; status = OTF_SK_NUMERICAL_BREAK; brk = it;
         } else {
             last_good = it; niter = it;
-            if ((it % p.check_every) == 0) {
-                T errv = s_E;
-                int stall = 0;
-                if (ncb > 1) {
-                    if (w == 0 && lane == 8) gstore(rs, rowx(e, cb) + 64 * 16, echunk(s_E, e));
-                    if (!err_total(e, errv)) stall = 1;
-                    if (stall) s_ep[4] = e;
-                    __syncthreads();
-                    stall = s_ep[4] == e;
-                }
-                if (stall) {
+            if (need && w == 0) {
+                // only wave 0 (the lead's) needs the total: it writes the log and the status
+                if (lane == 0) gstore(rs, rowx(e, cb) + 64 * 16, echunk(sE, e));
+                T errv;
+                if (!err_total(e, errv)) {
                     status = OTF_SK_TIMEOUT;
                 } else {
                     const double err = to_err(errv);
@@ -605,33 +651,29 @@ __global__ __launch_bounds__(256) void sk_mesh64_kernel(SkMesh64Args p) {
     OTF_M64PRO(3);
     __syncthreads();
     const int hs = last_good & 1;
-    D2 vo[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        vo[j] = last_good >= 0 ? *reinterpret_cast<const D2*>(&vhist[hs][(j >> 1) * 256 + lane * 4 + (j & 1) * 2])
-                               : D2{v0, v0};
-    if (cb == 0 && lane < R) p.u_out[row0 + lane] = last_good >= 0 ? uhist[hs][w * R + lane] : u0;
-    if (rb == 0 && w == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            *reinterpret_cast<D2*>(p.v_out + col0 + (j >> 1) * 256 + lane * 4 + (j & 1) * 2) = vo[j];
-    }
+    if (cb == 0 && tid < TR) p.u_out[row0 + tid] = last_good >= 0 ? uhist[hs][upos(tid)] : u0;
+    if (rb == 0 && tid < TC / 2)
+        *reinterpret_cast<D2*>(p.v_out + col0 + 2 * tid) =
+            last_good >= 0 ? *reinterpret_cast<const D2*>(&vhist[hs][2 * tid]) : D2{v0, v0};
     if (p.P) {
         TP* P = (TP*)p.P;
+        T uo[NA];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const T ur = last_good >= 0 ? uhist[hs][w * R + r] : u0;
-            TP* prow = P + (int64_t)(row0 + r) * p.ldp + col0 + lane * 4;
+        for (int a = 0; a < NA; ++a) uo[a] = last_good >= 0 ? uhist[hs][rr * 8 + a] : u0;
 #pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                const D2 k0 = kget(r, 2 * g), k1 = kget(r, 2 * g + 1);
-                const D2 o0 = (ur * k0) * vo[2 * g], o1 = (ur * k1) * vo[2 * g + 1];
+        for (int b = 0; b < NB; ++b) {
+            const D2 va = last_good >= 0 ? *reinterpret_cast<const D2*>(&vhist[hs][cw + 16 * b + 4 * g]) : D2{v0, v0};
+            const D2 vb = last_good >= 0 ? *reinterpret_cast<const D2*>(&vhist[hs][cw + 16 * b + 4 * g + 2]) : D2{v0, v0};
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                TP* prow = P + (int64_t)(row0 + rr + 16 * a) * p.ldp + col0 + cw + 16 * b + 4 * g;
+                const D2 o0 = (uo[a] * kget(a, b, 0)) * va, o1 = (uo[a] * kget(a, b, 1)) * vb;
                 if constexpr (sizeof(TP) == 8) {
-                    *reinterpret_cast<D2*>(prow + g * 256) = o0;
-                    *reinterpret_cast<D2*>(prow + g * 256 + 2) = o1;
+                    *reinterpret_cast<D2*>(prow) = o0;
+                    *reinterpret_cast<D2*>(prow + 2) = o1;
                 } else {
                     using F4 = __attribute__((ext_vector_type(4))) float;
-                    *reinterpret_cast<F4*>(prow + g * 256) = F4{(float)o0[0], (float)o0[1], (float)o1[0], (float)o1[1]};
+                    *reinterpret_cast<F4*>(prow) = F4{(float)o0[0], (float)o0[1], (float)o1[0], (float)o1[1]};
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -655,10 +697,10 @@ hipError_t launch_mesh64_t(int grid, SkMesh64Args& p, hipStream_t s) {
     const void* k = (p.nrb == 32 && p.ncb == 8) ? (const void*)sk_mesh64_kernel<TP, 32, 8>
                                                 : (const void*)sk_mesh64_kernel<TP, 0, 0>;
     int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
     if (e != hipSuccess) return e;
     if (per_cu < 1 || grid > per_cu * device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
-    return hipLaunchKernel(k, dim3(grid), dim3(256), args, 0, s);
+    return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
 }
 
 constexpr size_t kM64RegBytes = 9 * 256;  // 8 XCC counters + the barrier word, 256 B each

@@ -127,7 +127,8 @@ def test_precision_auto_promotes_when_the_shift_cannot_apply(orc, dev, metric_in
     assert nrel(r.plan.cpu().numpy(), Pr) < TOL32
     r = ops.sinkhorn(a, a, C, 1e-3, max_iter=100, stop_thr=0.0, cost_scale=cmax, precision="auto")
     assert r.u.dtype == torch.float64 and not r.shifted
-    Cs = (C / cmax).double().cpu().numpy()
+    # the device scales in float64 (C * (-1 / (reg cmax))): the same float64 quotient here
+    Cs = C.double().cpu().numpy() / float(cmax)
     Pr3, _, _, ir = orc.sinkhorn_knopp(np.full(N, 1.0 / N), np.full(N, 1.0 / N), Cs, 1e-3, 100, 0.0)
     i = r.info()
     assert (i["niter"], i["break_iter"]) == (ir["niter"], ir["break_iter"])

@@ -69,8 +69,8 @@ int main(int argc, char** argv) {
     printf("  roles -> K formed (C read, exp) %7.3f us\n", pa[1] / 256 * 0.01);
     printf("  K formed -> loop end            %7.3f us\n", pa[2] / 256 * 0.01);
     printf("  first start -> last loop end    %7.3f us\n", (tend - t0) * 0.01);
-    const char* names[7] = {"hop B wait + v + barrier", "row partials (2 x 16 rows)", "row hop (publish + gather)",
-                            "u + col partials", "barrier", "publish cols", "reduce (wave 0)"};
+    const char* names[7] = {"hop B (poll, v)", "row partials (8 rows x 16 cols)", "B1 + row publish (wave 0)",
+                            "row hop gather + u", "B2", "col partials + publish", "reduce (wave 0)"};
     double acc[8] = {0};
     int cnt = 0;
     for (int r = 0; r < 256; ++r)
