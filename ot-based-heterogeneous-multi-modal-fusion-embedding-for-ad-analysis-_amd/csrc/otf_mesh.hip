@@ -56,7 +56,8 @@ constexpr int kMeshRW = 16;     // rows per wave
 constexpr int kMeshTR = 128;    // rows per tile
 constexpr int kMeshTC = 512;    // columns per tile
 constexpr int kMeshNCH = 256;   // 16-B chunks (two {value, tag} granules) per 512 columns
-constexpr int kMeshMaxNcb = 8;  // row hop: ncb producers x 8 chunks <= one chunk per lane
+constexpr int kMeshMaxNcb = 16; // row hop: ncb members x 8 chunks <= two chunks per lane
+constexpr int kMeshXccNcb = 8;   // the XCC-local column path: one column tile per XCC
 constexpr int kMeshMinNrb = 4;  // reducer chunks per workgroup (CPR) <= 64
 constexpr int kMeshMaxNrb = 64; // hop-B error chunks: one per lane of one wave
 constexpr uint32_t kRowStride = 1280;  // per producer: 64 row chunks + the error chunk
@@ -85,6 +86,14 @@ struct SkMeshArgs {
     unsigned long long timeout_ticks;
     unsigned long long reg_ticks;  // the first wait (registration / first hop)
     ShiftArgs sh;                  // shifted kernel (SH instances): offsets + initial scalings
+    // cross-rank form (XR instances, otf_sinkhorn_xsweep on a shape the mesh takes): these
+    // are this rank's rows of a problem of n_total rows; after summing its producers every
+    // reducer stores its chunks' partial into every rank's exchange buffer (xr[r], the
+    // peers' buffers as mapped here; [2 solve parities][2 epoch parities][8 ranks][mc]
+    // chunks, the xsweep layout) and sums the world's partials in rank order
+    int n_total, xrank, xworld, xpar, mc;
+    unsigned xep;  // epoch base of this solve on the exchange (the same on every rank)
+    unsigned char* xr[8];
 };
 
 // Diagnostic build only (-DOTF_MESH_STAMPS, tools/stamps_mesh.hip): per-hop wall-clock
@@ -132,7 +141,7 @@ constexpr int pow2_at_least(int x) { return x <= 1 ? 1 : 2 * pow2_at_least((x + 
 // spills (v_readlane / v_writelane per branch) lengthened every phase of the generic form.
 // SH: the shifted POT kernel K~ = 2^(C ks + A_i + B_j) (otf_persist.h ShiftArgs), formed
 // once in the prologue like K; the loop is unchanged.
-template <typename CT, typename TP, int KQ, int SNRB, int SNCB, bool SH>
+template <typename CT, typename TP, int KQ, int SNRB, int SNCB, bool SH, bool XR = false>
 __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     using T = float;
     constexpr int G = 2, VEC = 4, R = kMeshRW, NW = kMeshNW, TR = kMeshTR, TC = kMeshTC;
@@ -311,7 +320,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     const bool rc0 = r_ok && 2 * r_ch < ncols, rc1 = r_ok && 2 * r_ch + 1 < ncols;
     T sp0 = 1, sp1 = 1;  // the reducer's previous sums S[k - 1]
 
-    const T u0 = (T)1 / (T)n_, v0 = (T)1 / (T)m_;
+    const T u0 = (T)1 / (T)(XR ? p.n_total : n_), v0 = (T)1 / (T)m_;
     if (tid < 5) s_ep[tid] = -1;
     if (tid < kWave) red_sp[tid] = F2{1.f, 1.f};
     if (tid == 0) red_cnt = 0;
@@ -447,7 +456,49 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         if (CPR <= 8) { s0 += wave_xor<T, 8>(s0); s1 += wave_xor<T, 8>(s1); }
         if (CPR <= 16) { s0 += wave_xor<T, 16>(s0); s1 += wave_xor<T, 16>(s1); }
         if (CPR <= 32) { s0 += wave_xor<T, 32>(s0); s1 += wave_xor<T, 32>(s1); }
-        const int bad = __any(fl) ? 1 : 0;
+        int bad = __any(fl) ? 1 : 0;
+        if constexpr (XR) {
+            // across ranks: this rank's partial of the reducer's chunks -> every rank's
+            // exchange buffer (system-scope stores over xGMI), then the world's partials
+            // of the same chunks from this rank's buffer, summed in rank order: every rank
+            // derives the same S, bit for bit, and takes POT's decisions at the same epoch
+            const unsigned ex = (p.xep + (unsigned)e) & 0x3fffffffu;
+            const bool xa = lane < CPR && r_ok;
+            const uint32_t gch = (uint32_t)(cb * kMeshNCH + r_ch);
+            const uint32_t xs0 = (uint32_t)((2 * (p.xpar & 1) + (int)(ex & 1)) * 8);
+            if (xa) {
+                const I4 mine = chunk2(s0, s1, (int)(ex << 2) | bad);
+                for (int r = 0; r < p.xworld; ++r)
+                    gstore_sys(sums_rsrc(p.xr[r]), ((xs0 + (uint32_t)p.xrank) * (uint32_t)p.mc + gch) * 16u, mine);
+            }
+            const __amdgpu_buffer_rsrc_t rxx = sums_rsrc(p.xr[p.xrank]);
+            I4 y[kXMaxRanks];
+            for (;;) {
+                unsigned pr = 0;
+#pragma unroll
+                for (int r = 0; r < kXMaxRanks; ++r)
+                    if (xa && r < p.xworld) {
+                        y[r] = gload_sys(rxx, ((xs0 + (uint32_t)r) * (uint32_t)p.mc + gch) * 16u);
+                        if (!chunk_at(y[r], ex)) pr |= 1u << r;
+                    }
+                if (!__any(pr != 0)) break;
+                if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
+                __builtin_amdgcn_s_sleep(OTF_MESH_SLEEP);
+            }
+            int xf = 0;
+            if (xa) {
+                s0 = 0;
+                s1 = 0;
+#pragma unroll
+                for (int r = 0; r < kXMaxRanks; ++r)
+                    if (r < p.xworld) {
+                        s0 += chunk_v0(y[r]);
+                        s1 += chunk_v1(y[r]);
+                        xf |= y[r][1] & 1;
+                    }
+            }
+            bad = __any(xf) ? 1 : 0;
+        }
         // POT's marginal error of the iterate whose v = b / S[e - 2]
         const F2 sp = RW > 1 ? red_sp[lane] : F2{sp0, sp1};
         T term = 0;
@@ -527,6 +578,7 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
         ev += wave_xor<T, 1>(ev);
         ev += wave_xor<T, 2>(ev);
         ev += wave_xor<T, 4>(ev);
+        if (ncb > 8) ev += wave_xor<T, 8>(ev);
         tot = __builtin_bit_cast(T, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ev)));
         return __all(ok);
     };
@@ -626,7 +678,20 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
             OTF_MSTAMP(it, 9, 448);
             t0 = act ? chunk_v0(x) : (T)0;
             t1 = act ? chunk_v1(x) : (T)0;
-            vbad = __any(act && (x[1] & 1)) ? 1 : 0;
+            int vb = act && (x[1] & 1);
+            if (ncb > 8) {
+                // more than 8 members (m > 4096): the lane also takes member q + 8
+                const bool act2 = q + 8 < ncb;
+                I4 x2 = I4{0, 0, 0, 0};
+                if (act2) {
+                    const uint32_t off = rowx(e, q + 8) + (uint32_t)(w * 8 + rc) * 16;
+                    if (!poll_chunk<OTF_MESH_SLEEP>(rs, off, (unsigned)e, deadline, x2)) stall = 1;
+                }
+                t0 += act2 ? chunk_v0(x2) : (T)0;
+                t1 += act2 ? chunk_v1(x2) : (T)0;
+                vb |= act2 && (x2[1] & 1);
+            }
+            vbad = __any(vb) ? 1 : 0;
             t0 += dpp_f<0xB1>(t0);
             t1 += dpp_f<0xB1>(t1);
             t0 += dpp_f<0x4E>(t0);
@@ -801,11 +866,20 @@ const void* mesh_kernel_for(const SkMeshArgs& p) {
            : pow2 ? (const void*)sk_mesh_kernel<CT, TP, 4, 0, 0, SH>
                   : (const void*)sk_mesh_kernel<CT, TP, 8, 0, 0, SH>;
 }
+// the cross-rank instances (the generic shape, no shifted kernel)
+template <typename CT, typename TP>
+const void* xmesh_kernel_for(const SkMeshArgs& p) {
+    const bool pow2 = (p.nrb & (p.nrb - 1)) == 0;
+    return pow2 ? (const void*)sk_mesh_kernel<CT, TP, 4, 0, 0, false, true>
+                : (const void*)sk_mesh_kernel<CT, TP, 8, 0, 0, false, true>;
+}
 
 template <typename CT, typename TP>
 hipError_t launch_mesh_t(int grid, SkMeshArgs& p, hipStream_t s) {
     void* args[] = {&p};
-    const void* k = p.sh.A ? mesh_kernel_for<CT, TP, true>(p) : mesh_kernel_for<CT, TP, false>(p);
+    const void* k = p.xworld > 1 ? xmesh_kernel_for<CT, TP>(p)
+                    : p.sh.A     ? mesh_kernel_for<CT, TP, true>(p)
+                                 : mesh_kernel_for<CT, TP, false>(p);
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
     if (e != hipSuccess) return e;
@@ -814,6 +888,7 @@ hipError_t launch_mesh_t(int grid, SkMeshArgs& p, hipStream_t s) {
 }
 
 constexpr size_t kMeshRegBytes = 9 * 256;  // 8 XCC counters + the barrier word, 256 B each
+inline int64_t align_up_mesh(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 struct MeshShape {
     int nrb, ncb, cpr;
@@ -855,8 +930,11 @@ template <typename CT>
 hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                    double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* shift) {
+                    double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* shift,
+                    const XSweep* xs) {
     if (!mesh_supported(n, m) || !region) return hipErrorInvalidValue;
+    const bool xr = xs && xs->world > 1;
+    if (xr && (shift || xs->world > kXMaxRanks || m % kMeshTC != 0)) return hipErrorInvalidValue;
     const MeshShape sh = mesh_shape(n, m);
     if (sh.nrb * sh.ncb > device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
     SkMeshArgs p{};
@@ -885,6 +963,18 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
         const char* e = getenv("OTF_MESH_XCC");  // 0: blockIdx roles, write-through everywhere
         p.xcc_local = e ? atoi(e) : 1;
     }
+    // one column tile per XCC: more tiles than XCCs take the blockIdx roles
+    if (sh.ncb > kMeshXccNcb) p.xcc_local = 0;
+    p.n_total = n;
+    if (xr) {
+        p.n_total = xs->n_total;
+        p.xrank = xs->rank;
+        p.xworld = xs->world;
+        p.xpar = xs->solve_par;
+        p.xep = xs->ep_base;
+        p.mc = (int)(align_up_mesh(m, 64) / 2);
+        for (int r = 0; r < xs->world; ++r) p.xr[r] = xs->xr[r];
+    }
     p.info = info;
     p.errlog = errlog;
     p.u_out = u_out;
@@ -910,10 +1000,10 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
 template hipError_t run_mesh<float>(const float*, int64_t, int, int, const float*, const float*,
                                     const float*, const otf_sinkhorn_opts&, void*, float*, float*,
                                     void*, int64_t, int, otf_sinkhorn_info*, double*, bool,
-                                    hipStream_t, const ShiftArgs*);
+                                    hipStream_t, const ShiftArgs*, const XSweep*);
 template hipError_t run_mesh<_Float16>(const _Float16*, int64_t, int, int, const float*, const float*,
                                        const float*, const otf_sinkhorn_opts&, void*, float*, float*,
                                        void*, int64_t, int, otf_sinkhorn_info*, double*, bool,
-                                       hipStream_t, const ShiftArgs*);
+                                       hipStream_t, const ShiftArgs*, const XSweep*);
 
 }  // namespace otf

@@ -29,8 +29,9 @@
 //   columns  K^T u over the lane's 8 rows, the 16 lanes of a column (lane bits 3..0) by a
 //            DPP halving butterfly, published per wave straight to the column tile's
 //            reducers (no workgroup reduction);
-//   reduce   wave 0 of workgroup rb sums chunks [rb CPR, +CPR) over the nrb producers in a
-//            fixed order and publishes S (and POT's marginal-error terms).
+//   reduce   workgroup rb owns chunks [rb CPR, +CPR) of the column tile, spread over its 8
+//            waves: each sums its chunks over the nrb producers in a fixed order and
+//            publishes S (and its share of POT's marginal-error terms).
 // POT's decisions (zero / non-finite v, non-finite u, the error check and stop) ride in the
 // tags and in LDS flags keyed by epoch, read after the barriers, so every wave of every
 // workgroup takes the same decision at the same iteration.  A 16-B chunk carries two
@@ -171,7 +172,6 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     constexpr int NW = kM64NW, TR = kM64TR, TC = kM64TC, WC = kM64WC, NA = kM64NA, NB = kM64NB,
                   RB = kM64RB;
     constexpr bool FULL = SNRB != 0 && SNCB != 0;
-    constexpr int KQ = 4;  // reducer loads per lane: nrb x CPR = 256 chunks over 64 lanes
     __shared__ __attribute__((aligned(16))) D2 sK[NW][NA][2][kWave];  // column block b = 3
     __shared__ __attribute__((aligned(16))) T rowbuf[NW][TR];         // per-wave row partials
     __shared__ __attribute__((aligned(16))) T vcur[NW][WC];           // v of this iteration
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     __shared__ __attribute__((aligned(16))) T uhist[2][TR];           // slot upos(r)
     __shared__ __attribute__((aligned(16))) T bsh[TC];                // b of the tile's columns
     __shared__ __attribute__((aligned(16))) T iash[TR];               // 1 / a of its rows
-    __shared__ __attribute__((aligned(16))) T spsh[2][kWave];         // the reducer's S[k - 1]
+    __shared__ __attribute__((aligned(16))) T spsh[2][kWave];         // the reducer's S[k - 1] by chunk
     __shared__ T s_err;
     // flags keyed by epoch / iteration (keys only grow): [0] non-finite u, [1] hop-B stall,
     // [2] hop-B producer flag, [3] zero / non-finite v, [4] row-hop stall, [5] a member's
@@ -281,13 +281,12 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     const int gc = 8 * w + (lane >> 3), gq = lane & 7;
     // hop B: lane < 32 polls chunk 32 w + lane of the tile (columns cw + 2 lane, + 1)
     const int hch = 32 * w + (lane & 31);
-    // reducer (wave 0): chunk r_cc = lane % CPR of this workgroup's range, producers
-    // q = lane / CPR + LPC k
-    const int LPC = kWave / CPR;
-    const int r_cc = lane & (CPR - 1), r_qlo = lane / CPR;
+    // reducer, spread over the 8 waves: wave w sums chunks w + 8 j (j < CPR / 8) of this
+    // workgroup's range [rb CPR, +CPR); lane l < 32 polls chunk j = l / nrb of producer
+    // q = l % nrb (CPR / 8 x nrb = 32 for every nrb)
+    const int r_j = (lane & 31) / nrb, r_q = (lane & 31) & (nrb - 1);
+    const int r_cc = w + 8 * r_j;
     const int r_ch = rb * CPR + r_cc;
-    const bool r_ok = r_ch < nch;
-
     // the marginals and the reducer's previous sums live in LDS (registers hold K)
     const T u0 = 1.0 / (T)n_, v0 = 1.0 / (T)m_;
     if (tid < 6) s_ep[tid] = -1;
@@ -354,92 +353,88 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
                            dchunk(t, o, e, flag), xl);
         }
     };
-    // reducer (wave 0): S[e - 1] of this workgroup's chunk range from the nrb producers of
-    // epoch e in a fixed order; hop B carries the OR of their flags and (need) the error
-    // terms of iterate e - 2.  Returns false on a stall.
+    // reducer (every wave, its chunks of this workgroup's range): S[e - 1] from the nrb
+    // producers of epoch e summed over the producer lanes in a fixed order; hop B carries
+    // the OR of their flags and (need) the wave's error terms of iterate e - 2 in error slot
+    // w of the range.  Returns false on a stall.
     auto reduce = [&](int e, bool need) -> bool {
-        I4 x[KQ];
-        bool act[KQ];
-#pragma unroll
-        for (int k = 0; k < KQ; ++k) act[k] = r_ok && (r_qlo + LPC * k) < nrb;
+        I4 x;
         bool ok = true;
+        const uint32_t off = cola(e, r_q) + (uint32_t)r_ch * 16;
         for (;;) {
-            unsigned pend = 0;
-#pragma unroll
-            for (int k = 0; k < KQ; ++k) {
-                const int q = r_qlo + LPC * k;
-                x[k] = gload(rs, cola(e, act[k] ? q : 0) + (uint32_t)(r_ok ? r_ch : 0) * 16);
-            }
-#pragma unroll
-            for (int k = 0; k < KQ; ++k)
-                if (act[k] && !dchunk_at(x[k], (unsigned)e)) pend |= 1u << k;
-            if (!__any(pend != 0)) break;
+            x = gload(rs, off);
+            if (!__any(lane < 32 && !dchunk_at(x, (unsigned)e))) break;
             if (__builtin_amdgcn_s_memrealtime() > deadline) { ok = false; break; }
             __builtin_amdgcn_s_sleep(1);
         }
-        T s0 = 0, s1 = 0;
-        int fl = 0;
-#pragma unroll
-        for (int k = 0; k < KQ; ++k)
-            if (act[k]) {
-                s0 += dchunk_v0(x[k]);
-                s1 += dchunk_v1(x[k]);
-                fl |= dchunk_flag(x[k]);
-            }
-        if (CPR <= 1) { s0 += wave_xor<T, 1>(s0); s1 += wave_xor<T, 1>(s1); }
-        if (CPR <= 2) { s0 += wave_xor<T, 2>(s0); s1 += wave_xor<T, 2>(s1); }
-        if (CPR <= 4) { s0 += wave_xor<T, 4>(s0); s1 += wave_xor<T, 4>(s1); }
-        if (CPR <= 8) { s0 += wave_xor<T, 8>(s0); s1 += wave_xor<T, 8>(s1); }
-        if (CPR <= 16) { s0 += wave_xor<T, 16>(s0); s1 += wave_xor<T, 16>(s1); }
-        if (CPR <= 32) { s0 += wave_xor<T, 32>(s0); s1 += wave_xor<T, 32>(s1); }
-        const int bad = __any(fl) ? 1 : 0;
-        T term = 0;
-        const T sp0 = spsh[0][lane], sp1 = spsh[1][lane];
+        T s0 = dchunk_v0(x), s1 = dchunk_v1(x);
+        if (nrb > 1) { s0 += wave_xor<T, 1>(s0); s1 += wave_xor<T, 1>(s1); }
+        if (nrb > 2) { s0 += wave_xor<T, 2>(s0); s1 += wave_xor<T, 2>(s1); }
+        if (nrb > 4) { s0 += wave_xor<T, 4>(s0); s1 += wave_xor<T, 4>(s1); }
+        if (nrb > 8) { s0 += wave_xor<T, 8>(s0); s1 += wave_xor<T, 8>(s1); }
+        if (nrb > 16) { s0 += wave_xor<T, 16>(s0); s1 += wave_xor<T, 16>(s1); }
+        const int bad = __any(lane < 32 && dchunk_flag(x)) ? 1 : 0;
+        const bool head = lane < 32 && r_q == 0;  // the lane that owns chunk r_cc
         if (need) {
-            if (r_ok) {
+            T term = 0;
+            if (head) {
+                const T sp0 = spsh[0][r_cc], sp1 = spsh[1][r_cc];
                 const T rb0 = bsh[2 * r_ch], rb1 = bsh[2 * r_ch + 1];
                 const T r0 = (rb0 / sp0) * s0 - rb0, r1 = (rb1 / sp1) * s1 - rb1;
                 term = r0 * r0 + r1 * r1;
             }
-            if (CPR > 1) term += wave_xor<T, 1>(term);
-            if (CPR > 2) term += wave_xor<T, 2>(term);
-            if (CPR > 4) term += wave_xor<T, 4>(term);
-            if (CPR > 8) term += wave_xor<T, 8>(term);
-            if (CPR > 16) term += wave_xor<T, 16>(term);
-            if (CPR > 32) term += wave_xor<T, 32>(term);
+            term = wave_sum<T>(term);
+            if (lane == 0) gstore_col(rs, colb(e, rb) + (uint32_t)(CPR + w) * 16, echunk(term, e), xl);
         }
-        spsh[0][lane] = s0;
-        spsh[1][lane] = s1;
-        if (lane < CPR && r_ok) gstore_col(rs, colb(e, rb) + (uint32_t)r_cc * 16, dchunk(s0, s1, e, bad), xl);
-        if (need && lane == 0 && rb < nred) gstore_col(rs, colb(e, rb) + (uint32_t)CPR * 16, echunk(term, e), xl);
+        if (head) {
+            spsh[0][r_cc] = s0;
+            spsh[1][r_cc] = s1;
+            gstore_col(rs, colb(e, rb) + (uint32_t)r_cc * 16, dchunk(s0, s1, e, bad), xl);
+        }
         deadline = __builtin_amdgcn_s_memrealtime() + p.timeout_ticks;
         return ok;
     };
     // hop B (per wave): S[e - 1] of this wave's 32 chunks -> v into vcur[w]; wave 0 also
     // (need) the error terms of the nred reducers -> its tile's error partial.  Returns
     // bit 0 = producer flag, 1 = stall, 2 = bad v (this wave's columns only).
+    // hop B of one chunk ch of this wave's stripe: S[e - 1] -> v of its two columns into
+    // vcur[w]; returns bit 0 = producer flag, 1 = stall, 2 = bad v
+    auto hop_v = [&](int e, int ch) -> int {
+        int fl = 0;
+        const uint32_t off = colb(e, ch / CPR) + (uint32_t)(ch & (CPR - 1)) * 16;
+        I4 x;
+        if (!poll64<false>(rs, off, (unsigned)e, deadline, x)) fl |= 2;
+        fl |= dchunk_flag(x);
+        const T s0 = dchunk_v0(x), s1 = dchunk_v1(x);
+        const D2 bb = *reinterpret_cast<const D2*>(&bsh[2 * ch]);
+        const T v0n = bb[0] / s0, v1n = bb[1] / s1;
+        if (s0 == 0.0 || !finite_val(v0n) || s1 == 0.0 || !finite_val(v1n)) fl |= 4;
+        *reinterpret_cast<D2*>(&vcur[w][2 * (ch - 32 * w)]) = D2{v0n, v1n};
+        return fl;
+    };
+    // wave 0 on check iterations: the 8 error slots of each of the nred reducers (lane l
+    // sums slots l + 64 k) -> this tile's error partial; returns bit 1 on a stall
+    auto hop_err = [&](int e, T& sE) -> int {
+        int fl = 0;
+        T ep = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = lane + 64 * k;
+            if (q < 8 * nred) {
+                I4 x;
+                if (!poll64<true>(rs, colb(e, q >> 3) + (uint32_t)(CPR + (q & 7)) * 16, (unsigned)e, deadline, x))
+                    fl |= 2;
+                ep += echunk_v(x);
+            }
+        }
+        sE = wave_sum<T>(ep);
+        return fl;
+    };
+    // hop B of the whole stripe (the post-loop check): returns the wave's flags
     auto gather_b = [&](int e, bool need, T& sE) -> int {
         int fl = 0;
-        if (lane < 32) {
-            const uint32_t off = colb(e, hch / CPR) + (uint32_t)(hch & (CPR - 1)) * 16;
-            I4 x;
-            if (!poll64<false>(rs, off, (unsigned)e, deadline, x)) fl |= 2;
-            fl |= dchunk_flag(x);
-            const T s0 = dchunk_v0(x), s1 = dchunk_v1(x);
-            const D2 bb = *reinterpret_cast<const D2*>(&bsh[2 * hch]);
-            const T v0n = bb[0] / s0, v1n = bb[1] / s1;
-            if (s0 == 0.0 || !finite_val(v0n) || s1 == 0.0 || !finite_val(v1n)) fl |= 4;
-            *reinterpret_cast<D2*>(&vcur[w][2 * lane]) = D2{v0n, v1n};
-        }
-        if (w == 0 && need) {
-            T ep = 0;
-            if (lane >= 32 && lane - 32 < nred) {
-                I4 x;
-                if (!poll64<true>(rs, colb(e, lane - 32) + (uint32_t)CPR * 16, (unsigned)e, deadline, x)) fl |= 2;
-                ep = echunk_v(x);
-            }
-            sE = wave_sum<T>(ep);
-        }
+        if (lane < 32) fl = hop_v(e, hch);
+        if (w == 0 && need) fl |= hop_err(e, sE);
         // the wave's own LDS writes complete before its reads (in-order LDS per wave); the
         // clobber keeps the compiler from moving the reads of vcur above the writes
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -473,7 +468,7 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     }
     int last_good = -1, niter = 0, status = OTF_SK_MAX_ITER, brk = -1, n_err = 0;
     bool done = false;
-    if (w == 0 && !reduce(1, false)) s_ep[1] = 1;
+    if (!reduce(1, false) && lane == 0) s_ep[1] = 1;
     int chk = 0;
     T sE = 0;
 
@@ -482,19 +477,21 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
         const int e = it + 1;
         const bool check = it >= 1 && chk == 0;
         OTF_M64ST(it, 0);
-        {
-            const int fl = gather_b(e, check, sE);
-            if (lane == 0) {
-                if (fl & 2) s_ep[1] = e;
-                if (fl & 1) s_ep[2] = e;
-                if (fl & 4) s_ep[3] = e;
-            }
-        }
         OTF_M64ST(it, 1);
         if (it >= 1) chk = chk + 1 == p.check_every ? 0 : chk + 1;
-        // row partials K v of the lane's 8 rows over its 16 columns, then the 4 lanes of a
-        // row (bits 5, 4: lane (b5, b4) ends with rows a = 4 b5 + 2 b4 + 0, 1)
+        // hop B (this wave's 32 chunks, all in flight), then the row partials K v of the
+        // lane's 8 rows over its 16 columns and the 4 lanes of a row (bits 5, 4: lane
+        // (b5, b4) ends with rows a = 4 b5 + 2 b4 + 0, 1).  (Polling block by block and
+        // summing each block as it arrives needed ~80 more spilled registers.)
         {
+            {
+                const int fl = gather_b(e, check, sE);
+                if (lane == 0) {
+                    if (fl & 2) s_ep[1] = e;
+                    if (fl & 1) s_ep[2] = e;
+                    if (fl & 4) s_ep[3] = e;
+                }
+            }
             T pr[NA];
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
@@ -529,14 +526,16 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
             break;
         }
         const int vbad_cb = s_ep[3] == e ? 1 : 0;
-        if (w == 0) {
-            // the tile's 128 row partials over its 512 columns: the 8 stripes in wave order
-            D2 s = *reinterpret_cast<const D2*>(&rowbuf[0][2 * lane]);
+        // the tile's 128 row partials over its 512 columns (the 8 stripes in wave order):
+        // wave w publishes chunks 8 w .. 8 w + 7, the ones its own lanes gather below
+        if (lane < 8) {
+            const int c = 8 * w + lane;
+            D2 s = *reinterpret_cast<const D2*>(&rowbuf[0][2 * c]);
 #pragma unroll
-            for (int ww = 1; ww < NW; ++ww) s += *reinterpret_cast<const D2*>(&rowbuf[ww][2 * lane]);
-            gstore(rs, rowx(e, cb) + (uint32_t)lane * 16, dchunk(s[0], s[1], e, vbad_cb));
-            if (check && lane == 0) gstore(rs, rowx(e, cb) + 64 * 16, echunk(sE, e));
+            for (int ww = 1; ww < NW; ++ww) s += *reinterpret_cast<const D2*>(&rowbuf[ww][2 * c]);
+            gstore(rs, rowx(e, cb) + (uint32_t)c * 16, dchunk(s[0], s[1], e, vbad_cb));
         }
+        if (w == 0 && check && lane == 8) gstore(rs, rowx(e, cb) + 64 * 16, echunk(sE, e));
         OTF_M64ST(it, 3);
         // row hop: the ncb members' chunk gc (lane (gc, gq): member gq), summed over the
         // 8 lanes in a fixed order -> u of rows 2 gc, 2 gc + 1
@@ -610,7 +609,7 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
             col_publish(uu, e + 1, s_ep[0] == it ? 1 : 0);
         }
         OTF_M64ST(it, 6);
-        if (w == 0 && !reduce(e + 1, chk == 0)) s_ep[1] = e + 1;
+        if (!reduce(e + 1, chk == 0) && lane == 0) s_ep[1] = e + 1;
         OTF_M64ST(it, 7);
     }
     if (!done && p.max_iter > 0) {
@@ -716,7 +715,7 @@ Mesh64Shape mesh64_shape(int64_t n, int64_t m) {
     s.nrb = (int)(n / kM64TR);
     s.ncb = (int)(m / kM64TC);
     s.cpr = pow2_ceil(kM64NCH / (s.nrb > 0 ? s.nrb : 1));
-    s.bstride = (uint32_t)((s.cpr + 1) * 16 + 255) / 256 * 256;
+    s.bstride = (uint32_t)((s.cpr + kM64NW) * 16 + 255) / 256 * 256;  // S chunks + 8 error slots
     s.row_bytes = 2 * (size_t)s.nrb * s.ncb * kM64RowStride;
     s.cola_bytes = 2 * (size_t)s.nrb * s.ncb * kM64ColStride;
     s.colb_bytes = 2 * (size_t)s.nrb * s.ncb * s.bstride;

@@ -354,6 +354,7 @@ template <typename CT>
 hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                    double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* sh = nullptr);
+                    double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* sh = nullptr,
+                    const XSweep* xs = nullptr);
 
 }  // namespace otf

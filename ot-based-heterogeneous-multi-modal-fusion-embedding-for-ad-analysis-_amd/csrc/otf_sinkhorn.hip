@@ -2453,11 +2453,26 @@ int run_xsweep(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_
     if (!u_out || !v_out) return OTF_EINVAL;
     if (P_out && (ldp < m || ldp % VEC != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
     if (o.max_iter < 1 || xs.n_total < n) return OTF_EINVAL;
-    if (!sweep_supported<T, CT>(n, m, ldc) || o.shift) return OTF_EUNSUPPORTED;
+    if (o.shift) return OTF_EUNSUPPORTED;
     SkSetup<T> su;
     int rc = sk_prepare<T, CT>(a, b, C, n, m, ldc, o, info, ws, ws_bytes, su);
     if (rc != OTF_OK) return rc;
     double* errlog = errlog_user ? errlog_user : su.w.errlog;
+    // the cross-rank mesh where this rank's slab fits the register files (whole 512-column
+    // tiles, one workgroup per tile on this device): K stays resident for the whole solve
+    // and the reducers exchange their column-sum partials; the cross-rank sweep otherwise
+    const bool mesh_fit = (o.engine == OTF_ENGINE_AUTO || o.engine == OTF_ENGINE_MESH) &&
+                          mesh_supported(n, m) && m % 512 == 0 && su.w.mesh_bytes > 0 &&
+                          ((n + 127) / 128) * (m / 512) <= device_cu_count();
+    if (o.engine == OTF_ENGINE_MESH && !mesh_fit) return OTF_EUNSUPPORTED;
+    if (mesh_fit) {
+        rc = sk_init<T>(su, a, b, n, m, info, s, su.w.mesh, su.w.mesh_bytes);
+        if (rc != OTF_OK) return rc;
+        return check_hip(run_mesh<CT>(C, ldc, (int)n, (int)m, (const float*)su.w.a_pad, (const float*)su.w.b_pad,
+                                      cost_scale, o, su.w.mesh, u_out, v_out, P_out, ldp, P_dtype, info,
+                                      errlog, /*zeroed=*/true, s, nullptr, &xs));
+    }
+    if (!sweep_supported<T, CT>(n, m, ldc)) return OTF_EUNSUPPORTED;
     rc = sk_init<T>(su, a, b, n, m, info, s);
     if (rc != OTF_OK) return rc;
     return check_hip(run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,

@@ -313,15 +313,22 @@ def sinkhorn_xsweep(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.Tenso
                     xpeer: XPeer, n_total: int, max_iter: int = 1000, stop_thr: float = 1e-9,
                     cost_scale: torch.Tensor | None = None, check_every: int = 10,
                     err_squared: bool = False, want_plan: bool = True, plan_dtype=None,
-                    workspace: torch.Tensor | None = None) -> ops.SinkhornResult:
+                    workspace: torch.Tensor | None = None, engine: str = "auto") -> ops.SinkhornResult:
     """POT ``sinkhorn_knopp`` on a problem whose cost rows are split over the ranks, as
     ONE persistent launch per rank (``otf_sinkhorn_xsweep``): the column sums are
     exchanged inside the launch through ``xpeer`` -- no all-reduce call per iteration.
     Same contract as ``sinkhorn_row_sharded`` (this rank's rows of u and the plan, the
-    full v); float32 compute, fp32 or fp16 cost rows."""
+    full v); float32 compute, fp32 or fp16 cost rows.
+
+    ``engine``: "mesh" keeps this rank's K in the register files for the whole solve
+    (whole 512-column tiles, one workgroup per 128 x 512 tile on the device; the mesh's
+    reducers exchange their column-sum partials, "xmesh"), "sweep" streams the cost rows
+    every iteration, "auto" takes the mesh where the slab fits."""
     ops._dev(C_local, "C_local")
     if C_local.dtype not in (torch.float32, torch.float16):
         raise TypeError("sinkhorn_xsweep: float32 or float16 cost rows")
+    if engine not in ("auto", "sweep", "mesh"):
+        raise ValueError(f"engine must be 'auto', 'sweep' or 'mesh', not {engine!r}")
     n, m = C_local.shape
     if m != xpeer.m:
         raise ValueError(f"C_local has {m} columns, the exchange was built for {xpeer.m}")
@@ -334,7 +341,7 @@ def sinkhorn_xsweep(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.Tenso
     cs = None if cost_scale is None else cost_scale.to(dev, torch.float32).contiguous()
     opts = L.SinkhornOpts(reg=float(reg), stop_thr=float(stop_thr), max_iter=int(max_iter),
                           check_every=int(check_every), flavor=L.OTF_FLAVOR_POT,
-                          err_squared=int(err_squared), sync_every=0, engine=L.ENGINE_SWEEP,
+                          err_squared=int(err_squared), sync_every=0, engine=L.ENGINES[engine],
                           cost_f16=int(C.dtype == torch.float16), n_total=int(n_total))
     if workspace is None:
         workspace = ops.sinkhorn_workspace(n, m, torch.float32, max_iter, dev)
@@ -357,14 +364,16 @@ def sinkhorn_xsweep(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.Tenso
 def coupled_solve_sharded(X_local: torch.Tensor, Y_local: torch.Tensor, reg: float,
                           max_iter: int = 200, stop_thr: float = 0.0, cost_dtype=torch.float16,
                           want_plan: bool = True, sync_every: int = 0, group=None, comm=None,
-                          xpeer: XPeer | None = None):
+                          xpeer: XPeer | None = None, engine: str = "auto"):
     """The per-epoch global OT of one large problem over the data-parallel ranks:
     all-gather the PET embedding shards (RCCL), cost rows of this rank's MRI shard
     against every PET embedding (fp16 storage by default, BASELINE config 5), one
     all-reduce(MAX) for scale_cost="max_cost", then the row-sharded Sinkhorn with
     uniform marginals.  With an ``xpeer`` exchange the solve is the in-kernel cross-rank
     sweep (``sinkhorn_xsweep``), otherwise the row-sharded solve with one all-reduce per
-    iteration.  Returns (SinkhornResult of this rank's rows, n_total)."""
+    iteration.  ``engine`` picks the cross-rank engine of the xpeer form ("auto": the
+    register-resident mesh where this rank's slab fits, else the sweep; sinkhorn_xsweep).
+    Returns (SinkhornResult of this rank's rows, n_total)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     x_sizes = None
     if comm is not None and comm.nranks > 1:
@@ -396,7 +405,7 @@ def coupled_solve_sharded(X_local: torch.Tensor, Y_local: torch.Tensor, reg: flo
     b = torch.full((m,), 1.0 / m, dtype=torch.float32, device=X_local.device)
     if xpeer is not None:
         return sinkhorn_xsweep(a, b, C, reg, xpeer, n_total, max_iter=max_iter, stop_thr=stop_thr,
-                               cost_scale=gmax / unit, want_plan=want_plan), n_total
+                               cost_scale=gmax / unit, want_plan=want_plan, engine=engine), n_total
     res = sinkhorn_row_sharded(a, b, C, reg, max_iter=max_iter, stop_thr=stop_thr,
                                cost_scale=gmax / unit, n_total=n_total, sync_every=sync_every,
                                want_plan=want_plan, group=group, comm=comm)

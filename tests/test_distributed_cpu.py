@@ -261,3 +261,98 @@ def test_per_epoch_label_split_world2(tmp_path):
     world = 2
     mp.spawn(_label_split_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     assert all((tmp_path / f"labels{r}").exists() for r in range(world))
+
+
+def _xmesh_model(K_loc, a_loc, b, n_total, reg_iters, check_every, stop_thr, exchange, tile=128):
+    """The cross-rank mesh's arithmetic order (csrc/otf_mesh.hip, XR instances), restated
+    for the protocol test: per iteration every row block (producer) forms its column
+    partials K_rb^T u, the rank's reducers sum them in producer order, the ranks' partials
+    are exchanged and summed in rank order (``exchange``: the stand-in for the stores into
+    the peers' buffers), v = b / S; the rows are local (u = a / K v).  POT's marginal error
+    of iterate it - 1 every check_every iterations, from the global S; stop below stop_thr."""
+    n_loc, m = K_loc.shape
+    u = np.full(n_loc, 1.0 / n_total)
+    nb = -(-n_loc // tile)
+
+    def colsum(u):
+        s = np.zeros(m)
+        for rb in range(nb):
+            sl = slice(rb * tile, min(n_loc, (rb + 1) * tile))
+            s = s + K_loc[sl].T @ u[sl]
+        return exchange(s)
+
+    S = colsum(u)
+    errs, niter = [], reg_iters - 1
+    for it in range(reg_iters):
+        v = b / S
+        u_new = a_loc / (K_loc @ v)
+        S_new = colsum(u_new)
+        if it % check_every == 0:
+            # POT: err of the current iterate (u_new, v): column marginal v * K^T u_new vs b
+            r = v * S_new - b
+            errs.append(float(np.sqrt(r @ r)))
+            if errs[-1] < stop_thr:
+                niter = it
+                u = u_new
+                break
+        u, S = u_new, S_new
+    return u[:, None] * K_loc * v[None, :], v, niter, errs
+
+
+def _xmesh_protocol_worker(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(13)
+    rows = [384, 256]                       # unequal slabs: 3 and 2 row blocks of 128
+    n, m = sum(rows), 1024
+    C = rng.random((n, m))
+    K = np.exp(-C / 0.05)
+    a = rng.random(n) + 0.5
+    a /= a.sum()
+    b = rng.random(m) + 0.5
+    b /= b.sum()
+    sl = slice(sum(rows[:rank]), sum(rows[:rank + 1]))
+
+    def exchange(s):
+        parts = [torch.empty(m, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(parts, torch.from_numpy(s))
+        out = np.zeros(m)
+        for p_ in parts:                     # rank order, every rank the same sum
+            out = out + p_.numpy()
+        return out
+
+    P, v, niter, errs = _xmesh_model(K[sl], a[sl], b, n, 300, 10, 1e-7, exchange)
+    np.savez(os.path.join(out_dir, f"xm{rank}.npz"), P=P, v=v, niter=niter, errs=np.array(errs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xmesh_exchange_protocol_world2(tmp_path):
+    """The cross-rank mesh's exchange protocol on CPU (gloo standing in for the xGMI
+    stores): rank slabs of unequal height, partials summed in rank order -- both ranks
+    derive the same v bit for bit, stop at the same check, and the assembled plan is POT's
+    (the float64 oracle on the whole problem, MRI_PET_OT_nojax.py:143)."""
+    from oracle import oracle as orc
+    world = 2
+    mp.spawn(_xmesh_protocol_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    zs = [np.load(tmp_path / f"xm{r}.npz") for r in range(world)]
+    assert np.array_equal(zs[0]["v"], zs[1]["v"])
+    assert int(zs[0]["niter"]) == int(zs[1]["niter"])
+    rng = np.random.default_rng(13)
+    rows = [384, 256]
+    n, m = sum(rows), 1024
+    C = rng.random((n, m))
+    a = rng.random(n) + 0.5
+    a /= a.sum()
+    b = rng.random(m) + 0.5
+    b /= b.sum()
+    P_ref, _, _, info_r = orc.sinkhorn_knopp(a, b, C, 0.05, 300, 1e-7)
+    assert int(zs[0]["niter"]) == info_r["niter"]
+    np.testing.assert_allclose(zs[0]["errs"], info_r["err"], rtol=1e-9, atol=1e-15)
+    P = np.concatenate([z["P"] for z in zs])
+    assert np.abs(P - P_ref).max() / np.abs(P_ref).max() < 1e-12

@@ -45,10 +45,11 @@ def test_metric_config_takes_mesh_and_matches_oracle(orc, dev):
 
 @pytest.mark.parametrize("n,m", [(512, 512), (640, 3000), (1000, 4096), (2048, 500),
                                  (4100, 1000), (4096, 4096), (8192, 2048), (3001, 2049),
-                                 (513, 7), (8100, 100)])
+                                 (513, 7), (8100, 100), (1024, 8192), (2048, 6000), (512, 4097)])
 def test_mesh_grid_shapes_vs_oracle(orc, dev, n, m):
-    """4..64 row tiles (powers of two and not: 8 reducer loads per lane), 1..8 column
-    tiles, ragged last row tile / column tile / chunk, non-uniform marginals."""
+    """4..64 row tiles (powers of two and not: 8 reducer loads per lane), 1..16 column
+    tiles (past 8 the row hop takes two members per lane and the roles are by blockIdx),
+    ragged last row tile / column tile / chunk, non-uniform marginals."""
     from otfuse import ops
     rng = np.random.default_rng(n * 3 + m)
     C = rng.random((n, m))
@@ -191,7 +192,7 @@ def test_mesh_float64_plan_output(dev):
 
 def test_mesh_unsupported_shapes_are_refused(dev):
     from otfuse import ops
-    for n, m, dt in [(300, 200, torch.float32), (1024, 4097, torch.float32),
+    for n, m, dt in [(300, 200, torch.float32), (1024, 8193, torch.float32),
                      (8193, 512, torch.float32), (1000, 1024, torch.float64),
                      (1024, 1000, torch.float64), (384, 512, torch.float64)]:
         C = torch.rand(n, m, device=dev, dtype=dt)

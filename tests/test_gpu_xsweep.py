@@ -64,6 +64,25 @@ def test_xsweep_single_rank_vs_oracle(orc, dev):
         xp.close()
 
 
+def test_xsweep_single_rank_mesh_is_the_mesh(dev):
+    """world = 1 on a shape the mesh takes (whole 512-column tiles): the cross-rank call
+    runs the register-resident mesh, bit for bit the single-GPU mesh solve."""
+    import otfuse.distributed as D
+    from otfuse import ops
+    g = torch.Generator(device=dev).manual_seed(9)
+    C = torch.rand(1024, 2048, device=dev, generator=g)
+    a = torch.full((1024,), 1.0 / 1024, device=dev)
+    b = torch.full((2048,), 1.0 / 2048, device=dev)
+    xp = D.XPeer(2048)
+    try:
+        rx = D.sinkhorn_xsweep(a, b, C, 0.05, xp, n_total=1024, max_iter=80, stop_thr=0.0)
+        rm = ops.sinkhorn(a, b, C, 0.05, max_iter=80, stop_thr=0.0, engine="mesh")
+        assert rx.info()["engine_name"] == rm.info()["engine_name"] == "mesh"
+        assert torch.equal(rx.plan, rm.plan) and torch.equal(rx.v, rm.v)
+    finally:
+        xp.close()
+
+
 def _worker(rank, world, port, out_dir):
     import sys
     for p in (PKG, REPO):
@@ -128,4 +147,82 @@ def test_xsweep_two_ranks_match_whole_problem(tmp_path, orc):
     Cd = np.concatenate([np.load(tmp_path / f"k{r}.npy") for r in range(world)])
     u = np.full(1536, 1.0 / 1536)
     Pr, *_ = orc.sinkhorn_knopp(u, u, Cd / Cd.max(), 0.1, 60, 0.0)
+    assert np.abs(Pc - Pr).max() / np.abs(Pr).max() < 1e-4
+
+
+def _xmesh_worker(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import otfuse.distributed as D
+    from otfuse import ops
+    from otfuse.synthetic import paired_embeddings
+    dev = torch.device("cuda", 0)
+    # (1) the metric shape's rows over two ranks: 2048 x 4096 float32 cost rows each
+    # (16 x 8 register tiles per rank, one device holding both grids)
+    N = 4096
+    Cn = np.random.default_rng(5).random((N, N)).astype(np.float32)
+    sl = slice(rank * N // world, (rank + 1) * N // world)
+    a = torch.full((N // world,), 1.0 / N, device=dev)
+    b = torch.full((N,), 1.0 / N, device=dev)
+    xp = D.XPeer(N)
+    res = D.sinkhorn_xsweep(a, b, torch.tensor(Cn[sl], device=dev), 0.05, xp, n_total=N,
+                            max_iter=200, stop_thr=1e-7, engine="mesh")
+    info = res.info()
+    np.savez(os.path.join(out_dir, f"m{rank}.npz"), P=res.plan.cpu().numpy(), niter=info["niter"],
+             err=np.array(info["err"]), v=res.v.cpu().numpy(), engine=info["engine_name"])
+    # a second solve on the same exchange (the other slot set, epochs continue): same bits
+    res2 = D.sinkhorn_xsweep(a, b, torch.tensor(Cn[sl], device=dev), 0.05, xp, n_total=N,
+                             max_iter=200, stop_thr=1e-7, engine="mesh")
+    assert torch.equal(res2.plan, res.plan)
+    xp.close()
+    # (2) BASELINE config 5's layout per rank at 8 ranks: 1024 fp16 cost rows x 8192 columns
+    # (16 column tiles: two row-hop members per lane, blockIdx roles), via the per-epoch
+    # pipeline (all-gathered PET shards, the max agreed over the ranks)
+    X, Y, _ = paired_embeddings(8192, 128, seed=21)
+    xs = torch.tensor(X[rank * 1024:(rank + 1) * 1024], device=dev, dtype=torch.float16)
+    ys = torch.tensor(Y[rank * 4096:(rank + 1) * 4096], device=dev, dtype=torch.float16)
+    xp2 = D.XPeer(8192)
+    res3, n_total = D.coupled_solve_sharded(xs, ys, 0.1, max_iter=60, xpeer=xp2, engine="mesh")
+    assert n_total == 2048 and res3.info()["engine_name"] == "mesh"
+    np.save(os.path.join(out_dir, f"p{rank}.npy"), res3.plan.cpu().numpy())
+    C16, _, unit = ops.pairwise_cost_ex(xs, D.all_gather_rows(ys), zero_diag=False,
+                                        out_dtype=torch.float16)
+    np.save(os.path.join(out_dir, f"q{rank}.npy"),
+            C16.float().cpu().numpy().astype(np.float64) * float(unit))
+    xp2.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xmesh_two_ranks_match_whole_problem(tmp_path, orc):
+    """The cross-rank mesh ("xmesh"): each rank's slab of K in its register files, the
+    column-sum partials of the mesh's reducers exchanged over the peers' buffers inside
+    the launch.  Two ranks on one device (N = 4096: 2048 x 4096 rows each; and config 5's
+    per-rank layout at 8 ranks, 1024 x 8192 fp16 rows) against the whole-problem float64
+    oracle: plans within 1e-4, the oracle's stop iteration and error log, and the same v
+    bit for bit on both ranks."""
+    world = 2
+    mp.spawn(_xmesh_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    N = 4096
+    Cn = np.random.default_rng(5).random((N, N)).astype(np.float32).astype(np.float64)
+    u = np.full(N, 1.0 / N)
+    P_ref, _, _, info_r = orc.sinkhorn_knopp(u, u, Cn, 0.05, 200, 1e-7)
+    zs = [np.load(tmp_path / f"m{r}.npz") for r in range(world)]
+    assert all(str(z["engine"]) == "mesh" for z in zs)
+    assert all(int(z["niter"]) == info_r["niter"] for z in zs)
+    for z in zs:
+        np.testing.assert_allclose(z["err"], info_r["err"], rtol=1e-4, atol=1e-8)
+    assert np.array_equal(zs[0]["v"], zs[1]["v"])
+    P = np.concatenate([z["P"] for z in zs])
+    assert np.abs(P - P_ref).max() / np.abs(P_ref).max() < 1e-4
+    Pc = np.concatenate([np.load(tmp_path / f"p{r}.npy") for r in range(world)])
+    Cd = np.concatenate([np.load(tmp_path / f"q{r}.npy") for r in range(world)])
+    Pr, *_ = orc.sinkhorn_knopp(np.full(2048, 1.0 / 2048), np.full(8192, 1.0 / 8192), Cd / Cd.max(),
+                                0.1, 60, 0.0)
     assert np.abs(Pc - Pr).max() / np.abs(Pr).max() < 1e-4
