@@ -93,11 +93,13 @@ enum {
  *   granules that every workgroup gathers and sums in a fixed order -- no atomics, no
  *   barrier, one memory hop per iteration, bitwise reproducible.  AUTO picks it first
  *   for such shapes (and for opts.deterministic).  POT flavour.
- * OTF_ENGINE_MESH: float32, 4..64 row tiles x 1..8 column tiles of 128 x 512 (the
- *   N = 4096 metric config): tiles of K in registers as in TILED, but both reductions
+ * OTF_ENGINE_MESH: float32, 4..64 row tiles x 1..16 column tiles of 128 x 512 (the
+ *   N = 4096 metric config; config 5's 8192 columns under otf_sinkhorn_xsweep): tiles of K in registers as in TILED, but both reductions
  *   are epoch-tagged granule hops -- row partials within the row block, column partials
  *   through one reducer workgroup per column slice -- no atomics, no barrier, three
- *   memory hops per iteration, bitwise reproducible.  AUTO picks it before TILED.     */
+ *   memory hops per iteration, bitwise reproducible.  AUTO picks it before TILED.
+ *   float64: whole 128 x 512 tiles, 4 / 8 / 16 / 32 row blocks x 1..8 column tiles,
+ *   eight waves a workgroup, K in registers + LDS (AUTO picks it for those shapes).   */
 typedef enum {
     OTF_ENGINE_AUTO = 0,
     OTF_ENGINE_STREAM = 1,
@@ -319,6 +321,11 @@ int otf_sinkhorn_finish(const void* a, const void* b, const void* C, int64_t n, 
  * of otf_sinkhorn_xsweep calls (the exchange's epochs advance in lock-step); the grids
  * of all ranks must run concurrently.  float32 compute (fp32 or fp16 cost: opts.cost_f16),
  * POT flavour; opts.n_total = rows over all ranks; u / plan: this rank's rows, v: all.
+ * opts.engine AUTO or MESH: when the rank's slab fits the register files (m a multiple
+ * of 512, <= 16 column tiles of 512, row tiles x column tiles <= the CUs) the launch is
+ * the register-resident mesh engine whose reducers do the exchange ("xmesh"); else (or
+ * with OTF_ENGINE_SWEEP) the streaming sweep engine.  Both take POT's decisions at the
+ * same iteration on every rank.
  * A stall (a rank that never launches) ends in OTF_SK_TIMEOUT + info.stalled. */
 typedef struct otf_xpeer otf_xpeer;
 size_t otf_xpeer_handle_size(void);
