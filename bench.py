@@ -701,8 +701,9 @@ def sharded_config5_leg(dev, world, N=8192, d=1024, iters=200, eps=0.1):
     ranks.  Rank r holds N / world MRI rows; the PET shards are all-gathered (RCCL), the
     rank builds its fp16 cost rows, the global max is agreed (all-reduce MAX), then the
     solve runs as ONE persistent launch per rank whose column sums are exchanged inside
-    the launch through the peers' exchange buffers over xGMI (otf_sinkhorn_xsweep, engine
-    "xsweep").  For comparison the previous form: the row-sharded solve with one RCCL
+    the launch through the peers' exchange buffers over xGMI (otf_sinkhorn_xsweep): the
+    "xmesh" leg keeps the rank's slab of K in the register files (from 4 ranks on), the
+    "xsweep" leg streams it.  For comparison the previous form: the row-sharded solve with one RCCL
     all-reduce(SUM) of m + 1 sums per iteration (otf_sinkhorn_row_sharded, "rccl").
     Reported per solve and per iteration, max over ranks.  Scaling 'strong'."""
     import numpy as np
@@ -736,18 +737,22 @@ def sharded_config5_leg(dev, world, N=8192, d=1024, iters=200, eps=0.1):
             return float(t[0]), res
 
         legs = {}
-        try:
-            xp = XPeer(N)
-            ms, res = timed(xpeer=xp)
-            legs["xsweep"] = {"status": res.info()["status_name"], "ms_per_solve": ms,
-                              "us_per_iteration": ms * 1e3 / (iters + 1)}
-            xp.close()
-        except Exception as e:  # noqa: BLE001 - the RCCL form below still reports
-            legs["xsweep"] = {"error": repr(e)}
+        # the in-kernel cross-rank engines on the peers' exchange buffers: "xmesh" (this
+        # rank's slab of K in the register files, where it fits: 8192 / world x 8192 needs
+        # world >= 4) and "xsweep" (the slab streamed every iteration)
+        for leg, eng in (("xmesh", "mesh"), ("xsweep", "sweep")):
+            try:
+                xp = XPeer(N)
+                ms, res = timed(xpeer=xp, engine=eng)
+                legs[leg] = {"status": res.info()["status_name"], "engine": res.info()["engine_name"],
+                             "ms_per_solve": ms, "us_per_iteration": ms * 1e3 / (iters + 1)}
+                xp.close()
+            except Exception as e:  # noqa: BLE001 - the other forms still report
+                legs[leg] = {"error": repr(e)[:300]}
         ms, res = timed()
         legs["rccl"] = {"status": res.info()["status_name"], "ms_per_solve": ms,
                         "us_per_iteration": ms * 1e3 / (iters + 1)}
-        best = "xsweep" if "ms_per_solve" in legs["xsweep"] else "rccl"
+        best = min((k for k in legs if "ms_per_solve" in legs[k]), key=lambda k: legs[k]["ms_per_solve"])
         ms = legs[best]["ms_per_solve"]
         out.update({"engine": best, "status": legs[best]["status"], "ms_per_solve": ms,
                     "us_per_iteration": ms * 1e3 / (iters + 1), "legs": legs,
