@@ -242,6 +242,9 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
 #endif
     OTF_M64PRO(1);
     const int rr = lane & 15, g = lane >> 4;
+    // slot h of a column block holds the lane's column pair h ^ b3 (b3 = lane bit 3): the
+    // row-mirror step of the column reduction then reads slot 1 in every lane (no selects)
+    const int b3 = (lane >> 3) & 1;
     const int row0 = rb * TR;
     const int col0 = cb * TC;
     const int cw = w * WC;
@@ -252,8 +255,8 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     if (p.cost_scale) cinv = 1.0 / p.cost_scale[0];
     const T ks = -1.0 / p.reg * cinv;
 
-    // ---- K: rows rr + 16 a, columns cw + 16 b + 4 g + (0..3) as two pairs h; blocks
-    // b < 3 in registers, b = 3 in LDS
+    // ---- K: rows rr + 16 a, columns cw + 16 b + 4 g + 2 (h ^ b3) + (0, 1) in slot (b, h);
+    // blocks b < 3 in registers, b = 3 in LDS
     D2 kr[NA][RB][2];
     {
         const T* cbase = p.C + (int64_t)(row0 + rr) * p.ldc + col0 + cw + 4 * g;
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
             for (int b = 0; b < NB; ++b) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const D2 c = *reinterpret_cast<const D2*>(crow + 16 * b + 2 * h);
+                    const D2 c = *reinterpret_cast<const D2*>(crow + 16 * b + 2 * (h ^ b3));
                     const D2 e = D2{exp(c[0] * ks), exp(c[1] * ks)};
                     if (b < RB) kr[a][b][h] = e;
                     else sK[w][a][h][lane] = e;
@@ -313,10 +316,15 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     };
 
     // K^T u over the lane's 8 rows for each column block b, summed over the 16 lanes of a
-    // column (lane bits 3..0: row mirror and half mirror with keep / send, then quad ^2,
-    // ^1 -- every step adds two disjoint lane sets), then published per wave as chunks
-    // (columns i = 0, 1 and 2, 3 of the lane group) by lanes rr = 0 and 8
+    // column (lane bits 3..0): row mirror (slot 0 keeps, the partner's slot 1 holds the
+    // same pair), half mirror with keep / send of the pair's two columns, then quad ^2, ^1
+    // -- every step adds two disjoint lane sets -- and published per wave as chunks
+    // (columns 2 b3, 2 b3 + 1 of the block) by lanes rr = 0 and 8
     auto col_publish = [&](const T (&u)[NA], int e, int flag) {
+        // the lane's chunk offset, formed here (held across the loop it took a register
+        // per block)
+        uint32_t pub = (uint32_t)(32 * w + 2 * g + b3) * 16;
+        asm volatile("" : "+v"(pub));
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             T c0, c1, c2, c3;
@@ -335,21 +343,18 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
                 c2 = fma(k1[0], u[a], c2);
                 c3 = fma(k1[1], u[a], c3);
             }
-            const D2 q01 = D2{c0, c1}, q23 = D2{c2, c3};
-            const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0;
-            // bit 3: keep i in {2, 3} (upper) or {0, 1}
-            const T k0 = b3 ? q23[0] : q01[0], k1 = b3 ? q23[1] : q01[1];
-            const T s0 = b3 ? q01[0] : q23[0], s1 = b3 ? q01[1] : q23[1];
-            const T r0 = k0 + dpp_lane<0x140>(s0), r1 = k1 + dpp_lane<0x140>(s1);
-            // bit 2: keep i = 2 b3 + b2
+            // pair b3: slot 0 here, slot 1 in the mirror partner (bit 3 flipped)
+            const T r0 = c0 + dpp_lane<0x140>(c2), r1 = c1 + dpp_lane<0x140>(c3);
+            // bit 2: keep column 2 b3 + b2
+            const bool b2 = (lane & 4) != 0;
             const T kk = b2 ? r1 : r0, ss = b2 ? r0 : r1;
             T t = kk + dpp_lane<0x141>(ss);
             t += dpp_lane<0x4E>(t);
             t += dpp_lane<0xB1>(t);
-            // the chunk's second column (i + 1) sits in the lanes with bit 2 flipped
+            // the chunk's second column sits in the lanes with bit 2 flipped
             const T o = dpp_lane<0x141>(t);
             if ((lane & 7) == 0)
-                gstore_col(rs, cola(e, rb) + (uint32_t)(32 * w + 8 * b + 2 * g + (b3 ? 1 : 0)) * 16,
+                gstore_col(rs, cola(e, rb) + pub + (uint32_t)(128 * b),
                            dchunk(t, o, e, flag), xl);
         }
     };
@@ -495,8 +500,8 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
             T pr[NA];
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-                const D2 va = *reinterpret_cast<const D2*>(&vcur[w][16 * b + 4 * g]);
-                const D2 vb = *reinterpret_cast<const D2*>(&vcur[w][16 * b + 4 * g + 2]);
+                const D2 va = *reinterpret_cast<const D2*>(&vcur[w][16 * b + 4 * g + 2 * b3]);
+                const D2 vb = *reinterpret_cast<const D2*>(&vcur[w][16 * b + 4 * g + 2 - 2 * b3]);
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
                     const D2 k0 = kget(a, b, 0), k1 = kget(a, b, 1);
@@ -661,18 +666,19 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
         for (int a = 0; a < NA; ++a) uo[a] = last_good >= 0 ? uhist[hs][rr * 8 + a] : u0;
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            const D2 va = last_good >= 0 ? *reinterpret_cast<const D2*>(&vhist[hs][cw + 16 * b + 4 * g]) : D2{v0, v0};
-            const D2 vb = last_good >= 0 ? *reinterpret_cast<const D2*>(&vhist[hs][cw + 16 * b + 4 * g + 2]) : D2{v0, v0};
+            const D2 va = last_good >= 0 ? *reinterpret_cast<const D2*>(&vhist[hs][cw + 16 * b + 4 * g + 2 * b3]) : D2{v0, v0};
+            const D2 vb = last_good >= 0 ? *reinterpret_cast<const D2*>(&vhist[hs][cw + 16 * b + 4 * g + 2 - 2 * b3]) : D2{v0, v0};
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
                 TP* prow = P + (int64_t)(row0 + rr + 16 * a) * p.ldp + col0 + cw + 16 * b + 4 * g;
                 const D2 o0 = (uo[a] * kget(a, b, 0)) * va, o1 = (uo[a] * kget(a, b, 1)) * vb;
                 if constexpr (sizeof(TP) == 8) {
-                    *reinterpret_cast<D2*>(prow) = o0;
-                    *reinterpret_cast<D2*>(prow + 2) = o1;
+                    *reinterpret_cast<D2*>(prow + 2 * b3) = o0;
+                    *reinterpret_cast<D2*>(prow + 2 - 2 * b3) = o1;
                 } else {
                     using F4 = __attribute__((ext_vector_type(4))) float;
-                    *reinterpret_cast<F4*>(prow) = F4{(float)o0[0], (float)o0[1], (float)o1[0], (float)o1[1]};
+                    const D2 x0 = b3 ? o1 : o0, x1 = b3 ? o0 : o1;
+                    *reinterpret_cast<F4*>(prow) = F4{(float)x0[0], (float)x0[1], (float)x1[0], (float)x1[1]};
                 }
             }
             __builtin_amdgcn_sched_barrier(0);

@@ -8,7 +8,12 @@
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_sweep.hip"
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_gather.hip"
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_mesh.hip"
+// OTF_M64_ALT: an alternative float64 mesh source to time in place of the library's (A/B)
+#ifdef OTF_M64_ALT
+#include OTF_M64_ALT
+#else
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_mesh64.hip"
+#endif
 #include "../ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/csrc/otf_comm.hip"
 
 #include <algorithm>

@@ -21,7 +21,8 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 PROF = os.path.join(REPO, "profiles")
-HOT = ("sk_resident_kernel", "sk_tiled_kernel", "sk_mesh_kernel", "sk_gather_kernel", "sk_pass_kernel", "sk_sweep_kernel", "cost_big_kernel", "cost_big16_kernel", "cost_split16_kernel",
+HOT = ("sk_mesh64_kernel", "dist_mfma_f64_kernel", "sqnorm_f64_kernel", "dist_scale_kernel",
+       "sk_resident_kernel", "sk_tiled_kernel", "sk_mesh_kernel", "sk_gather_kernel", "sk_pass_kernel", "sk_sweep_kernel", "cost_big_kernel", "cost_big16_kernel", "cost_split16_kernel",
        "split16_prep2_kernel", "cost_f16_kernel", "sk_init_kernel", "sk_plan_kernel")
 LIB = os.path.join(REPO, "ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd",
                    "otfuse", "lib", "libotfuse.so")
@@ -76,18 +77,23 @@ def main():
     if os.path.exists(c5trace):
         d5, n5 = medians(c5trace)
         summary["config5_kernels"] = {k: {"median_us": d5[k] / 1e3, "launches": n5[k]} for k in d5}
-    # float64 metric leg (bench.py --profile-only --profile-f64): cost + float64 mesh
-    summary["f64_kernels"] = {}
-    f64trace = os.path.join(OUT, "prof_f64", "run_kernel_trace.csv")
-    if os.path.exists(f64trace):
-        d6, n6 = medians(f64trace)
-        summary["f64_kernels"] = {k: {"median_us": d6[k] / 1e3, "launches": n6[k]} for k in d6}
-        shutil.copy(os.path.join(OUT, "prof_f64", "run_kernel_stats.csv"),
-                    os.path.join(PROF, f"{tag}_f64_kernel_stats.csv"))
+    # the float32 metric leg (bench.py --profile-only --profile-f32: split-fp16 cost + float32
+    # mesh); since r05 "prof" / pmc_*_auto are the float64 headline step
+    summary["f32_kernels"] = {}
+    f32trace = os.path.join(OUT, "prof_f32", "run_kernel_trace.csv")
+    if os.path.exists(f32trace):
+        d6, n6 = medians(f32trace)
+        summary["f32_kernels"] = {k: {"median_us": d6[k] / 1e3, "launches": n6[k]} for k in d6}
+        shutil.copy(os.path.join(OUT, "prof_f32", "run_kernel_stats.csv"),
+                    os.path.join(PROF, f"{tag}_f32_kernel_stats.csv"))
+    if os.path.exists(c5trace):
+        shutil.copy(os.path.join(OUT, "prof_c5", "run_kernel_stats.csv"),
+                    os.path.join(PROF, f"{tag}_config5_kernel_stats.csv"))
     for ctr, factor in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
         for p in glob.glob(os.path.join(OUT, f"pmc_{ctr}*", "run_counter_collection.csv")):
             med, _ = medians(p, "Counter_Value")
-            sect = "config5_kernels" if os.path.basename(os.path.dirname(p)).endswith("_c5") else "kernels"
+            leaf = os.path.basename(os.path.dirname(p))
+            sect = "config5_kernels" if leaf.endswith("_c5") else "f32_kernels" if leaf.endswith("_f32") else "kernels"
             for k, v in med.items():
                 summary[sect].setdefault(k, {})[ctr + "_bytes_corrected"] = v * 1024 * factor
     # MFMA utilisation pass: busy fraction = MFMA busy cycles / (1024 SIMDs x kernel
@@ -113,7 +119,7 @@ def main():
             cfg = summary["bench"].get("config", {})
     json.dump(summary, open(os.path.join(PROF, f"{tag}_summary.json"), "w"), indent=1)
     traffic = {}
-    for k, v in summary["kernels"].items():
+    for k, v in list(summary["f32_kernels"].items()) + list(summary["kernels"].items()):
         b = base_name(k)
         if b in HOT and "FETCH_SIZE_bytes_corrected" in v:
             traffic[b] = {"kernel": k, "median_us": v.get("median_us"),
