@@ -2,22 +2,27 @@
 
 Workload (one "step" = one solve): seeded paired MRI/PET embeddings
 X, Y in HBM (N = 4096, d = 512, float32) -> pairwise squared-Euclidean cost in float64
-(POT euclidean_distances order, the max-normalisation applied inside the solve) -> 100
-POT-semantics Sinkhorn iterations in float64 (eps = 0.1, stopThr = 0, so every iteration
-runs) -> N x N float64 transport plan written to HBM.  float64 is the reference's own
-precision (POT on NumPy float64, MRI_PET_OT_nojax.py:121-143), so the headline is
-like-for-like with the CPU path; parity: tests/test_gpu_precision.py (1e-9 of the oracle).
+(POT euclidean_distances order, divided by its max) -> 100 POT-semantics Sinkhorn
+iterations in float64 (eps = 0.1, stopThr = 0, so every iteration runs) -> N x N float64
+transport plan written to HBM.  float64 is the reference's own precision (POT on NumPy
+float64, MRI_PET_OT_nojax.py:70-75, 121-143), so the headline is like-for-like with the
+CPU path; parity: tests/test_gpu_pairwise.py, tests/test_gpu_precision.py (1e-9 of the
+oracle).  The step is ONE solve launch (ops.sinkhorn_pairwise -> otf_sinkhorn_pairwise_f64):
+the cost is built inside it, tile by tile, on the float64 matrix cores (--two-call: the
+cost kernel, then the solve on the stored cost).
 
   value            = MRI+PET pairs aligned per second, whole job (N x ranks / step time)
-  sinkhorn_iters_per_sec = iterations / time of the Sinkhorn call (incl. plan write)
-  roofline         = the dominant kernel, sk_mesh64_kernel (one launch runs all 100
-                     iterations with the float64 K = exp(-C/eps) held in the register files
-                     and LDS): its bound is LATENCY (per iteration three in-launch granule
-                     hops), reported as us per iteration against the VALU floor of the
-                     iteration's 2 N^2 float64 FMAs; the PMC traffic
-                     (profiles/kernel_traffic.json, only when measured on this exact library
-                     build) beside it
-  cost_roofline    = the float64 cost on v_mfma_f64_16x16x4_f64 vs the float64 matrix peak
+  sinkhorn_iters_per_sec = iterations / time of the solve call (incl. the cost build and
+                     the plan write for the fused step)
+  roofline         = the dominant kernel, sk_mesh64_kernel (the fused launch: cost tiles on
+                     v_mfma_f64_16x16x4_f64, then all 100 iterations with the float64
+                     K = exp(-C/eps) held in the register files and LDS): the step's float64
+                     FLOP (2 N^2 d for the cost + 4 N^2 per iteration) per second of the call
+                     against the float64 peak (78.6 TFLOP/s, matrix and vector alike); the
+                     per-iteration slope (latency-bound: three in-launch granule hops) and
+                     the intercept beside it; the PMC traffic (profiles/kernel_traffic.json,
+                     only when measured on this exact library build)
+  cost_roofline    = the two-call path's float64 cost kernel vs the float64 matrix peak
   metric_f32       = the same workload at float32 compute (split-fp16 cost, float32 mesh):
                      faster, within 1e-4 of the float64 oracle, NOT the reference's precision
   sweep_config5    = BASELINE config 5 on one GPU (N = 8192, d = 1024, fp16 cost, 200
@@ -97,6 +102,9 @@ def parse():
                    help="skip the per-training-step OT block leg (config 2)")
     p.add_argument("--multi-legs", action="store_true",
                    help="run the sharded RCCL legs also at world = 1 (they always run at world > 1)")
+    p.add_argument("--two-call", action="store_true",
+                   help="headline step as two calls (gw.pairwise_cost_f64 + ops.sinkhorn) instead of "
+                        "the fused ops.sinkhorn_pairwise")
     p.add_argument("--engine", default="auto",
                    choices=("auto", "stream", "resident", "tiled", "sweep", "gather", "mesh"),
                    help="Sinkhorn engine (auto = mesh / tiled / resident when the cost fits the "
@@ -138,10 +146,11 @@ def main():
     # Sinkhorn, float64 plan
     a64 = torch.full((N,), 1.0 / N, device=dev, dtype=torch.float64)
     ws64 = ops.sinkhorn_workspace(N, N, torch.float64, iters, dev)
+    wsp = ops.sinkhorn_pairwise_workspace(N, N, iters, dev)
     P64 = torch.empty((N, N), dtype=torch.float64, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 
-    def step(record):
+    def step_two_call(record, it=iters):
         if record:
             ev[0].record()
         # the max-normalisation (MRI_PET_OT_nojax.py:75) is applied inside the solve through
@@ -149,11 +158,26 @@ def main():
         C, cmax = gw.pairwise_cost_f64(X, Y, scale_max=False)
         if record:
             ev[1].record()
-        res = ops.sinkhorn(a64, a64, C, eps, max_iter=iters, stop_thr=0.0, cost_scale=cmax,
+        res = ops.sinkhorn(a64, a64, C, eps, max_iter=it, stop_thr=0.0, cost_scale=cmax,
                            workspace=ws64, plan_out=P64, engine=args.engine)
         if record:
             ev[2].record()
         return res
+
+    def step_fused(record, it=iters):
+        # MRI_PET_OT_nojax.py:70-75 + :143 as ONE solve launch: every workgroup builds its
+        # tile of the float64 cost on the matrix cores, the grid agrees on max(C), then the
+        # float64 mesh runs the 100 iterations on K held on chip (otf_sinkhorn_pairwise_f64)
+        if record:
+            ev[0].record()
+            ev[1].record()
+        res = ops.sinkhorn_pairwise(X, Y, eps, max_iter=it, stop_thr=0.0, workspace=wsp, plan_out=P64,
+                                    engine=args.engine)
+        if record:
+            ev[2].record()
+        return res
+
+    step = step_two_call if args.two_call else step_fused
 
     for _ in range(args.warmup):
         step(False)
@@ -191,6 +215,28 @@ def main():
     cost_ms = sorted(e[0].elapsed_time(e[1]) for e in evs[1:])[2]
     sk_ms = sorted(e[1].elapsed_time(e[2]) for e in evs[1:])[2]
     info = res.info()
+    # the solve launch split by iteration count: the same step at iters / 5 iterations, the
+    # per-iteration slope and the intercept (registration, the in-launch cost build for the
+    # fused step, K = exp, the plan write, the small launches)
+    it_lo = max(1, iters // 5)
+    evl = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(6)]
+    for k in range(6):
+        ev[:] = evl[k]
+        step(True, it_lo)
+    torch.cuda.synchronize()
+    sk_lo_ms = sorted(e[1].elapsed_time(e[2]) for e in evl[1:])[2]
+    slope_us = (sk_ms - sk_lo_ms) * 1e3 / (iters - it_lo)
+    intercept_us = sk_ms * 1e3 - iters * slope_us
+    two_call_ms = None
+    if not args.two_call:
+        # the same step as two calls (cost kernel, then the solve on the stored cost)
+        evt = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(6)]
+        for k in range(6):
+            ev[:] = evt[k]
+            step_two_call(True)
+        torch.cuda.synchronize()
+        two_call_ms = sorted(e[0].elapsed_time(e[2]) for e in evt[1:])[2]
+        cost_ms = sorted(e[0].elapsed_time(e[1]) for e in evt[1:])[2]
     engine = info["engine_name"]
     kernel_name = {"mesh": "sk_mesh64_kernel", "sweep": "sk_sweep_kernel", "tiled": "sk_tiled_kernel",
                    "resident": "sk_resident_kernel"}.get(engine, "sk_pass_kernel")
@@ -217,7 +263,28 @@ def main():
     # the float64 vector peak (78.6 TFLOP/s = 39.3 T FMA/s)
     floor_us = 2.0 * N * N / (F64_VALU_TFLOPS / 2 * 1e12) * 1e6
     algo_gbs = iter_bytes * iters / sk_s / 1e9
-    if engine in ("mesh", "tiled", "resident"):
+    cost_flops = 2.0 * N * N * d
+    iter_flops = 4.0 * N * N  # K v and K^T u: 2 N^2 FMAs
+    if not args.two_call and engine == "mesh":
+        # the fused launch does all the step's arithmetic: the cost on the float64 matrix
+        # cores, then the iterations on the float64 vector units -- both at 78.6 TFLOP/s
+        flops = cost_flops + iters * iter_flops
+        tf = flops / sk_s / 1e12
+        roofline = {"bound": "mfma", "kernel": kernel_name, "achieved": tf, "peak": F64_VALU_TFLOPS,
+                    "unit": "TFLOP/s", "frac": tf / F64_VALU_TFLOPS, "traffic": traffic,
+                    "flops_per_launch": flops, "launch_us": sk_ms * 1e3,
+                    "floor_us": flops / (F64_VALU_TFLOPS * 1e12) * 1e6,
+                    "per_iteration_us": slope_us, "per_iteration_floor_us": floor_us,
+                    "intercept_us": intercept_us,
+                    "note": ("ONE launch per step (otf_sinkhorn_pairwise_f64, csrc/otf_mesh64.hip PW): "
+                             "every workgroup builds its 128 x 512 tile of the float64 cost on "
+                             "v_mfma_f64_16x16x4_f64, the grid agrees on max(C), K = exp(-C/(eps max)) "
+                             "stays on chip (register files + LDS) for the 100 iterations (three "
+                             "in-launch granule hops each), then the N x N float64 plan; achieved = "
+                             "(2 N^2 d + iters 4 N^2) FLOP / the call's device time (incl. the norm and "
+                             "init launches); per_iteration_us / intercept_us: slope and intercept of "
+                             "the call's time at iters and iters / 5 iterations")}
+    elif engine in ("mesh", "tiled", "resident"):
         roofline = {"bound": "latency", "kernel": kernel_name, "achieved": us_per_iter,
                     "peak": floor_us, "unit": "us per iteration", "frac": floor_us / us_per_iter,
                     "traffic": traffic,
@@ -236,7 +303,6 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": algo_gbs / HBM_PEAK_GBS,
                     "traffic": traffic, "algorithmic_bytes_per_launch": iter_bytes * iters,
                     "note": "N*N*8 B per sweep"}
-    cost_flops = 2.0 * N * N * d
     cost_tflops = cost_flops / (cost_ms * 1e-3) / 1e12
 
     ms_per_step = elapsed * 1e3 / args.steps
@@ -257,25 +323,33 @@ def main():
         "config": {"workload": f"sinkhorn_pairwise_N{N}_d{d}_it{iters}", "N": N, "d": d,
                    "iters": iters, "eps": eps,
                    "cost": "sqeuclidean float64 from the float32 embeddings (POT euclidean_distances "
-                           "order), max applied in the solve",
+                           "order), max applied in the solve" + ("" if args.two_call else
+                                                                 ", built inside the solve launch"),
                    "sinkhorn": "POT sinkhorn_knopp semantics in float64, stopThr=0",
                    "plan": "N x N float64 written per step", "global_batch": N * world,
                    "parallelism": f"replicas x{world} (independent problems)"},
         "sinkhorn_iters_per_sec": iters / sk_s,
         "engine": engine,
         "status": info["status_name"],
-        "breakdown_ms": {"cost": cost_ms, "sinkhorn_incl_plan": sk_ms},
+        "breakdown_ms": ({"cost": cost_ms, "sinkhorn_incl_plan": sk_ms} if args.two_call else
+                         {"fused_call": sk_ms, "per_iteration": slope_us * 1e-3,
+                          "intercept": intercept_us * 1e-3, "two_call_step": two_call_ms,
+                          "two_call_cost": cost_ms}),
         "roofline": roofline,
         "cost_roofline": {"bound": "mfma", "kernel": "dist_mfma_f64_kernel",
                           "achieved": cost_tflops, "peak": F64_VALU_TFLOPS, "unit": "TFLOP/s",
                           "frac": cost_tflops / F64_VALU_TFLOPS, "op_us": cost_ms * 1e3,
                           "traffic": pmc_traffic("dist_mfma_f64_kernel"),
-                          "note": "2 N^2 d float64 FLOP on v_mfma_f64_16x16x4_f64 over the whole "
-                                  "host call (norm kernels, tile kernel, max) against the float64 "
-                                  "matrix peak (78.6 TFLOP/s)"},
+                          "note": ("the two-call path's cost (gw.pairwise_cost_f64: norm kernels, the "
+                                   "128 x 128 tile kernel on v_mfma_f64_16x16x4_f64, max) against the "
+                                   "float64 matrix peak (78.6 TFLOP/s); the headline step builds the "
+                                   "cost inside its solve launch instead" if not args.two_call else
+                                   "2 N^2 d float64 FLOP on v_mfma_f64_16x16x4_f64 over the whole "
+                                   "host call (norm kernels, tile kernel, max) against the float64 "
+                                   "matrix peak (78.6 TFLOP/s)")},
         "traffic_profile": {"fresh": fresh, "round": tj.get("round"), "lib_md5": lib_md5()},
     }
-    del ws64, P64
+    del ws64, wsp, P64
     if rank == 0 and not args.no_f32:
         out["metric_f32"] = metric_f32_leg(dev, X, Y, N, d, iters, eps, args.engine, pmc_traffic)
     if not args.no_hbm_probe:

@@ -309,6 +309,22 @@ int otf_sinkhorn_finish(const void* a, const void* b, const void* C, int64_t n, 
                         int64_t ldp, int32_t P_dtype, otf_sinkhorn_info* info, double* errlog,
                         void* workspace, size_t ws_bytes, otf_stream_t stream);
 
+/* Pairwise cost + Sinkhorn in float64, fused (MRI_PET_OT_nojax.py:70-75 the cost -- POT
+ * euclidean_distances of the float32 embeddings, squared, divided by its max -- and :143
+ * ot.sinkhorn on it).  For the float64 mesh's shapes (n a power-of-two multiple of 128 from
+ * 512 to 4096, m a multiple of 512 up to 4096, d a multiple of 16, 16-B aligned rows) the
+ * cost tile of every workgroup is built on v_mfma_f64_16x16x4_f64 inside the solve's
+ * launch (no n x m cost in HBM); other shapes run otf_cost_pairwise_f64 + otf_sinkhorn on
+ * the workspace.  metric OTF_SQEUCLIDEAN / OTF_EUCLIDEAN; scale_max: divide by the cost's
+ * max (POT's M /= M.max()), returned in *cmax_out (device, nullable) either way.  POT
+ * flavour; opts as otf_sinkhorn.  Workspace: otf_sinkhorn_pairwise_f64_workspace_size. */
+size_t otf_sinkhorn_pairwise_f64_workspace_size(int64_t n, int64_t m, int32_t max_iter);
+int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n, int64_t m,
+                              int64_t d, int32_t metric, int32_t scale_max, const double* a, const double* b,
+                              const otf_sinkhorn_opts* opts, double* u_out, double* v_out, void* P_out,
+                              int64_t ldp, int32_t P_dtype, double* cmax_out, otf_sinkhorn_info* info,
+                              double* errlog, void* workspace, size_t ws_bytes, otf_stream_t stream);
+
 /* Cross-rank persistent sweep (BASELINE config 5 on several GPUs of one node): one
  * problem's rows sharded over world <= 8 ranks, each rank one persistent launch that
  * streams its cost rows; the m column sums are exchanged INSIDE the launch as

@@ -79,9 +79,13 @@ struct SkMesh64Args {
     int64_t ldp;
     unsigned long long timeout_ticks;
     unsigned long long reg_ticks;
+    // pairwise form (PW kernels): the cost tile built in the prologue from the float32 rows
+    PairwiseF64 pw;
 };
 
 using D2 = __attribute__((ext_vector_type(2))) double;
+using D4 = __attribute__((ext_vector_type(4))) double;
+using F4 = __attribute__((ext_vector_type(4))) float;
 using ull = unsigned long long;
 
 // two float64 values, tag = epoch mod 4 | flag << 2 in their three low mantissa bits
@@ -160,13 +164,226 @@ __device__ unsigned long long g_m64pro[256 * 4];  // kernel start, roles known, 
     } while (0)
 #endif
 
+constexpr size_t kM64RegBytes = 11 * 256;  // 8 XCC counters, the registration barrier, the
+                                           // PW max barrier and the PW max, 256 B each
+constexpr int kM64MaxBar = 9 * 64, kM64MaxWord = 10 * 64;  // int offsets in xreg
+
+// PW prologue (sk_mesh64_kernel<..., PW = true>): the workgroup's 128 x 512 tile of
+// C = |x|^2 + |y|^2 - 2 x.y (POT euclidean_distances order, MRI_PET_OT_nojax.py:70-75) on
+// v_mfma_f64_16x16x4_f64 straight from the float32 rows -- float4 buffer loads per lane,
+// the k order inside each 16-deep chunk permuted the same way for both operands (lane
+// group g holds k = 16 t + 4 g + q, step q takes element q), no LDS staging -- with the
+// columns as the M index: Y row 4 (rr & 3) + (rr >> 2) of a 16-column block lands in
+// accumulator element r of lane (rr, g) as column 4 g + r, the K layout.  Block 3 first
+// (into LDS), then blocks 0..2 accumulate in the K registers themselves; clamped at 0 (and
+// the square root for the euclidean metric).  The grid's max: one atomic max per workgroup
+// + a flat barrier; then K = exp(-C / (reg max)) in place.  Returns false on a stall.
+template <typename SK>
+__device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM64NA][kM64RB], SK& sK, int w,
+                                             int lane, int rr, int g, int row0, int col0, int cw,
+                                             int target, bool lead, unsigned long long& deadline,
+                                             int* s_flag, double* s_red, double* s_nx, double* s_ny) {
+    constexpr int NA = kM64NA, RB = kM64RB;
+    const PairwiseF64& q = p.pw;
+    const int cm = 4 * (rr & 3) + (rr >> 2);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(q.X), 0, (int)q.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(q.Y), 0, (int)q.ybytes, 0x00020000);
+    const uint32_t xo = (uint32_t)(((int64_t)(row0 + rr) * q.ldx + 4 * g) * 4);
+    const uint32_t yo = (uint32_t)(((int64_t)(col0 + cw + cm) * q.ldy + 4 * g) * 4);
+    const uint32_t xs16 = (uint32_t)(16 * q.ldx * 4), ys16 = (uint32_t)(16 * q.ldy * 4);
+    const int nt = q.d / 16;
+    auto ldx4 = [&](int a, int t) -> F4 {
+        return __builtin_bit_cast(F4, __builtin_amdgcn_raw_buffer_load_b128(rx, xo, (uint32_t)a * xs16 + (uint32_t)t * 64u, 0));
+    };
+    auto ldy4 = [&](int b, int t) -> F4 {
+        return __builtin_bit_cast(F4, __builtin_amdgcn_raw_buffer_load_b128(ry, yo, (uint32_t)b * ys16 + (uint32_t)t * 64u, 0));
+    };
+    // POT's order: -2 x.y + |x|^2 + |y|^2, clamped at 0 (the euclidean root in its own pass)
+    auto fin = [&](double acc, double nxi, double nyj) -> double {
+        double v = -2.0 * acc;
+        v += nxi;
+        v += nyj;
+        return v > 0 ? v : 0.0;
+    };
+    // the squared norms come out of the same loads: a lane sums the squares of its k
+    // quarter, the 4 lanes of a row (lane bits 5, 4) add them up; the column norms reach the
+    // lanes of the accumulator layout (column 4 g + r is Y row cm = 4 r + g) by a shuffle
+    auto sum_g = [&](double x) -> double {
+        x += __shfl_xor(x, 16);
+        return x + __shfl_xor(x, 32);
+    };
+    auto col_norms = [&](double ysq) -> D4 {
+        D4 r4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) r4[r] = __shfl(ysq, 4 * r + g);
+        return r4;
+    };
+    double lmax = 0.0;
+    // block 3 -> LDS
+    {
+        D4 acc[NA];
+        double nxr[NA];
+        double ysq = 0.0, ysq_o[RB] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            acc[a] = D4{0.0, 0.0, 0.0, 0.0};
+            nxr[a] = 0.0;
+        }
+        for (int t = 0; t < nt; ++t) {
+            const F4 yv = ldy4(3, t);
+            // blocks 0..2's column norms here, where registers are free
+#pragma unroll
+            for (int b = 0; b < RB; ++b) {
+                const F4 yo = ldy4(b, t);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) ysq_o[b] = fma((double)yo[k], (double)yo[k], ysq_o[b]);
+            }
+            F4 xv[NA];
+#pragma unroll
+            for (int a = 0; a < NA; ++a) xv[a] = ldx4(a, t);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const double yk = (double)yv[k];
+                ysq = fma(yk, yk, ysq);
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    const double xk = (double)xv[a][k];
+                    nxr[a] = fma(xk, xk, nxr[a]);
+                    acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(yk, xk, acc[a], 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            nxr[a] = sum_g(nxr[a]);
+            if (g == 0) s_nx[rr + 16 * a] = nxr[a];  // this wave's copy, read back after pass 2
+        }
+        const D4 nyv = col_norms(sum_g(ysq));
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+            const D4 ny4 = col_norms(sum_g(ysq_o[b]));
+            if (rr == 0) *reinterpret_cast<D4*>(s_ny + 16 * b + 4 * g) = ny4;  // this wave's copy
+        }
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            const double nxi = nxr[a];
+            D4 c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                c[r] = fin(acc[a][r], nxi, nyv[r]);
+                if (q.euclid) c[r] = sqrt(c[r]);
+                lmax = fmax(lmax, c[r]);
+            }
+            sK[w][a][0][lane] = D2{c[0], c[1]};
+            sK[w][a][1][lane] = D2{c[2], c[3]};
+        }
+        // block 3 lives in LDS from here: no register copy kept across the second pass
+        asm volatile("" : "+v"(lmax) :: "memory");
+    }
+    // blocks 0..2 in the K registers
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int b = 0; b < RB; ++b) kr[a][b] = D4{0.0, 0.0, 0.0, 0.0};
+    // the 192 accumulators leave ~40 registers: one row block's X operand in flight ahead of
+    // its 12 MFMAs (768 cycles), the next chunk's Y operands loaded during the last row blocks
+    {
+        F4 yv[RB], yn[RB];
+#pragma unroll
+        for (int b = 0; b < RB; ++b) yv[b] = ldy4(b, 0);
+        F4 xn = ldx4(0, 0);
+        for (int t = 0; t < nt; ++t) {
+            const bool more = t + 1 < nt;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                const F4 xv = xn;
+                if (a + 1 < NA) xn = ldx4(a + 1, t);
+                else if (more) xn = ldx4(0, t + 1);
+                if (a == NA / 2 && more) {
+#pragma unroll
+                    for (int b = 0; b < RB; ++b) yn[b] = ldy4(b, t + 1);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const double xk = (double)xv[k];
+#pragma unroll
+                    for (int b = 0; b < RB; ++b)
+                        kr[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)yv[b][k], xk, kr[a][b], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (more) {
+#pragma unroll
+                for (int b = 0; b < RB; ++b) yv[b] = yn[b];
+            }
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < RB; ++b) {
+        const D4 nyv = *reinterpret_cast<const D4*>(s_ny + 16 * b + 4 * g);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            const double nxi = s_nx[rr + 16 * a];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) kr[a][b][r] = fin(kr[a][b][r], nxi, nyv[r]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (q.euclid) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+#pragma unroll
+            for (int b = 0; b < RB; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) kr[a][b][r] = sqrt(kr[a][b][r]);
+    }
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) lmax = fmax(lmax, kr[a][b][r]);
+    // the grid's max (costs are >= 0: the bit patterns order like the values)
+    lmax = wave_max(lmax);
+    if (lane == 0) s_red[w] = lmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double mx = s_red[0];
+        for (int ww = 1; ww < kM64NW; ++ww) mx = fmax(mx, s_red[ww]);
+        __hip_atomic_fetch_max(reinterpret_cast<unsigned long long*>(p.xreg + kM64MaxWord),
+                               __builtin_bit_cast(unsigned long long, mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!grid_barrier(p.xreg + kM64MaxBar, target, deadline, p.timeout_ticks, s_flag)) return false;
+    const double cmax = __builtin_bit_cast(
+        double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(p.xreg + kM64MaxWord), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT));
+    if (lead && q.cmax_out) *q.cmax_out = cmax;
+    const double cinv = q.scale ? 1.0 / cmax : 1.0;
+    const double ks = -1.0 / p.reg * cinv;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) kr[a][b][r] = exp(kr[a][b][r] * ks);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const D2 c = sK[w][a][h][lane];
+            sK[w][a][h][lane] = D2{exp(c[0] * ks), exp(c[1] * ks)};
+        }
+    }
+    return true;
+}
+
 constexpr int pow2_ceil(int x) { return x <= 1 ? 1 : 2 * pow2_ceil((x + 1) / 2); }
 // u history slot of tile row r: lane rr = r & 15 reads its 8 rows rr + 16 a as one run
 __device__ __forceinline__ int upos(int r) { return (r & 15) * 8 + (r >> 4); }
 
 // SNRB, SNCB: the shape compiled in (0 = from the arguments).  Every shape is a mesh of
-// whole tiles (n = nrb * 128, m = ncb * 512), so there are no bound tests.
-template <typename TP, int SNRB, int SNCB>
+// whole tiles (n = nrb * 128, m = ncb * 512), so there are no bound tests.  PW: the cost
+// tile is built in the prologue from the float32 rows (p.pw) instead of read from C.
+template <typename TP, int SNRB, int SNCB, bool PW>
 __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     using T = double;
     constexpr int NW = kM64NW, TR = kM64TR, TC = kM64TC, WC = kM64WC, NA = kM64NA, NB = kM64NB,
@@ -254,8 +471,21 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
 
     // ---- K: rows rr + 16 a, columns cw + 16 b + 4 g + (0..3) as two pairs h; blocks
     // b < 3 in registers, b = 3 in LDS
-    D2 kr[NA][RB][2];
-    {
+    // lane (rr, g) of wave w holds rows rr + 16 a x columns cw + 16 b + 4 g + (0..3) of
+    // block b < 3 as one 4-vector (the v_mfma_f64_16x16x4_f64 accumulator of that 16 x 16
+    // block with the columns as its M index: PW builds the cost right there)
+    D4 kr[NA][RB];
+    if constexpr (PW) {
+        if (!pw_cost_tile(p, kr, sK, w, lane, rr, g, row0, col0, cw, nrb * ncb, lead, deadline, &s_reg[3],
+                          &spsh[0][0], &rowbuf[w][0], &vcur[w][0])) {
+            // the max barrier stalled: a mid-solve stall (OTF_SK_TIMEOUT), every workgroup leaves
+            if (tid == 0) {
+                mark_stalled(&p.info->stalled, kStallMid);
+                if (lead) p.info->status = OTF_SK_TIMEOUT;
+            }
+            return;
+        }
+    } else {
         const T* cbase = p.C + (int64_t)(row0 + rr) * p.ldc + col0 + cw + 4 * g;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
@@ -266,8 +496,12 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
                 for (int h = 0; h < 2; ++h) {
                     const D2 c = *reinterpret_cast<const D2*>(crow + 16 * b + 2 * h);
                     const D2 e = D2{exp(c[0] * ks), exp(c[1] * ks)};
-                    if (b < RB) kr[a][b][h] = e;
-                    else sK[w][a][h][lane] = e;
+                    if (b < RB) {
+                        kr[a][b][2 * h] = e[0];
+                        kr[a][b][2 * h + 1] = e[1];
+                    } else {
+                        sK[w][a][h][lane] = e;
+                    }
                 }
             }
             // one row group's loads in flight at a time: hoisting them all needs 256
@@ -276,7 +510,9 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
         }
     }
     OTF_M64PRO(2);
-    auto kget = [&](int a, int b, int h) -> D2 { return b < RB ? kr[a][b][h] : sK[w][a][h][lane]; };
+    auto kget = [&](int a, int b, int h) -> D2 {
+        return b < RB ? D2{kr[a][b][2 * h], kr[a][b][2 * h + 1]} : sK[w][a][h][lane];
+    };
     // row hop: thread -> chunk gc (rows 2 gc, 2 gc + 1 of the tile), member gq
     const int gc = 8 * w + (lane >> 3), gq = lane & 7;
     // hop B: lane < 32 polls chunk 32 w + lane of the tile (columns cw + 2 lane, + 1)
@@ -690,11 +926,11 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     }
 }
 
-template <typename TP>
+template <typename TP, bool PW>
 hipError_t launch_mesh64_t(int grid, SkMesh64Args& p, hipStream_t s) {
     void* args[] = {&p};
-    const void* k = (p.nrb == 32 && p.ncb == 8) ? (const void*)sk_mesh64_kernel<TP, 32, 8>
-                                                : (const void*)sk_mesh64_kernel<TP, 0, 0>;
+    const void* k = (p.nrb == 32 && p.ncb == 8) ? (const void*)sk_mesh64_kernel<TP, 32, 8, PW>
+                                                : (const void*)sk_mesh64_kernel<TP, 0, 0, PW>;
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 512, 0);
     if (e != hipSuccess) return e;
@@ -702,7 +938,6 @@ hipError_t launch_mesh64_t(int grid, SkMesh64Args& p, hipStream_t s) {
     return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
 }
 
-constexpr size_t kM64RegBytes = 9 * 256;  // 8 XCC counters + the barrier word, 256 B each
 
 struct Mesh64Shape {
     int nrb, ncb, cpr;
@@ -738,12 +973,18 @@ size_t mesh64_region_bytes(int64_t n, int64_t m) {
     return kM64RegBytes + s.row_bytes + s.cola_bytes + s.colb_bytes;
 }
 
+bool mesh64_pairwise_ok(int64_t n, int64_t m, int64_t d, int64_t ldx, int64_t ldy, const void* X, const void* Y) {
+    return mesh64_supported(n, m) && d >= 16 && d % 16 == 0 && ldx >= d && ldy >= d && ldx % 4 == 0 &&
+           ldy % 4 == 0 && (uintptr_t)X % 16 == 0 && (uintptr_t)Y % 16 == 0 && n * ldx * 4 < (1ll << 31) &&
+           m * ldy * 4 < (1ll << 31);
+}
+
 hipError_t run_mesh64(const double* C, int64_t ldc, int n, int m, const double* a_pad, const double* b_pad,
                       const double* cost_scale, const otf_sinkhorn_opts& o, void* region, double* u_out,
                       double* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                      double* errlog, bool zeroed, hipStream_t s) {
+                      double* errlog, bool zeroed, hipStream_t s, const PairwiseF64* pw) {
     if (!mesh64_supported(n, m) || !region) return hipErrorInvalidValue;
-    if (ldc % 2 != 0 || ((uintptr_t)C % 16) != 0) return hipErrorInvalidValue;
+    if (!pw && (ldc % 2 != 0 || ((uintptr_t)C % 16) != 0)) return hipErrorInvalidValue;
     if (P_out && (ldp % 4 != 0 || ((uintptr_t)P_out % 16) != 0)) return hipErrorInvalidValue;
     const Mesh64Shape sh = mesh64_shape(n, m);
     SkMesh64Args p{};
@@ -788,8 +1029,14 @@ hipError_t run_mesh64(const double* C, int64_t ldc, int n, int m, const double* 
     if (grid > device_cu_count()) return hipErrorCooperativeLaunchTooLarge;
     if (p.xcc_local && 8 * sh.nrb <= device_cu_count()) grid = 8 * sh.nrb;
     else p.xcc_local = 0;
-    if (P_out && P_dtype == OTF_F32) return launch_mesh64_t<float>(grid, p, s);
-    return launch_mesh64_t<double>(grid, p, s);
+    if (pw) {
+        p.pw = *pw;
+        p.cost_scale = nullptr;
+        if (P_out && P_dtype == OTF_F32) return launch_mesh64_t<float, true>(grid, p, s);
+        return launch_mesh64_t<double, true>(grid, p, s);
+    }
+    if (P_out && P_dtype == OTF_F32) return launch_mesh64_t<float, false>(grid, p, s);
+    return launch_mesh64_t<double, false>(grid, p, s);
 }
 
 }  // namespace otf

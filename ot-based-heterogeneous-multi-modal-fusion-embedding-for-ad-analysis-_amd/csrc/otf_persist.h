@@ -346,10 +346,31 @@ size_t mesh_region_bytes(int64_t n, int64_t m);
 // split between the register files and LDS
 bool mesh64_supported(int64_t n, int64_t m);
 size_t mesh64_region_bytes(int64_t n, int64_t m);
+// The pairwise form of the float64 mesh (otf_sinkhorn_pairwise_f64): the cost tile is built
+// in the kernel's prologue from the float32 rows X (n x d) and Y (m x d) (their squared
+// norms from the same loads), and max-scaled when `scale` (the grid's max: one atomic + a
+// barrier).
+struct PairwiseF64 {
+    const float* X;
+    int64_t ldx;
+    const float* Y;
+    int64_t ldy;
+    int d, euclid, scale;
+    double* cmax_out;  // the cost's max (device, nullable)
+    uint32_t xbytes, ybytes;
+};
+// otf_gw.hip: the guarded one-workgroup cost build behind a pairwise mesh launch (runs only
+// after a registration give-up)
+hipError_t pairwise_fallback_cost_f64(const int* stalled, const float* X, int64_t ldx, const float* Y, int64_t ldy,
+                                      int64_t n, int64_t m, int64_t d, double* nx, double* ny,
+                                      int euclid, double* C, int64_t ldc, double* cmax, double* cmax_out,
+                                      hipStream_t s);
+// d a multiple of 16, X / Y 16-B aligned with ld a multiple of 4, each < 2 GiB
+bool mesh64_pairwise_ok(int64_t n, int64_t m, int64_t d, int64_t ldx, int64_t ldy, const void* X, const void* Y);
 hipError_t run_mesh64(const double* C, int64_t ldc, int n, int m, const double* a_pad, const double* b_pad,
                       const double* cost_scale, const otf_sinkhorn_opts& o, void* region, double* u_out,
                       double* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                      double* errlog, bool zeroed, hipStream_t s);
+                      double* errlog, bool zeroed, hipStream_t s, const PairwiseF64* pw = nullptr);
 template <typename CT>
 hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,

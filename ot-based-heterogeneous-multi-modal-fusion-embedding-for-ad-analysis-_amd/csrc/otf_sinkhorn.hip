@@ -2630,6 +2630,99 @@ int otf_sinkhorn(const void* a, const void* b, const void* C, int64_t n, int64_t
     return OTF_EINVAL;
 }
 
+// ---------------------------------------------------------------------------------------
+// Pairwise cost + Sinkhorn, float64 (include/otfuse.h).  Workspace: [the float64 Sinkhorn
+// workspace][the n x m float64 cost (the unfused path and the fallback)][the cost call's
+// workspace (norms, per-tile maxima)][the max].
+namespace otf {
+namespace {
+struct PwLayout {
+    size_t sk, c, cost, total;
+};
+PwLayout pw_layout(int64_t n, int64_t m, int32_t max_iter) {
+    PwLayout l;
+    l.sk = (otf_sinkhorn_workspace_size(n, m, OTF_F64, max_iter) + 255) / 256 * 256;
+    l.c = ((size_t)n * (size_t)m * 8 + 255) / 256 * 256;
+    l.cost = (otf_cost_pairwise_f64_workspace_size(n, m) + 255) / 256 * 256;
+    l.total = l.sk + l.c + l.cost + 256;
+    return l;
+}
+}  // namespace
+}  // namespace otf
+
+size_t otf_sinkhorn_pairwise_f64_workspace_size(int64_t n, int64_t m, int32_t max_iter) {
+    if (n <= 0 || m <= 0) return 0;
+    return otf::pw_layout(n, m, max_iter).total;
+}
+
+int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n, int64_t m,
+                              int64_t d, int32_t metric, int32_t scale_max, const double* a, const double* b,
+                              const otf_sinkhorn_opts* opts, double* u_out, double* v_out, void* P_out,
+                              int64_t ldp, int32_t P_dtype, double* cmax_out, otf_sinkhorn_info* info,
+                              double* errlog, void* workspace, size_t ws_bytes, otf_stream_t stream) {
+    using namespace otf;
+    if (!opts || !X || !Y || !workspace || n <= 0 || m <= 0 || d <= 0) return OTF_EINVAL;
+    if (ldx < d || ldy < d) return OTF_EINVAL;
+    if (metric != OTF_SQEUCLIDEAN && metric != OTF_EUCLIDEAN) return OTF_EINVAL;
+    if (P_out && P_dtype != OTF_F32 && P_dtype != OTF_F64) return OTF_EINVAL;
+    if (opts->flavor != OTF_FLAVOR_POT) return OTF_EUNSUPPORTED;
+    const otf_sinkhorn_opts& o = *opts;
+    const PwLayout L = pw_layout(n, m, o.max_iter);
+    if (ws_bytes < L.total) return OTF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    char* base = (char*)workspace;
+    void* ws_sk = base;
+    double* Cw = (double*)(base + L.sk);
+    char* ws_cost = base + L.sk + L.c;
+    double* cmax = (double*)(base + L.sk + L.c + L.cost);
+    double* nx = (double*)ws_cost;  // the cost call's layout: norms of X, then of Y
+    double* ny = (double*)(ws_cost + (8 * (size_t)n + 255) / 256 * 256);
+    const bool whole = o.n_total <= 0 || o.n_total == n;
+    const bool engine_ok = o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled());
+    bool fused = whole && !o.shift && o.max_iter >= 1 && engine_ok && u_out && v_out &&
+                 mesh64_pairwise_ok(n, m, d, ldx, ldy, X, Y);
+    if (!u_out || !v_out) return OTF_EINVAL;
+    if (P_out && (ldp < m || ldp % 2 != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
+    if (fused) {
+        SkSetup<double> su;
+        int rc = sk_prepare<double, double>(a, b, Cw, n, m, m, o, info, ws_sk, L.sk, su);
+        if (rc != OTF_OK) return rc;
+        // AUTO takes the float64 mesh where it takes it on a given cost (past one tiled-engine
+        // tile per CU)
+        if (su.w.mesh_bytes == 0 ||
+            (o.engine == OTF_ENGINE_AUTO && su.w.t_nrb * su.w.t_ncb <= device_cu_count()))
+            fused = false;
+        if (fused) {
+            rc = sk_init<double>(su, a, b, n, m, info, s, su.w.mesh, su.w.mesh_bytes);
+            if (rc != OTF_OK) return rc;
+            double* errl = errlog ? errlog : su.w.errlog;
+            PairwiseF64 pw{X, ldx, Y, ldy, (int)d, metric == OTF_EUCLIDEAN ? 1 : 0, scale_max ? 1 : 0,
+                           cmax_out, (uint32_t)(n * ldx * 4), (uint32_t)(m * ldy * 4)};
+            const hipError_t e = run_mesh64(nullptr, m, (int)n, (int)m, (const double*)su.w.a_pad,
+                                            (const double*)su.w.b_pad, nullptr, o, su.w.mesh, u_out, v_out, P_out,
+                                            ldp, P_dtype, info, errl, /*zeroed=*/true, s, &pw);
+            if (e == hipSuccess) {
+                // the fallback: the cost (one workgroup) and the solve, both only after a
+                // registration give-up
+                OTF_HIP(pairwise_fallback_cost_f64(&info->stalled, X, ldx, Y, ldy, n, m, d, nx, ny,
+                                                   metric == OTF_EUCLIDEAN ? 1 : 0, Cw, m, cmax, cmax_out, s));
+                return check_hip(launch_solo<double, double>(su, Cw, m, n, m, scale_max ? cmax : nullptr, o, u_out,
+                                                             v_out, P_out, ldp, P_dtype, info, errl, s));
+            }
+            (void)hipGetLastError();
+            if (o.engine == OTF_ENGINE_MESH) return check_hip(e);
+        }
+    }
+    // the cost, then the solve on it
+    int rc = otf_cost_pairwise_f64(X, ldx, Y, ldy, n, m, d, metric, 0, 0, Cw, m, cmax, ws_cost, L.cost, stream);
+    if (rc != OTF_OK) return rc;
+    if (cmax_out) OTF_HIP(hipMemcpyAsync(cmax_out, cmax, 8, hipMemcpyDeviceToDevice, s));
+    otf_sinkhorn_opts o2 = o;
+    if (o2.engine == OTF_ENGINE_MESH && !mesh64_supported(n, m)) o2.engine = OTF_ENGINE_AUTO;
+    return otf_sinkhorn(a, b, Cw, n, m, m, OTF_F64, scale_max ? cmax : nullptr, &o2, u_out, v_out, P_out, ldp,
+                        P_dtype, info, errlog, ws_sk, L.sk, stream);
+}
+
 int otf_sinkhorn_profile(const void* a, const void* b, const void* C, int64_t n, int64_t m,
                          int64_t ldc, int32_t dtype, const void* cost_scale,
                          const otf_sinkhorn_opts* opts, void* u_out, void* v_out,

@@ -259,6 +259,7 @@ class SinkhornResult:
     # POT's scalings are u = 2^A u~, v = 2^B v~ (see pot_scalings)
     shift_a: torch.Tensor | None = None
     shift_b: torch.Tensor | None = None
+    cost_max: torch.Tensor | None = None  # sinkhorn_pairwise: max of the unscaled cost (device)
     _info: dict | None = field(default=None, repr=False)
 
     @property
@@ -471,6 +472,68 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
         sb = workspace[ob.value: ob.value + 4 * m].view(torch.float32)
     return SinkhornResult(u=u, v=v, plan=P, info_dev=info, errlog_dev=errlog, flavor=flavor,
                           shift_a=sa, shift_b=sb)
+
+
+def sinkhorn_pairwise_workspace(n: int, m: int, max_iter: int, device) -> torch.Tensor:
+    wsb = L.lib().otf_sinkhorn_pairwise_f64_workspace_size(n, m, max_iter)
+    return torch.empty(wsb, dtype=torch.uint8, device=device)
+
+
+def sinkhorn_pairwise(X: torch.Tensor, Y: torch.Tensor, reg: float, a: torch.Tensor | None = None,
+                      b: torch.Tensor | None = None, metric: str = "sqeuclidean", scale_max: bool = True,
+                      max_iter: int = 1000, stop_thr: float = 1e-9, check_every: int = 10,
+                      err_squared: bool = False, want_plan: bool = True, plan_dtype=torch.float64,
+                      workspace: torch.Tensor | None = None, plan_out: torch.Tensor | None = None,
+                      engine: str = "auto") -> SinkhornResult:
+    """The reference's cost + solve in float64, fused where the shape allows: POT's
+    ``M = euclidean_distances(X, Y, squared=True); M /= M.max(); ot.sinkhorn(a, b, M, reg)``
+    (MRI_PET_OT_nojax.py:70-75, :143) from float32 embeddings ``X`` (n, d), ``Y`` (m, d).
+
+    For the float64 mesh's shapes (n = 512..4096 a power-of-two multiple of 128, m a
+    multiple of 512 up to 4096, d a multiple of 16) every workgroup of the solve's launch
+    builds its tile of the cost on the float64 matrix cores in its prologue (no n x m cost
+    in HBM, otf_sinkhorn_pairwise_f64); other shapes run the cost and the solve as two
+    calls.  ``a``/``b`` default to the uniform marginals.  The result's ``cost_max`` holds
+    max(M) before the scaling (a device scalar)."""
+    _dev(X, "X")
+    _dev(Y, "Y")
+    if metric not in ("sqeuclidean", "euclidean"):
+        raise ValueError(f"metric {metric!r} not supported (sqeuclidean | euclidean)")
+    if X.dim() != 2 or Y.dim() != 2 or X.shape[1] != Y.shape[1]:
+        raise ValueError(f"X {tuple(X.shape)} and Y {tuple(Y.shape)} must be (n, d) and (m, d)")
+    X = X.float().contiguous()
+    Y = Y.float().contiguous()
+    n, d = X.shape
+    m = Y.shape[0]
+    dev = X.device
+    a = uniform(n, torch.float64, dev) if a is None else _dev(a, "a").double().contiguous()
+    b = uniform(m, torch.float64, dev) if b is None else _dev(b, "b").double().contiguous()
+    if a.numel() != n or b.numel() != m:
+        raise ValueError(f"a ({a.numel()}) / b ({b.numel()}) do not match ({n}, {m})")
+    u = torch.empty(n, dtype=torch.float64, device=dev)
+    v = torch.empty(m, dtype=torch.float64, device=dev)
+    cmax = torch.empty(1, dtype=torch.float64, device=dev)
+    info = torch.empty(L.INFO_INT32S, dtype=torch.int32, device=dev)
+    errlog = torch.empty(max_iter // max(check_every, 1) + 2, dtype=torch.float64, device=dev)
+    if workspace is None:
+        workspace = sinkhorn_pairwise_workspace(n, m, max_iter, dev)
+    P = None
+    if want_plan:
+        P = plan_out if plan_out is not None else _alloc_rowmajor(n, m, plan_dtype, dev, 4)
+        if P.dtype not in _DT or tuple(P.shape) != (n, m):
+            raise ValueError("plan_out must be (n, m) float32/float64")
+    opts = L.SinkhornOpts(reg=float(reg), stop_thr=float(stop_thr), max_iter=int(max_iter),
+                          check_every=int(check_every), flavor=L.OTF_FLAVOR_POT,
+                          err_squared=int(err_squared), sync_every=0, engine=L.ENGINES[engine],
+                          cost_f16=0, deterministic=0, shift=0)
+    met = L.OTF_EUCLIDEAN if metric == "euclidean" else L.OTF_SQEUCLIDEAN
+    L.check(L.lib().otf_sinkhorn_pairwise_f64(
+        X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, m, d, met, int(bool(scale_max)),
+        a.data_ptr(), b.data_ptr(), ctypes.byref(opts), u.data_ptr(), v.data_ptr(), L.ptr(P),
+        P.stride(0) if P is not None else 0, _DT[P.dtype] if P is not None else 0, cmax.data_ptr(),
+        info.data_ptr(), errlog.data_ptr(), workspace.data_ptr(), workspace.numel(),
+        L.stream_handle(dev)), "otf_sinkhorn_pairwise_f64")
+    return SinkhornResult(u=u, v=v, plan=P, info_dev=info, errlog_dev=errlog, flavor="pot", cost_max=cmax)
 
 
 def sinkhorn_profile(a, b, C, reg, iters, cost_scale=None, flavor="pot", workspace=None) -> float:

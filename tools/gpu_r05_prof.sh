@@ -22,4 +22,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
   run pmc_${c}_f32 240 --pmc $c --kernel-trace -d gpurun_out/pmc_${c}_f32 -o run --output-format csv -- $B --profile-f32
   run pmc_${c}_c5 240 --pmc $c --kernel-trace -d gpurun_out/pmc_${c}_c5 -o run --output-format csv -- $B --profile-config5
 done
+run pmc_MFMA_auto 240 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_MFMA_auto -o run --output-format csv -- $B
 echo done
