@@ -127,7 +127,8 @@ def test_pairwise_registration_fallback(orc, dev, monkeypatch):
     one-workgroup solve queued behind it return the oracle's plan (info fallback = 1)."""
     from otfuse import ops
     monkeypatch.setenv("OTF_REG_MS", "1")
-    X, Y = _emb(1024, 2048, 64, 21)
+    # the whole-chip shape (256 workgroups): the blocker's CUs keep some of them out
+    X, Y = _emb(4096, 4096, 64, 21)
     P_r, u_r, v_r, info_r, mx = _oracle(orc, X, Y, 0.05, 20)
     Xd, Yd = torch.from_numpy(X).to(dev), torch.from_numpy(Y).to(dev)
     g = torch.Generator(device=dev).manual_seed(3)
