@@ -47,7 +47,6 @@
 
 #include "otf_device.h"
 #include "otf_emd.h"
-#include "otf_persist.h"
 
 namespace otf {
 namespace {
@@ -1418,68 +1417,9 @@ __global__ __launch_bounds__(256) void dist_scale_kernel(double* C, int64_t ldc,
 
 constexpr int DIST_PARTS = 512;
 
-// Behind the pairwise float64 mesh (otf_sinkhorn_pairwise_f64): only when that grid gave
-// up at its registration (info->stalled == kStallRegistration, the one-workgroup solve
-// fallback follows) this single workgroup builds the cost the mesh would have built --
-// the dist_mfma_f64_kernel epilogue's order, the max -- into the workspace; otherwise it
-// returns at once.
-__global__ __launch_bounds__(512) void pw_fallback_cost_kernel(const int* stalled, const float* X, int64_t ldx,
-                                                               const float* Y, int64_t ldy, int n, int m, int d,
-                                                               double* nx, double* ny, int euclid,
-                                                               double* C, int64_t ldc, double* cmax,
-                                                               double* cmax_out) {
-    __shared__ int s_go;
-    __shared__ double red[8];
-    if (threadIdx.x == 0)
-        s_go = __hip_atomic_load(stalled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kStallRegistration;
-    __syncthreads();
-    if (!s_go) return;
-    // the squared norms (the fused launch forms its own; nothing else wrote these)
-    for (int i = threadIdx.x; i < n + m; i += blockDim.x) {
-        const float* r = i < n ? X + (int64_t)i * ldx : Y + (int64_t)(i - n) * ldy;
-        double s = 0;
-        for (int k = 0; k < d; ++k) s = fma((double)r[k], (double)r[k], s);
-        (i < n ? nx[i] : ny[i - n]) = s;
-    }
-    __syncthreads();
-    double mx = 0.0;
-    for (int64_t e = threadIdx.x; e < (int64_t)n * m; e += blockDim.x) {
-        const int i = (int)(e / m), j = (int)(e % m);
-        const float* x = X + (int64_t)i * ldx;
-        const float* y = Y + (int64_t)j * ldy;
-        double acc = 0;
-        for (int k = 0; k < d; ++k) acc = fma((double)x[k], (double)y[k], acc);
-        double v = -2.0 * acc;
-        v += nx[i];
-        v += ny[j];
-        v = v > 0 ? v : 0.0;
-        if (euclid) v = sqrt(v);
-        C[(int64_t)i * ldc + j] = v;
-        mx = fmax(mx, v);
-    }
-    mx = wave_max(mx);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double r = red[0];
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = fmax(r, red[w]);
-        *cmax = r;
-        if (cmax_out) *cmax_out = r;
-    }
-}
-
 size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 
 }  // namespace
-
-hipError_t pairwise_fallback_cost_f64(const int* stalled, const float* X, int64_t ldx, const float* Y, int64_t ldy,
-                                      int64_t n, int64_t m, int64_t d, double* nx, double* ny,
-                                      int euclid, double* C, int64_t ldc, double* cmax, double* cmax_out,
-                                      hipStream_t s) {
-    pw_fallback_cost_kernel<<<1, 512, 0, s>>>(stalled, X, ldx, Y, ldy, (int)n, (int)m, (int)d, nx, ny, euclid, C,
-                                               ldc, cmax, cmax_out);
-    return hipGetLastError();
-}
 
 // Generic tiled GEMM from otf_linalg.hip (same template, instantiated there too).
 template <typename TA, typename TB, typename TACC, typename TOUT>

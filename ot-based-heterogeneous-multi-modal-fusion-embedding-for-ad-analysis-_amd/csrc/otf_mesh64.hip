@@ -229,18 +229,21 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
             acc[a] = D4{0.0, 0.0, 0.0, 0.0};
             nxr[a] = 0.0;
         }
+        // software-pipelined: chunk t + 1's operands in flight during chunk t's 32 MFMAs (the
+        // norm-only loads of blocks 0..2 are consumed after them)
+        F4 yv = ldy4(3, 0), xv[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) xv[a] = ldx4(a, 0);
         for (int t = 0; t < nt; ++t) {
-            const F4 yv = ldy4(3, t);
-            // blocks 0..2's column norms here, where registers are free
+            const bool more = t + 1 < nt;
+            F4 yvn, xvn[NA], yo[RB];
 #pragma unroll
-            for (int b = 0; b < RB; ++b) {
-                const F4 yo = ldy4(b, t);
+            for (int b = 0; b < RB; ++b) yo[b] = ldy4(b, t);
+            if (more) {
+                yvn = ldy4(3, t + 1);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) ysq_o[b] = fma((double)yo[k], (double)yo[k], ysq_o[b]);
+                for (int a = 0; a < NA; ++a) xvn[a] = ldx4(a, t + 1);
             }
-            F4 xv[NA];
-#pragma unroll
-            for (int a = 0; a < NA; ++a) xv[a] = ldx4(a, t);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const double yk = (double)yv[k];
@@ -251,6 +254,16 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
                     nxr[a] = fma(xk, xk, nxr[a]);
                     acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(yk, xk, acc[a], 0, 0, 0);
                 }
+            }
+            // blocks 0..2's column norms here, where registers are free
+#pragma unroll
+            for (int b = 0; b < RB; ++b)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) ysq_o[b] = fma((double)yo[b][k], (double)yo[b][k], ysq_o[b]);
+            if (more) {
+                yv = yvn;
+#pragma unroll
+                for (int a = 0; a < NA; ++a) xv[a] = xvn[a];
             }
         }
 #pragma unroll

@@ -359,12 +359,6 @@ struct PairwiseF64 {
     double* cmax_out;  // the cost's max (device, nullable)
     uint32_t xbytes, ybytes;
 };
-// otf_gw.hip: the guarded one-workgroup cost build behind a pairwise mesh launch (runs only
-// after a registration give-up)
-hipError_t pairwise_fallback_cost_f64(const int* stalled, const float* X, int64_t ldx, const float* Y, int64_t ldy,
-                                      int64_t n, int64_t m, int64_t d, double* nx, double* ny,
-                                      int euclid, double* C, int64_t ldc, double* cmax, double* cmax_out,
-                                      hipStream_t s);
 // d a multiple of 16, X / Y 16-B aligned with ld a multiple of 4, each < 2 GiB
 bool mesh64_pairwise_ok(int64_t n, int64_t m, int64_t d, int64_t ldx, int64_t ldy, const void* X, const void* Y);
 hipError_t run_mesh64(const double* C, int64_t ldc, int n, int m, const double* a_pad, const double* b_pad,

@@ -686,7 +686,59 @@ template <typename T> struct SoloArgs {
     int64_t ldp;
     int p_f64;
     const T* v0v;       // shifted kernel: the initial column scalings (else null)
+    // behind the pairwise float64 mesh (otf_sinkhorn_pairwise_f64): the cost to build into
+    // p.C (with its max into pw_cmax = p.cost_scale when scaled) before the solve (else null)
+    const float* pw_X;
+    const float* pw_Y;
+    int64_t pw_ldx, pw_ldy;
+    int pw_d, pw_euclid;
+    double* pw_cmax;
+    double* pw_cmax_out;
+    double* pw_nx;      // n + m scratch doubles for the squared norms
 };
+
+// One workgroup builds the pairwise float64 cost the fused mesh launch would have built
+// (dist_mfma_f64_kernel's epilogue order), and its max.
+template <typename T>
+__device__ void pw_solo_cost(const SkArgs<T>& p, const SoloArgs<T>& x) {
+    const int tid = threadIdx.x, NT = blockDim.x;
+    __shared__ double red[16];
+    const int n = p.n, m = p.m, d = x.pw_d;
+    double* nx = x.pw_nx;
+    double* ny = x.pw_nx + n;
+    for (int i = tid; i < n + m; i += NT) {
+        const float* r = i < n ? x.pw_X + (int64_t)i * x.pw_ldx : x.pw_Y + (int64_t)(i - n) * x.pw_ldy;
+        double s = 0;
+        for (int k = 0; k < d; ++k) s = fma((double)r[k], (double)r[k], s);
+        (i < n ? nx[i] : ny[i - n]) = s;
+    }
+    __syncthreads();
+    double* C = (double*)p.C;
+    double mx = 0.0;
+    for (int64_t e = tid; e < (int64_t)n * m; e += NT) {
+        const int i = (int)(e / m), j = (int)(e % m);
+        const float* xr = x.pw_X + (int64_t)i * x.pw_ldx;
+        const float* yr = x.pw_Y + (int64_t)j * x.pw_ldy;
+        double acc = 0;
+        for (int k = 0; k < d; ++k) acc = fma((double)xr[k], (double)yr[k], acc);
+        double v = -2.0 * acc;
+        v += nx[i];
+        v += ny[j];
+        v = v > 0 ? v : 0.0;
+        if (x.pw_euclid) v = sqrt(v);
+        C[(int64_t)i * p.ldc + j] = v;
+        mx = fmax(mx, v);
+    }
+    mx = wave_max(mx);
+    if ((tid & 63) == 0) red[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        double r = red[0];
+        for (int w = 1; w < NT / 64; ++w) r = fmax(r, red[w]);
+        *x.pw_cmax = r;
+        if (x.pw_cmax_out) *x.pw_cmax_out = r;
+    }
+}
 
 template <typename T, typename CT, int G, int R, bool SH>
 __global__ __launch_bounds__(512) void sk_solo_kernel(SkArgs<T> p, SoloArgs<T> x) {
@@ -707,6 +759,12 @@ __global__ __launch_bounds__(512) void sk_solo_kernel(SkArgs<T> p, SoloArgs<T> x
         }
         __syncthreads();
     };
+    if constexpr (sizeof(T) == 8 && std::is_same<CT, double>::value) {
+        if (x.pw_X) {
+            pw_solo_cost<T>(p, x);
+            sync_mem();
+        }
+    }
     // fresh state: the abandoned persistent solve may have written the info words
     for (int64_t j = tid; j < 3 * x.cs_stride; j += NT) x.cs[j] = 0;
     for (int j = tid; j < 2 * p.n; j += NT) x.u2[j] = 0;
@@ -2077,10 +2135,21 @@ template <typename T, typename CT>
 hipError_t launch_solo(const SkSetup<T>& su, const CT* C, int64_t ldc, int64_t n, int64_t m,
                        const T* cost_scale, const otf_sinkhorn_opts& o, T* u_out, T* v_out,
                        void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
-                       double* errlog, hipStream_t s) {
+                       double* errlog, hipStream_t s, const SoloArgs<T>* pw = nullptr) {
     SkArgs<T> p = sk_args<T, CT, false>(su, C, ldc, n, m, cost_scale, o, info, errlog, false);
     SoloArgs<T> x{(T*)su.w.cs, (T*)su.w.u2, (T*)su.w.v2, su.w.cs_stride, o.max_iter, u_out, v_out,
                   P_out, ldp, P_dtype == OTF_F64 ? 1 : 0, p.v0v};
+    if (pw) {
+        x.pw_X = pw->pw_X;
+        x.pw_Y = pw->pw_Y;
+        x.pw_ldx = pw->pw_ldx;
+        x.pw_ldy = pw->pw_ldy;
+        x.pw_d = pw->pw_d;
+        x.pw_euclid = pw->pw_euclid;
+        x.pw_cmax = pw->pw_cmax;
+        x.pw_cmax_out = pw->pw_cmax_out;
+        x.pw_nx = pw->pw_nx;
+    }
     const PassCfg& c = su.cfg;
     if (p.shA) {
         if constexpr (sizeof(T) == 4) {
@@ -2675,8 +2744,7 @@ int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64
     double* Cw = (double*)(base + L.sk);
     char* ws_cost = base + L.sk + L.c;
     double* cmax = (double*)(base + L.sk + L.c + L.cost);
-    double* nx = (double*)ws_cost;  // the cost call's layout: norms of X, then of Y
-    double* ny = (double*)(ws_cost + (8 * (size_t)n + 255) / 256 * 256);
+    double* nx = (double*)ws_cost;  // the fallback's norms (n + m doubles)
     const bool whole = o.n_total <= 0 || o.n_total == n;
     const bool engine_ok = o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled());
     bool fused = whole && !o.shift && o.max_iter >= 1 && engine_ok && u_out && v_out &&
@@ -2702,12 +2770,20 @@ int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64
                                             (const double*)su.w.b_pad, nullptr, o, su.w.mesh, u_out, v_out, P_out,
                                             ldp, P_dtype, info, errl, /*zeroed=*/true, s, &pw);
             if (e == hipSuccess) {
-                // the fallback: the cost (one workgroup) and the solve, both only after a
-                // registration give-up
-                OTF_HIP(pairwise_fallback_cost_f64(&info->stalled, X, ldx, Y, ldy, n, m, d, nx, ny,
-                                                   metric == OTF_EUCLIDEAN ? 1 : 0, Cw, m, cmax, cmax_out, s));
+                // the fallback (only after a registration give-up): the one-workgroup solve
+                // builds the cost first
+                SoloArgs<double> fb{};
+                fb.pw_X = X;
+                fb.pw_Y = Y;
+                fb.pw_ldx = ldx;
+                fb.pw_ldy = ldy;
+                fb.pw_d = (int)d;
+                fb.pw_euclid = metric == OTF_EUCLIDEAN ? 1 : 0;
+                fb.pw_cmax = cmax;
+                fb.pw_cmax_out = cmax_out;
+                fb.pw_nx = nx;
                 return check_hip(launch_solo<double, double>(su, Cw, m, n, m, scale_max ? cmax : nullptr, o, u_out,
-                                                             v_out, P_out, ldp, P_dtype, info, errl, s));
+                                                             v_out, P_out, ldp, P_dtype, info, errl, s, &fb));
             }
             (void)hipGetLastError();
             if (o.engine == OTF_ENGINE_MESH) return check_hip(e);
