@@ -145,6 +145,12 @@ __device__ __forceinline__ bool poll64(__amdgpu_buffer_rsrc_t rs, uint32_t off, 
 #ifdef OTF_M64_STAMPS
 __device__ unsigned long long g_m64st[256 * 16 * 8];
 __device__ unsigned long long g_m64pro[256 * 4];  // kernel start, roles known, K formed, loop end
+// the pairwise prologue: block 3 built, blocks 0..2 built, the grid max known, K formed
+__device__ unsigned long long g_m64pw[256 * 4];
+#define OTF_M64PW(ph)                                                                            \
+    do {                                                                                         \
+        if (threadIdx.x == 0 && sid < 256) g_m64pw[sid * 4 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 #define OTF_M64PRO(ph)                                                                          \
     do {                                                                                        \
         if (threadIdx.x == 0 && rb * ncb + cb < 256)                                            \
@@ -161,6 +167,9 @@ __device__ unsigned long long g_m64pro[256 * 4];  // kernel start, roles known, 
     } while (0)
 #define OTF_M64PRO(ph) \
     do {               \
+    } while (0)
+#define OTF_M64PW(ph) \
+    do {              \
     } while (0)
 #endif
 
@@ -182,7 +191,9 @@ template <typename SK>
 __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM64NA][kM64RB], SK& sK, int w,
                                              int lane, int rr, int g, int row0, int col0, int cw,
                                              int target, bool lead, unsigned long long& deadline,
-                                             int* s_flag, double* s_red, double* s_nx, double* s_ny) {
+                                             int* s_flag, double* s_red, double* s_nx, double* s_ny,
+                                             int sid) {
+    (void)sid;
     constexpr int NA = kM64NA, RB = kM64RB;
     const PairwiseF64& q = p.pw;
     const int cm = 4 * (rr & 3) + (rr >> 2);
@@ -293,6 +304,7 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
         // block 3 lives in LDS from here: no register copy kept across the second pass
         asm volatile("" : "+v"(lmax) :: "memory");
     }
+    OTF_M64PW(0);
     // blocks 0..2 in the K registers
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -361,6 +373,7 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
     lmax = wave_max(lmax);
     if (lane == 0) s_red[w] = lmax;
     __syncthreads();
+    OTF_M64PW(1);  // every wave of the workgroup done
     if (threadIdx.x == 0) {
         double mx = s_red[0];
         for (int ww = 1; ww < kM64NW; ++ww) mx = fmax(mx, s_red[ww]);
@@ -368,6 +381,7 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
                                __builtin_bit_cast(unsigned long long, mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!grid_barrier(p.xreg + kM64MaxBar, target, deadline, p.timeout_ticks, s_flag)) return false;
+    OTF_M64PW(2);
     const double cmax = __builtin_bit_cast(
         double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(p.xreg + kM64MaxWord), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT));
@@ -386,6 +400,7 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
             sK[w][a][h][lane] = D2{exp(c[0] * ks), exp(c[1] * ks)};
         }
     }
+    OTF_M64PW(3);
     return true;
 }
 
@@ -490,7 +505,7 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     D4 kr[NA][RB];
     if constexpr (PW) {
         if (!pw_cost_tile(p, kr, sK, w, lane, rr, g, row0, col0, cw, nrb * ncb, lead, deadline, &s_reg[3],
-                          &spsh[0][0], &rowbuf[w][0], &vcur[w][0])) {
+                          &spsh[0][0], &rowbuf[w][0], &vcur[w][0], rb * ncb + cb)) {
             // the max barrier stalled: a mid-solve stall (OTF_SK_TIMEOUT), every workgroup leaves
             if (tid == 0) {
                 mark_stalled(&p.info->stalled, kStallMid);

@@ -96,6 +96,33 @@ int main(int argc, char** argv) {
     printf("  roles -> K formed (C / cost, exp) %7.3f us\n", pa[1] / 256 * 0.01);
     printf("  K formed -> loop end            %7.3f us\n", pa[2] / 256 * 0.01);
     printf("  first start -> last loop end    %7.3f us\n", (tend - t0) * 0.01);
+    if (pw) {
+        std::vector<unsigned long long> q(256 * 4);
+        (void)hipMemcpyFromSymbol(q.data(), HIP_SYMBOL(otf::g_m64pw), q.size() * 8);
+        double m[4] = {0}, mx[4] = {0}, mn[4] = {1e30, 1e30, 1e30, 1e30};
+        for (int r = 0; r < 256; ++r) {
+            const unsigned long long prev[4] = {pro[r * 4 + 1], q[r * 4], q[r * 4 + 1], q[r * 4 + 2]};
+            for (int k = 0; k < 4; ++k) {
+                const double dt = (double)(q[r * 4 + k] - prev[k]) * 0.01;
+                m[k] += dt / 256;
+                mx[k] = std::max(mx[k], dt);
+                mn[k] = std::min(mn[k], dt);
+            }
+        }
+        const char* nm[4] = {"block 3 (wave 0)", "blocks 0..2 (until all waves)", "grid max (atomic + barrier)",
+                             "K = exp in place"};
+        for (int k = 0; k < 4; ++k)
+            printf("    %-30s mean %8.3f us  min %8.3f  max %8.3f us\n", nm[k], m[k], mn[k], mx[k]);
+        // when the workgroups finished their tiles, relative to the first one
+        unsigned long long f0 = ~0ull;
+        for (int r = 0; r < 256; ++r) f0 = std::min(f0, q[r * 4 + 1]);
+        double sk[8] = {0};
+        int nx[8] = {0};
+        for (int r = 0; r < 256; ++r) { sk[r % 8] += (q[r * 4 + 1] - f0) * 0.01; nx[r % 8]++; }
+        printf("    tile done after the first, by role %% 8:");
+        for (int x = 0; x < 8; ++x) printf(" %.1f", sk[x] / nx[x]);
+        printf(" us\n");
+    }
     const char* names[7] = {"hop B (poll, v)", "row partials (8 rows x 16 cols)", "B1 + row publish (wave 0)",
                             "row hop gather + u", "B2", "col partials + publish", "reduce (wave 0)"};
     double acc[8] = {0};
