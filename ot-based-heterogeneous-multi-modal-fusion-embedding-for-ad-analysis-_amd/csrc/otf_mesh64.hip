@@ -192,22 +192,29 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
                                              int lane, int rr, int g, int row0, int col0, int cw,
                                              int target, bool lead, unsigned long long& deadline,
                                              int* s_flag, double* s_red, double* s_nx, double* s_ny,
-                                             int sid) {
+                                             F4* s_xs2, int sid) {
     (void)sid;
     constexpr int NA = kM64NA, RB = kM64RB;
     const PairwiseF64& q = p.pw;
     const int cm = 4 * (rr & 3) + (rr >> 2);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(q.X), 0, (int)q.xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(q.Y), 0, (int)q.ybytes, 0x00020000);
-    const uint32_t xo = (uint32_t)(((int64_t)(row0 + rr) * q.ldx + 4 * g) * 4);
     const uint32_t yo = (uint32_t)(((int64_t)(col0 + cw + cm) * q.ldy + 4 * g) * 4);
-    const uint32_t xs16 = (uint32_t)(16 * q.ldx * 4), ys16 = (uint32_t)(16 * q.ldy * 4);
+    const uint32_t ys16 = (uint32_t)(16 * q.ldy * 4);
     const int nt = q.d / 16;
-    auto ldx4 = [&](int a, int t) -> F4 {
-        return __builtin_bit_cast(F4, __builtin_amdgcn_raw_buffer_load_b128(rx, xo, (uint32_t)a * xs16 + (uint32_t)t * 64u, 0));
-    };
     auto ldy4 = [&](int b, int t) -> F4 {
         return __builtin_bit_cast(F4, __builtin_amdgcn_raw_buffer_load_b128(ry, yo, (uint32_t)b * ys16 + (uint32_t)t * 64u, 0));
+    };
+    // X is the same for the 8 waves: each chunk (128 rows x 16 k, 8 KiB) is loaded once per
+    // workgroup -- thread (cr, cq) one float4 -- and staged in LDS, slot r * 4 + (q ^ (r >> 2
+    // & 3)) (conflict-free: the 16 rows of a lane group spread over the 64 banks); a lane
+    // reads row rr + 16 a, quarter g at rslot + 64 a
+    const int cr = (int)threadIdx.x >> 2, cq = (int)threadIdx.x & 3;
+    const uint32_t xco = (uint32_t)(((int64_t)(row0 + cr) * q.ldx + 4 * cq) * 4);
+    const int cslot = cr * 4 + (cq ^ ((cr >> 2) & 3));
+    const int rslot = rr * 4 + (g ^ ((rr >> 2) & 3));
+    auto ldxc = [&](int t) -> F4 {
+        return __builtin_bit_cast(F4, __builtin_amdgcn_raw_buffer_load_b128(rx, xco, (uint32_t)t * 64u, 0));
     };
     // POT's order: -2 x.y + |x|^2 + |y|^2, clamped at 0 (the euclidean root in its own pass)
     auto fin = [&](double acc, double nxi, double nyj) -> double {
@@ -241,20 +248,23 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
             nxr[a] = 0.0;
         }
         // software-pipelined: chunk t + 1's operands in flight during chunk t's 32 MFMAs (the
-        // norm-only loads of blocks 0..2 are consumed after them)
-        F4 yv = ldy4(3, 0), xv[NA];
-#pragma unroll
-        for (int a = 0; a < NA; ++a) xv[a] = ldx4(a, 0);
+        // norm-only loads of blocks 0..2 are consumed after them); X double-buffered in
+        // wave 0's block-3 LDS area (free until the epilogue), one barrier per chunk
+        F4* xs1 = reinterpret_cast<F4*>(&sK[0][0][0][0]);
+        xs1[cslot] = ldxc(0);
+        __syncthreads();
+        F4 yv = ldy4(3, 0);
         for (int t = 0; t < nt; ++t) {
             const bool more = t + 1 < nt;
-            F4 yvn, xvn[NA], yo[RB];
+            F4 yvn, xr, yo[RB], xv[NA];
+            if (more) {
+                xr = ldxc(t + 1);
+                yvn = ldy4(3, t + 1);
+            }
 #pragma unroll
             for (int b = 0; b < RB; ++b) yo[b] = ldy4(b, t);
-            if (more) {
-                yvn = ldy4(3, t + 1);
 #pragma unroll
-                for (int a = 0; a < NA; ++a) xvn[a] = ldx4(a, t + 1);
-            }
+            for (int a = 0; a < NA; ++a) xv[a] = xs1[(t & 1) * 512 + rslot + 64 * a];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const double yk = (double)yv[k];
@@ -273,9 +283,9 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
                 for (int k = 0; k < 4; ++k) ysq_o[b] = fma((double)yo[b][k], (double)yo[b][k], ysq_o[b]);
             if (more) {
                 yv = yvn;
-#pragma unroll
-                for (int a = 0; a < NA; ++a) xv[a] = xvn[a];
+                xs1[((t + 1) & 1) * 512 + cslot] = xr;
             }
+            __syncthreads();
         }
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
@@ -310,20 +320,21 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
     for (int a = 0; a < NA; ++a)
 #pragma unroll
         for (int b = 0; b < RB; ++b) kr[a][b] = D4{0.0, 0.0, 0.0, 0.0};
-    // the 192 accumulators leave ~40 registers: one row block's X operand in flight ahead of
-    // its 12 MFMAs (768 cycles), the next chunk's Y operands loaded during the last row blocks
+    // the 192 accumulators leave ~40 registers: X staged in LDS (one 8-KiB buffer, two
+    // barriers per chunk), the next chunk's X and Y in flight during this chunk's MFMAs
     {
         F4 yv[RB], yn[RB];
 #pragma unroll
         for (int b = 0; b < RB; ++b) yv[b] = ldy4(b, 0);
-        F4 xn = ldx4(0, 0);
+        s_xs2[cslot] = ldxc(0);
+        __syncthreads();
         for (int t = 0; t < nt; ++t) {
             const bool more = t + 1 < nt;
+            F4 xr;
+            if (more) xr = ldxc(t + 1);
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
-                const F4 xv = xn;
-                if (a + 1 < NA) xn = ldx4(a + 1, t);
-                else if (more) xn = ldx4(0, t + 1);
+                const F4 xv = s_xs2[rslot + 64 * a];
                 if (a == NA / 2 && more) {
 #pragma unroll
                     for (int b = 0; b < RB; ++b) yn[b] = ldy4(b, t + 1);
@@ -338,10 +349,13 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
+            __syncthreads();  // every wave is done with chunk t
             if (more) {
+                s_xs2[cslot] = xr;
 #pragma unroll
                 for (int b = 0; b < RB; ++b) yv[b] = yn[b];
             }
+            __syncthreads();
         }
     }
 #pragma unroll
@@ -505,7 +519,8 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     D4 kr[NA][RB];
     if constexpr (PW) {
         if (!pw_cost_tile(p, kr, sK, w, lane, rr, g, row0, col0, cw, nrb * ncb, lead, deadline, &s_reg[3],
-                          &spsh[0][0], &rowbuf[w][0], &vcur[w][0], rb * ncb + cb)) {
+                          &spsh[0][0], &rowbuf[w][0], &vcur[w][0], reinterpret_cast<F4*>(&vhist[0][0]),
+                          rb * ncb + cb)) {
             // the max barrier stalled: a mid-solve stall (OTF_SK_TIMEOUT), every workgroup leaves
             if (tid == 0) {
                 mark_stalled(&p.info->stalled, kStallMid);
