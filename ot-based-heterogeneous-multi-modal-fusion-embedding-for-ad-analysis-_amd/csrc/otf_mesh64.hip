@@ -191,8 +191,7 @@ template <typename SK>
 __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM64NA][kM64RB], SK& sK, int w,
                                              int lane, int rr, int g, int row0, int col0, int cw,
                                              int target, bool lead, unsigned long long& deadline,
-                                             int* s_flag, double* s_red, double* s_nx, double* s_ny,
-                                             F4* s_xs2, int sid) {
+                                             int* s_flag, double* s_red, F4* s_xs2, int sid) {
     (void)sid;
     constexpr int NA = kM64NA, RB = kM64RB;
     const PairwiseF64& q = p.pw;
@@ -223,30 +222,12 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
         v += nyj;
         return v > 0 ? v : 0.0;
     };
-    // the squared norms come out of the same loads: a lane sums the squares of its k
-    // quarter, the 4 lanes of a row (lane bits 5, 4) add them up; the column norms reach the
-    // lanes of the accumulator layout (column 4 g + r is Y row cm = 4 r + g) by a shuffle
-    auto sum_g = [&](double x) -> double {
-        x += __shfl_xor(x, 16);
-        return x + __shfl_xor(x, 32);
-    };
-    auto col_norms = [&](double ysq) -> D4 {
-        D4 r4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) r4[r] = __shfl(ysq, 4 * r + g);
-        return r4;
-    };
     double lmax = 0.0;
     // block 3 -> LDS
     {
         D4 acc[NA];
-        double nxr[NA];
-        double ysq = 0.0, ysq_o[RB] = {0.0, 0.0, 0.0};
 #pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            acc[a] = D4{0.0, 0.0, 0.0, 0.0};
-            nxr[a] = 0.0;
-        }
+        for (int a = 0; a < NA; ++a) acc[a] = D4{0.0, 0.0, 0.0, 0.0};
         // software-pipelined: chunk t + 1's operands in flight during chunk t's 32 MFMAs (the
         // norm-only loads of blocks 0..2 are consumed after them); X double-buffered in
         // wave 0's block-3 LDS area (free until the epilogue), one barrier per chunk
@@ -256,51 +237,30 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
         F4 yv = ldy4(3, 0);
         for (int t = 0; t < nt; ++t) {
             const bool more = t + 1 < nt;
-            F4 yvn, xr, yo[RB], xv[NA];
+            F4 yvn, xr, xv[NA];
             if (more) {
                 xr = ldxc(t + 1);
                 yvn = ldy4(3, t + 1);
             }
 #pragma unroll
-            for (int b = 0; b < RB; ++b) yo[b] = ldy4(b, t);
-#pragma unroll
             for (int a = 0; a < NA; ++a) xv[a] = xs1[(t & 1) * 512 + rslot + 64 * a];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const double yk = (double)yv[k];
-                ysq = fma(yk, yk, ysq);
 #pragma unroll
-                for (int a = 0; a < NA; ++a) {
-                    const double xk = (double)xv[a][k];
-                    nxr[a] = fma(xk, xk, nxr[a]);
-                    acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(yk, xk, acc[a], 0, 0, 0);
-                }
+                for (int a = 0; a < NA; ++a)
+                    acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(yk, (double)xv[a][k], acc[a], 0, 0, 0);
             }
-            // blocks 0..2's column norms here, where registers are free
-#pragma unroll
-            for (int b = 0; b < RB; ++b)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) ysq_o[b] = fma((double)yo[b][k], (double)yo[b][k], ysq_o[b]);
             if (more) {
                 yv = yvn;
                 xs1[((t + 1) & 1) * 512 + cslot] = xr;
             }
             __syncthreads();
         }
+        const D4 nyv = *reinterpret_cast<const D4*>(q.ny + col0 + cw + 48 + 4 * g);
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-            nxr[a] = sum_g(nxr[a]);
-            if (g == 0) s_nx[rr + 16 * a] = nxr[a];  // this wave's copy, read back after pass 2
-        }
-        const D4 nyv = col_norms(sum_g(ysq));
-#pragma unroll
-        for (int b = 0; b < RB; ++b) {
-            const D4 ny4 = col_norms(sum_g(ysq_o[b]));
-            if (rr == 0) *reinterpret_cast<D4*>(s_ny + 16 * b + 4 * g) = ny4;  // this wave's copy
-        }
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            const double nxi = nxr[a];
+            const double nxi = q.nx[row0 + rr + 16 * a];
             D4 c;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -360,10 +320,10 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
     }
 #pragma unroll
     for (int b = 0; b < RB; ++b) {
-        const D4 nyv = *reinterpret_cast<const D4*>(s_ny + 16 * b + 4 * g);
+        const D4 nyv = *reinterpret_cast<const D4*>(q.ny + col0 + cw + 16 * b + 4 * g);
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-            const double nxi = s_nx[rr + 16 * a];
+            const double nxi = q.nx[row0 + rr + 16 * a];
 #pragma unroll
             for (int r = 0; r < 4; ++r) kr[a][b][r] = fin(kr[a][b][r], nxi, nyv[r]);
         }
@@ -519,7 +479,7 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     D4 kr[NA][RB];
     if constexpr (PW) {
         if (!pw_cost_tile(p, kr, sK, w, lane, rr, g, row0, col0, cw, nrb * ncb, lead, deadline, &s_reg[3],
-                          &spsh[0][0], &rowbuf[w][0], &vcur[w][0], reinterpret_cast<F4*>(&vhist[0][0]),
+                          &spsh[0][0], reinterpret_cast<F4*>(&vhist[0][0]),
                           rb * ncb + cb)) {
             // the max barrier stalled: a mid-solve stall (OTF_SK_TIMEOUT), every workgroup leaves
             if (tid == 0) {

@@ -347,15 +347,16 @@ size_t mesh_region_bytes(int64_t n, int64_t m);
 bool mesh64_supported(int64_t n, int64_t m);
 size_t mesh64_region_bytes(int64_t n, int64_t m);
 // The pairwise form of the float64 mesh (otf_sinkhorn_pairwise_f64): the cost tile is built
-// in the kernel's prologue from the float32 rows X (n x d) and Y (m x d) (their squared
-// norms from the same loads), and max-scaled when `scale` (the grid's max: one atomic + a
-// barrier).
+// in the kernel's prologue from the float32 rows X (n x d) and Y (m x d) and their squared
+// norms nx, ny, and max-scaled when `scale` (the grid's max: one atomic + a barrier).
 struct PairwiseF64 {
     const float* X;
     int64_t ldx;
     const float* Y;
     int64_t ldy;
     int d, euclid, scale;
+    const double* nx;  // squared row norms of X (n) and Y (m), float64
+    const double* ny;
     double* cmax_out;  // the cost's max (device, nullable)
     uint32_t xbytes, ybytes;
 };

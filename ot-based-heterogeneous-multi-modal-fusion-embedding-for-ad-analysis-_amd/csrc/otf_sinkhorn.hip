@@ -2705,6 +2705,19 @@ int otf_sinkhorn(const void* a, const void* b, const void* C, int64_t n, int64_t
 // workspace (norms, per-tile maxima)][the max].
 namespace otf {
 namespace {
+// the squared norms of X's and Y's float32 rows in float64 (one wave per row), for the
+// pairwise mesh's epilogue (kept out of its matrix-core loops)
+__global__ __launch_bounds__(256) void pw_norms_kernel(const float* X, int64_t ldx, int n, const float* Y,
+                                                       int64_t ldy, int m, int d, double* nx, double* ny) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= n + m) return;
+    const float* r = i < n ? X + (int64_t)i * ldx : Y + (int64_t)(i - n) * ldy;
+    double s = 0;
+    for (int k = lane; k < d; k += 64) s = fma((double)r[k], (double)r[k], s);
+    s = wave_sum(s);
+    if (lane == 0) (i < n ? nx[i] : ny[i - n]) = s;
+}
 struct PwLayout {
     size_t sk, c, cost, total;
 };
@@ -2764,8 +2777,11 @@ int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64
             rc = sk_init<double>(su, a, b, n, m, info, s, su.w.mesh, su.w.mesh_bytes);
             if (rc != OTF_OK) return rc;
             double* errl = errlog ? errlog : su.w.errlog;
+            pw_norms_kernel<<<(unsigned)((n + m + 3) / 4), 256, 0, s>>>(X, ldx, (int)n, Y, ldy, (int)m, (int)d, nx,
+                                                                       nx + n);
+            OTF_HIP(hipGetLastError());
             PairwiseF64 pw{X, ldx, Y, ldy, (int)d, metric == OTF_EUCLIDEAN ? 1 : 0, scale_max ? 1 : 0,
-                           cmax_out, (uint32_t)(n * ldx * 4), (uint32_t)(m * ldy * 4)};
+                           nx, nx + n, cmax_out, (uint32_t)(n * ldx * 4), (uint32_t)(m * ldy * 4)};
             const hipError_t e = run_mesh64(nullptr, m, (int)n, (int)m, (const double*)su.w.a_pad,
                                             (const double*)su.w.b_pad, nullptr, o, su.w.mesh, u_out, v_out, P_out,
                                             ldp, P_dtype, info, errl, /*zeroed=*/true, s, &pw);
