@@ -235,13 +235,13 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
         xs1[cslot] = ldxc(0);
         __syncthreads();
         F4 yv = ldy4(3, 0);
+        // the next chunk's loads are issued unconditionally (the last chunk reloads itself):
+        // with a path-independent count of loads in flight the compiler waits for exactly the
+        // older ones (vmcnt(2)) instead of draining everything (vmcnt(0)) at the loop top
         for (int t = 0; t < nt; ++t) {
-            const bool more = t + 1 < nt;
-            F4 yvn, xr, xv[NA];
-            if (more) {
-                xr = ldxc(t + 1);
-                yvn = ldy4(3, t + 1);
-            }
+            const int tn = t + 1 < nt ? t + 1 : t;
+            const F4 xr = ldxc(tn), yvn = ldy4(3, tn);
+            F4 xv[NA];
 #pragma unroll
             for (int a = 0; a < NA; ++a) xv[a] = xs1[(t & 1) * 512 + rslot + 64 * a];
 #pragma unroll
@@ -251,10 +251,8 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
                 for (int a = 0; a < NA; ++a)
                     acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(yk, (double)xv[a][k], acc[a], 0, 0, 0);
             }
-            if (more) {
-                yv = yvn;
-                xs1[((t + 1) & 1) * 512 + cslot] = xr;
-            }
+            yv = yvn;
+            xs1[((t + 1) & 1) * 512 + cslot] = xr;
             __syncthreads();
         }
         const D4 nyv = *reinterpret_cast<const D4*>(q.ny + col0 + cw + 48 + 4 * g);
@@ -289,15 +287,14 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
         s_xs2[cslot] = ldxc(0);
         __syncthreads();
         for (int t = 0; t < nt; ++t) {
-            const bool more = t + 1 < nt;
-            F4 xr;
-            if (more) xr = ldxc(t + 1);
+            const int tn = t + 1 < nt ? t + 1 : t;
+            const F4 xr = ldxc(tn);
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
                 const F4 xv = s_xs2[rslot + 64 * a];
-                if (a == NA / 2 && more) {
+                if (a == NA / 2) {
 #pragma unroll
-                    for (int b = 0; b < RB; ++b) yn[b] = ldy4(b, t + 1);
+                    for (int b = 0; b < RB; ++b) yn[b] = ldy4(b, tn);
                 }
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -310,11 +307,9 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
                 __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();  // every wave is done with chunk t
-            if (more) {
-                s_xs2[cslot] = xr;
+            s_xs2[cslot] = xr;
 #pragma unroll
-                for (int b = 0; b < RB; ++b) yv[b] = yn[b];
-            }
+            for (int b = 0; b < RB; ++b) yv[b] = yn[b];
             __syncthreads();
         }
     }
