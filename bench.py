@@ -76,8 +76,8 @@ def lib_md5():
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--n", type=int, default=4096)
     p.add_argument("--d", type=int, default=512)
     p.add_argument("--iters", type=int, default=100)

@@ -147,9 +147,19 @@ __device__ unsigned long long g_m64st[256 * 16 * 8];
 __device__ unsigned long long g_m64pro[256 * 4];  // kernel start, roles known, K formed, loop end
 // the pairwise prologue: block 3 built, blocks 0..2 built, the grid max known, K formed
 __device__ unsigned long long g_m64pw[256 * 4];
+// the shader clock (s_memtime) at the entry of the cost build and at the same four points:
+// the effective core clock of each phase
+__device__ unsigned long long g_m64pwc[256 * 5];
 #define OTF_M64PW(ph)                                                                            \
     do {                                                                                         \
-        if (threadIdx.x == 0 && sid < 256) g_m64pw[sid * 4 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == 0 && sid < 256) {                                                     \
+            g_m64pw[sid * 4 + (ph)] = __builtin_amdgcn_s_memrealtime();                          \
+            g_m64pwc[sid * 5 + (ph) + 1] = __builtin_amdgcn_s_memtime();                         \
+        }                                                                                        \
+    } while (0)
+#define OTF_M64PWC0()                                                                            \
+    do {                                                                                         \
+        if (threadIdx.x == 0 && sid < 256) g_m64pwc[sid * 5] = __builtin_amdgcn_s_memtime();     \
     } while (0)
 #define OTF_M64PRO(ph)                                                                          \
     do {                                                                                        \
@@ -169,6 +179,9 @@ __device__ unsigned long long g_m64pw[256 * 4];
     do {               \
     } while (0)
 #define OTF_M64PW(ph) \
+    do {              \
+    } while (0)
+#define OTF_M64PWC0() \
     do {              \
     } while (0)
 #endif
@@ -193,6 +206,7 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
                                              int target, bool lead, unsigned long long& deadline,
                                              int* s_flag, double* s_red, F4* s_xs2, int sid) {
     (void)sid;
+    OTF_M64PWC0();
     constexpr int NA = kM64NA, RB = kM64RB;
     const PairwiseF64& q = p.pw;
     const int cm = 4 * (rr & 3) + (rr >> 2);

@@ -375,11 +375,10 @@ __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
 }
 
 template <typename T>
-__global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, T* a_pad, T* b_pad,
-                               T* cs, int cs_stride, T* u2, T* v2, int* cmin_key,
-                               otf_sinkhorn_info* info, uint4* zero, int64_t zero_n) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int stride = gridDim.x * blockDim.x;
+__device__ __forceinline__ void sk_init_body(int t, int stride, const T* a, const T* b, int n, int m, int m_pad,
+                                             T* a_pad, T* b_pad, T* cs, int cs_stride, T* u2, T* v2,
+                                             int* cmin_key, otf_sinkhorn_info* info, uint4* zero,
+                                             int64_t zero_n) {
     // a persistent engine's granule region (mesh), zeroed here instead of by a memset launch
     for (int64_t j = t; j < zero_n; j += stride) zero[j] = make_uint4(0u, 0u, 0u, 0u);
     for (int j = t; j < m_pad; j += stride) {
@@ -404,6 +403,13 @@ __global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, 
         info->stalled = 0;
         info->fallback = 0;
     }
+}
+template <typename T>
+__global__ void sk_init_kernel(const T* a, const T* b, int n, int m, int m_pad, T* a_pad, T* b_pad,
+                               T* cs, int cs_stride, T* u2, T* v2, int* cmin_key,
+                               otf_sinkhorn_info* info, uint4* zero, int64_t zero_n) {
+    sk_init_body<T>(blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x, a, b, n, m, m_pad, a_pad,
+                    b_pad, cs, cs_stride, u2, v2, cmin_key, info, zero, zero_n);
 }
 
 // Column minima of C (OTT prologue shift), ordered-int atomicMin per column.
@@ -2706,9 +2712,16 @@ int otf_sinkhorn(const void* a, const void* b, const void* C, int64_t n, int64_t
 namespace otf {
 namespace {
 // the squared norms of X's and Y's float32 rows in float64 (one wave per row), for the
-// pairwise mesh's epilogue (kept out of its matrix-core loops)
+// pairwise mesh's epilogue (kept out of its matrix-core loops), and sk_init's work (the
+// marginals, the zeroed granule region, info) in the same launch
 __global__ __launch_bounds__(256) void pw_norms_kernel(const float* X, int64_t ldx, int n, const float* Y,
-                                                       int64_t ldy, int m, int d, double* nx, double* ny) {
+                                                       int64_t ldy, int m, int d, double* nx, double* ny,
+                                                       const double* a, const double* b, int m_pad,
+                                                       double* a_pad, double* b_pad, double* cs, int cs_stride,
+                                                       double* u2, double* v2, int* cmin_key,
+                                                       otf_sinkhorn_info* info, uint4* zero, int64_t zero_n) {
+    sk_init_body<double>(blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x, a, b, n, m, m_pad, a_pad,
+                         b_pad, cs, cs_stride, u2, v2, cmin_key, info, zero, zero_n);
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= n + m) return;
@@ -2774,11 +2787,11 @@ int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64
             (o.engine == OTF_ENGINE_AUTO && su.w.t_nrb * su.w.t_ncb <= device_cu_count()))
             fused = false;
         if (fused) {
-            rc = sk_init<double>(su, a, b, n, m, info, s, su.w.mesh, su.w.mesh_bytes);
-            if (rc != OTF_OK) return rc;
             double* errl = errlog ? errlog : su.w.errlog;
-            pw_norms_kernel<<<(unsigned)((n + m + 3) / 4), 256, 0, s>>>(X, ldx, (int)n, Y, ldy, (int)m, (int)d, nx,
-                                                                       nx + n);
+            pw_norms_kernel<<<(unsigned)((n + m + 3) / 4), 256, 0, s>>>(
+                X, ldx, (int)n, Y, ldy, (int)m, (int)d, nx, nx + n, a, b, su.m_pad, (double*)su.w.a_pad,
+                (double*)su.w.b_pad, (double*)su.w.cs, (int)su.w.cs_stride, (double*)su.w.u2, (double*)su.w.v2,
+                su.w.cmin_key, info, (uint4*)su.w.mesh, (int64_t)(su.w.mesh_bytes / 16));
             OTF_HIP(hipGetLastError());
             PairwiseF64 pw{X, ldx, Y, ldy, (int)d, metric == OTF_EUCLIDEAN ? 1 : 0, scale_max ? 1 : 0,
                            nx, nx + n, cmax_out, (uint32_t)(n * ldx * 4), (uint32_t)(m * ldy * 4)};

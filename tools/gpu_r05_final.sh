@@ -25,7 +25,7 @@ if [ "${FULL:-1}" = "1" ]; then
 fi
 if [ "${BENCH:-1}" = "1" ]; then
   cp /dev/null $OUT/bench.log
-  step bench 600 python bench.py --steps 20 --warmup 3
+  step bench 600 python bench.py
 fi
 if [ "${PROF:-1}" = "1" ]; then
   bash tools/gpu_r05_prof.sh || exit $?

@@ -119,6 +119,26 @@ int main(int argc, char** argv) {
         double sk[8] = {0};
         int nx[8] = {0};
         for (int r = 0; r < 256; ++r) { sk[r % 8] += (q[r * 4 + 1] - f0) * 0.01; nx[r % 8]++; }
+        // effective shader clock per phase: s_memtime cycles over s_memrealtime (100 MHz) ticks
+        std::vector<unsigned long long> c(256 * 5);
+        (void)hipMemcpyFromSymbol(c.data(), HIP_SYMBOL(otf::g_m64pwc), c.size() * 8);
+        double cyc[4] = {0}, tk[4] = {0};
+        for (int r = 0; r < 256; ++r) {
+            const unsigned long long rt[5] = {0, q[r * 4], q[r * 4 + 1], q[r * 4 + 2], q[r * 4 + 3]};
+            for (int k = 1; k < 4; ++k) {
+                cyc[k] += (double)(c[r * 5 + k + 1] - c[r * 5 + k]);
+                tk[k] += (double)(rt[k + 1] - rt[k]);
+            }
+            cyc[0] += (double)(c[r * 5 + 1] - c[r * 5]);
+        }
+        printf("    shader clock: entry -> block 3 done %.1f Mcycles/WG", cyc[0] / 256 / 1e6);
+        printf("; blocks 0..2 %.3f GHz, grid max %.3f GHz, exp %.3f GHz\n", cyc[1] / tk[1] / 10.0,
+               cyc[2] / tk[2] / 10.0, cyc[3] / tk[3] / 10.0);
+        {
+            double t3 = 0;
+            for (int r = 0; r < 256; ++r) t3 += (double)(q[r * 4] - pro[r * 4 + 1]);
+            printf("    block 3 (roles -> block 3 done, incl. entry) %.3f GHz\n", cyc[0] / t3 / 10.0);
+        }
         printf("    tile done after the first, by role %% 8:");
         for (int x = 0; x < 8; ++x) printf(" %.1f", sk[x] / nx[x]);
         printf(" us\n");
