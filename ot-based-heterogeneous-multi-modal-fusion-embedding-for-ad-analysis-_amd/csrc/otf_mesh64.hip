@@ -245,19 +245,24 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
         // software-pipelined: chunk t + 1's operands in flight during chunk t's 32 MFMAs (the
         // norm-only loads of blocks 0..2 are consumed after them); X double-buffered in
         // wave 0's block-3 LDS area (free until the epilogue), one barrier per chunk
+        // X ring of three chunks in the first block-3 areas (free until the epilogue): chunk
+        // t + 1 is read into registers while chunk t's MFMAs run, chunk t + 2 is written
         F4* xs1 = reinterpret_cast<F4*>(&sK[0][0][0][0]);
         xs1[cslot] = ldxc(0);
-        __syncthreads();
+        xs1[512 + cslot] = ldxc(nt > 1 ? 1 : 0);
         F4 yv = ldy4(3, 0);
-        // the next chunk's loads are issued unconditionally (the last chunk reloads itself):
-        // with a path-independent count of loads in flight the compiler waits for exactly the
-        // older ones (vmcnt(2)) instead of draining everything (vmcnt(0)) at the loop top
-        for (int t = 0; t < nt; ++t) {
-            const int tn = t + 1 < nt ? t + 1 : t;
-            const F4 xr = ldxc(tn), yvn = ldy4(3, tn);
-            F4 xv[NA];
+        __syncthreads();
+        F4 xv[NA];
 #pragma unroll
-            for (int a = 0; a < NA; ++a) xv[a] = xs1[(t & 1) * 512 + rslot + 64 * a];
+        for (int a = 0; a < NA; ++a) xv[a] = xs1[rslot + 64 * a];
+        int s1 = 1, s2 = 2;  // ring slots of chunks t + 1, t + 2
+        for (int t = 0; t < nt; ++t) {
+            const int t1 = t + 1 < nt ? t + 1 : t;
+            const int t2 = t + 2 < nt ? t + 2 : nt - 1;
+            const F4 xr = ldxc(t2), yvn = ldy4(3, t1);
+            F4 xn[NA];
+#pragma unroll
+            for (int a = 0; a < NA; ++a) xn[a] = xs1[s1 * 512 + rslot + 64 * a];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const double yk = (double)yv[k];
@@ -265,8 +270,12 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
                 for (int a = 0; a < NA; ++a)
                     acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(yk, (double)xv[a][k], acc[a], 0, 0, 0);
             }
+            xs1[s2 * 512 + cslot] = xr;
             yv = yvn;
-            xs1[((t + 1) & 1) * 512 + cslot] = xr;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) xv[a] = xn[a];
+            s1 = s1 == 2 ? 0 : s1 + 1;
+            s2 = s2 == 2 ? 0 : s2 + 1;
             __syncthreads();
         }
         const D4 nyv = *reinterpret_cast<const D4*>(q.ny + col0 + cw + 48 + 4 * g);
