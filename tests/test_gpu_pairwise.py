@@ -35,10 +35,12 @@ def _oracle(orc, X, Y, reg, iters, metric="sqeuclidean", scale_max=True, a=None,
     return P, u, v, info, mx
 
 
-@pytest.mark.parametrize("n,m,d", [(512, 512, 64), (1024, 2048, 128), (2048, 4096, 256)])
+@pytest.mark.parametrize("n,m,d", [(512, 512, 64), (1024, 2048, 128), (2048, 4096, 256), (512, 1024, 48),
+                                   (512, 512, 16)])
 def test_pairwise_fused_vs_oracle(orc, dev, n, m, d):
     """4 / 8 / 16 row blocks x 1 / 4 / 8 column tiles, the fused launch (engine="mesh"):
-    plan, scalings, iteration count and the cost's max of the oracle."""
+    plan, scalings, iteration count and the cost's max of the oracle; d = 48 and 16 give an
+    odd number of 16-deep chunks and a single one (the prologue's X ring wraps / clamps)."""
     from otfuse import ops
     X, Y = _emb(n, m, d, n + m + d)
     P_r, u_r, v_r, info_r, mx = _oracle(orc, X, Y, 0.05, 40)
