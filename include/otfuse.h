@@ -317,7 +317,11 @@ int otf_sinkhorn_finish(const void* a, const void* b, const void* C, int64_t n, 
  * launch (no n x m cost in HBM); other shapes run otf_cost_pairwise_f64 + otf_sinkhorn on
  * the workspace.  metric OTF_SQEUCLIDEAN / OTF_EUCLIDEAN; scale_max: divide by the cost's
  * max (POT's M /= M.max()), returned in *cmax_out (device, nullable) either way.  POT
- * flavour; opts as otf_sinkhorn.  Workspace: otf_sinkhorn_pairwise_f64_workspace_size. */
+ * flavour; opts as otf_sinkhorn.  The fused launch also needs a plan leading dimension
+ * ldp % 4 == 0 (else the two calls run).  Workspace:
+ * otf_sinkhorn_pairwise_f64_workspace_size -- it always holds the n x m float64 cost, which
+ * the two-call path and the fused launch's fallback (a grid that could not become
+ * co-resident) build there. */
 size_t otf_sinkhorn_pairwise_f64_workspace_size(int64_t n, int64_t m, int32_t max_iter);
 int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n, int64_t m,
                               int64_t d, int32_t metric, int32_t scale_max, const double* a, const double* b,

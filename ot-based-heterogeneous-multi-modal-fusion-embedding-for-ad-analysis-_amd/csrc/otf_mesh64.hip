@@ -204,7 +204,7 @@ template <typename SK>
 __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM64NA][kM64RB], SK& sK, int w,
                                              int lane, int rr, int g, int row0, int col0, int cw,
                                              int target, bool lead, unsigned long long& deadline,
-                                             int* s_flag, double* s_red, F4* s_xs2, int sid) {
+                                             int* s_flag, double* s_red, F4* s_xs2, int sid, int* abandon) {
     (void)sid;
     OTF_M64PWC0();
     constexpr int NA = kM64NA, RB = kM64RB;
@@ -372,7 +372,10 @@ __device__ __forceinline__ bool pw_cost_tile(const SkMesh64Args& p, D4 (&kr)[kM6
         __hip_atomic_fetch_max(reinterpret_cast<unsigned long long*>(p.xreg + kM64MaxWord),
                                __builtin_bit_cast(unsigned long long, mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!grid_barrier(p.xreg + kM64MaxBar, target, deadline, p.timeout_ticks, s_flag)) return false;
+    // blockIdx roles (no registration barrier ran): this is the launch's first device-wide
+    // wait, so a grid that never became co-resident gives up here as a registration give-up
+    // (abandon = info->stalled) and the fallback queued behind the launch solves the problem
+    if (!grid_barrier(p.xreg + kM64MaxBar, target, deadline, p.timeout_ticks, s_flag, abandon)) return false;
     OTF_M64PW(2);
     const double cmax = __builtin_bit_cast(
         double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(p.xreg + kM64MaxWord), __ATOMIC_RELAXED,
@@ -498,8 +501,9 @@ __global__ __launch_bounds__(512) void sk_mesh64_kernel(SkMesh64Args p) {
     if constexpr (PW) {
         if (!pw_cost_tile(p, kr, sK, w, lane, rr, g, row0, col0, cw, nrb * ncb, lead, deadline, &s_reg[3],
                           &spsh[0][0], reinterpret_cast<F4*>(&vhist[0][0]),
-                          rb * ncb + cb)) {
-            // the max barrier stalled: a mid-solve stall (OTF_SK_TIMEOUT), every workgroup leaves
+                          rb * ncb + cb, p.xcc_local ? nullptr : &p.info->stalled)) {
+            // the max barrier stalled: a mid-solve stall (OTF_SK_TIMEOUT; kept at the registration
+            // give-up when the barrier gave up as one), every workgroup leaves
             if (tid == 0) {
                 mark_stalled(&p.info->stalled, kStallMid);
                 if (lead) p.info->status = OTF_SK_TIMEOUT;

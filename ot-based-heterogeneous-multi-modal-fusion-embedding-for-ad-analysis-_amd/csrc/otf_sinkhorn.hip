@@ -2535,8 +2535,14 @@ int run_xsweep(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int64_
     double* errlog = errlog_user ? errlog_user : su.w.errlog;
     // the cross-rank mesh where this rank's slab fits the register files (whole 512-column
     // tiles, one workgroup per tile on this device): K stays resident for the whole solve
-    // and the reducers exchange their column-sum partials; the cross-rank sweep otherwise
+    // and the reducers exchange their column-sum partials; the cross-rank sweep otherwise.
+    // Every rank must take the same engine (the mesh's error sums follow its tiling, so two
+    // engines -- or two tilings -- round POT's error differently and could stop at different
+    // checks, leaving a peer waiting on the exchange): the mesh only on equal shards
+    // (n * world == n_total; otfuse.distributed.sinkhorn_xsweep agrees on the shard sizes
+    // over the group before the call), so the decision depends on (n, m, device) alone
     const bool mesh_fit = (o.engine == OTF_ENGINE_AUTO || o.engine == OTF_ENGINE_MESH) &&
+                          (int64_t)n * xs.world == (int64_t)xs.n_total &&
                           mesh_supported(n, m) && m % 512 == 0 && su.w.mesh_bytes > 0 &&
                           ((n + 127) / 128) * (m / 512) <= device_cu_count();
     if (o.engine == OTF_ENGINE_MESH && !mesh_fit) return OTF_EUNSUPPORTED;
@@ -2773,8 +2779,10 @@ int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64
     double* nx = (double*)ws_cost;  // the fallback's norms (n + m doubles)
     const bool whole = o.n_total <= 0 || o.n_total == n;
     const bool engine_ok = o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled());
+    // the fused launch writes the plan in 16-B pieces of four elements (ldp % 4 == 0); decided
+    // here, before any launch, so an unaligned plan takes the two calls without a wasted norms pass
     bool fused = whole && !o.shift && o.max_iter >= 1 && engine_ok && u_out && v_out &&
-                 mesh64_pairwise_ok(n, m, d, ldx, ldy, X, Y);
+                 (!P_out || ldp % 4 == 0) && mesh64_pairwise_ok(n, m, d, ldx, ldy, X, Y);
     if (!u_out || !v_out) return OTF_EINVAL;
     if (P_out && (ldp < m || ldp % 2 != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
     if (fused) {

@@ -309,6 +309,23 @@ class XPeer:
             pass
 
 
+def xsweep_engine(engine: str, n_local: int, world: int, group=None) -> str:
+    """The cross-rank engine every rank of the exchange takes: the shard row
+    counts are all-gathered over the group; with unequal shards "auto" becomes "sweep" on
+    every rank and "mesh" is refused on every rank (the same exception everywhere, so no
+    rank is left waiting on the exchange).  Equal shards keep the request, and the library
+    then decides from (n, m, device), which are the same on every rank."""
+    if engine == "sweep" or world <= 1:
+        return engine
+    sizes = [None] * world
+    dist.all_gather_object(sizes, int(n_local), group=group)
+    if len(set(sizes)) == 1:
+        return engine
+    if engine == "mesh":
+        raise ValueError(f"engine='mesh' needs equal row shards over the ranks, got {sizes}")
+    return "sweep"
+
+
 def sinkhorn_xsweep(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.Tensor, reg: float,
                     xpeer: XPeer, n_total: int, max_iter: int = 1000, stop_thr: float = 1e-9,
                     cost_scale: torch.Tensor | None = None, check_every: int = 10,
@@ -323,7 +340,9 @@ def sinkhorn_xsweep(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.Tenso
     ``engine``: "mesh" keeps this rank's K in the register files for the whole solve
     (whole 512-column tiles, one workgroup per 128 x 512 tile on the device; the mesh's
     reducers exchange their column-sum partials, "xmesh"), "sweep" streams the cost rows
-    every iteration, "auto" takes the mesh where the slab fits."""
+    every iteration, "auto" takes the mesh where the slab fits.  The ranks agree on it
+    first (``xsweep_engine``: the mesh only on equal shards), so every rank runs the same
+    engine and reduces POT's error in the same order."""
     ops._dev(C_local, "C_local")
     if C_local.dtype not in (torch.float32, torch.float16):
         raise TypeError("sinkhorn_xsweep: float32 or float16 cost rows")
@@ -339,6 +358,7 @@ def sinkhorn_xsweep(a_local: torch.Tensor, b: torch.Tensor, C_local: torch.Tenso
     if a.numel() != n or bb.numel() != m:
         raise ValueError("a_local / b do not match C_local")
     cs = None if cost_scale is None else cost_scale.to(dev, torch.float32).contiguous()
+    engine = xsweep_engine(engine, n, xpeer.world, xpeer._group)
     opts = L.SinkhornOpts(reg=float(reg), stop_thr=float(stop_thr), max_iter=int(max_iter),
                           check_every=int(check_every), flavor=L.OTF_FLAVOR_POT,
                           err_squared=int(err_squared), sync_every=0, engine=L.ENGINES[engine],

@@ -414,7 +414,10 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
             if shifts:
                 shift = True
             else:
+                # promoted: the float64 solve needs no shift (and takes none: the shifted
+                # kernel is a float32 form), whatever the caller asked for
                 precision = "fp64"
+                shift = False
     if precision == "fp64" and C.dtype != torch.float64:
         C = C.double()
         if cost_scale is not None:

@@ -356,3 +356,45 @@ def test_xmesh_exchange_protocol_world2(tmp_path):
     np.testing.assert_allclose(zs[0]["errs"], info_r["err"], rtol=1e-9, atol=1e-15)
     P = np.concatenate([z["P"] for z in zs])
     assert np.abs(P - P_ref).max() / np.abs(P_ref).max() < 1e-12
+
+
+def _engine_agreement_worker(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import otfuse.distributed as D
+    res = {}
+    # uneven shards (rank 0: 1024 rows = a mesh slab, rank 1: 1536): "auto" -> the sweep on
+    # both ranks; "mesh" refused on both; "sweep" unchanged
+    n = 1024 if rank == 0 else 1536
+    res["auto_uneven"] = D.xsweep_engine("auto", n, world)
+    try:
+        D.xsweep_engine("mesh", n, world)
+        res["mesh_uneven"] = "accepted"
+    except ValueError:
+        res["mesh_uneven"] = "refused"
+    res["sweep_uneven"] = D.xsweep_engine("sweep", n, world)
+    # equal shards keep the request
+    res["auto_equal"] = D.xsweep_engine("auto", 1024, world)
+    res["mesh_equal"] = D.xsweep_engine("mesh", 1024, world)
+    np.save(os.path.join(out_dir, f"e{rank}.npy"), np.array([res[k] for k in sorted(res)]))
+    dist.destroy_process_group()
+
+
+def test_xsweep_engine_agreed_over_ranks(tmp_path):
+    """the cross-rank engine is agreed over the exchange's group, never picked
+    by each rank from its own shard -- two engines (or two mesh tilings) round POT's error
+    differently and could stop at different checks, leaving a peer waiting on the
+    exchange.  Uneven shards: every rank takes the sweep (auto) or refuses the mesh."""
+    world = 2
+    mp.spawn(_engine_agreement_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    e0, e1 = (list(np.load(tmp_path / f"e{r}.npy")) for r in range(world))
+    assert e0 == e1
+    keys = sorted(["auto_uneven", "mesh_uneven", "sweep_uneven", "auto_equal", "mesh_equal"])
+    got = dict(zip(keys, e0))
+    assert got == {"auto_uneven": "sweep", "mesh_uneven": "refused", "sweep_uneven": "sweep",
+                   "auto_equal": "auto", "mesh_equal": "mesh"}

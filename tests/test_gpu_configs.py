@@ -359,6 +359,7 @@ def test_solo_fallback_when_registration_cannot_complete(dev, monkeypatch, dt):
 
 @pytest.mark.parametrize("engine,n,m,dt,iters", [("tiled", 4096, 4096, torch.float32, 20000),
                                                  ("mesh", 4096, 4096, torch.float32, 40000),
+                                                 ("mesh", 4096, 4096, torch.float64, 12000),
                                                  ("mesh", 4096, 4096, torch.float64, 30000),
                                                  ("resident", 512, 512, torch.float64, 30000),
                                                  ("gather", 512, 512, torch.float64, 60000),

@@ -75,6 +75,47 @@ def test_pairwise_metric_shape_matches_unfused(dev):
     assert nrel(r1.plan.cpu().numpy(), ru.plan.cpu().numpy()) < 1e-11
 
 
+@pytest.fixture(scope="module")
+def bench_shape_oracle(orc):
+    """The bench's own inputs (bench.py: paired_embeddings(4096, 512, seed=1234)) through the
+    oracle's float64 cost once; the POT solves per eps are computed on demand."""
+    from otfuse.synthetic import paired_embeddings
+    X, Y, _ = paired_embeddings(4096, 512, seed=1234)
+    C, mx = orc.pairwise_cost(X, Y)
+    a = np.full(4096, 1.0 / 4096)
+    cache = {}
+
+    def get(reg):
+        if reg not in cache:
+            cache[reg] = orc.sinkhorn_knopp(a, a, C, reg, 100, 0.0, cscale=1.0 / mx)
+        return cache[reg]
+    return X, Y, mx, get
+
+
+@pytest.mark.parametrize("reg", [0.1, 5e-3])
+def test_pairwise_bench_shape_vs_oracle(bench_shape_oracle, dev, reg):
+    """The headline launch itself at the exact bench shape (N = 4096, d = 512, 100 iterations,
+    stopThr = 0, the bench's seeded inputs): AUTO takes the fused float64 mesh launch, whose
+    plan is within 1e-9 of the float64 oracle (cost + POT sinkhorn_knopp), with the oracle's
+    iteration count, cost max and scalings (modulo the Sinkhorn scale mode) -- at the bench's
+    eps = 0.1 and the reference's per-epoch eps = 5e-3 (MRI_PET_OT_OT_per_epoch_attn.py)."""
+    from otfuse import ops
+    X, Y, mx, get = bench_shape_oracle
+    P_r, u_r, v_r, info_r = get(reg)
+    res = ops.sinkhorn_pairwise(torch.from_numpy(X).to(dev), torch.from_numpy(Y).to(dev), reg,
+                                max_iter=100, stop_thr=0.0)
+    info = res.info()
+    assert info["engine_name"] == "mesh" and info["fallback"] == 0
+    assert info["status_name"] == "max_iter" and info["niter"] == info_r["niter"] == 99
+    assert info["break_iter"] == info_r["break_iter"]
+    assert abs(float(res.cost_max) - mx) / mx < 1e-12
+    assert nrel(res.plan.cpu().numpy(), P_r) < TOL64
+    u, v = res.u.cpu().numpy(), res.v.cpu().numpy()
+    c = float(np.median(u / u_r))
+    np.testing.assert_allclose(u / c, u_r, rtol=1e-9)
+    np.testing.assert_allclose(v * c, v_r, rtol=1e-9)
+
+
 def test_pairwise_euclidean_unscaled_vs_oracle(orc, dev):
     """The euclidean metric without the max scaling (cost in data units, reg to match)."""
     from otfuse import ops
@@ -123,12 +164,16 @@ def test_pairwise_unfused_shapes_vs_oracle(orc, dev, n, m, d):
     assert nrel(res.plan.cpu().numpy(), P_r) < TOL64
 
 
-def test_pairwise_registration_fallback(orc, dev, monkeypatch):
+@pytest.mark.parametrize("xcc", ["1", "0"])
+def test_pairwise_registration_fallback(orc, dev, monkeypatch, xcc):
     """A fused grid that cannot become co-resident (a persistent blocker on another stream,
-    a 1-ms registration window) gives up; the guarded one-workgroup cost build and the
-    one-workgroup solve queued behind it return the oracle's plan (info fallback = 1)."""
+    a 1-ms registration window) gives up; the fallback queued behind it builds the cost and
+    solves, returning the oracle's plan (info fallback = 1).  OTF_MESH_XCC=0: blockIdx roles,
+    no registration barrier -- the grid-max barrier of the cost build is the first
+    device-wide wait and gives up as a registration give-up."""
     from otfuse import ops
     monkeypatch.setenv("OTF_REG_MS", "1")
+    monkeypatch.setenv("OTF_MESH_XCC", xcc)
     # the whole-chip shape (256 workgroups): the blocker's CUs keep some of them out
     X, Y = _emb(4096, 4096, 64, 21)
     P_r, u_r, v_r, info_r, mx = _oracle(orc, X, Y, 0.05, 20)

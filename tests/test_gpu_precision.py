@@ -133,6 +133,17 @@ def test_precision_auto_promotes_when_the_shift_cannot_apply(orc, dev, metric_in
     i = r.info()
     assert (i["niter"], i["break_iter"]) == (ir["niter"], ir["break_iter"])
     assert nrel(r.plan.cpu().numpy(), Pr3) < 1e-9
+    # an explicit shift=True on an engine without the shifted kernel (tiled; a 1024^2 block
+    # of the metric cost, so that the float64 tiles fit the CUs): promoted to float64 like
+    # shift=None, not rejected (the shift is a float32 form)
+    Cb = C[:1024, :1024].contiguous()
+    ab = torch.full((1024,), 1.0 / 1024, device=dev)
+    r = ops.sinkhorn(ab, ab, Cb, 0.01, max_iter=100, stop_thr=0.0, cost_scale=cmax, precision="auto",
+                     shift=True, engine="tiled")
+    assert r.u.dtype == torch.float64 and not r.shifted and r.info()["engine_name"] == "tiled"
+    u1 = np.full(1024, 1.0 / 1024)
+    Prb, *_ = orc.sinkhorn_knopp(u1, u1, Cb.double().cpu().numpy() / float(cmax), 0.01, 100, 0.0)
+    assert nrel(r.plan.cpu().numpy(), Prb) < 1e-9
 
 
 def test_pot_sinkhorn_log_returns_pot_scalings_when_shifted(dev, metric_inputs, oracle_plans):

@@ -226,3 +226,52 @@ def test_xmesh_two_ranks_match_whole_problem(tmp_path, orc):
     Pr, *_ = orc.sinkhorn_knopp(np.full(2048, 1.0 / 2048), np.full(8192, 1.0 / 8192), Cd / Cd.max(),
                                 0.1, 60, 0.0)
     assert np.abs(Pc - Pr).max() / np.abs(Pr).max() < 1e-4
+
+
+def _uneven_worker(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["OTF_SWEEP_GRID"] = "96"      # two ranks' grids resident on one device
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import otfuse.distributed as D
+    dev = torch.device("cuda", 0)
+    rows = [1024, 1536]
+    n, m = sum(rows), 1024
+    rng = np.random.default_rng(17)
+    C = rng.random((n, m))
+    r0 = sum(rows[:rank])
+    sl = slice(r0, r0 + rows[rank])
+    xp = D.XPeer(m)
+    res = D.sinkhorn_xsweep(torch.full((rows[rank],), 1.0 / n, device=dev), torch.full((m,), 1.0 / m, device=dev),
+                            torch.tensor(C[sl], device=dev, dtype=torch.float32), 0.05, xp, n_total=n,
+                            max_iter=500, stop_thr=1e-6)
+    info = res.info()
+    np.savez(os.path.join(out_dir, f"u{rank}.npz"), P=res.plan.cpu().numpy(), niter=info["niter"],
+             status=info["status"], engine=info["engine_name"], v=res.v.cpu().numpy())
+    xp.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xsweep_uneven_mesh_shaped_shards_agree(tmp_path, orc):
+    """shards of 1024 and 1536 rows x 1024 columns -- each alone a float32 mesh
+    slab, with different tilings -- under a converging stop (stopThr 1e-6): the ranks agree
+    on one engine (the sweep, otfuse.distributed.xsweep_engine), stop at the oracle's
+    iteration together and assemble its plan."""
+    world = 2
+    mp.spawn(_uneven_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    rows = [1024, 1536]
+    n, m = sum(rows), 1024
+    C = np.random.default_rng(17).random((n, m))
+    P_ref, _, _, info_r = orc.sinkhorn_knopp(np.full(n, 1.0 / n), np.full(m, 1.0 / m), C, 0.05, 500, 1e-6)
+    zs = [np.load(tmp_path / f"u{r}.npz") for r in range(world)]
+    assert all(str(z["engine"]) == "sweep" for z in zs)
+    assert all(int(z["niter"]) == info_r["niter"] < 499 for z in zs)
+    assert np.array_equal(zs[0]["v"], zs[1]["v"])
+    P = np.concatenate([z["P"] for z in zs])
+    assert np.abs(P - P_ref).max() / np.abs(P_ref).max() < 1e-4

@@ -1,0 +1,93 @@
+#!/bin/bash
+# One GPU-box session: every step under its own time limit, the session stops at the first
+# fatal status (anything but 0, or pytest's 1 for failed tests).  Steps run in this order,
+# each only when its variable is set; outputs go to gpurun_out/$TAG (default "run"):
+#   FIRST="tests/x.py::t ..."  targeted tests, -x (FIRST_LIMIT, default 400 s)
+#   FULL=1                     the whole -m gpu suite (gpu_tests.log)
+#   PROBE=1                    tools/pw_probe.py (fused call vs the two calls)
+#   RUN="bin args;bin args"    prebuilt stamp / microbenchmark binaries (tools/bin/...), each
+#                              once per REPS, interleaved (A/B of alternative builds)
+#   LIBAB="z a b"              the headline step of prebuilt library variants
+#                              tools/alt/lib_<v>.so, interleaved, REPS rounds (the tree's
+#                              library is restored afterwards)
+#   BENCH=1                    bench.py with the driver's --steps 20 --warmup 5 (BENCH_ARGS)
+#   PROF=1                     rocprofv3 kernel traces of the float64 headline step (the bench's
+#                              own --steps 20 --warmup 5), the float32 leg and config 5
+#   PMC=1                      FETCH_SIZE / WRITE_SIZE / MFMA-busy passes, one counter set per run
+# Example:  TAG=r06a FIRST=tests/test_gpu_pairwise.py BENCH=1 PROF=1 bash tools/gpu_run.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-run}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+LIB=ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd/otfuse/lib/libotfuse.so
+export LD_LIBRARY_PATH=$PWD/$(dirname $LIB):${LD_LIBRARY_PATH:-}
+REPS=${REPS:-2}
+
+step() {  # $1 = log name, $2 = limit (s), $3 = 1 if pytest's rc 1 is not fatal, rest = command
+  local name=$1 lim=$2 soft=$3; shift 3
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -"${TAILN:-6}" "$OUT/$name.log"
+  if [ $rc -ne 0 ] && ! { [ "$soft" = 1 ] && [ $rc -eq 1 ]; }; then exit $rc; fi
+}
+PYT="python -u -m pytest -m gpu -v --timeout 180 --timeout-method thread -p no:cacheprovider"
+
+if [ -n "${FIRST:-}" ]; then step first "${FIRST_LIMIT:-400}" 0 $PYT -x $FIRST; fi
+if [ "${FULL:-0}" = 1 ]; then step gpu_tests 900 1 $PYT tests; fi
+if [ "${PROBE:-0}" = 1 ]; then step probe 200 0 python tools/pw_probe.py; fi
+if [ -n "${RUN:-}" ]; then
+  IFS=';' read -r -a cmds <<< "$RUN"
+  for rep in $(seq 1 "$REPS"); do
+    k=0
+    for c in "${cmds[@]}"; do
+      k=$((k + 1))
+      TAILN=${TAILN:-12} step "run${k}_$rep" 150 0 $c
+    done
+  done
+fi
+if [ -n "${LIBAB:-}" ]; then
+  cp $LIB /tmp/libotfuse.tree.so
+  for rep in $(seq 1 "$REPS"); do
+    for v in $LIBAB; do
+      cp tools/alt/lib_$v.so $LIB
+      timeout -k 10 240 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-hbm-probe --no-gw \
+          --no-f32 --no-config5 --no-batch-ot > "$OUT/libab_$v.$rep.log" 2>&1
+      rc=$?
+      if [ $rc -ne 0 ]; then cp /tmp/libotfuse.tree.so $LIB; tail "$OUT/libab_$v.$rep.log"; exit $rc; fi
+      python3 - "$OUT/libab_$v.$rep.log" "$v" "$rep" <<'PY'
+import json, sys
+d = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
+b = d.get("breakdown_ms", {})
+print(sys.argv[2], sys.argv[3], "ms_per_step %.4f fused_call %.4f per_iter_us %.3f intercept_us %.1f" % (
+    d["ms_per_step"], b.get("fused_call", 0), 1e3 * b.get("per_iteration", 0), 1e3 * b.get("intercept", 0)),
+    flush=True)
+PY
+    done
+  done
+  cp /tmp/libotfuse.tree.so $LIB
+fi
+if [ "${BENCH:-0}" = 1 ]; then
+  TAILN=1 step bench 600 0 python bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-}
+fi
+B="python3 bench.py --profile-only --steps ${PSTEPS:-20} --warmup ${PWARM:-5}"
+prof() {  # $1 = name, rest = rocprofv3 options, then `--` and the bench flags
+  local name=$1; shift
+  TAILN=2 step "$name" 300 0 rocprofv3 "$@"
+}
+if [ "${PROF:-0}" = 1 ]; then
+  prof prof --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- $B
+  prof prof_f32 --kernel-trace --stats -d "$OUT/prof_f32" -o run --output-format csv -- $B --profile-f32
+  prof prof_c5 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv -- $B --profile-config5
+fi
+if [ "${PMC:-0}" = 1 ]; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    prof pmc_${c}_auto --pmc $c --kernel-trace -d "$OUT/pmc_${c}_auto" -o run --output-format csv -- $B
+    prof pmc_${c}_f32 --pmc $c --kernel-trace -d "$OUT/pmc_${c}_f32" -o run --output-format csv -- $B --profile-f32
+    prof pmc_${c}_c5 --pmc $c --kernel-trace -d "$OUT/pmc_${c}_c5" -o run --output-format csv -- $B --profile-config5
+  done
+  prof pmc_MFMA_auto --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmc_MFMA_auto" -o run \
+      --output-format csv -- $B
+fi
+echo "session done"

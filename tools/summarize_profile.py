@@ -1,10 +1,11 @@
-"""Summarise a gpu_session.sh run (gpurun_out/) into tracked files under profiles/.
+"""Summarise a tools/gpu_run.sh session (gpurun_out/<TAG>/) into tracked files under profiles/.
 
-Writes, for round tag T (argv[1], e.g. r01):
+Usage: python tools/summarize_profile.py <round tag, e.g. r06> [session dir, default gpurun_out]
+Writes, for round tag T:
   profiles/T_kernel_stats.csv      rocprofv3 --kernel-trace --stats summary (copied)
   profiles/T_summary.json          per-kernel median durations + PMC HBM bytes per launch
   profiles/kernel_traffic.json     HBM bytes per launch of each hot kernel (read by bench.py)
-PMC runs: gpurun_out/pmc_<COUNTER>_<engine>/ (separate --pmc passes per counter, one per
+PMC runs: <session dir>/pmc_<COUNTER>_<leg>/ (separate --pmc passes per counter, one per
 Sinkhorn engine so both the resident kernel and the streaming pass are counted).
 Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE / WRITE_SIZE are KiB; on
 gfx950 FETCH_SIZE reports half the bytes of a wide coalesced stream, so it is doubled;
@@ -64,7 +65,10 @@ def base_name(k):
 
 
 def main():
+    global OUT
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    if len(sys.argv) > 2:
+        OUT = os.path.abspath(sys.argv[2])
     os.makedirs(PROF, exist_ok=True)
     shutil.copy(os.path.join(OUT, "prof", "run_kernel_stats.csv"),
                 os.path.join(PROF, f"{tag}_kernel_stats.csv"))
