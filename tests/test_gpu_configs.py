@@ -381,4 +381,4 @@ def test_long_persistent_solve_outlives_the_stall_limit(dev, monkeypatch, engine
     elapsed = time.perf_counter() - t0
     assert info["engine_name"] == engine
     assert info["status_name"] == "max_iter" and not info["stalled"]
-    assert elapsed > 0.04 * 2       # the solve really outlived the stall limit
+    assert elapsed > 0.04 * 1.5     # the solve really outlived the stall limit

@@ -32,7 +32,7 @@ step() {  # $1 = log name, $2 = limit (s), $3 = 1 if pytest's rc 1 is not fatal,
   tail -"${TAILN:-6}" "$OUT/$name.log"
   if [ $rc -ne 0 ] && ! { [ "$soft" = 1 ] && [ $rc -eq 1 ]; }; then exit $rc; fi
 }
-PYT="python -u -m pytest -m gpu -v --timeout 180 --timeout-method thread -p no:cacheprovider"
+PYT="python -u -m pytest -m gpu -v -rP --timeout 180 --timeout-method thread -p no:cacheprovider"
 
 if [ -n "${FIRST:-}" ]; then step first "${FIRST_LIMIT:-400}" 0 $PYT -x $FIRST; fi
 if [ "${FULL:-0}" = 1 ]; then step gpu_tests 900 1 $PYT tests; fi
