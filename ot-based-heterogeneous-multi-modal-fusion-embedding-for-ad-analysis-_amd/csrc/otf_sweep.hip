@@ -111,6 +111,43 @@ template <typename T> struct SkSweepArgs {
 };
 constexpr int kSwSlices = 32;  // column slices of the granule reduction
 
+// Slab granules (r06): FOUR float32 column partials per 16-B chunk, the tag folded into
+// each value's three low mantissa bits -- bits 0..1 = (epoch mod 3) + 1 (never 0, so the
+// zero fill never matches), bit 2 = the non-finite-u flag -- instead of chunk2's {value,
+// tag} pairs: half the slab bytes per sweep.  A slab row is single-buffered, so a slice
+// owner waiting for epoch e finds e - 1 or e there (a member writes e + 1 only after S[e],
+// which needs this owner's slice), and epoch mod 3 tells them apart.  The value is
+// ROUNDED to a 21-bit mantissa (relative 2^-21 on one workgroup's partial, unbiased:
+// truncation's one-sided 2^-20 lifted the converged marginal-error floor of a
+// 400-iteration xsweep to 1.1e-8 against 1e-8 for the float32 sums); 0 and +-inf come
+// back exact once the bits are cleared.
+using F4v = __attribute__((ext_vector_type(4))) float;
+__device__ __forceinline__ unsigned qtag(unsigned e) { return e % 3u + 1u; }
+__device__ __forceinline__ I4 chunk4(float v0, float v1, float v2, float v3, unsigned tag, int flag) {
+    const unsigned low = tag | ((unsigned)flag << 2);
+    // round half away from zero at bit 3 (a carry into the exponent is the correct
+    // rounding; +-inf stays +-inf)
+    auto rnd = [&](float v) -> int { return (int)(((__builtin_bit_cast(unsigned, v) + 4u) & ~7u) | low); };
+    I4 x;
+    x[0] = rnd(v0);
+    x[1] = rnd(v1);
+    x[2] = rnd(v2);
+    x[3] = rnd(v3);
+    return x;
+}
+__device__ __forceinline__ bool chunk4_at(const I4 x, unsigned tag) {
+    return (((unsigned)x[0] & 3u) == tag) && (((unsigned)x[1] & 3u) == tag) && (((unsigned)x[2] & 3u) == tag) &&
+           (((unsigned)x[3] & 3u) == tag);
+}
+// element copies first (ROCm 7.2: a bit_cast of a vector ELEMENT reads element 0)
+__device__ __forceinline__ float chunk4_v(const I4 x, int i) {
+    const unsigned w = (unsigned)x[i] & ~7u;
+    return __builtin_bit_cast(float, w);
+}
+__device__ __forceinline__ int chunk4_flag(const I4 x) {
+    return (int)((((unsigned)x[0] | (unsigned)x[1] | (unsigned)x[2] | (unsigned)x[3]) >> 2) & 1u);
+}
+
 using Raw = __attribute__((ext_vector_type(4))) unsigned int;  // 16 B of cost
 
 template <typename CT> struct RawN {
@@ -205,6 +242,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
     __shared__ int s_pop[6];
     __shared__ int mrow[256];     // granule flush: this XCC's members by blockIdx rank
     __shared__ int s_or[6][NW];  // [0..1] v-update checks, [2..3] flushes, [4..5] S slices
+    __shared__ int s_fq[NW];     // granule flush stage b: the waves' slab flags
     const bool gran = sizeof(T) == 4 && p.gran;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -341,7 +379,7 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         // VC sums (plain floats: half the bytes of tagged granules)
         const __amdgpu_buffer_rsrc_t rfs = sums_rsrc(p.gfs);
         const unsigned e = (p.ep_base + (unsigned)(k + 1)) & 0x3fffffffu;
-        const int swc = (mc + kSwSlices - 1) / kSwSlices;
+        const int swc = 2 * ((p.m_pad / 4 + kSwSlices - 1) / kSwSlices);  // pairs per slice (flush_gran)
         const int slot = xcc_id() * 4 + (int)(e & 3);
         const uint32_t fo = (uint32_t)(32 * p.m_pad) * 4u + (uint32_t)(slot * kSwSlices + (colc[g] / 2) / swc) * 4u;
         int fw = __builtin_amdgcn_raw_buffer_load_b32(rfs, fo, 0, 16 /* sc1 */);
@@ -734,22 +772,28 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         const __amdgpu_buffer_rsrc_t rxx = sums_rsrc(p.xr[p.world > 1 ? p.rank : 0]);
         const __amdgpu_buffer_rsrc_t rxp = sums_rsrc(p.gxp);
         const __amdgpu_buffer_rsrc_t rfs = sums_rsrc(p.gfs);
-        const int sw = (mc + kSwSlices - 1) / kSwSlices;         // granule pairs per slice (<= 256)
-        const int swp = sw <= 64 ? 64 : sw <= 128 ? 128 : 256;   // lanes per row group
+        static_assert(!(sizeof(T) == 4) || VC % 4 == 0, "slab quads: whole 4-column groups per chunk");
+        const int mq = p.m_pad / 4;                              // slab quads per row
+        const int sw4 = (mq + kSwSlices - 1) / kSwSlices;        // slab quads per slice (<= 128)
+        const int sw = 2 * sw4;                                  // granule pairs per slice (<= 256)
+        const int swp = sw4 <= 64 ? 64 : 128;                    // stage b: lanes per row group
         const int Q = kSwNT / swp, sq = tid / swp, sj = tid % swp;
         const unsigned e = (p.ep_base + (unsigned)(k + 1)) & 0x3fffffffu;
+        const unsigned et = qtag(e);
         const int xsp = 2 * (p.solve_par & 1);  // exchange slot set of this solve
         bool ok = true;
-        // a. this workgroup's partials -> its slab row
-        const uint32_t rowo = (uint32_t)blockIdx.x * (uint32_t)mc * 16u;
+        // a. this workgroup's partials -> its slab row (four columns per chunk)
+        const uint32_t rowo = (uint32_t)blockIdx.x * (uint32_t)mq * 16u;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int c0 = (tid + kSwNT * g) * VC;
             if (c0 < p.m_pad) {
 #pragma unroll
-                for (int h = 0; h < VP2; ++h)
-                    gstore_col(rsl, rowo + (uint32_t)(c0 / 2 + h) * 16u,
-                               chunk2((float)colacc[g][h].x, (float)colacc[g][h].y, (int)(e << 2) | badu), 1);
+                for (int h = 0; h < VC / 4; ++h)
+                    gstore_col(rsl, rowo + (uint32_t)(c0 / 4 + h) * 16u,
+                               chunk4((float)colacc[g][2 * h].x, (float)colacc[g][2 * h].y,
+                                      (float)colacc[g][2 * h + 1].x, (float)colacc[g][2 * h + 1].y, et, badu),
+                               1);
             }
         }
         badu = 0;
@@ -760,10 +804,13 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         }
 #endif
         // b. owned slices: sum over the XCC's members (rank order), publish the XCC partial
+        // (lane sj of row group sq: slab quad sl * sw4 + sj of members sq, sq + Q, ...).
+        // A member's flag rides in every chunk of its row, so the workgroup-wide OR of the
+        // flags the slice's lanes saw is the OR over the XCC's members
         for (int sl = gslot_r; sl < kSwSlices; sl += nx) {
-            const int cch = sl * sw + sj;
-            const bool act = sj < sw && cch < mc;
-            float a0 = 0.f, a1 = 0.f;
+            const int cq = sl * sw4 + sj;
+            const bool act = sj < sw4 && cq < mq;
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
             int fl = 0;
             for (int rb = sq; rb < nx; rb += NBT * Q) {
                 I4 x[NBT];
@@ -772,46 +819,48 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
                 for (int i = 0; i < NBT; ++i) {
                     const int r = rb + i * Q;
                     if (act && r < nx) {
-                        x[i] = gload(rsl, (uint32_t)mrow[r] * (uint32_t)mc * 16u + (uint32_t)cch * 16u);
+                        x[i] = gload(rsl, (uint32_t)mrow[r] * (uint32_t)mq * 16u + (uint32_t)cq * 16u);
                         pend |= 1u << i;
                     }
                 }
 #pragma unroll
                 for (int i = 0; i < NBT; ++i)
-                    if ((pend & (1u << i)) && chunk_at(x[i], e)) pend &= ~(1u << i);
+                    if ((pend & (1u << i)) && chunk4_at(x[i], et)) pend &= ~(1u << i);
                 while (pend && ok) {
                     __builtin_amdgcn_s_sleep(1);
 #pragma unroll
                     for (int i = 0; i < NBT; ++i)
                         if (pend & (1u << i))
-                            x[i] = gload(rsl, (uint32_t)mrow[rb + i * Q] * (uint32_t)mc * 16u + (uint32_t)cch * 16u);
+                            x[i] = gload(rsl, (uint32_t)mrow[rb + i * Q] * (uint32_t)mq * 16u + (uint32_t)cq * 16u);
 #pragma unroll
                     for (int i = 0; i < NBT; ++i)
-                        if ((pend & (1u << i)) && chunk_at(x[i], e)) pend &= ~(1u << i);
+                        if ((pend & (1u << i)) && chunk4_at(x[i], et)) pend &= ~(1u << i);
                     if (pend && __builtin_amdgcn_s_memrealtime() > deadline) ok = false;
                 }
 #pragma unroll
                 for (int i = 0; i < NBT; ++i)
                     if (act && rb + i * Q < nx) {
-                        a0 += chunk_v0(x[i]);
-                        a1 += chunk_v1(x[i]);
-                        fl |= (x[i][1] | x[i][3]) & 3;
+                        a0 += chunk4_v(x[i], 0);
+                        a1 += chunk4_v(x[i], 1);
+                        a2 += chunk4_v(x[i], 2);
+                        a3 += chunk4_v(x[i], 3);
+                        fl |= chunk4_flag(x[i]);
                     }
             }
             float* st = reinterpret_cast<float*>(gred);
-            st[tid * 4] = a0;
-            st[tid * 4 + 1] = a1;
-            st[tid * 4 + 2] = __builtin_bit_cast(float, fl);
+            *reinterpret_cast<F4v*>(&st[tid * 4]) = F4v{a0, a1, a2, a3};
+            const bool wfl = __any(fl != 0);
+            if (lane == 0) s_fq[w] = wfl ? 1 : 0;
             __syncthreads();
             if (sq == 0 && act) {
-                float s0 = st[sj * 4], s1 = st[sj * 4 + 1];
-                int f = __builtin_bit_cast(int, st[sj * 4 + 2]);
-                for (int qq = 1; qq < Q; ++qq) {
-                    s0 += st[(qq * swp + sj) * 4];
-                    s1 += st[(qq * swp + sj) * 4 + 1];
-                    f |= __builtin_bit_cast(int, st[(qq * swp + sj) * 4 + 2]);
-                }
-                gstore(rxp, (uint32_t)(((e & 1) * 8 + xcd) * mc + cch) * 16u, chunk2(s0, s1, (int)(e << 2) | f));
+                F4v s = *reinterpret_cast<const F4v*>(&st[sj * 4]);
+                int f = 0;
+#pragma unroll
+                for (int ww = 0; ww < NW; ++ww) f |= s_fq[ww];
+                for (int qq = 1; qq < Q; ++qq) s += *reinterpret_cast<const F4v*>(&st[(qq * swp + sj) * 4]);
+                const uint32_t xo = (uint32_t)(((e & 1) * 8 + xcd) * mc + 2 * cq) * 16u;
+                gstore(rxp, xo, chunk2(s[0], s[1], (int)(e << 2) | f));
+                gstore(rxp, xo + 16u, chunk2(s[2], s[3], (int)(e << 2) | f));
             }
             __syncthreads();
         }
@@ -827,8 +876,8 @@ __global__ __launch_bounds__(kSwNT) void sk_sweep_kernel(SkSweepArgs<T> p) {
         // ready word per slice carries the epoch and the OR of the flags
         int nsl = 0;
         for (int sl = gslot_r; sl < kSwSlices; sl += nx, ++nsl) {
-            const int cch = sl * sw + sj;
-            const bool act = sq == 0 && sj < sw && cch < mc;
+            const int cch = sl * sw + tid;  // one thread per granule pair of the slice
+            const bool act = tid < sw && cch < mc;
             float s0 = 0.f, s1 = 0.f;
             int f = 0;
             if (act) {
