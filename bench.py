@@ -495,15 +495,24 @@ def metric_f32_leg(dev, X, Y, N, d, iters, eps, engine, pmc_traffic, steps=20, w
     """The metric config at float32 compute (not the reference's precision; reported beside
     the float64 headline): split-fp16 cost on fp16 MFMA (fp32-accurate: x.y = hi.hi + hi.lo
     + lo.hi), float32 POT Sinkhorn on the float32 mesh (csrc/otf_mesh.hip), float32 plan.
-    Parity: within 1e-4 of the float64 oracle at eps 0.1 ... 5e-3
-    (tests/test_gpu_precision.py)."""
+    The step is the two calls (pairwise_cost + sinkhorn); the r06 fused form
+    (ops.sinkhorn_pairwise(precision="fp32", engine="mesh"), otf_sinkhorn_pairwise_f32: every
+    workgroup builds its cost tile in the solve's prologue from the split-fp16 images, bitwise
+    the two calls' results, tests/test_gpu_pairwise32.py) is timed beside it -- measured slower,
+    so AUTO keeps the two calls.  Parity: within 1e-4 of the float64 oracle at eps 0.1 ... 5e-3
+    (tests/test_gpu_precision.py, tests/test_gpu_pairwise32.py)."""
     from otfuse import ops
     a = torch.full((N,), 1.0 / N, device=dev)
     ws = ops.sinkhorn_workspace(N, N, torch.float32, iters, dev)
+    ws32 = ops.sinkhorn_pairwise_workspace(N, N, iters, dev, d=d, precision="fp32")
     P = torch.empty((N, N), dtype=torch.float32, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 
-    def step(record):
+    def fused(it=iters):
+        return ops.sinkhorn_pairwise(X, Y, eps, max_iter=it, stop_thr=0.0, workspace=ws32, plan_out=P,
+                                     engine="mesh", precision="fp32")
+
+    def two_call(record):
         if record:
             ev[0].record()
         C, cmax = ops.pairwise_cost(X, Y)
@@ -516,25 +525,51 @@ def metric_f32_leg(dev, X, Y, N, d, iters, eps, engine, pmc_traffic, steps=20, w
         return r
 
     for _ in range(warmup):
-        step(False)
+        two_call(False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step(False)
+        two_call(False)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if profile_only:
         return None
+
+    def call_ms(fn, reps=7):
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return sorted(ts)[reps // 2]
+
+    fused_ms = call_ms(fused)
+    short = max(iters // 5, 1)
+    # the step's solve at iters and iters / 5 on one cost: slope and intercept of the mesh launch
+    C0, cm0 = ops.pairwise_cost(X, Y)
+    solve = lambda it: ops.sinkhorn(a, a, C0, eps, max_iter=it, stop_thr=0.0, cost_scale=cm0, workspace=ws,
+                                    plan_out=P, engine=engine)
+    sk_long_ms = call_ms(lambda: solve(iters))
+    sk_short_ms = call_ms(lambda: solve(short))
+    per_it_ms = (sk_long_ms - sk_short_ms) / (iters - short)
+    intercept_ms = sk_long_ms - per_it_ms * iters
+    del C0
+    rf = fused()
+    for _ in range(2):
+        two_call(False)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(6)]
     res = None
     for k in range(6):
         ev[:] = evs[k]
-        res = step(True)
+        res = two_call(True)
     torch.cuda.synchronize()
     cost_ms = sorted(e[0].elapsed_time(e[1]) for e in evs[1:])[2]
     sk_ms = sorted(e[1].elapsed_time(e[2]) for e in evs[1:])[2]
-    # the cost op split into its prep (norms / scales) and the MFMA kernel (device events
-    # recorded by the library around each, OTF_COST_PHASES)
+    # the two-call cost op split into its prep (norms / scales) and the MFMA kernel (device
+    # events recorded by the library around each, OTF_COST_PHASES)
     os.environ["OTF_COST_PHASES"] = "1"
     ph = []
     for _ in range(5):
@@ -548,17 +583,22 @@ def metric_f32_leg(dev, X, Y, N, d, iters, eps, engine, pmc_traffic, steps=20, w
     kname = {"mesh": "sk_mesh_kernel", "tiled": "sk_tiled_kernel", "sweep": "sk_sweep_kernel",
              "resident": "sk_resident_kernel", "gather": "sk_gather_kernel"}.get(eng, "sk_pass_kernel")
     floor_us = 2.0 * N * N / (VALU_F32_PEAK_TFMA * 1e12) * 1e6
-    it_us = sk_ms * 1e3 / iters
+    it_us = per_it_ms * 1e3
     traffic = pmc_traffic(kname) if pmc_traffic else None
     cost_flops = 2.0 * N * N * d
     ms_per_step = elapsed * 1e3 / steps
     return {"dtype": "f32", "N": N, "d": d, "iters": iters, "eps": eps, "engine": eng,
             "status": info["status_name"], "ms_per_step": ms_per_step,
             "pairs_per_s": N / (ms_per_step * 1e-3), "sinkhorn_iters_per_s": iters / (sk_ms * 1e-3),
-            "breakdown_ms": {"cost": cost_ms, "sinkhorn_incl_plan": sk_ms},
+            "step": "two calls: pairwise_cost (split-fp16 prep + cost_big16_kernel) + sinkhorn (float32 mesh)",
+            "breakdown_ms": {"cost": cost_ms, "sinkhorn_incl_plan": sk_ms,
+                             "fused_call": fused_ms, "fused_engine": rf.info()["engine_name"],
+                             "fused_fallback": rf.info()["fallback"], "sinkhorn_per_iteration": per_it_ms,
+                             "sinkhorn_intercept": intercept_ms},
             "roofline": {"bound": "latency", "kernel": kname, "achieved": it_us, "peak": floor_us,
                          "unit": "us per iteration", "frac": floor_us / it_us, "traffic": traffic,
-                         "note": "K in registers for the whole solve; VALU floor of 2 N^2 float32 "
+                         "note": "K in registers for the whole solve; the solve's per-iteration slope "
+                                 "(between iters / 5 and iters) against the VALU floor of 2 N^2 float32 "
                                  "FMAs at 78.6 T FMA/s"},
             "cost_roofline": {"bound": "mfma", "kernel": "cost_big16_kernel",
                               "achieved": 3.0 * cost_flops / (kern_ms * 1e-3) / 1e12,
@@ -569,8 +609,9 @@ def metric_f32_leg(dev, X, Y, N, d, iters, eps, engine, pmc_traffic, steps=20, w
                               "note": "the fp32-accurate product x.y = hi.hi + hi.lo + lo.hi runs as "
                                       "three fp16 MFMA contractions: achieved = 3 x 2*N*N*d / the MFMA "
                                       "kernel's device time vs the dense fp16 MFMA peak"},
-            "note": "float32 compute: within 1e-4 of the float64 oracle (tests/test_gpu_precision.py), "
-                    "not the reference's precision -- the headline is the float64 step"}
+            "note": "float32 compute: within 1e-4 of the float64 oracle (tests/test_gpu_precision.py, "
+                    "tests/test_gpu_pairwise32.py), not the reference's precision -- the headline is the "
+                    "float64 step"}
 
 
 def gw_leg(dev, with_cpu, labels=2, per_label=64, d=512, eps=5e-3):

@@ -329,6 +329,26 @@ int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64
                               int64_t ldp, int32_t P_dtype, double* cmax_out, otf_sinkhorn_info* info,
                               double* errlog, void* workspace, size_t ws_bytes, otf_stream_t stream);
 
+/* The same segment in float32 compute (the float32 leg of bench.py): the cost is the
+ * split-fp16 one of otf_cost_pairwise_ex (x.y = hi.hi + hi.lo + lo.hi on fp16 MFMA, within
+ * 1e-4 of POT's float64 plan at the metric shape), the solve the float32 POT engines'.  With
+ * opts->engine == OTF_ENGINE_MESH and the float32 mesh's whole-tile shapes (n a multiple of
+ * 128, m a multiple of 512 up to 4096, the tiles fitting the CUs) every workgroup of the
+ * solve's launch builds its 128 x 512 cost tile in its prologue from the split-fp16 images (one
+ * prep launch writes them): no n x m cost in HBM, the costs -- and so the solve -- bitwise
+ * those of the two calls (otf_cost_pairwise_ex + otf_sinkhorn), which run otherwise: for AUTO
+ * (the two calls measured faster at the metric shape), other shapes and opts->shift (a pass
+ * over C).  a, b, u, v and *cmax_out (device, nullable) are float32; the plan float32 or
+ * float64 with ldp % 4 == 0.  Workspace: otf_sinkhorn_pairwise_f32_workspace_size (it holds
+ * the n x m float32 cost for the two calls and for the fallback of a grid that could not
+ * become co-resident). */
+size_t otf_sinkhorn_pairwise_f32_workspace_size(int64_t n, int64_t m, int64_t d, int32_t max_iter);
+int otf_sinkhorn_pairwise_f32(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n, int64_t m,
+                              int64_t d, int32_t metric, int32_t scale_max, const float* a, const float* b,
+                              const otf_sinkhorn_opts* opts, float* u_out, float* v_out, void* P_out,
+                              int64_t ldp, int32_t P_dtype, float* cmax_out, otf_sinkhorn_info* info,
+                              double* errlog, void* workspace, size_t ws_bytes, otf_stream_t stream);
+
 /* Cross-rank persistent sweep (BASELINE config 5 on several GPUs of one node): one
  * problem's rows sharded over world <= 8 ranks, each rank one persistent launch that
  * streams its cost rows; the m column sums are exchanged INSIDE the launch as

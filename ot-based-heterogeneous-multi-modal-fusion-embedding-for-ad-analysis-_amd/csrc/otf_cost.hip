@@ -14,7 +14,7 @@
 // MFMA 32x32 tiles), BK = 32, LDS double buffer in k-major [BK][128 + 1] images
 // (row-contiguous fragment reads, conflict-free transposed writes), XCD-grouped
 // block order.
-#include "otf_device.h"
+#include "otf_persist.h"
 
 namespace otf {
 namespace {
@@ -1061,6 +1061,33 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
 
 
 }  // namespace
+
+// Split-fp16 images + row scales + squared norms of two float32 operands in the workspace
+// layout of otf_cost_pairwise_ex (one split16_prep2_kernel launch): the fused float32
+// pairwise solve's prologue reads them (otf_persist.h PairwiseF32); the same bits as the
+// images the 256 x 256 cost kernel splits in registers, so the same costs.
+hipError_t split16_images(const float* X, int64_t ldx, int n, const float* Y, int64_t ldy, int m, int d,
+                          void* ws, Split16Images& out, unsigned int* cmax_word, hipStream_t s) {
+    const int64_t ldh = (d + SBK - 1) / SBK * SBK;
+    char* p = (char*)ws;
+    auto take = [&](size_t bytes) { void* q = p; p += (bytes + 255) / 256 * 256; return q; };
+    out.Xh = (_Float16*)take((size_t)n * ldh * 2);
+    out.Xl = (_Float16*)take((size_t)n * ldh * 2);
+    out.Yh = (_Float16*)take((size_t)m * ldh * 2);
+    out.Yl = (_Float16*)take((size_t)m * ldh * 2);
+    out.xs = (float*)take((size_t)n * 4);
+    out.xx = (float*)take((size_t)n * 4);
+    out.ys = (float*)take((size_t)m * 4);
+    out.yy = (float*)take((size_t)m * 4);
+    out.ldh = ldh;
+    const int rows = n + m;
+    const int nblk = (rows + 3) / 4 < 1024 ? (rows + 3) / 4 : 1024;
+    const int vec = (ldx * 4 % 16 == 0 && ldy * 4 % 16 == 0 && (uintptr_t)X % 16 == 0 && (uintptr_t)Y % 16 == 0) ? 1 : 0;
+    const PrepSide<float> A{X, ldx, n, out.Xh, out.Xl, out.xs, out.xx, nullptr};
+    const PrepSide<float> B{Y, ldy, m, out.Yh, out.Yl, out.ys, out.yy, nullptr};
+    split16_prep2_kernel<float, true><<<nblk, 256, 0, s>>>(A, B, d, (int)ldh, vec, cmax_word, nullptr);
+    return hipGetLastError();
+}
 }  // namespace otf
 
 extern "C" {

@@ -94,6 +94,7 @@ struct SkMeshArgs {
     int n_total, xrank, xworld, xpar, mc;
     unsigned xep;  // epoch base of this solve on the exchange (the same on every rank)
     unsigned char* xr[8];
+    PairwiseF32 pw;  // PW instances: the cost tile built in the prologue (otf_persist.h)
 };
 
 // Diagnostic build only (-DOTF_MESH_STAMPS, tools/stamps_mesh.hip): per-hop wall-clock
@@ -133,6 +134,183 @@ using F2 = __attribute__((ext_vector_type(2))) float;
 
 constexpr int pow2_at_least(int x) { return x <= 1 ? 1 : 2 * pow2_at_least((x + 1) / 2); }
 
+// ---- PW prologue (sk_mesh_kernel<..., PW = true>, otf_sinkhorn_pairwise_f32; r06) ----------
+// The workgroup's 128 x 512 tile of C = |x|^2 + |y|^2 - 2 x.y (MRI_PET_OT_nojax.py:70-75)
+// built where its K will live instead of read from a cost the cost kernel wrote, in two column
+// halves of 128 x 256: eight waves of 64 rows x 64 columns (wave w: rows 64 (w >> 2), columns
+// 64 (w & 3) of the half) on v_mfma_f32_16x16x32_f16, x.y = hi.hi + hi.lo + lo.hi of the
+// split-fp16 images, with the Y fragment as the A operand -- per 16 x 16 block the MFMA
+// sequence and the epilogue of cost_big16_kernel (otf_cost.hip), so every cost value is
+// bitwise the two-call path's.  The 32-deep stages are double-buffered in LDS (the next
+// stage's images in registers during this stage's MFMAs, one barrier a stage); each half then
+// moves to the mesh's K layout (wave w: 16 rows x 8 columns a lane) through LDS; one atomic
+// max per workgroup + a flat barrier give the grid max(C), then K = exp(-C / (reg max)) in place.
+constexpr int kPwK = 32;                        // K per stage (one 16x16x32 MFMA)
+constexpr int kPwRS = 264;                      // re-layout row pitch (floats): 2-way writes
+constexpr size_t kPwLds = (size_t)kMeshTR * kPwRS * 4;  // 135 168 B (a half's stages take 96 KiB of it)
+constexpr int kMeshMaxBar = 9 * 64, kMeshMaxWord = 10 * 64;  // int offsets in xreg
+using H8 = __attribute__((ext_vector_type(8))) _Float16;
+using F4 = __attribute__((ext_vector_type(4))) float;
+using U4 = __attribute__((ext_vector_type(4))) unsigned int;
+// 16-B chunk kc of a 64-B stage row, XOR-permuted by the row quad (otf_cost.hip g16swz)
+__device__ __forceinline__ int pw_swz(int row, int kc) {
+    return row * kPwK + ((kc ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3)) << 3);
+}
+
+template <int R, int G>
+__device__ __forceinline__ bool pw_cost_tile32(const SkMeshArgs& p, F2 (&kv)[R][G][2], unsigned char* lds, int rb,
+                                               int cb, int target, bool lead, unsigned long long& deadline,
+                                               int* s_flag, float* s_wmx, int* abandon) {
+    static_assert(R == 16 && G == 2, "the mesh's K layout: 16 rows x 2 x 4 columns a lane");
+    const PairwiseF32& q = p.pw;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 2, wn = w & 3;
+    const int row0 = rb * kMeshTR, col0 = cb * kMeshTC;
+    constexpr int HC = kMeshTC / 2;                       // 256 columns per half
+    constexpr int AS = kMeshTR * kPwK, BS = HC * kPwK;    // halves per image and stage buffer
+    _Float16* As = reinterpret_cast<_Float16*>(lds);      // [2 buffers][2 images][128 x 32]
+    _Float16* Bs = As + 4 * AS;                           // [2 buffers][2 images][256 x 32]
+    const __amdgpu_buffer_rsrc_t rxh = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(q.Xh), 0, (int)q.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rxl = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(q.Xl), 0, (int)q.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ryh = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(q.Yh), 0, (int)q.ybytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ryl = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(q.Yl), 0, (int)q.ybytes, 0x00020000);
+    // staging: X chunk (row tid >> 2, 16-B chunk tid & 3) and Y chunks tid + 512 c of a stage
+    const int xr = tid >> 2, xk = tid & 3;
+    const uint32_t xo = (uint32_t)(((int64_t)(row0 + xr) * q.ldh + 8 * xk) * 2);
+    const int nk = q.kpad / kPwK;
+    const int kc = lane >> 4;
+    const int rr = wm * 64 + (lane & 15);
+    float lmax = 0.f;
+    float* st = reinterpret_cast<float*>(lds);
+    // the tile in two column halves (operand stages double-buffered in LDS, one barrier a
+    // stage); each half moves to the K layout (kv[.][h]) before the next one is built
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint32_t yo[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int ch = tid + 512 * c;
+            yo[c] = (uint32_t)(((int64_t)(col0 + HC * h + (ch >> 2)) * q.ldh + 8 * (ch & 3)) * 2);
+        }
+        U4 sx[2], sy[2][2];
+        auto gl = [&](int k0) {
+            const uint32_t kb = (uint32_t)k0 * 2u;
+            sx[0] = __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(rxh, xo, kb, 0));
+            sx[1] = __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(rxl, xo, kb, 0));
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                sy[c][0] = __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(ryh, yo[c], kb, 0));
+                sy[c][1] = __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(ryl, yo[c], kb, 0));
+            }
+        };
+        auto ls = [&](int buf) {
+#pragma unroll
+            for (int img = 0; img < 2; ++img) {
+                *reinterpret_cast<U4*>(&As[(2 * buf + img) * AS + pw_swz(xr, xk)]) = sx[img];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int ch = tid + 512 * c;
+                    *reinterpret_cast<U4*>(&Bs[(2 * buf + img) * BS + pw_swz(ch >> 2, ch & 3)]) = sy[c][img];
+                }
+            }
+        };
+        F4 acc[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) acc[a][b] = F4{0.f, 0.f, 0.f, 0.f};
+        gl(0);
+        ls(0);
+        __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            const int buf = kt & 1;
+            if (kt + 1 < nk) gl((kt + 1) * kPwK);
+            const _Float16* A0 = As + 2 * buf * AS;
+            const _Float16* B0 = Bs + 2 * buf * BS;
+            H8 ah[4], al[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int ar = wm * 64 + t * 16 + (lane & 15);
+                ah[t] = *reinterpret_cast<const H8*>(&A0[pw_swz(ar, kc)]);
+                al[t] = *reinterpret_cast<const H8*>(&A0[AS + pw_swz(ar, kc)]);
+            }
+#pragma unroll
+            for (int nj = 0; nj < 4; ++nj) {
+                const int br = wn * 64 + nj * 16 + (lane & 15);
+                const H8 bh = *reinterpret_cast<const H8*>(&B0[pw_swz(br, kc)]);
+                const H8 bl = *reinterpret_cast<const H8*>(&B0[BS + pw_swz(br, kc)]);
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) {
+                    // cost_big16_kernel's order: hi.lo, lo.hi, then hi.hi into the same block
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, al[mi], acc[mi][nj], 0, 0, 0);
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, ah[mi], acc[mi][nj], 0, 0, 0);
+                    acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, ah[mi], acc[mi][nj], 0, 0, 0);
+                }
+            }
+            if (kt + 1 < nk) ls(buf ^ 1);
+            __syncthreads();
+        }
+        // epilogue (cost_big16's): lane holds cost row rr + 16 mi at half columns cc + 16 nj + e
+        const int cc = wn * 64 + 4 * (lane >> 4);
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj) {
+            const int cl = HC * h + cc + nj * 16;
+            const F4 ys4 = *reinterpret_cast<const F4*>(q.ys + col0 + cl);
+            const F4 yy4 = *reinterpret_cast<const F4*>(q.yy + col0 + cl);
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int rl = rr + mi * 16;
+                const float a = -2.f * q.xs[row0 + rl], b = q.xx[row0 + rl];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float c = fmaf(acc[mi][nj][e], a * ys4[e], b + yy4[e]);
+                    c = fmaxf(c, 0.f);
+                    if (q.euclid) c = sqrtf(c);
+                    acc[mi][nj][e] = c;
+                    lmax = fmaxf(lmax, c);
+                }
+                *reinterpret_cast<F4*>(&st[rl * kPwRS + cc + 16 * nj]) = acc[mi][nj];
+            }
+        }
+        __syncthreads();
+        // to the K layout: wave w's 16 rows, four columns 4 lane + 256 h a lane
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const F4 v = *reinterpret_cast<const F4*>(&st[(16 * w + r) * kPwRS + 4 * lane]);
+            kv[r][h][0] = F2{v[0], v[1]};
+            kv[r][h][1] = F2{v[2], v[3]};
+        }
+        __syncthreads();  // the staging area is the next half's operand buffers
+    }
+    // the grid's max (costs >= 0: the bit patterns order like the values)
+    lmax = wave_max(lmax);
+    if (lane == 0) s_wmx[w] = lmax;
+    __syncthreads();
+    if (tid == 0) {
+        float mx = s_wmx[0];
+        for (int ww = 1; ww < kMeshNW; ++ww) mx = fmaxf(mx, s_wmx[ww]);
+        __hip_atomic_fetch_max(reinterpret_cast<unsigned int*>(p.xreg + kMeshMaxWord), __float_as_uint(mx),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // blockIdx roles (no registration barrier ran): the launch's first device-wide wait gives
+    // up as a registration give-up (abandon = info->stalled), so the relay fallback solves
+    if (!grid_barrier(p.xreg + kMeshMaxBar, target, deadline, p.timeout_ticks, s_flag, abandon)) return false;
+    const float cmax = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned int*>(p.xreg + kMeshMaxWord),
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (lead && q.cmax_out) *q.cmax_out = cmax;
+    // the two-call path's K: ks = -unit / reg / cost_scale in float64, then float32
+    const double cinv = q.scale ? 1.0 / (double)cmax : 1.0;
+    const float ks = (float)(-exp_unit<float>() / p.reg * cinv);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh)
+                kv[r][g][hh] = F2{fast_exp(kv[r][g][hh][0] * ks), fast_exp(kv[r][g][hh][1] * ks)};
+    return true;
+}
+
 // KQ: reducer loads per lane, ceil(nrb * CPR / 64): 4 when nrb is a power of two
 // (nrb * CPR = 256), up to 8 otherwise.
 // SNRB, SNCB: the shape compiled in (0 = read from the arguments).  A compiled-in shape
@@ -141,8 +319,11 @@ constexpr int pow2_at_least(int x) { return x <= 1 ? 1 : 2 * pow2_at_least((x + 
 // spills (v_readlane / v_writelane per branch) lengthened every phase of the generic form.
 // SH: the shifted POT kernel K~ = 2^(C ks + A_i + B_j) (otf_persist.h ShiftArgs), formed
 // once in the prologue like K; the loop is unchanged.
-template <typename CT, typename TP, int KQ, int SNRB, int SNCB, bool SH, bool XR = false>
+// PW: the cost tile is built in the prologue from the split-fp16 images (p.pw) instead of read
+// from C (pw_cost_tile32 above).
+template <typename CT, typename TP, int KQ, int SNRB, int SNCB, bool SH, bool XR = false, bool PW = false>
 __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
+    static_assert(!(PW && (SH || XR)), "pairwise form: the plain single-rank POT kernel");
     using T = float;
     constexpr int G = 2, VEC = 4, R = kMeshRW, NW = kMeshNW, TR = kMeshTR, TC = kMeshTC;
     using V = Vec<float>::type;
@@ -164,6 +345,10 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     __shared__ int red_f[RW][kWave];  // and their producer flags
     __shared__ F2 red_sp[kWave];      // previous sums S[k - 1] of the reducer's lanes
     __shared__ int red_cnt;           // reducer-wave ticket of this epoch
+    // PW: the prologue's operand stages, then the cost tile's re-layout (kPwLds bytes)
+    __shared__ __attribute__((aligned(16))) unsigned char pwb[PW ? kPwLds : 16];
+    __shared__ float pw_wmx[kMeshNW];
+    __shared__ int pw_flag;
     int tid = threadIdx.x, lane = tid & 63;
     const int w = (int)threadIdx.x >> 6;
     unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + p.reg_ticks;
@@ -257,7 +442,18 @@ __global__ __launch_bounds__(512) void sk_mesh_kernel(SkMeshArgs p) {
     // ---- K for this wave's 16 rows x this lane's 8 columns, once (0 outside C), as
     // pairs of adjacent columns: the row and column partials run on v_pk_fma_f32
     F2 kv[R][G][2];
-    {
+    if constexpr (PW) {
+        if (!pw_cost_tile32<R, G>(p, kv, pwb, rb, cb, nrb * ncb, lead, deadline, &pw_flag, pw_wmx,
+                                  xl ? nullptr : &p.info->stalled)) {
+            // the max barrier stalled: a mid-solve stall (OTF_SK_TIMEOUT; kept at the registration
+            // give-up when the barrier gave up as one), every workgroup leaves
+            if (tid == 0) {
+                mark_stalled(&p.info->stalled, kStallMid);
+                if (lead) p.info->status = OTF_SK_TIMEOUT;
+            }
+            return;
+        }
+    } else {
         int colc[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -866,6 +1062,14 @@ const void* mesh_kernel_for(const SkMeshArgs& p) {
            : pow2 ? (const void*)sk_mesh_kernel<CT, TP, 4, 0, 0, SH>
                   : (const void*)sk_mesh_kernel<CT, TP, 8, 0, 0, SH>;
 }
+// the pairwise instances (whole tiles, float32 cost built in the prologue)
+template <typename TP>
+const void* pw_mesh_kernel_for(const SkMeshArgs& p) {
+    const bool pow2 = (p.nrb & (p.nrb - 1)) == 0;
+    return (p.nrb == 32 && p.ncb == 8) ? (const void*)sk_mesh_kernel<float, TP, 4, 32, 8, false, false, true>
+           : pow2 ? (const void*)sk_mesh_kernel<float, TP, 4, 0, 0, false, false, true>
+                  : (const void*)sk_mesh_kernel<float, TP, 8, 0, 0, false, false, true>;
+}
 // the cross-rank instances (the generic shape, no shifted kernel)
 template <typename CT, typename TP>
 const void* xmesh_kernel_for(const SkMeshArgs& p) {
@@ -877,7 +1081,8 @@ const void* xmesh_kernel_for(const SkMeshArgs& p) {
 template <typename CT, typename TP>
 hipError_t launch_mesh_t(int grid, SkMeshArgs& p, hipStream_t s) {
     void* args[] = {&p};
-    const void* k = p.xworld > 1 ? xmesh_kernel_for<CT, TP>(p)
+    const void* k = p.pw.Xh      ? pw_mesh_kernel_for<TP>(p)
+                    : p.xworld > 1 ? xmesh_kernel_for<CT, TP>(p)
                     : p.sh.A     ? mesh_kernel_for<CT, TP, true>(p)
                                  : mesh_kernel_for<CT, TP, false>(p);
     int per_cu = 0;
@@ -887,7 +1092,8 @@ hipError_t launch_mesh_t(int grid, SkMeshArgs& p, hipStream_t s) {
     return hipLaunchKernel(k, dim3(grid), dim3(512), args, 0, s);
 }
 
-constexpr size_t kMeshRegBytes = 9 * 256;  // 8 XCC counters + the barrier word, 256 B each
+// 8 XCC counters, the registration barrier, the PW max barrier and the PW max, 256 B each
+constexpr size_t kMeshRegBytes = 11 * 256;
 inline int64_t align_up_mesh(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 struct MeshShape {
@@ -920,6 +1126,11 @@ bool mesh_supported(int64_t n, int64_t m) {
            (int64_t)s.nrb * s.ncb <= 1024;
 }
 
+bool mesh_pairwise_ok(int64_t n, int64_t m, int64_t d) {
+    return mesh_supported(n, m) && n % kMeshTR == 0 && m % kMeshTC == 0 && m / kMeshTC <= kMeshXccNcb &&
+           d >= 1 && d <= (1 << 16);
+}
+
 size_t mesh_region_bytes(int64_t n, int64_t m) {
     if (!mesh_supported(n, m)) return 0;
     const MeshShape s = mesh_shape(n, m);
@@ -931,8 +1142,11 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                     double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* shift,
-                    const XSweep* xs) {
+                    const XSweep* xs, const PairwiseF32* pw) {
     if (!mesh_supported(n, m) || !region) return hipErrorInvalidValue;
+    if (pw && (shift || (xs && xs->world > 1) || n % kMeshTR != 0 || m % kMeshTC != 0 || pw->kpad % kPwK != 0 ||
+               pw->ldh % 8 != 0))
+        return hipErrorInvalidValue;
     const bool xr = xs && xs->world > 1;
     if (xr && (shift || xs->world > kXMaxRanks || m % kMeshTC != 0)) return hipErrorInvalidValue;
     const MeshShape sh = mesh_shape(n, m);
@@ -984,6 +1198,11 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
     p.timeout_ticks = stall_ticks();
     p.reg_ticks = reg_stall_ticks();
     if (shift) p.sh = *shift;
+    if (pw) {
+        p.pw = *pw;
+        p.C = nullptr;
+        p.cost_scale = nullptr;  // the max is applied when K is formed
+    }
     if (!zeroed) {  // else the Sinkhorn init kernel zeroed it
         const hipError_t e = hipMemsetAsync(region, 0, mesh_region_bytes(n, m), s);
         if (e != hipSuccess) return e;
@@ -1000,10 +1219,10 @@ hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, 
 template hipError_t run_mesh<float>(const float*, int64_t, int, int, const float*, const float*,
                                     const float*, const otf_sinkhorn_opts&, void*, float*, float*,
                                     void*, int64_t, int, otf_sinkhorn_info*, double*, bool,
-                                    hipStream_t, const ShiftArgs*, const XSweep*);
+                                    hipStream_t, const ShiftArgs*, const XSweep*, const PairwiseF32*);
 template hipError_t run_mesh<_Float16>(const _Float16*, int64_t, int, int, const float*, const float*,
                                        const float*, const otf_sinkhorn_opts&, void*, float*, float*,
                                        void*, int64_t, int, otf_sinkhorn_info*, double*, bool,
-                                       hipStream_t, const ShiftArgs*, const XSweep*);
+                                       hipStream_t, const ShiftArgs*, const XSweep*, const PairwiseF32*);
 
 }  // namespace otf

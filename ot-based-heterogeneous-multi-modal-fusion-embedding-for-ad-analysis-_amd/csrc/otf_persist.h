@@ -366,11 +366,42 @@ hipError_t run_mesh64(const double* C, int64_t ldc, int n, int m, const double* 
                       const double* cost_scale, const otf_sinkhorn_opts& o, void* region, double* u_out,
                       double* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                       double* errlog, bool zeroed, hipStream_t s, const PairwiseF64* pw = nullptr);
+// The pairwise form of the float32 mesh (otf_sinkhorn_pairwise_f32): every workgroup builds its
+// 128 x 512 cost tile in the prologue on v_mfma_f32_16x16x32_f16 from the split-fp16 images of
+// the float32 rows (hi / lo, power-of-two row scales: split16_prep2_kernel's), in
+// cost_big16_kernel's per-block MFMA order and epilogue, so C -- and the whole solve -- is
+// bitwise the two-call path's; the grid agrees on max(C) (scale) before K = exp(-C / (reg max)).
+struct PairwiseF32 {
+    const _Float16* Xh;  // n x ldh hi / lo images of X, m x ldh of Y (ldh = d rounded up to 64)
+    const _Float16* Xl;
+    const _Float16* Yh;
+    const _Float16* Yl;
+    int64_t ldh;
+    const float* xs;  // inverse row scales and squared norms of X (n) and Y (m)
+    const float* xx;
+    const float* ys;
+    const float* yy;
+    int kpad, euclid, scale;
+    float* cmax_out;  // the cost's max (device, nullable)
+    uint32_t xbytes, ybytes;  // image bytes (buffer bounds)
+};
+// whole 128 x 512 tiles the float32 mesh takes (n % 128 == 0, m % 512 == 0)
+bool mesh_pairwise_ok(int64_t n, int64_t m, int64_t d);
 template <typename CT>
 hipError_t run_mesh(const CT* C, int64_t ldc, int n, int m, const float* a_pad, const float* b_pad,
                     const float* cost_scale, const otf_sinkhorn_opts& o, void* region, float* u_out,
                     float* v_out, void* P_out, int64_t ldp, int P_dtype, otf_sinkhorn_info* info,
                     double* errlog, bool zeroed, hipStream_t s, const ShiftArgs* sh = nullptr,
-                    const XSweep* xs = nullptr);
+                    const XSweep* xs = nullptr, const PairwiseF32* pw = nullptr);
+// Split-fp16 images of two float32 operands (otf_cost.hip, split16_prep2_kernel) carved from
+// `ws` (otf_cost_ex_workspace_size(n, m, d, OTF_F32) bytes), for the fused float32 pairwise
+// solve; cmax_word (nullable) is zeroed by the same launch.
+struct Split16Images {
+    _Float16 *Xh, *Xl, *Yh, *Yl;
+    float *xs, *xx, *ys, *yy;
+    int64_t ldh;
+};
+hipError_t split16_images(const float* X, int64_t ldx, int n, const float* Y, int64_t ldy, int m, int d,
+                          void* ws, Split16Images& out, unsigned int* cmax_word, hipStream_t s);
 
 }  // namespace otf

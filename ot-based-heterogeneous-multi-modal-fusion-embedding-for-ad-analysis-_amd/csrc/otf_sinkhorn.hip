@@ -729,14 +729,16 @@ template <typename T> struct SoloArgs {
     int* relay;         // the relay counters (kRelayInts)
     int vg;             // pieces per pass / reset / output phase
     unsigned long long stall;  // no progress for this long at a wait: OTF_SK_TIMEOUT
-    // behind the pairwise float64 mesh (otf_sinkhorn_pairwise_f64): the float32 rows, their
-    // squared norms (the norms launch wrote them) and where the cost's max goes
+    // behind the pairwise meshes (otf_sinkhorn_pairwise_f64 / _f32): the float32 rows, their
+    // squared norms (the norms / prep launch wrote them) and where the cost's max goes
     const float* pw_X;
     const float* pw_Y;
     int64_t pw_ldx, pw_ldy;
     int pw_d, pw_euclid, pw_scale, pw_vec;
-    const double* pw_nx;  // n + m squared norms (X's, then Y's)
-    double* pw_cmax_out;
+    const double* pw_nx;   // float64 pairwise: n + m squared norms (X's, then Y's)
+    const float* pw_nxf;   // float32 pairwise (pw_nx null): X's n and Y's m squared norms
+    const float* pw_nyf;
+    T* pw_cmax_out;
     int pw_tiles_m, pw_ntiles;
 };
 
@@ -746,7 +748,7 @@ template <typename T> struct SoloArgs {
 // the float32 rows widened into a double-buffered LDS stage.  Returns the tile's max (thread 0).
 constexpr int RL_T = 128, RL_K = 16;
 template <typename T>
-__device__ double relay_cost_tile(const SoloArgs<T>& x, double* C, int64_t ldc, int n, int m, int tile) {
+__device__ double relay_cost_tile(const SoloArgs<T>& x, T* C, int64_t ldc, int n, int m, int tile) {
     using D4 = __attribute__((ext_vector_type(4))) double;
     __shared__ __attribute__((aligned(16))) double As[2][RL_K][RL_T];
     __shared__ __attribute__((aligned(16))) double Bs[2][RL_K][RL_T];
@@ -828,7 +830,7 @@ __device__ double relay_cost_tile(const SoloArgs<T>& x, double* C, int64_t ldc, 
         for (int b = 0; b < 4; ++b) {
             const int j = j0 + wn * 64 + b * 16 + li;
             const bool jok = j < m;
-            const double ry = jok ? x.pw_nx[n + j] : 0.0;
+            const double ry = !jok ? 0.0 : x.pw_nx ? x.pw_nx[n + j] : (double)x.pw_nyf[j];
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -836,12 +838,13 @@ __device__ double relay_cost_tile(const SoloArgs<T>& x, double* C, int64_t ldc, 
                     const int i = i0 + wm * 64 + a * 16 + lk + 4 * r;
                     if (i >= n || !jok) continue;
                     double v = -2.0 * acc[a][b][r];
-                    v += x.pw_nx[i];
+                    v += x.pw_nx ? x.pw_nx[i] : (double)x.pw_nxf[i];
                     v += ry;
                     v = v > 0 ? v : 0.0;
                     if (x.pw_euclid) v = sqrt(v);
-                    C[(int64_t)i * ldc + j] = v;
-                    mx = fmax(mx, v);
+                    const T vt = (T)v;  // float32 pairwise: the float cost, its max as stored
+                    C[(int64_t)i * ldc + j] = vt;
+                    mx = fmax(mx, (double)vt);
                 }
         }
     }
@@ -855,7 +858,7 @@ __device__ double relay_cost_tile(const SoloArgs<T>& x, double* C, int64_t ldc, 
 
 template <typename T, typename CT, int G, int R, bool SH, bool PW>
 __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> x) {
-    static_assert(!PW || (sizeof(T) == 8 && std::is_same<CT, double>::value), "pairwise: float64");
+    static_assert(!PW || std::is_same<CT, T>::value, "pairwise: the cost (then K) in the solve's type");
     __shared__ int s_t[2];
     const int tid = threadIdx.x, NT = blockDim.x;
     // only a grid that never became co-resident (registration give-up) is re-solved here;
@@ -944,7 +947,7 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
             }
         } else if (t < s_k) {
             if constexpr (PW) {
-                const double mx = relay_cost_tile<T>(x, (double*)p.C, p.ldc, p.n, p.m, t - s_cost);
+                const double mx = relay_cost_tile<T>(x, (T*)p.C, p.ldc, p.n, p.m, t - s_cost);
                 if (tid == 0)
                     __hip_atomic_fetch_max(reinterpret_cast<unsigned long long*>(ctr + kRelayMax),
                                            __builtin_bit_cast(unsigned long long, mx), __ATOMIC_RELAXED,
@@ -958,15 +961,15 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
                     double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(ctr + kRelayMax),
                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 const int q = t - s_k;
-                if (q == 0 && tid == 0 && x.pw_cmax_out) *x.pw_cmax_out = cmax;
-                const double ks = -1.0 / p.reg * (x.pw_scale ? 1.0 / cmax : 1.0);
-                using D2 = __attribute__((ext_vector_type(2))) double;
-                double* C = (double*)p.C;
+                if (q == 0 && tid == 0 && x.pw_cmax_out) *x.pw_cmax_out = (T)cmax;
+                // the engines' K: float64 exp, or the float32 engines' fast_exp with log2(e) folded in
+                const T ks = (T)(-exp_unit<T>() / p.reg * (x.pw_scale ? 1.0 / cmax : 1.0));
+                T* C = (T*)p.C;
                 for (int row = q; row < p.n; row += VG) {
-                    D2* cr = reinterpret_cast<D2*>(C + (int64_t)row * p.ldc);
-                    for (int j = tid; j < p.m / 2; j += NT) {
-                        const D2 c = cr[j];
-                        cr[j] = D2{exp(c[0] * ks), exp(c[1] * ks)};
+                    T* cr = C + (int64_t)row * p.ldc;
+                    for (int j = tid; j < p.m; j += NT) {
+                        if constexpr (sizeof(T) == 8) cr[j] = exp(cr[j] * ks);
+                        else cr[j] = fast_exp(cr[j] * ks);
                     }
                 }
             }
@@ -2357,7 +2360,7 @@ hipError_t launch_solo(const SkSetup<T>& su, const CT* C, int64_t ldc, int64_t n
     x.vg = (int)vg;
     const int grid = (int)vg;
     const PassCfg& c = su.cfg;
-    if constexpr (sizeof(T) == 8 && std::is_same<CT, double>::value) {
+    if constexpr (std::is_same<CT, T>::value) {
         if (pw) {
             p.cost_scale = nullptr;  // the relay's passes run on K (max applied when K is formed)
             switch (c.G) {
@@ -3067,6 +3070,118 @@ int otf_sinkhorn_pairwise_f64(const float* X, int64_t ldx, const float* Y, int64
     otf_sinkhorn_opts o2 = o;
     if (o2.engine == OTF_ENGINE_MESH && !mesh64_supported(n, m)) o2.engine = OTF_ENGINE_AUTO;
     return otf_sinkhorn(a, b, Cw, n, m, m, OTF_F64, scale_max ? cmax : nullptr, &o2, u_out, v_out, P_out, ldp,
+                        P_dtype, info, errlog, ws_sk, L.sk, stream);
+}
+
+// ---------------------------------------------------------------------------------------
+// Pairwise cost + Sinkhorn, float32 (include/otfuse.h).  Workspace: [the float32 Sinkhorn
+// workspace][the n x m float32 cost (the unfused path and the fallback)][the split-fp16 cost
+// workspace (images, row scales, norms)][the max].
+namespace otf {
+namespace {
+PwLayout pw32_layout(int64_t n, int64_t m, int64_t d, int32_t max_iter) {
+    PwLayout l;
+    l.sk = (otf_sinkhorn_workspace_size(n, m, OTF_F32, max_iter) + 255) / 256 * 256;
+    l.c = ((size_t)n * (size_t)m * 4 + 255) / 256 * 256;
+    l.cost = (otf_cost_ex_workspace_size(n, m, d, OTF_F32) + 255) / 256 * 256;
+    l.total = l.sk + l.c + l.cost + 256;
+    return l;
+}
+}  // namespace
+}  // namespace otf
+
+size_t otf_sinkhorn_pairwise_f32_workspace_size(int64_t n, int64_t m, int64_t d, int32_t max_iter) {
+    if (n <= 0 || m <= 0 || d <= 0) return 0;
+    return otf::pw32_layout(n, m, d, max_iter).total;
+}
+
+int otf_sinkhorn_pairwise_f32(const float* X, int64_t ldx, const float* Y, int64_t ldy, int64_t n, int64_t m,
+                              int64_t d, int32_t metric, int32_t scale_max, const float* a, const float* b,
+                              const otf_sinkhorn_opts* opts, float* u_out, float* v_out, void* P_out,
+                              int64_t ldp, int32_t P_dtype, float* cmax_out, otf_sinkhorn_info* info,
+                              double* errlog, void* workspace, size_t ws_bytes, otf_stream_t stream) {
+    using namespace otf;
+    if (!opts || !X || !Y || !workspace || n <= 0 || m <= 0 || d <= 0) return OTF_EINVAL;
+    if (ldx < d || ldy < d) return OTF_EINVAL;
+    if (metric != OTF_SQEUCLIDEAN && metric != OTF_EUCLIDEAN) return OTF_EINVAL;
+    if (P_out && P_dtype != OTF_F32 && P_dtype != OTF_F64) return OTF_EINVAL;
+    if (opts->flavor != OTF_FLAVOR_POT) return OTF_EUNSUPPORTED;
+    if (n > INT32_MAX || m > INT32_MAX || d > (1 << 20)) return OTF_EUNSUPPORTED;
+    const otf_sinkhorn_opts& o = *opts;
+    const PwLayout L = pw32_layout(n, m, d, o.max_iter);
+    if (ws_bytes < L.total) return OTF_EINVAL;
+    if (!u_out || !v_out) return OTF_EINVAL;
+    if (P_out && (ldp < m || ldp % 4 != 0 || ((uintptr_t)P_out % 16) != 0)) return OTF_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    char* base = (char*)workspace;
+    void* ws_sk = base;
+    float* Cw = (float*)(base + L.sk);
+    char* ws_cost = base + L.sk + L.c;
+    float* cmax = (float*)(base + L.sk + L.c + L.cost);
+    const bool whole = o.n_total <= 0 || o.n_total == n;
+    // the fused launch on request (engine MESH) only: at the metric shape it measured 0.529 ms
+    // against 0.495 ms for the two calls (its in-prologue cost build runs at ~1/4 of the fp16
+    // MFMA peak, one register stage of prefetch against the L2 latency, so the 67-MB round trip
+    // it saves does not pay), so AUTO keeps the two calls
+    const bool engine_ok = o.engine == OTF_ENGINE_MESH;
+    bool fused = whole && !o.shift && o.max_iter >= 1 && engine_ok && mesh_pairwise_ok(n, m, d) &&
+                 (size_t)n * (size_t)((d + 63) / 64 * 64) * 2 < ((size_t)1 << 31) &&
+                 (size_t)m * (size_t)((d + 63) / 64 * 64) * 2 < ((size_t)1 << 31);
+    if (fused) {
+        SkSetup<float> su;
+        int rc = sk_prepare<float, float>(a, b, Cw, n, m, m, o, info, ws_sk, L.sk, su);
+        if (rc != OTF_OK) return rc;
+        if (su.w.mesh_bytes == 0) fused = false;
+        if (fused) {
+            double* errl = errlog ? errlog : su.w.errlog;
+            rc = sk_init<float>(su, a, b, n, m, info, s, su.w.mesh, su.w.mesh_bytes);
+            if (rc != OTF_OK) return rc;
+            Split16Images im{};
+            OTF_HIP(split16_images(X, ldx, (int)n, Y, ldy, (int)m, (int)d, ws_cost, im, nullptr, s));
+            PairwiseF32 pw{im.Xh, im.Xl, im.Yh, im.Yl, im.ldh, im.xs, im.xx, im.ys, im.yy, (int)im.ldh,
+                           metric == OTF_EUCLIDEAN ? 1 : 0, scale_max ? 1 : 0, cmax_out,
+                           (uint32_t)(n * im.ldh * 2), (uint32_t)(m * im.ldh * 2)};
+            hipError_t e;
+            if (force_giveup()) {
+                // test path (OTF_FORCE_REG_GIVEUP=1): the fallback at the caller's full shape
+                sk_giveup_kernel<<<1, 64, 0, s>>>(info);
+                e = hipGetLastError();
+            } else {
+                e = run_mesh<float>(nullptr, m, (int)n, (int)m, (const float*)su.w.a_pad, (const float*)su.w.b_pad,
+                                    nullptr, o, su.w.mesh, u_out, v_out, P_out, ldp, P_dtype, info, errl,
+                                    /*zeroed=*/true, s, nullptr, nullptr, &pw);
+            }
+            if (e == hipSuccess) {
+                // the fallback (only after a registration give-up): the relay builds the float32
+                // cost into the workspace on the float64 matrix cores (from the prep's norms), K
+                // over it, then solves
+                SoloArgs<float> fb{};
+                fb.pw_X = X;
+                fb.pw_Y = Y;
+                fb.pw_ldx = ldx;
+                fb.pw_ldy = ldy;
+                fb.pw_d = (int)d;
+                fb.pw_euclid = metric == OTF_EUCLIDEAN ? 1 : 0;
+                fb.pw_scale = scale_max ? 1 : 0;
+                fb.pw_vec = (ldx % 4 == 0) && (ldy % 4 == 0) && ((uintptr_t)X % 16 == 0) && ((uintptr_t)Y % 16 == 0);
+                fb.pw_cmax_out = cmax_out;
+                fb.pw_nxf = im.xx;
+                fb.pw_nyf = im.yy;
+                fb.pw_tiles_m = (int)((n + RL_T - 1) / RL_T);
+                fb.pw_ntiles = fb.pw_tiles_m * (int)((m + RL_T - 1) / RL_T);
+                return check_hip(launch_solo<float, float>(su, Cw, m, n, m, nullptr, o, u_out, v_out, P_out, ldp,
+                                                           P_dtype, info, errl, s, &fb));
+            }
+            (void)hipGetLastError();
+            if (o.engine == OTF_ENGINE_MESH) return check_hip(e);
+        }
+    }
+    // the cost, then the solve on it (the split-fp16 cost kernel: the same costs)
+    int rc = otf_cost_pairwise_ex(X, ldx, Y, ldy, OTF_F32, n, m, d, metric, 0, Cw, m, OTF_F32, cmax, nullptr, ws_cost,
+                                  L.cost, stream);
+    if (rc != OTF_OK) return rc;
+    if (cmax_out) OTF_HIP(hipMemcpyAsync(cmax_out, cmax, 4, hipMemcpyDeviceToDevice, s));
+    return otf_sinkhorn(a, b, Cw, n, m, m, OTF_F32, scale_max ? cmax : nullptr, &o, u_out, v_out, P_out, ldp,
                         P_dtype, info, errlog, ws_sk, L.sk, stream);
 }
 

@@ -155,6 +155,10 @@ _SIGS = {
     "otf_sinkhorn_pairwise_f64": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _vp,
                                                  ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _i64, _i32, _vp,
                                                  _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "otf_sinkhorn_pairwise_f32_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i32]),
+    "otf_sinkhorn_pairwise_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _vp,
+                                                 ctypes.POINTER(SinkhornOpts), _vp, _vp, _vp, _i64, _i32, _vp,
+                                                 _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "otf_emd_max_nodes": (ctypes.c_int, []),
     "otf_emd_lds_nodes": (ctypes.c_int, []),
     "otf_emd_solve": (ctypes.c_int, [_i32, ctypes.POINTER(EmdProblem), _i64, _vp, _vp]),

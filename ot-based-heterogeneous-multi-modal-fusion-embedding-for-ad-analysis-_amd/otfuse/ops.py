@@ -477,17 +477,23 @@ def sinkhorn(a: torch.Tensor, b: torch.Tensor, C: torch.Tensor, reg: float, max_
                           shift_a=sa, shift_b=sb)
 
 
-def sinkhorn_pairwise_workspace(n: int, m: int, max_iter: int, device) -> torch.Tensor:
-    wsb = L.lib().otf_sinkhorn_pairwise_f64_workspace_size(n, m, max_iter)
+def sinkhorn_pairwise_workspace(n: int, m: int, max_iter: int, device, d: int | None = None,
+                                precision: str = "fp64") -> torch.Tensor:
+    if precision == "fp32":
+        if d is None:
+            raise ValueError("the float32 pairwise workspace depends on d")
+        wsb = L.lib().otf_sinkhorn_pairwise_f32_workspace_size(n, m, d, max_iter)
+    else:
+        wsb = L.lib().otf_sinkhorn_pairwise_f64_workspace_size(n, m, max_iter)
     return torch.empty(wsb, dtype=torch.uint8, device=device)
 
 
 def sinkhorn_pairwise(X: torch.Tensor, Y: torch.Tensor, reg: float, a: torch.Tensor | None = None,
                       b: torch.Tensor | None = None, metric: str = "sqeuclidean", scale_max: bool = True,
                       max_iter: int = 1000, stop_thr: float = 1e-9, check_every: int = 10,
-                      err_squared: bool = False, want_plan: bool = True, plan_dtype=torch.float64,
+                      err_squared: bool = False, want_plan: bool = True, plan_dtype=None,
                       workspace: torch.Tensor | None = None, plan_out: torch.Tensor | None = None,
-                      engine: str = "auto") -> SinkhornResult:
+                      engine: str = "auto", precision: str = "fp64") -> SinkhornResult:
     """The reference's cost + solve in float64, fused where the shape allows: POT's
     ``M = euclidean_distances(X, Y, squared=True); M /= M.max(); ot.sinkhorn(a, b, M, reg)``
     (MRI_PET_OT_nojax.py:70-75, :143) from float32 embeddings ``X`` (n, d), ``Y`` (m, d).
@@ -497,13 +503,28 @@ def sinkhorn_pairwise(X: torch.Tensor, Y: torch.Tensor, reg: float, a: torch.Ten
     builds its tile of the cost on the float64 matrix cores in its prologue (no n x m cost
     in HBM, otf_sinkhorn_pairwise_f64); other shapes run the cost and the solve as two
     calls.  ``a``/``b`` default to the uniform marginals.  The result's ``cost_max`` holds
-    max(M) before the scaling (a device scalar)."""
+    max(M) before the scaling (a device scalar).
+
+    ``precision="fp32"``: the same segment in float32 compute (otf_sinkhorn_pairwise_f32): the
+    split-fp16 cost (``pairwise_cost``'s) and the float32 POT engines, within 1e-4 of the
+    float64 plan; with ``engine="mesh"`` and the float32 mesh's whole-tile shapes (n a multiple
+    of 128, m a multiple of 512 up to 4096) the cost tiles are built in the solve's prologue,
+    bitwise the two calls' results (AUTO runs the two calls: measured faster).  Where ``sinkhorn`` would take the shifted kernel (reg < 1/64 with
+    ``scale_max``; and without ``scale_max``) the two calls run.  ``plan_dtype`` defaults to
+    the compute precision (float64 / float32)."""
     _dev(X, "X")
     _dev(Y, "Y")
     if metric not in ("sqeuclidean", "euclidean"):
         raise ValueError(f"metric {metric!r} not supported (sqeuclidean | euclidean)")
     if X.dim() != 2 or Y.dim() != 2 or X.shape[1] != Y.shape[1]:
         raise ValueError(f"X {tuple(X.shape)} and Y {tuple(Y.shape)} must be (n, d) and (m, d)")
+    if precision not in ("fp64", "fp32"):
+        raise ValueError(f"precision {precision!r} (fp64 | fp32)")
+    if precision == "fp32":
+        return _sinkhorn_pairwise_f32(X, Y, reg, a, b, metric, scale_max, max_iter, stop_thr, check_every,
+                                      err_squared, want_plan, plan_dtype, workspace, plan_out, engine)
+    if plan_dtype is None:
+        plan_dtype = torch.float64
     X = X.float().contiguous()
     Y = Y.float().contiguous()
     n, d = X.shape
@@ -537,6 +558,54 @@ def sinkhorn_pairwise(X: torch.Tensor, Y: torch.Tensor, reg: float, a: torch.Ten
         info.data_ptr(), errlog.data_ptr(), workspace.data_ptr(), workspace.numel(),
         L.stream_handle(dev)), "otf_sinkhorn_pairwise_f64")
     return SinkhornResult(u=u, v=v, plan=P, info_dev=info, errlog_dev=errlog, flavor="pot", cost_max=cmax)
+
+
+def _sinkhorn_pairwise_f32(X, Y, reg, a, b, metric, scale_max, max_iter, stop_thr, check_every, err_squared,
+                           want_plan, plan_dtype, workspace, plan_out, engine) -> SinkhornResult:
+    """sinkhorn_pairwise(precision="fp32"): otf_sinkhorn_pairwise_f32, or -- where the float32
+    solve takes the shifted kernel -- pairwise_cost + sinkhorn (the same two calls)."""
+    X = _rowmajor(X.float(), 4)
+    Y = _rowmajor(Y.float(), 4)
+    n, d = X.shape
+    m = Y.shape[0]
+    dev = X.device
+    a = uniform(n, torch.float32, dev) if a is None else _dev(a, "a").float().contiguous()
+    b = uniform(m, torch.float32, dev) if b is None else _dev(b, "b").float().contiguous()
+    if a.numel() != n or b.numel() != m:
+        raise ValueError(f"a ({a.numel()}) / b ({b.numel()}) do not match ({n}, {m})")
+    pdt = torch.float32 if plan_dtype is None else plan_dtype
+    if not scale_max or 1.0 / float(reg) > SHIFT_RANGE:
+        # the shifted kernel (or, unscaled, the test for it) needs a pass over C: the two calls,
+        # sinkhorn deciding the shift as it does for any float32 cost
+        C, cmax = pairwise_cost(X, Y, metric, zero_diag=False)
+        return sinkhorn(a, b, C, reg, max_iter=max_iter, stop_thr=stop_thr, check_every=check_every,
+                        err_squared=err_squared, cost_scale=cmax if scale_max else None, want_plan=want_plan,
+                        plan_dtype=pdt, plan_out=plan_out, engine=engine)
+    u = torch.empty(n, dtype=torch.float32, device=dev)
+    v = torch.empty(m, dtype=torch.float32, device=dev)
+    cmax = torch.empty(1, dtype=torch.float32, device=dev)
+    info = torch.empty(L.INFO_INT32S, dtype=torch.int32, device=dev)
+    errlog = torch.empty(max_iter // max(check_every, 1) + 2, dtype=torch.float64, device=dev)
+    if workspace is None:
+        workspace = sinkhorn_pairwise_workspace(n, m, max_iter, dev, d=d, precision="fp32")
+    P = None
+    if want_plan:
+        P = plan_out if plan_out is not None else _alloc_rowmajor(n, m, pdt, dev, 4)
+        if P.dtype not in _DT or tuple(P.shape) != (n, m):
+            raise ValueError("plan_out must be (n, m) float32/float64")
+    opts = L.SinkhornOpts(reg=float(reg), stop_thr=float(stop_thr), max_iter=int(max_iter),
+                          check_every=int(check_every), flavor=L.OTF_FLAVOR_POT,
+                          err_squared=int(err_squared), sync_every=0, engine=L.ENGINES[engine],
+                          cost_f16=0, deterministic=0, shift=0)
+    met = L.OTF_EUCLIDEAN if metric == "euclidean" else L.OTF_SQEUCLIDEAN
+    L.check(L.lib().otf_sinkhorn_pairwise_f32(
+        X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0), n, m, d, met, int(bool(scale_max)),
+        a.data_ptr(), b.data_ptr(), ctypes.byref(opts), u.data_ptr(), v.data_ptr(), L.ptr(P),
+        P.stride(0) if P is not None else 0, _DT[P.dtype] if P is not None else 0, cmax.data_ptr(),
+        info.data_ptr(), errlog.data_ptr(), workspace.data_ptr(), workspace.numel(),
+        L.stream_handle(dev)), "otf_sinkhorn_pairwise_f32")
+    return SinkhornResult(u=u, v=v, plan=P, info_dev=info, errlog_dev=errlog, flavor="pot",
+                          cost_max=mark_cost_max(cmax))
 
 
 def sinkhorn_profile(a, b, C, reg, iters, cost_scale=None, flavor="pot", workspace=None) -> float:
