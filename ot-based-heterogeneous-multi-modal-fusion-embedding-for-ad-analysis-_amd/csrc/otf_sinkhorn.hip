@@ -145,8 +145,19 @@ __device__ __forceinline__ double marginal_err(const SkArgs<T>& p, const T* vit,
 // vb / vg: this workgroup's place in the pass (blockIdx.x / gridDim.x of a pass launch, a
 // piece of the relay fallback's ticket sequence otherwise).  KIN: the array holds K itself
 // (the relay fallback's K written once), no exp per element.
-template <typename T, typename CT, bool LOG, int G, int R, bool SH = false, bool KIN = false>
-__device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p, int vb, int vg) {
+// RELAY (a piece of sk_relay_kernel): `wait` is the piece's dependency wait (poll + acquire +
+// barrier, false on abort), run by the body after the first row block's loads are issued when
+// `early` (the array is K, complete and L1-fresh since this workgroup's last acquire, or the
+// caller's C: its rows stream during the wait; a second row block in flight measured as
+// 45-330 spilled VGPRs); scalings and the zeroed sums are stored write-through (sc1) so that
+// only the piece that writes the info words needs an agent release.
+struct NoWait {
+    __device__ bool operator()() const { return true; }
+};
+template <typename T, typename CT, bool LOG, int G, int R, bool SH = false, bool KIN = false, bool RELAY = false,
+          typename WaitFn = NoWait>
+__device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p, int vb, int vg, const WaitFn& wait = WaitFn{},
+                                             bool early = false) {
     static_assert(!(LOG && SH), "the shifted kernel is a POT-flavour form");
     static_assert(!(KIN && (LOG || SH)), "K input: the plain POT kernel only");
     constexpr int VEC = Vec<T>::N;
@@ -154,23 +165,13 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p, int vb, int vg)
     __shared__ __attribute__((aligned(16))) T colbuf[512 * G * VEC];  // column partials
     __shared__ __attribute__((aligned(16))) T tbuf[512 * R];          // row-sum transpose
     __shared__ T red[17 * R + 17];
-    __shared__ int s_flag;
     const int tid = threadIdx.x;
     const int NT = blockDim.x;
-
-    // stop flag: written by an earlier launch (a flag raised by WG0 of THIS launch is
-    // a decision every workgroup re-derives identically), so a uniform plain load.
-    if (__builtin_amdgcn_readfirstlane(*(volatile const int*)&p.info->stop)) return;
-    (void)s_flag;
-
-    const bool lead = (vb == 0 && tid == 0);
-    // exponent units: float works in log2 (v_exp_f32), double in natural log
-    const double unit = exp_unit<T>();
-    double cinv = 1.0;
-    if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
-    const T ks = (T)(-unit / p.reg * cinv);  // multiplies C
-    const T gl = (T)(unit / p.reg);          // potential -> exponent units (OTT)
-    const T regn = (T)(p.reg / unit);        // unit log -> potential
+    // write-through stores for the relay (see above)
+    auto wstore = [](T* dst, T v) {
+        if constexpr (RELAY) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *dst = v;
+    };
 
     // ---- per-thread column ownership; clamped addresses + masks (branch-free loads)
     int colc[G];
@@ -182,6 +183,44 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p, int vb, int vg)
 #pragma unroll
         for (int k = 0; k < VEC; ++k) cok[g][k] = c0 + k < p.m;
     }
+    const int nrb = (p.n + R - 1) / R;
+    auto load_block = [&](int rb, T (&dst)[R][G][VEC]) {
+        const int r0 = rb * R;
+        const CT* crow = (const CT*)p.C + (int64_t)r0 * p.ldc;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const CT* src = (r0 + r < p.n) ? crow : (const CT*)p.C;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const V c = load_cost<T>(src + colc[g]);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) dst[r][g][k] = c[k];
+            }
+            crow += p.ldc;
+        }
+    };
+    T kv[R][G][VEC];
+    bool kv_loaded = false;
+    if constexpr (RELAY) {
+        if (early && vb < nrb) {
+            load_block(vb, kv);
+            kv_loaded = true;
+        }
+        if (!wait()) return;
+    }
+
+    // stop flag: written by an earlier launch (a flag raised by WG0 of THIS launch is
+    // a decision every workgroup re-derives identically), so a uniform plain load.
+    if (__builtin_amdgcn_readfirstlane(*(volatile const int*)&p.info->stop)) return;
+
+    const bool lead = (vb == 0 && tid == 0);
+    // exponent units: float works in log2 (v_exp_f32), double in natural log
+    const double unit = exp_unit<T>();
+    double cinv = 1.0;
+    if (p.cost_scale) cinv = 1.0 / (double)p.cost_scale[0];
+    const T ks = (T)(-unit / p.reg * cinv);  // multiplies C
+    const T gl = (T)(unit / p.reg);          // potential -> exponent units (OTT)
+    const T regn = (T)(p.reg / unit);        // unit log -> potential
 
     // ---- decisions about iteration it-1 (identical in every workgroup)
     if (p.it >= 1) {
@@ -208,7 +247,6 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p, int vb, int vg)
     // column-scaling prologue (its loads, arithmetic and barrier), so the prologue's
     // latency hides under the stream instead of preceding it.
     const bool have_prev = p.it >= 0;
-    const int nrb = (p.n + R - 1) / R;
     T vw[G][VEC];  // POT: v_j (row-sum weights); OTT: 1
     T go[G][VEC];  // OTT: g_j in exponent units; POT: 0
     T colacc[G][VEC];
@@ -219,21 +257,8 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p, int vb, int vg)
 
     for (int rb = vb; rb < nrb || rb == vb; rb += vg) {
         const int r0 = rb * R;
-        T kv[R][G][VEC];
-        if (rb < nrb) {
-            const CT* crow = (const CT*)p.C + (int64_t)r0 * p.ldc;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const CT* src = (r0 + r < p.n) ? crow : (const CT*)p.C;
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const V c = load_cost<T>(src + colc[g]);
-#pragma unroll
-                    for (int k = 0; k < VEC; ++k) kv[r][g][k] = c[k];
-                }
-                crow += p.ldc;
-            }
-        }
+        if (rb < nrb && !kv_loaded) load_block(rb, kv);
+        kv_loaded = false;
         if (rb == vb) {
             // column scaling of iteration it (POT: v; OTT: g), every workgroup, all columns
             if (have_prev) {
@@ -343,7 +368,7 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p, int vb, int vg)
                     }
                 const int row = r0 + tid;
                 if (row < p.n) {
-                    p.u_cur[row] = mine;
+                    wstore(p.u_cur + row, mine);
                     if (!finite_val(mine) || !finite_val(wmine)) atomicAdd(p.cs_dst + p.m_pad, (T)1);
                 }
             }
@@ -380,8 +405,9 @@ __device__ __forceinline__ void sk_pass_body(const SkArgs<T>& p, int vb, int vg)
     for (int j = tid; j < p.m; j += NT) atomicAdd(p.cs_dst + j, colbuf[j]);
 
     // ---- zero the column-sum buffer of the next pass (nobody touches it now)
-    for (int j = vb * NT + tid; j <= p.m_pad; j += vg * NT) p.cs_zero[j] = 0;
+    for (int j = vb * NT + tid; j <= p.m_pad; j += vg * NT) wstore(p.cs_zero + j, (T)0);
 }
+
 template <typename T, typename CT, bool LOG, int G, int R, bool SH>
 __global__ __launch_bounds__(512) void sk_pass_kernel(SkArgs<T> p) {
     sk_pass_body<T, CT, LOG, G, R, SH>(p, (int)blockIdx.x, (int)gridDim.x);
@@ -706,11 +732,16 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const CT* C, int64_t ldc, 
 //   outputs  (vg pieces)      u, v of last_good and the plan rows of the piece
 // Once a pass has stopped the solve (info->stop), the workgroup that sees it first moves the
 // ticket counter past the remaining passes in one compare-and-swap and counts them done.
-// Hand-off: a piece's stores drain (vmcnt(0)), an agent-scope release fence makes them
-// visible device-wide before its completion count; the waiter's acquire fence drops stale
-// cache lines.  Every fallback bumps g_sk_fallbacks (otf_sinkhorn_fallback_count) and sets
-// info->fallback.  (r06: replaces the one-workgroup re-solve, whose pass loop on a single CU
-// took tens of ms at the metric shape.)
+// Hand-off: a piece's stores drain (vmcnt(0)) and its completion is counted after a barrier;
+// an agent-scope release fence precedes the count except in pass pieces after a pass's first
+// (those store only write-through words and memory-side atomics).  The waiter: one poll and
+// one agent acquire by thread 0, then a barrier.  A pass piece of a workgroup whose previous
+// piece was a pass piece puts its first K row block in flight BEFORE that wait (K is complete
+// and L1-fresh by then).  Measured at the float64 bench shape (tools/relay_probe.py): 62.6 ->
+// 39.5 us per pass, 7.0 -> 4.6 ms per call; ablations of the old form: 21 us of each pass was
+// the dependency wait, 14 the K loads, 8 the column atomics.  Every fallback bumps
+// g_sk_fallbacks (otf_sinkhorn_fallback_count) and sets info->fallback.  (r06: replaces the
+// one-workgroup re-solve, whose pass loop on a single CU took tens of ms at the metric shape.)
 // ============================================================================
 __device__ unsigned long long g_sk_fallbacks;
 
@@ -859,7 +890,7 @@ __device__ double relay_cost_tile(const SoloArgs<T>& x, T* C, int64_t ldc, int n
 template <typename T, typename CT, int G, int R, bool SH, bool PW>
 __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> x) {
     static_assert(!PW || std::is_same<CT, T>::value, "pairwise: the cost (then K) in the solve's type");
-    __shared__ int s_t[2];
+    __shared__ int s_t[3];
     const int tid = threadIdx.x, NT = blockDim.x;
     // only a grid that never became co-resident (registration give-up) is re-solved here;
     // a mid-solve stall stays an OTF_SK_TIMEOUT for the caller to see
@@ -896,6 +927,10 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
         q.v_prev = x.v2 + (size_t)((it - 1) & 1) * p.m_pad;
     };
     unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + x.stall;
+    // this workgroup's previous piece was a pass piece: it acquired after K was complete, so
+    // a pass piece may stream its first K rows before its own wait (the input C of a
+    // non-pairwise solve never changes in the launch)
+    bool prev_pass = false;
     for (;;) {
         if (tid == 0) {
             int t;
@@ -913,25 +948,47 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
                 t = __hip_atomic_fetch_add(ctr + kRelayTicket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
-            if (t < s_end) {
-                const int nd = need(t);
-                while (aload(ctr + kRelayDone) < nd) {
-                    if (aload(ctr + kRelayAbort)) { t = s_end; break; }
-                    __builtin_amdgcn_s_sleep(2);
-                    if (__builtin_amdgcn_s_memrealtime() > deadline) {
-                        __hip_atomic_store(ctr + kRelayAbort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        p.info->status = OTF_SK_TIMEOUT;
-                        t = s_end;
-                        break;
-                    }
-                }
-            }
             s_t[1] = t;
         }
         __syncthreads();
         const int t = s_t[1];
         if (t >= s_end) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // the ticket's dependency: one poll and one agent acquire by thread 0, then the
+        // barrier (false: the relay was aborted)
+        auto wait = [&]() -> bool {
+            if (tid == 0) {
+                int ok = 1;
+                const int nd = need(t);
+                while (aload(ctr + kRelayDone) < nd) {
+                    if (aload(ctr + kRelayAbort)) { ok = 0; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() > deadline) {
+                        __hip_atomic_store(ctr + kRelayAbort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        p.info->status = OTF_SK_TIMEOUT;
+                        ok = 0;
+                        break;
+                    }
+                }
+                if (ok) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                s_t[2] = ok;
+            }
+            __syncthreads();
+            return s_t[2] != 0;
+        };
+        const bool is_pass = t >= s_pass && t < s_fin;
+        if (is_pass) {
+            SkArgs<T> q = p;
+            set_pass(q, (t - s_pass) / VG);
+            sk_pass_body<T, CT, false, G, R, SH, PW, true>(q, (t - s_pass) % VG, VG, wait, PW ? prev_pass : true);
+            if (!s_t[2]) return;
+            prev_pass = true;
+        } else {
+            if (!wait()) return;
+            prev_pass = false;
+        }
         if (t < s_cost) {
             // reset: fresh state (the abandoned persistent solve may have written these)
             for (int64_t j = (int64_t)t * NT + tid; j < 3 * x.cs_stride; j += (int64_t)VG * NT) x.cs[j] = 0;
@@ -973,10 +1030,8 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
                     }
                 }
             }
-        } else if (t < s_fin) {
-            SkArgs<T> q = p;
-            set_pass(q, (t - s_pass) / VG);
-            sk_pass_body<T, CT, false, G, R, SH, PW>(q, (t - s_pass) % VG, VG);
+        } else if (is_pass) {
+            // (run above)
         } else if (t < s_out) {
             SkArgs<T> q = p;
             set_pass(q, x.max_iter + 1);
@@ -1019,11 +1074,17 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
             }
             if (q == VG - 1 && tid == 0) p.info->stalled = 0;
         }
-        // completion: this piece's stores drained and released device-wide, then counted
+        // completion: this piece's stores drained and released device-wide, then counted.  A
+        // pass piece other than the pass's first stores only write-through (sc1) words and
+        // memory-side atomics: its drained stores need no release (MI355X_MICROARCH.md,
+        // hand-off table); the first piece also writes v and the info words plainly.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (!is_pass || (t - s_pass) % VG == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             __hip_atomic_fetch_add(ctr + kRelayDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         deadline = __builtin_amdgcn_s_memrealtime() + x.stall;

@@ -292,7 +292,7 @@ def test_persistent_engine_beside_a_concurrent_persistent_grid(dev, monkeypatch,
     """A persistent solve launched together with a full-grid persistent solve on another
     stream (the r02 stall scenario: e.g. RCCL kernels holding CUs) cannot always become
     co-resident.  It must never hang, never return a silently wrong plan and -- with the
-    one-workgroup fallback queued behind every persistent launch -- never lose the
+    relay fallback queued behind every persistent launch -- never lose the
     answer: each solve ends max_iter with the reference plan, either from its engine or
     from the fallback (info fallback = 1, counted in otf_sinkhorn_fallback_count)."""
     from otfuse import _lib as L, ops
@@ -331,8 +331,8 @@ def test_solo_fallback_when_registration_cannot_complete(dev, monkeypatch, dt):
     """Force the fallback: a long gather solve (its XCC team holds 8 CUs for ~0.1 s) on
     one stream, then a mesh solve (a whole grid, one workgroup per CU) on another with a
     1-ms registration window: 8 of its workgroups cannot start, its registration gives
-    up, the late workgroups see the give-up word and leave, and the one-workgroup
-    fallback queued behind it returns the right plan (info fallback = 1)."""
+    up, the late workgroups see the give-up word and leave, and the relay fallback
+    queued behind it returns the right plan (info fallback = 1)."""
     from otfuse import ops
     monkeypatch.setenv("OTF_REG_MS", "1")
     g = torch.Generator(device=dev).manual_seed(3)

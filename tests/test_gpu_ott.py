@@ -57,7 +57,7 @@ def test_solve_ott_takes_the_resident_form_and_matches_oracle(orc, dev):
 
 
 def test_solve_ott_falls_back_to_log_passes_when_the_grid_is_not_co_resident(dev, monkeypatch):
-    """The scaling form has no one-workgroup fallback (that one is POT-flavour): a resident
+    """The scaling form has no relay fallback (that one is POT-flavour): a resident
     OTT grid that cannot register (8 CUs held by a long gather solve on another stream,
     1-ms registration window) ends in OTF_SK_TIMEOUT, and solve_ott re-solves with the
     log-domain passes -- the same plan as an uncontended solve."""
