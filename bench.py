@@ -580,6 +580,8 @@ def metric_f32_leg(dev, X, Y, N, d, iters, eps, engine, pmc_traffic, steps=20, w
     kern_ms = sorted(k for _, k in ph)[2]
     info = res.info()
     eng = info["engine_name"]
+    # the 256 x 256 cost kernel the library ran (OTF_COST_8PH=0: the register-staged one)
+    cname = "cost_big16_kernel" if os.environ.get("OTF_COST_8PH") == "0" else "cost_8ph_kernel"
     kname = {"mesh": "sk_mesh_kernel", "tiled": "sk_tiled_kernel", "sweep": "sk_sweep_kernel",
              "resident": "sk_resident_kernel", "gather": "sk_gather_kernel"}.get(eng, "sk_pass_kernel")
     floor_us = 2.0 * N * N / (VALU_F32_PEAK_TFMA * 1e12) * 1e6
@@ -590,7 +592,7 @@ def metric_f32_leg(dev, X, Y, N, d, iters, eps, engine, pmc_traffic, steps=20, w
     return {"dtype": "f32", "N": N, "d": d, "iters": iters, "eps": eps, "engine": eng,
             "status": info["status_name"], "ms_per_step": ms_per_step,
             "pairs_per_s": N / (ms_per_step * 1e-3), "sinkhorn_iters_per_s": iters / (sk_ms * 1e-3),
-            "step": "two calls: pairwise_cost (split-fp16 prep + cost_big16_kernel) + sinkhorn (float32 mesh)",
+            "step": "two calls: pairwise_cost (split-fp16 prep + %s) + sinkhorn (float32 mesh)" % cname,
             "breakdown_ms": {"cost": cost_ms, "sinkhorn_incl_plan": sk_ms,
                              "fused_call": fused_ms, "fused_engine": rf.info()["engine_name"],
                              "fused_fallback": rf.info()["fallback"], "sinkhorn_per_iteration": per_it_ms,
@@ -600,12 +602,12 @@ def metric_f32_leg(dev, X, Y, N, d, iters, eps, engine, pmc_traffic, steps=20, w
                          "note": "K in registers for the whole solve; the solve's per-iteration slope "
                                  "(between iters / 5 and iters) against the VALU floor of 2 N^2 float32 "
                                  "FMAs at 78.6 T FMA/s"},
-            "cost_roofline": {"bound": "mfma", "kernel": "cost_big16_kernel",
+            "cost_roofline": {"bound": "mfma", "kernel": cname,
                               "achieved": 3.0 * cost_flops / (kern_ms * 1e-3) / 1e12,
                               "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": 3.0 * cost_flops / (kern_ms * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS,
                               "kernel_us": kern_ms * 1e3, "prep_us": prep_ms * 1e3,
-                              "op_us": cost_ms * 1e3, "traffic": pmc_traffic("cost_big16_kernel") if pmc_traffic else None,
+                              "op_us": cost_ms * 1e3, "traffic": pmc_traffic(cname) if pmc_traffic else None,
                               "note": "the fp32-accurate product x.y = hi.hi + hi.lo + lo.hi runs as "
                                       "three fp16 MFMA contractions: achieved = 3 x 2*N*N*d / the MFMA "
                                       "kernel's device time vs the dense fp16 MFMA peak"},

@@ -1060,6 +1060,228 @@ __global__ __launch_bounds__(512) void cost_big16_kernel(
 }
 
 
+
+// ---------------------------------------------------------------------------------------
+// The 256 x 256 tile as an 8-phase LDS-DMA pipeline (cdna_hip_programming.md "The 256²
+// 8-phase template"): operands move global -> LDS by global_load_lds_dwordx4 only, in
+// HALF-TILES of 16 KB (128 operand rows x 64 B x 2 sub-buffers: the two 32-deep k halves of
+// a 64-deep K-tile for fp16 operands, NI = 1; the hi and lo images of a 32-deep K-tile for
+// split-fp16, NI = 2), two K-tiles of four half-tiles in 128 KB of LDS.  The waves are
+// 2 (Y, the MFMA A operand) x 4 (X) of 128 Y x 64 X -- cost_big16_kernel's per-wave block,
+// so its epilogue -- and a K-tile runs as four PHASES, one output quadrant each
+// (Y half x X half: A0.B0, A0.B1, A1.B1, A1.B0 -- each phase reads only the fragments the
+// previous one did not leave in registers): ds_read the new fragments, put one half-tile of
+// the NEXT K-tile in flight (2 glds a thread), a counted vmcnt, raw barrier, lgkmcnt(0), the
+// quadrant's 16 (NI = 1) / 24 (NI = 2) MFMAs at raised priority, raw barrier.  Half-tile
+// order per K-tile A0, B0, B1, A1 (first use order): vmcnt(4) in phases 0, 1, 3 retires what
+// the next phase reads and keeps two half-tiles in flight across every barrier; a half-tile
+// is restaged >= 2 phases after its last read.  Each 16 x 16 block gets cost_big16's MFMA
+// sequence (for NI = 2: hi.lo, lo.hi, hi.hi per 32-deep step, in k order), so the same bits.
+// LDS rows are 64 B with cost_big16's XOR chunk permutation (g16swz), applied to each lane's
+// SOURCE chunk since the DMA writes lane-linear (rule 21).  All LDS is one array (a second
+// __shared__ object makes hipcc drain the DMA early).
+typedef __attribute__((address_space(3))) void p8_lds_t;
+typedef __attribute__((address_space(1))) void p8_gbl_t;
+constexpr int P8_SUB = 8192, P8_HT = 2 * P8_SUB, P8_BUF = 4 * P8_HT;
+constexpr int P8_LDS = 2 * P8_BUF + 4 * 256 * 4 + 64;
+__device__ __forceinline__ int p8_byte(int row, int kc) {
+    return row * 64 + ((kc ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3)) << 4);
+}
+template <int N> __device__ __forceinline__ void p8_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <int NI, typename TC>
+__global__ __launch_bounds__(512) void cost_8ph_kernel(
+    const _Float16* __restrict__ Xh, const _Float16* __restrict__ Xl, const float* __restrict__ xs,
+    const float* __restrict__ xx, const _Float16* __restrict__ Yh, const _Float16* __restrict__ Yl,
+    const float* __restrict__ ys, const float* __restrict__ yy, int64_t ldxh, int64_t ldyh, int n, int m, int kpad,
+    int metric, int zero_diag, TC* __restrict__ C, int64_t ldc, unsigned int* cmax, int tiles_n,
+    const float* __restrict__ store_scale) {
+    __shared__ __attribute__((aligned(16))) char smem[P8_LDS];
+    float* sxs = reinterpret_cast<float*>(smem + 2 * P8_BUF);
+    float* sxx = sxs + 256;
+    float* sys = sxx + 256;
+    float* syy = sys + 256;
+    float* wmx = syy + 256;
+
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+    int tm, tn;
+    grouped_tile(wg, nwg, tiles_n, tm, tn);
+    const int i0 = tm * GBM, j0 = tn * GBN;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wn = wid >> 2, wm = wid & 3;  // Y half (128 columns), X quarter (64 rows)
+
+    // norms first: ordinary loads, none while a DMA is in flight
+    if (tid < 256) {
+        const int gi = i0 + tid < n ? i0 + tid : n - 1;
+        sxs[tid] = xs[gi];
+        sxx[tid] = xx[gi];
+    } else {
+        const int c = tid - 256;
+        const int gj = j0 + c < m ? j0 + c : m - 1;
+        sys[c] = ys[gj];
+        syy[c] = yy[gj];
+    }
+
+    // this thread's DMA sources: slot tid of every sub-buffer = local row tid / 4, stored
+    // chunk tid % 4, which holds logical chunk (tid % 4) ^ g(row)
+    const int drow = tid >> 2;
+    const int dkc = (tid & 3) ^ ((0x78 >> (2 * ((drow >> 2) & 3))) & 3);
+    const _Float16* src[4][2];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const bool isy = h < 2;
+        const int hh = h & 1;
+        const int tr = isy ? (drow >> 6) * 128 + hh * 64 + (drow & 63) : (drow >> 5) * 64 + hh * 32 + (drow & 31);
+        const int gr = isy ? (j0 + tr < m ? j0 + tr : m - 1) : (i0 + tr < n ? i0 + tr : n - 1);
+        const _Float16* hi = isy ? Yh + (int64_t)gr * ldyh : Xh + (int64_t)gr * ldxh;
+        if constexpr (NI == 2) {
+            const _Float16* lo = isy ? Yl + (int64_t)gr * ldyh : Xl + (int64_t)gr * ldxh;
+            src[h][0] = hi + dkc * 8;
+            src[h][1] = lo + dkc * 8;
+        } else {
+            src[h][0] = hi + dkc * 8;
+            src[h][1] = hi + 32 + dkc * 8;
+        }
+    }
+    constexpr int BK = NI == 1 ? 64 : 32;
+    // half-tile h of K-tile kt into buffer b
+    auto stage = [&](int h, int kt, int b) {
+        char* dst = smem + b * P8_BUF + h * P8_HT + wid * 1024;
+        const int k0 = kt * BK;
+        __builtin_amdgcn_global_load_lds((p8_gbl_t*)(src[h][0] + k0), (p8_lds_t*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((p8_gbl_t*)(src[h][1] + k0), (p8_lds_t*)(dst + P8_SUB), 16, 0, 0);
+    };
+
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f16x8 fa[4][2], fb[2][2];  // Y fragments of the current Y half, X fragments of the current X half
+    const int kc = lane >> 4, lr = lane & 15;
+    auto read_a = [&](int b, int yh) {
+        const char* base = smem + b * P8_BUF + yh * P8_HT;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int off = p8_byte(wn * 64 + t * 16 + lr, kc);
+            fa[t][0] = *reinterpret_cast<const f16x8*>(base + off);
+            fa[t][1] = *reinterpret_cast<const f16x8*>(base + P8_SUB + off);
+        }
+    };
+    auto read_b = [&](int b, int xh) {
+        const char* base = smem + b * P8_BUF + (2 + xh) * P8_HT;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int off = p8_byte(wm * 32 + t * 16 + lr, kc);
+            fb[t][0] = *reinterpret_cast<const f16x8*>(base + off);
+            fb[t][1] = *reinterpret_cast<const f16x8*>(base + P8_SUB + off);
+        }
+    };
+    auto mfma_quadrant = [&](int yh, int xh) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                f32x4& a = acc[xh * 2 + u][yh * 4 + t];
+                if constexpr (NI == 2) {
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][0], fb[u][1], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][1], fb[u][0], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][0], fb[u][0], a, 0, 0, 0);
+                } else {
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][0], fb[u][0], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][1], fb[u][1], a, 0, 0, 0);
+                }
+            }
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto sync_compute = [&](int yh, int xh) {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mfma_quadrant(yh, xh);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");  // the next phase's reads and DMA stay behind the barrier
+    };
+
+    // prologue: K-tile 0 in the order A0, B0, B1, A1; A0 and B0 landed before the first phase
+    const int nk = kpad / BK;
+    stage(0, 0, 0);
+    stage(2, 0, 0);
+    stage(3, 0, 0);
+    stage(1, 0, 0);
+    p8_vmcnt<4>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // the two wave groups (wn, one wave of each on every SIMD) run one barrier apart, so one
+    // group's MFMAs overlap the other's fragment reads and DMA issue (the template's
+    // stagger); every read stays one phase behind its wait and every restage >= 2 phases
+    // behind its last read, which is what that offset needs
+    const int wsg = __builtin_amdgcn_readfirstlane(wn);
+    if (wsg == 1) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int kt = 0; kt < nk; ++kt) {
+        const int b = kt & 1;
+        const bool more = kt + 1 < nk;
+        // phase 0: A0 x B0
+        read_b(b, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(b, 0);
+        if (more) {
+            stage(0, kt + 1, b ^ 1);
+            p8_vmcnt<4>();  // B1 of this K-tile landed
+        } else {
+            p8_vmcnt<2>();
+        }
+        sync_compute(0, 0);
+        // phase 1: A0 x B1
+        read_b(b, 1);
+        if (more) {
+            stage(2, kt + 1, b ^ 1);
+            p8_vmcnt<4>();  // A1 of this K-tile landed
+        } else {
+            p8_vmcnt<0>();
+        }
+        sync_compute(0, 1);
+        // phase 2: A1 x B1
+        read_a(b, 1);
+        if (more) stage(3, kt + 1, b ^ 1);
+        sync_compute(1, 1);
+        // phase 3: A1 x B0
+        read_b(b, 0);
+        if (more) {
+            stage(1, kt + 1, b ^ 1);
+            p8_vmcnt<4>();  // A0, B0 of the next K-tile landed
+        }
+        sync_compute(1, 0);
+    }
+    if (wsg == 0) __builtin_amdgcn_s_barrier();  // the groups' barrier counts agree again
+
+    const float os = store_scale ? store_scale[0] : 1.0f;
+    const bool vec = i0 + 256 <= n && j0 + 256 <= m && !(zero_diag && i0 == j0) && (ldc % 4) == 0 &&
+                     ((uintptr_t)C % 16) == 0;
+    float lmax;
+    if (metric == OTF_EUCLIDEAN)
+        lmax = vec ? epilogue_tile256_16t<TC, true, true>(acc, sxs, sxx, sys, syy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os)
+                   : epilogue_tile256_16t<TC, true, false>(acc, sxs, sxx, sys, syy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
+    else
+        lmax = vec ? epilogue_tile256_16t<TC, false, true>(acc, sxs, sxx, sys, syy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os)
+                   : epilogue_tile256_16t<TC, false, false>(acc, sxs, sxx, sys, syy, wm, wn, lane, i0, j0, n, m, zero_diag, C, ldc, os);
+    if (cmax) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmx[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            float v = wmx[0];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) v = fmaxf(v, wmx[w]);
+            const unsigned int u = __float_as_uint(v);
+            if (u > __hip_atomic_load(cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(cmax, u);
+        }
+    }
+}
+
 }  // namespace
 
 // Split-fp16 images + row scales + squared norms of two float32 operands in the workspace
@@ -1125,6 +1347,10 @@ static size_t otf_al(size_t x) { return (x + 255) / 256 * 256; }
 // Measured and removed in r05 (numbers in DESIGN.md 4.2): the LDS-DMA ring and the
 // warp-specialised persistent kernels, the 128 x 128 tile at every shape, the split after
 // the MFMA groups.
+// r06: every 256 x 256 tile runs cost_8ph_kernel (OTF_COST_8PH=0 restores the kernels
+// above): same bits as cost_big16_kernel for float32 storage; measured in one process
+// (tools/cost8_probe.py) 66.2 -> 54.0 us at the metric shape (the prep then writes the
+// images: 8.3 -> 13.3 us), config 5 166.5 -> 146.0 us.
 
 size_t otf_cost_ex_workspace_size(int64_t n, int64_t m, int64_t d, int32_t in_dtype) {
     const size_t ldh = (size_t)((d + otf::SBK - 1) / otf::SBK * otf::SBK);
@@ -1141,6 +1367,14 @@ size_t otf_cost_split16_workspace_size(int64_t n, int64_t m, int64_t d) {
 // every otf_cost_pairwise_ex call; otf_cost_last_phases reports the last call's split
 static hipEvent_t g_cost_ev[3];
 static int g_cost_ev_state = 0;  // 0 none, 1 created, 2 recorded
+// OTF_COST_8PH (read per call; default 1): the 8-phase LDS-DMA kernel (cost_8ph_kernel) for
+// the 256 x 256 tile instead of the register-staged kernels; 0 keeps cost_big16_kernel /
+// cost_big_kernel (A/B and bit-identity tests)
+static bool cost_8ph_on() {
+    const char* e = getenv("OTF_COST_8PH");
+    return !(e && atoi(e) == 0);
+}
+
 static bool cost_phases_on() {
     const char* e = getenv("OTF_COST_PHASES");
     if (!(e && atoi(e) != 0)) return false;
@@ -1206,7 +1440,8 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     const int64_t small_rounds = (((n + otf::BM - 1) / otf::BM) * ((m + otf::BN - 1) / otf::BN) + 2 * cus0 - 1) / (2 * cus0);
     const bool big0 = 18 * big_rounds < 10 * small_rounds;
     const bool mfma16 = !f16out;
-    const bool f32in = split && big0 && mfma16 && d % otf::SBK == 0 && ldx % 4 == 0 &&
+    const bool p8 = big0 && cost_8ph_on();
+    const bool f32in = !p8 && split && big0 && mfma16 && d % otf::SBK == 0 && ldx % 4 == 0 &&
                        ldy % 4 == 0 && (uintptr_t)X % 16 == 0 && (uintptr_t)Y % 16 == 0;
     {
         const int rows = (int)n + (same ? 0 : (int)m);
@@ -1258,7 +1493,11 @@ int otf_cost_pairwise_ex(const void* X, int64_t ldx, const void* Y, int64_t ldy,
     if (nwg > INT32_MAX) return OTF_EUNSUPPORTED;
 #define OTF_COST_LAUNCH(NS, TC)                                                                   \
     do {                                                                                          \
-        if (big && mfma16 && f32in)                                                               \
+        if (p8)                                                                                   \
+            otf::cost_8ph_kernel<NS == 3 ? 2 : 1, TC><<<(int)nwg, 512, 0, s>>>(                  \
+                Xh, Xl, xs, xx, Yh, Yl, ys, yy, ldxh, ldyh, (int)n, (int)m, ldh, metric,         \
+                zero_diag, (TC*)C, ldc, (unsigned int*)cmax, tiles_n, store_scale);              \
+        else if (big && mfma16 && f32in)                                                          \
             otf::cost_big16_kernel<NS, TC, NS == 3, NS == 3><<<(int)nwg, 512, 0, s>>>(           \
                 (const _Float16*)X, nullptr, xs, xx, (const _Float16*)Y, nullptr, ys, yy, ldx,   \
                 ldy, (int)n, (int)m, (int)d, metric, zero_diag, (TC*)C, ldc, (unsigned int*)cmax, \

@@ -422,3 +422,50 @@ def test_plan_postprocess_nan_and_zero_rows(ops, dev):
 def test_smoke_entry_point_runs(dev):
     import __graft_entry__ as g
     g.smoke()
+
+
+@pytest.mark.parametrize("n,m,d,in_dt,metric,same", [
+    (4096, 4096, 512, torch.float32, "sqeuclidean", False),
+    (4000, 3900, 256, torch.float32, "euclidean", False),
+    (3000, 3000, 128, torch.float32, "sqeuclidean", True),
+    (4096, 4096, 300, torch.float32, "sqeuclidean", False),
+    (4096, 4096, 40, torch.float32, "sqeuclidean", False),
+    (4096, 4096, 512, torch.float16, "sqeuclidean", False),
+    (4000, 3900, 192, torch.float16, "euclidean", False)])
+def test_cost_8ph_kernel_is_bit_identical_to_register_staged(ops, dev, monkeypatch, n, m, d, in_dt, metric, same):
+    """The 8-phase LDS-DMA cost kernel (cost_8ph_kernel, the default) gives every 16 x 16
+    block cost_big16_kernel's MFMA sequence (split-fp16: hi.lo, lo.hi, hi.hi per 32-deep
+    step; fp16 operands: one MFMA per 32-deep step, in k order) and its epilogue: float32
+    costs, cmax and unit bitwise those of the register-staged kernel (OTF_COST_8PH=0) --
+    ragged tiles, one or two K-tiles (d = 40), d not a multiple of 64, X is Y (zero
+    diagonal), the Euclidean metric, fp16 operands."""
+    g = torch.Generator(device=dev).manual_seed(n + d + 11)
+    X = (torch.randn(n, d, device=dev, generator=g) * torch.logspace(-1, 1, n, device=dev)[:, None]).to(in_dt)
+    Y = X if same else (torch.randn(m, d, device=dev, generator=g) * 0.7 + 0.2).to(in_dt)
+    C1, mx1, u1 = ops.pairwise_cost_ex(X, Y, metric=metric, out_dtype=torch.float32)
+    monkeypatch.setenv("OTF_COST_8PH", "0")
+    C0, mx0, u0 = ops.pairwise_cost_ex(X, Y, metric=metric, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert torch.equal(C0, C1) and torch.equal(mx0, mx1) and torch.equal(u0, u1)
+
+
+@pytest.mark.parametrize("n,m,d,in_dt", [(8192, 8192, 1024, torch.float16), (4000, 3900, 256, torch.float32)])
+def test_cost_8ph_fp16_storage_vs_register_staged_and_oracle(ops, orc, dev, monkeypatch, n, m, d, in_dt):
+    """fp16 cost storage (config 5's form): the 8-phase kernel on 16x16x32 MFMAs against the
+    32x32x16 register-staged kernel (OTF_COST_8PH=0; a different accumulation order, so
+    within fp16 rounding: 1 ulp of the scaled cost) and the oracle on sampled rows; the same
+    store scale (unit) and a cmax within one fp16 ulp."""
+    g = torch.Generator(device=dev).manual_seed(n + d + 13)
+    X = torch.randn(n, d, device=dev, generator=g).to(in_dt)
+    Y = (torch.randn(m, d, device=dev, generator=g) * 0.7 + 0.2).to(in_dt)
+    C1, mx1, u1 = ops.pairwise_cost_ex(X, Y, out_dtype=torch.float16)
+    monkeypatch.setenv("OTF_COST_8PH", "0")
+    C0, mx0, u0 = ops.pairwise_cost_ex(X, Y, out_dtype=torch.float16)
+    torch.cuda.synchronize()
+    assert torch.equal(u0, u1)
+    diff = (C1.float() - C0.float()).abs()
+    assert float((diff / C0.float().abs().clamp_min(2.0 ** -14)).max()) <= 2.0 ** -10
+    assert abs(float(mx1) - float(mx0)) <= float(mx0) * 2.0 ** -10
+    rows = torch.cat([torch.arange(0, 200, device=dev), torch.arange(n - 40, n, device=dev)])
+    Cr, _ = orc.pairwise_cost(X[rows].double().cpu().numpy(), Y.double().cpu().numpy())
+    assert nrel(C1[rows].double().cpu().numpy() * float(u1), Cr) < 2e-3

@@ -23,7 +23,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 PROF = os.path.join(REPO, "profiles")
 HOT = ("sk_mesh64_kernel", "dist_mfma_f64_kernel", "sqnorm_f64_kernel", "dist_scale_kernel",
-       "sk_resident_kernel", "sk_tiled_kernel", "sk_mesh_kernel", "sk_gather_kernel", "sk_pass_kernel", "sk_sweep_kernel", "cost_big_kernel", "cost_big16_kernel", "cost_split16_kernel",
+       "sk_resident_kernel", "sk_tiled_kernel", "sk_mesh_kernel", "sk_gather_kernel", "sk_pass_kernel", "sk_sweep_kernel", "cost_8ph_kernel", "cost_big_kernel", "cost_big16_kernel", "cost_split16_kernel",
        "split16_prep2_kernel", "cost_f16_kernel", "sk_init_kernel", "sk_plan_kernel")
 LIB = os.path.join(REPO, "ot-based-heterogeneous-multi-modal-fusion-embedding-for-ad-analysis-_amd",
                    "otfuse", "lib", "libotfuse.so")
