@@ -82,10 +82,12 @@ __device__ __forceinline__ void sk_stop(otf_sinkhorn_info* info, int last_good, 
     __hip_atomic_store(&info->stop, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The relay fallback's counters (sk_relay_kernel), ints in a 256-B workspace region zeroed
-// by the init kernel: the ticket and the completion count on lines of their own, the cost
-// build's max (float64 bits) and the abort word
-constexpr int kRelayInts = 64, kRelayTicket = 0, kRelayDone = 32, kRelayMax = 48, kRelayAbort = 56;
+// The relay fallback's counters (sk_relay_kernel), ints in a workspace region zeroed by the
+// init kernel: the ticket, the cost build's max (float64 bits), the abort word, and the
+// completion count as 8 shards 256 B apart (a piece adds to shard blockIdx % 8, a waiter sums
+// them: 32 instead of 256 arrivals on one word per pass)
+constexpr int kRelayTicket = 0, kRelayMax = 16, kRelayAbort = 32, kRelayDone = 64, kRelayDoneStride = 64,
+              kRelayShards = 8, kRelayInts = kRelayDone + kRelayShards * kRelayDoneStride;
 
 // ordered int key of a float (monotone), for atomicMin on signed ints
 __device__ __forceinline__ int ord_key(float x) {
@@ -421,7 +423,7 @@ __device__ __forceinline__ void sk_init_body(int t, int stride, const T* a, cons
     // a persistent engine's granule region (mesh), zeroed here instead of by a memset launch
     for (int64_t j = t; j < zero_n; j += stride) zero[j] = make_uint4(0u, 0u, 0u, 0u);
     // the relay fallback's counters (sk_relay_kernel): fresh for every solve
-    if (t < kRelayInts) relay[t] = 0;
+    for (int j = t; j < kRelayInts; j += stride) relay[j] = 0;
     for (int j = t; j < m_pad; j += stride) {
         b_pad[j] = j < m ? b[j] : (T)0;
         cs[j] = cs[cs_stride + j] = cs[2 * cs_stride + j] = 0;
@@ -737,9 +739,10 @@ __global__ __launch_bounds__(256) void sk_plan_kernel(const CT* C, int64_t ldc, 
 // (those store only write-through words and memory-side atomics).  The waiter: one poll and
 // one agent acquire by thread 0, then a barrier.  A pass piece of a workgroup whose previous
 // piece was a pass piece puts its first K row block in flight BEFORE that wait (K is complete
-// and L1-fresh by then).  Measured at the float64 bench shape (tools/relay_probe.py): 62.6 ->
-// 39.5 us per pass, 7.0 -> 4.6 ms per call; ablations of the old form: 21 us of each pass was
-// the dependency wait, 14 the K loads, 8 the column atomics.  Every fallback bumps
+// and L1-fresh by then).  The completion count is sharded (kRelayDone).  Measured at the
+// float64 bench shape (tools/relay_probe.py): 62.6 -> 34.0 us per pass, 7.0 -> 4.0 ms per call;
+// ablations of the old form: 21 us of each pass was the dependency wait, 14 the K loads, 8 the
+// column atomics.  Every fallback bumps
 // g_sk_fallbacks (otf_sinkhorn_fallback_count) and sets info->fallback.  (r06: replaces the
 // one-workgroup re-solve, whose pass loop on a single CU took tens of ms at the metric shape.)
 // ============================================================================
@@ -915,6 +918,14 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
         return t < s_out ? s_fin : s_out;
     };
     auto aload = [](const int* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    // completed tickets: the sum of the shards (each a lower bound of its own count)
+    auto done_count = [&]() -> int {
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < kRelayShards; ++q) c += aload(ctr + kRelayDone + q * kRelayDoneStride);
+        return c;
+    };
+    int* const my_done = ctr + kRelayDone + (int)(blockIdx.x % kRelayShards) * kRelayDoneStride;
     auto set_pass = [&](SkArgs<T>& q, int pass) {
         const int it = pass - 1;
         q.it = it;
@@ -938,11 +949,11 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
                 t = aload(ctr + kRelayTicket);
                 // the solve has stopped (only a pass raises stop, after the reset cleared
                 // it): skip the remaining passes in one step
-                if (t >= s_pass && t < s_fin && aload(ctr + kRelayDone) >= s_pass && aload(&p.info->stop)) {
+                if (t >= s_pass && t < s_fin && done_count() >= s_pass && aload(&p.info->stop)) {
                     int want = t;
                     if (__hip_atomic_compare_exchange_strong(ctr + kRelayTicket, &want, s_fin, __ATOMIC_RELAXED,
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                        __hip_atomic_fetch_add(ctr + kRelayDone, s_fin - t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_fetch_add(my_done, s_fin - t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     continue;
                 }
                 t = __hip_atomic_fetch_add(ctr + kRelayTicket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -959,7 +970,7 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
             if (tid == 0) {
                 int ok = 1;
                 const int nd = need(t);
-                while (aload(ctr + kRelayDone) < nd) {
+                while (done_count() < nd) {
                     if (aload(ctr + kRelayAbort)) { ok = 0; break; }
                     __builtin_amdgcn_s_sleep(2);
                     if (__builtin_amdgcn_s_memrealtime() > deadline) {
@@ -1085,7 +1096,7 @@ __global__ __launch_bounds__(512) void sk_relay_kernel(SkArgs<T> p, SoloArgs<T> 
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            __hip_atomic_fetch_add(ctr + kRelayDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(my_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         deadline = __builtin_amdgcn_s_memrealtime() + x.stall;
     }

@@ -292,7 +292,7 @@ class SinkhornResult:
                 warnings.warn(
                     "persistent Sinkhorn engine could not become co-resident within OTF_REG_MS "
                     "(another persistent kernel held the CUs); the relay fallback solved the "
-                    "problem instead (same POT result, slower: ~4.6 ms at 4096^2 float64)",
+                    "problem instead (same POT result, slower: ~4 ms at 4096^2 float64)",
                     RuntimeWarning, stacklevel=2)
             if d["status"] == L.SK_RUNNING or not d["stop"]:
                 # every engine writes a final status and stop = 1; a solve that left

@@ -469,3 +469,33 @@ def test_cost_8ph_fp16_storage_vs_register_staged_and_oracle(ops, orc, dev, monk
     rows = torch.cat([torch.arange(0, 200, device=dev), torch.arange(n - 40, n, device=dev)])
     Cr, _ = orc.pairwise_cost(X[rows].double().cpu().numpy(), Y.double().cpu().numpy())
     assert nrel(C1[rows].double().cpu().numpy() * float(u1), Cr) < 2e-3
+
+
+@pytest.mark.parametrize("n,m,d,in_dt", [(4096, 4096, 512, torch.float32), (4000, 3900, 192, torch.float16),
+                                         (8192, 8192, 1024, torch.float16)])
+def test_cost_8ph_kernel_race_screen_under_uneven_load(ops, dev, n, m, d, in_dt):
+    """Race screen of the 8-phase kernel's DMA / barrier schedule (a misplaced read passes a
+    single check whenever the DMA happens to land first): 24 launches, half of them beside a
+    memory-bound copy stream and a GEMM on two other streams (uneven load), every result
+    bitwise equal to the first launch alone."""
+    g = torch.Generator(device=dev).manual_seed(n + d + 17)
+    X = torch.randn(n, d, device=dev, generator=g).to(in_dt)
+    Y = (torch.randn(m, d, device=dev, generator=g) * 0.7 + 0.2).to(in_dt)
+    ref, mref, _ = ops.pairwise_cost_ex(X, Y, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    big = torch.empty(64 << 20, device=dev)
+    dst = torch.empty_like(big)
+    A = torch.randn(4096, 4096, device=dev)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    bad = 0
+    for k in range(24):
+        if k % 2:
+            with torch.cuda.stream(s1):
+                for _ in range(3):
+                    dst.copy_(big)
+            with torch.cuda.stream(s2):
+                A @ A
+        C, mx, _ = ops.pairwise_cost_ex(X, Y, out_dtype=torch.float32)
+        torch.cuda.synchronize()
+        bad += int(not (torch.equal(C, ref) and torch.equal(mx, mref)))
+    assert bad == 0
