@@ -431,13 +431,14 @@ def test_smoke_entry_point_runs(dev):
     (4096, 4096, 300, torch.float32, "sqeuclidean", False),
     (4096, 4096, 40, torch.float32, "sqeuclidean", False),
     (4096, 4096, 512, torch.float16, "sqeuclidean", False),
+    (4096, 4096, 48, torch.float16, "sqeuclidean", False),    # one 64-deep K-tile
     (4000, 3900, 192, torch.float16, "euclidean", False)])
 def test_cost_8ph_kernel_is_bit_identical_to_register_staged(ops, dev, monkeypatch, n, m, d, in_dt, metric, same):
     """The 8-phase LDS-DMA cost kernel (cost_8ph_kernel, the default) gives every 16 x 16
     block cost_big16_kernel's MFMA sequence (split-fp16: hi.lo, lo.hi, hi.hi per 32-deep
     step; fp16 operands: one MFMA per 32-deep step, in k order) and its epilogue: float32
     costs, cmax and unit bitwise those of the register-staged kernel (OTF_COST_8PH=0) --
-    ragged tiles, one or two K-tiles (d = 40), d not a multiple of 64, X is Y (zero
+    ragged tiles, one or two K-tiles (d = 48 fp16, d = 40 split), d not a multiple of 64, X is Y (zero
     diagonal), the Euclidean metric, fp16 operands."""
     g = torch.Generator(device=dev).manual_seed(n + d + 11)
     X = (torch.randn(n, d, device=dev, generator=g) * torch.logspace(-1, 1, n, device=dev)[:, None]).to(in_dt)
