@@ -2398,6 +2398,21 @@ int sk_finish(SkArgs<T>& p, const SkSetup<T>& su, const CT* C, int64_t ldc, int6
     return OTF_OK;
 }
 
+// OTF_FORCE_REG_GIVEUP=1 (tests, probes; read per call): every persistent launch (the
+// engines below and the fused pairwise launches) is replaced by a registration give-up, so
+// the relay fallback runs the solve at the caller's full shape without a contending grid
+inline bool force_giveup() {
+    const char* e = getenv("OTF_FORCE_REG_GIVEUP");
+    return e && atoi(e) != 0;
+}
+__global__ void sk_giveup_kernel(otf_sinkhorn_info* info) {
+    if (threadIdx.x == 0) mark_stalled(&info->stalled, kStallRegistration);
+}
+inline hipError_t forced_giveup(otf_sinkhorn_info* info, hipStream_t s) {
+    sk_giveup_kernel<<<1, 64, 0, s>>>(info);
+    return hipGetLastError();
+}
+
 // The relay fallback behind a persistent engine launch (sk_relay_kernel): one no-op dispatch
 // unless the persistent solve's registration gave up.  pw: the pairwise float64 form (the
 // relay builds the cost into C = the workspace's n x m float64 buffer, then K over it).
@@ -2572,7 +2587,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
 
     if (o.engine == OTF_ENGINE_GATHER && !gfits) return OTF_EUNSUPPORTED;
     if (gather_pick) {
-        const hipError_t e = run_gather<T, CT>(C, ldc, (int)n, (int)m, (const T*)su.w.a_pad,
+        const hipError_t e = force_giveup() ? forced_giveup(info, s) : run_gather<T, CT>(C, ldc, (int)n, (int)m, (const T*)su.w.a_pad,
                                                (const T*)su.w.b_pad, cost_scale, o, su.w.gather, u_out,
                                                v_out, P_out, ldp, P_dtype, info, errlog,
                                                /*zeroed=*/true, s);
@@ -2589,7 +2604,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     if (o.engine == OTF_ENGINE_MESH && !mfits) return OTF_EUNSUPPORTED;
     if constexpr (kMesh64) {
         if (mfits && (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled() && mesh_auto_ok))) {
-            const hipError_t e = run_mesh64((const double*)C, ldc, (int)n, (int)m, (const double*)su.w.a_pad,
+            const hipError_t e = force_giveup() ? forced_giveup(info, s) : run_mesh64((const double*)C, ldc, (int)n, (int)m, (const double*)su.w.a_pad,
                                             (const double*)su.w.b_pad, (const double*)cost_scale, o, su.w.mesh,
                                             (double*)u_out, (double*)v_out, P_out, ldp, P_dtype, info, errlog,
                                             /*zeroed=*/mesh_pick, s);
@@ -2600,7 +2615,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     }
     if constexpr (sizeof(T) == 4) {
         if (mfits && (o.engine == OTF_ENGINE_MESH || (o.engine == OTF_ENGINE_AUTO && mesh_enabled()))) {
-            const hipError_t e = run_mesh<CT>(C, ldc, (int)n, (int)m, (const float*)su.w.a_pad,
+            const hipError_t e = force_giveup() ? forced_giveup(info, s) : run_mesh<CT>(C, ldc, (int)n, (int)m, (const float*)su.w.a_pad,
                                               (const float*)su.w.b_pad, cost_scale, o, su.w.mesh,
                                               u_out, v_out, P_out, ldp, P_dtype, info, errlog,
                                               /*zeroed=*/mesh_pick, s, shp);
@@ -2614,7 +2629,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
         if (LOG || avg_pass_ms || !(o.engine == OTF_ENGINE_AUTO || o.engine == OTF_ENGINE_SWEEP) ||
             o.max_iter < 1 || !sweep_supported<T, CT>(n, m, ldc) || !whole)
             return OTF_EUNSUPPORTED;
-        const hipError_t e = run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
+        const hipError_t e = force_giveup() ? forced_giveup(info, s) : run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
                                               (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
                                               v_out, P_out, ldp, P_dtype, info, errlog, s, nullptr, shp,
                                               kstream_buf(su, ws_bytes));
@@ -2639,7 +2654,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     if (o.engine == OTF_ENGINE_TILED && (LOG || sh || !tfits)) return OTF_EUNSUPPORTED;
     if (want_tiled) {
         Workspace w = su.w;
-        const hipError_t e = run_tiled<T, CT>(C, ldc, (int)n, (int)m, cost_scale, o, w, u_out, v_out,
+        const hipError_t e = force_giveup() ? forced_giveup(info, s) : run_tiled<T, CT>(C, ldc, (int)n, (int)m, cost_scale, o, w, u_out, v_out,
                                               P_out, ldp, P_dtype, info, errlog, s);
         if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
         (void)hipGetLastError();
@@ -2662,7 +2677,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
     if (o.engine == OTF_ENGINE_RESIDENT && (LOG || sh || !fits)) return OTF_EUNSUPPORTED;
     if (want_res) {
         Workspace w = su.w;
-        const hipError_t e = run_resident<T, CT>(su.cfg, su.nrb, C, ldc, (int)n, (int)m, cost_scale,
+        const hipError_t e = force_giveup() ? forced_giveup(info, s) : run_resident<T, CT>(su.cfg, su.nrb, C, ldc, (int)n, (int)m, cost_scale,
                                                  o, w, u_out, v_out, P_out, ldp, P_dtype, info,
                                                  errlog, s);
         if (e == hipSuccess) return check_hip(launch_solo<T, CT>(su, C, ldc, n, m, cost_scale, o, u_out, v_out, P_out, ldp, P_dtype, info, errlog, s));
@@ -2676,7 +2691,7 @@ int run_sinkhorn(const T* a, const T* b, const CT* C, int64_t n, int64_t m, int6
                        sweep_supported<T, CT>(n, m, ldc);
     if (o.engine == OTF_ENGINE_SWEEP && !sfits) return OTF_EUNSUPPORTED;
     if (sfits && (o.engine == OTF_ENGINE_SWEEP || o.engine == OTF_ENGINE_AUTO)) {
-        const hipError_t e = run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
+        const hipError_t e = force_giveup() ? forced_giveup(info, s) : run_sweep<T, CT>(C, ldc, (int)n, (int)m, su.m_pad, (const T*)su.w.a_pad,
                                               (const T*)su.w.b_pad, cost_scale, o, su.w.sweep, u_out,
                                               v_out, P_out, ldp, P_dtype, info, errlog, s, nullptr, shp,
                                               kstream_buf(su, ws_bytes));
@@ -3025,15 +3040,6 @@ __global__ __launch_bounds__(256) void pw_norms_kernel(const float* X, int64_t l
     for (int k = lane; k < d; k += 64) s = fma((double)r[k], (double)r[k], s);
     s = wave_sum(s);
     if (lane == 0) (i < n ? nx[i] : ny[i - n]) = s;
-}
-// OTF_FORCE_REG_GIVEUP=1 (tests, probes): the fused launch is replaced by a registration
-// give-up, read per call
-inline bool force_giveup() {
-    const char* e = getenv("OTF_FORCE_REG_GIVEUP");
-    return e && atoi(e) != 0;
-}
-__global__ void sk_giveup_kernel(otf_sinkhorn_info* info) {
-    if (threadIdx.x == 0) mark_stalled(&info->stalled, kStallRegistration);
 }
 struct PwLayout {
     size_t sk, c, cost, total;

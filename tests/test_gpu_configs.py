@@ -382,3 +382,43 @@ def test_long_persistent_solve_outlives_the_stall_limit(dev, monkeypatch, engine
     assert info["engine_name"] == engine
     assert info["status_name"] == "max_iter" and not info["stalled"]
     assert elapsed > 0.04 * 1.5     # the solve really outlived the stall limit
+
+
+@pytest.mark.parametrize("engine,n,dt,reg,shift,tol", [
+    ("mesh", 2048, torch.float32, 0.1, False, 1e-5),
+    ("mesh", 2048, torch.float32, 5e-3, True, 1e-4),     # the shifted kernel's relay
+    ("sweep", 4096, torch.float16, 0.1, False, 1e-4),    # fp16 cost storage, float32 compute
+    ("tiled", 4096, torch.float32, 0.1, False, 1e-5),
+    ("gather", 512, torch.float64, 0.05, False, 1e-9),
+    ("resident", 512, torch.float64, 0.05, False, 1e-9),
+    ("mesh", 4096, torch.float64, 0.1, False, 1e-9)])
+def test_forced_relay_fallback_matches_the_engine(dev, monkeypatch, engine, n, dt, reg, shift, tol):
+    """Every persistent engine's registration give-up (forced, OTF_FORCE_REG_GIVEUP=1: the
+    launch is replaced by the give-up) hands the whole solve to the relay fallback, whose
+    ticketed streaming passes must give the engine's own POT result: the plan within the
+    compute precision's tolerance, the same status and iteration count (float64: POT's
+    converged stop), info fallback = 1 -- for the float32 mesh (plain and
+    shifted kernel), the sweep engine on an fp16 cost, the tiled, gather and resident
+    engines and the float64 mesh on a float64 cost."""
+    from otfuse import ops
+    g = torch.Generator(device=dev).manual_seed(n + 31)
+    X = torch.randn(n, 48, device=dev, generator=g, dtype=torch.float64)
+    C = torch.cdist(X, X * 0.9 + 0.1) ** 2
+    C = (C / C.max()).to(dt)
+    cdt = torch.float64 if dt == torch.float64 else torch.float32
+    a = torch.full((n,), 1.0 / n, device=dev, dtype=cdt)
+    # float64: POT's converged stop (checked every 10 iterations); float32: a fixed count (its
+    # error near a threshold may round either way between two summation orders)
+    kw = dict(max_iter=300, stop_thr=1e-7, engine=engine) if dt == torch.float64 else \
+        dict(max_iter=100, stop_thr=0.0, engine=engine)
+    if shift:
+        kw["shift"] = True
+    r0 = ops.sinkhorn(a, a, C, reg, **kw)
+    i0 = r0.info()
+    assert i0["fallback"] == 0
+    monkeypatch.setenv("OTF_FORCE_REG_GIVEUP", "1")
+    r1 = ops.sinkhorn(a, a, C, reg, **kw)
+    i1 = r1.info()
+    assert i1["fallback"] == 1 and i1["engine_name"] == "stream" and i1["stalled"] == 0
+    assert i1["status_name"] == i0["status_name"] and i1["niter"] == i0["niter"]
+    assert ((r1.plan.double() - r0.plan.double()).abs().max() / r0.plan.double().abs().max()).item() < tol
